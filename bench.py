@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DeepSpeech2 (2x conv + 5x BiGRU-800) bf16 training throughput.
+
+Metric (BASELINE.json): audio-sec/sec training throughput of the whole job, on synthetic
+LibriSpeech-shaped spectrogram batches with random-init weights (no dataset/checkpoint
+is available offline). Every step is a full training step: forward, CTC loss, backward,
+RCCL gradient all-reduce (N > 1), fused Adam + weight EMA.
+
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Batch: 32 utterances per GPU (the reference's headline batch, src/train.sh:42), each
+padded to 1000 frames (10 s) with per-utterance lengths in (900, 1000] frames (one
+100-frame bucket, as bucket_by_sequence_length does in src/deepSpeech_input.py:53-60) and
+~15 characters/second of labels. audio-seconds = sum of true lengths / 100 (10 ms frames).
+Scaling is weak: per-GPU work is fixed as N grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch_size", type=int, default=32, help="utterances per GPU")
+    p.add_argument("--frames", type=int, default=1000, help="padded utterance length (10 ms frames)")
+    p.add_argument("--num_hidden", type=int, default=800)
+    p.add_argument("--num_rnn_layers", type=int, default=5)
+    p.add_argument("--num_filters", type=int, default=32)
+    p.add_argument("--cell", type=str, default="gru")
+    p.add_argument("--engine", type=str, default="hip", choices=["hip", "ref"])
+    p.add_argument("--bucket_mb", type=float, default=32.0)
+    p.add_argument("--allreduce_bf16", action="store_true")
+    p.add_argument("--profile_dir", type=str, default="", help="write a torch.profiler trace here")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    from deepspeech_amd.parallel.dist import init_distributed, shutdown
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+    from deepspeech_amd.trainer import Trainer, LRSchedule
+    from deepspeech_amd.ops import rnn as RNN
+
+    ctx = init_distributed("auto")
+    dev = ctx.device
+    if dev.type != "cuda" and args.engine == "hip":
+        args.engine = "ref"
+    torch.manual_seed(1234)
+    model = DeepSpeech2(num_filters=args.num_filters, num_hidden=args.num_hidden,
+                        num_rnn_layers=args.num_rnn_layers, cell=args.cell, bidirectional=True,
+                        stack_fix=True, seq_bn="frozen").to(dev)
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    model.set_engine(args.engine, dtype)
+    trainer = Trainer(model, LRSchedule(1e-4, 10 ** 9, 0.9), moving_avg_decay=0.9999,
+                      world_size=ctx.world_size, bucket_mb=args.bucket_mb,
+                      allreduce_bf16=args.allreduce_bf16)
+    feed = FixedShapeBatches(args.batch_size, max_frames=args.frames, seed=1000 + ctx.rank, pool=4)
+    batches = [to_device(feed.next(), dev) for _ in range(4)]
+    audio_per_step = [float(b["seq_lens"].sum().item()) / 100.0 for b in batches]
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for i in range(args.warmup):
+        trainer.step(batches[i % len(batches)])
+    sync()
+    if dev.type == "cuda":
+        RNN.check_errors()
+    ctx.barrier()
+    sync()
+    prof = None
+    if args.profile_dir and ctx.is_main:
+        from torch.profiler import profile, ProfilerActivity
+        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    audio = 0.0
+    loss = None
+    for i in range(args.steps):
+        loss = trainer.step(batches[i % len(batches)])
+        audio += audio_per_step[i % len(batches)]
+    sync()
+    ctx.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(args.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(args.profile_dir, "bench_trace.json"))
+        with open(os.path.join(args.profile_dir, "bench_ops.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    if dev.type == "cuda":
+        RNN.check_errors()
+    elapsed = ctx.all_reduce_max(elapsed)
+    total_audio = ctx.all_reduce_sum(audio)
+    ms = 1000.0 * elapsed / args.steps
+    value = total_audio / elapsed
+    flops = model.flops_per_step(args.batch_size, args.frames) * ctx.world_size
+    lossv = float(loss.float().item()) if loss is not None else float("nan")
+    if ctx.is_main:
+        out = {
+            "metric": "audio-sec/sec training throughput (whole node), DS2 BiGRU",
+            "value": round(value, 2),
+            "unit": "audio-sec/sec",
+            "n_gpus": ctx.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (LibriSpeech-shaped spectrograms, random-init weights)",
+            "config": {
+                "model": "DeepSpeech2 2xconv(32) + %dx%s-%d bidirectional + CTC" % (
+                    args.num_rnn_layers, "BiGRU" if args.cell == "gru" else "BiRNN", args.num_hidden),
+                "global_batch": args.batch_size * ctx.world_size,
+                "seq_len": args.frames,
+                "parallelism": "dp%d" % ctx.world_size,
+                "engine": args.engine,
+            },
+            "per_gpu_audio_sec_per_sec": round(value / ctx.world_size, 2),
+            "utterances_per_sec": round(args.batch_size * ctx.world_size * args.steps / elapsed, 2),
+            "achieved_tflops": round(flops * args.steps / elapsed / 1e12, 2),
+            "final_loss": round(lossv, 4),
+        }
+        print(json.dumps(out), flush=True)
+    shutdown(ctx)
+
+
+if __name__ == "__main__":
+    main()

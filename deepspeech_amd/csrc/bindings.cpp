@@ -1,0 +1,285 @@
+// Python bindings of the deepspeech_amd gfx950 kernels (module deepspeech_amd._C).
+//
+// The .hip translation units expose plain extern "C" launchers that take raw pointers
+// and a hipStream_t; this file validates tensors (device, dtype, contiguity, shapes)
+// and launches on PyTorch's current HIP stream, so every op composes with torch streams
+// and can be captured into a hipGraph.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+extern "C" {
+struct DS2RnnFwd {
+  int T, N, NP, H, S, BG, steps, gstride, ndir, cell, nw, mt, persistent;
+  const int* lens;
+  const void* gx;
+  const void* U[2];
+  const float* bh[2];
+  void* y[2];
+  void* hx[2];
+  float* hsave[2];
+  float* gates[2];
+  unsigned* flags;
+  unsigned* err;
+  long long timeout;
+};
+struct DS2RnnBwd {
+  int T, N, NP, H, S, BG, steps, gstride, ndir, cell, nw, mt, persistent;
+  const int* lens;
+  const void* dy;
+  const void* U[2];
+  const float* hsave[2];
+  const float* gates[2];
+  void* dgh[2];
+  void* dgx;
+  float* carry[2];
+  unsigned* flags;
+  unsigned* err;
+  long long timeout;
+};
+int ds2_rnn_fwd(const DS2RnnFwd* d, hipStream_t st);
+int ds2_rnn_bwd(const DS2RnnBwd* d, hipStream_t st);
+int ds2_rnn_kpw(int H, int G, int nw, int fwd);
+int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const int* labels, const int* label_lens,
+                  float* loss, void* grad, float* lp_ws, float* alpha_ws, int T, int N, int K, int Lmax, int blank,
+                  int zero_inf, hipStream_t st);
+int ds2_bn_stats(const void* y, int y_bf16, int N, int C, int T, int F, float* part, int nb, float eps, float* mean,
+                 float* invstd, float* run_mean, float* run_var, float momentum, hipStream_t st);
+int ds2_bn_chunks(int N, int T, int F);
+int ds2_bn_apply(const void* y, int y_bf16, const float* mean, const float* invstd, const float* gamma,
+                 const float* beta, void* out, int out_bf16, int N, int C, int T, int F, int layout, hipStream_t st);
+int ds2_bn_bwd(const void* dout, int dout_bf16, const void* y, int y_bf16, const float* mean, const float* invstd,
+               const float* gamma, const float* beta, float* part, int nb, float* dgamma, float* dbeta, void* dy,
+               int dy_bf16, int N, int C, int T, int F, int layout, hipStream_t st);
+int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
+                 float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, hipStream_t st);
+int ds2_grad_norm_blocks(long long n);
+int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
+int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
+}
+
+namespace {
+
+using OptT = c10::optional<at::Tensor>;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "deepspeech_amd kernel launch failed in ", what, " (code ", rc, ")");
+}
+
+void need_gpu(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+template <typename T>
+T* ptr_or_null(const OptT& t, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  need_gpu(*t, name);
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+int is_bf16(const at::Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return 1;
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "expected float32 or bfloat16 tensor");
+  return 0;
+}
+
+// --------------------------------------------------------------------------- RNN
+void rnn_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_f, OptT bh_b, at::Tensor y_f,
+             OptT y_b, at::Tensor hx_f, OptT hx_b, at::Tensor hs_f, OptT hs_b, OptT gates_f, OptT gates_b,
+             at::Tensor flags, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t steps,
+             int64_t gstride, int64_t ndir, int64_t cell, int64_t nw, int64_t mt, bool persistent, int64_t timeout) {
+  need_gpu(gx, "gx");
+  TORCH_CHECK(gx.scalar_type() == at::kBFloat16, "gx must be bf16");
+  TORCH_CHECK(lens.scalar_type() == at::kInt, "lens must be int32");
+  TORCH_CHECK(gx.numel() >= T * N * gstride, "gx too small");
+  DS2RnnFwd d{};
+  d.T = (int)T; d.N = (int)N; d.NP = (int)NP; d.H = (int)H; d.S = (int)(H / 16); d.BG = (int)BG;
+  d.steps = (int)steps; d.gstride = (int)gstride; d.ndir = (int)ndir; d.cell = (int)cell; d.nw = (int)nw;
+  d.mt = (int)mt; d.persistent = persistent ? 1 : 0;
+  TORCH_CHECK(NP == BG * 16 * mt, "NP must equal BG*16*mt");
+  TORCH_CHECK(hx_f.numel() >= (steps + 1) * NP * H, "hx too small");
+  d.lens = lens.data_ptr<int>();
+  d.gx = gx.data_ptr();
+  d.U[0] = U_f.data_ptr();
+  d.U[1] = U_b.has_value() ? U_b->data_ptr() : nullptr;
+  d.bh[0] = ptr_or_null<const float>(bh_f, "bh_f");
+  d.bh[1] = ptr_or_null<const float>(bh_b, "bh_b");
+  d.y[0] = y_f.data_ptr();
+  d.y[1] = ptr_or_null<void>(y_b, "y_b");
+  d.hx[0] = hx_f.data_ptr();
+  d.hx[1] = ptr_or_null<void>(hx_b, "hx_b");
+  d.hsave[0] = hs_f.data_ptr<float>();
+  d.hsave[1] = ptr_or_null<float>(hs_b, "hsave_b");
+  d.gates[0] = ptr_or_null<float>(gates_f, "gates_f");
+  d.gates[1] = ptr_or_null<float>(gates_b, "gates_b");
+  TORCH_CHECK(ndir == 1 || (d.U[1] && d.y[1] && d.hx[1] && d.hsave[1]), "backward-direction buffers missing");
+  TORCH_CHECK(cell == 0 || (d.gates[0] && (ndir == 1 || d.gates[1])), "GRU needs gate buffers");
+  d.flags = reinterpret_cast<unsigned*>(flags.data_ptr<int>());
+  d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  d.timeout = timeout;
+  check(ds2_rnn_fwd(&d, cur_stream()), "rnn_fwd");
+}
+
+void rnn_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tensor hs_f, OptT hs_b, OptT gates_f,
+             OptT gates_b, at::Tensor dgh_f, OptT dgh_b, at::Tensor dgx, OptT carry_f, OptT carry_b,
+             at::Tensor flags, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t steps,
+             int64_t gstride, int64_t ndir, int64_t cell, int64_t nw, int64_t mt, bool persistent, int64_t timeout) {
+  need_gpu(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dgx.scalar_type() == at::kBFloat16, "dy/dgx must be bf16");
+  TORCH_CHECK(dgx.numel() >= T * N * gstride, "dgx too small");
+  DS2RnnBwd d{};
+  d.T = (int)T; d.N = (int)N; d.NP = (int)NP; d.H = (int)H; d.S = (int)(H / 16); d.BG = (int)BG;
+  d.steps = (int)steps; d.gstride = (int)gstride; d.ndir = (int)ndir; d.cell = (int)cell; d.nw = (int)nw;
+  d.mt = (int)mt; d.persistent = persistent ? 1 : 0;
+  TORCH_CHECK(NP == BG * 16 * mt, "NP must equal BG*16*mt");
+  d.lens = lens.data_ptr<int>();
+  d.dy = dy.data_ptr();
+  d.U[0] = U_f.data_ptr();
+  d.U[1] = U_b.has_value() ? U_b->data_ptr() : nullptr;
+  d.hsave[0] = hs_f.data_ptr<float>();
+  d.hsave[1] = ptr_or_null<float>(hs_b, "hsave_b");
+  d.gates[0] = ptr_or_null<float>(gates_f, "gates_f");
+  d.gates[1] = ptr_or_null<float>(gates_b, "gates_b");
+  d.dgh[0] = dgh_f.data_ptr();
+  d.dgh[1] = ptr_or_null<void>(dgh_b, "dgh_b");
+  d.dgx = dgx.data_ptr();
+  d.carry[0] = ptr_or_null<float>(carry_f, "carry_f");
+  d.carry[1] = ptr_or_null<float>(carry_b, "carry_b");
+  TORCH_CHECK(ndir == 1 || (d.U[1] && d.hsave[1] && d.dgh[1]), "backward-direction buffers missing");
+  d.flags = reinterpret_cast<unsigned*>(flags.data_ptr<int>());
+  d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  d.timeout = timeout;
+  check(ds2_rnn_bwd(&d, cur_stream()), "rnn_bwd");
+}
+
+int64_t rnn_kpw(int64_t H, int64_t G, int64_t nw, bool fwd) { return ds2_rnn_kpw((int)H, (int)G, (int)nw, fwd ? 1 : 0); }
+
+// --------------------------------------------------------------------------- CTC
+void ctc_fused(at::Tensor logits, at::Tensor lens, at::Tensor labels, at::Tensor label_lens, at::Tensor loss,
+               at::Tensor grad, at::Tensor lp_ws, at::Tensor alpha_ws, int64_t blank, bool zero_inf) {
+  need_gpu(logits, "logits");
+  need_gpu(labels, "labels");
+  TORCH_CHECK(logits.dim() == 3, "logits must be [T, N, K]");
+  TORCH_CHECK(grad.scalar_type() == logits.scalar_type() && grad.sizes() == logits.sizes(), "grad mismatch");
+  const int T = (int)logits.size(0), N = (int)logits.size(1), K = (int)logits.size(2);
+  const int Lmax = (int)labels.size(1);
+  TORCH_CHECK(labels.size(0) == N && lens.numel() == N && label_lens.numel() == N, "batch mismatch");
+  TORCH_CHECK(lp_ws.numel() >= (int64_t)N * T * 32, "lp workspace too small");
+  TORCH_CHECK(alpha_ws.numel() >= (int64_t)N * T * (2 * Lmax + 1), "alpha workspace too small");
+  check(ds2_ctc_fused(logits.data_ptr(), is_bf16(logits), lens.data_ptr<int>(), labels.data_ptr<int>(),
+                      label_lens.data_ptr<int>(), loss.data_ptr<float>(), grad.data_ptr(), lp_ws.data_ptr<float>(),
+                      alpha_ws.data_ptr<float>(), T, N, K, Lmax, (int)blank, zero_inf ? 1 : 0, cur_stream()),
+        "ctc_fused");
+}
+
+// --------------------------------------------------------------------------- BN
+int64_t bn_chunks(int64_t N, int64_t T, int64_t F) { return ds2_bn_chunks((int)N, (int)T, (int)F); }
+
+void bn_stats(at::Tensor y, at::Tensor part, double eps, at::Tensor mean, at::Tensor invstd, OptT run_mean,
+              OptT run_var, double momentum) {
+  need_gpu(y, "y");
+  TORCH_CHECK(y.dim() == 4, "y must be NCHW");
+  const int N = (int)y.size(0), C = (int)y.size(1), T = (int)y.size(2), F = (int)y.size(3);
+  const int nb = (int)(part.numel() / (2 * C));
+  check(ds2_bn_stats(y.data_ptr(), is_bf16(y), N, C, T, F, part.data_ptr<float>(), nb, (float)eps,
+                     mean.data_ptr<float>(), invstd.data_ptr<float>(), ptr_or_null<float>(run_mean, "run_mean"),
+                     ptr_or_null<float>(run_var, "run_var"), (float)momentum, cur_stream()),
+        "bn_stats");
+}
+
+void bn_apply(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor beta, at::Tensor out,
+              int64_t layout) {
+  need_gpu(y, "y");
+  need_gpu(out, "out");
+  const int N = (int)y.size(0), C = (int)y.size(1), T = (int)y.size(2), F = (int)y.size(3);
+  TORCH_CHECK(out.numel() == y.numel(), "out size mismatch");
+  check(ds2_bn_apply(y.data_ptr(), is_bf16(y), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                     gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), is_bf16(out), N, C, T, F,
+                     (int)layout, cur_stream()),
+        "bn_apply");
+}
+
+void bn_bwd(at::Tensor dout, at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor beta,
+            at::Tensor part, at::Tensor dgamma, at::Tensor dbeta, at::Tensor dy, int64_t layout) {
+  need_gpu(dout, "dout");
+  need_gpu(y, "y");
+  need_gpu(dy, "dy");
+  const int N = (int)y.size(0), C = (int)y.size(1), T = (int)y.size(2), F = (int)y.size(3);
+  const int nb = (int)(part.numel() / (2 * C));
+  TORCH_CHECK(dout.numel() == y.numel() && dy.numel() == y.numel(), "size mismatch");
+  check(ds2_bn_bwd(dout.data_ptr(), is_bf16(dout), y.data_ptr(), is_bf16(y), mean.data_ptr<float>(),
+                   invstd.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(), part.data_ptr<float>(),
+                   nb, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dy.data_ptr(), is_bf16(dy), N, C, T, F,
+                   (int)layout, cur_stream()),
+        "bn_bwd");
+}
+
+// --------------------------------------------------------------------------- optimizer
+void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, OptT p16, double lr_t, double b1,
+              double b2, double eps, double gscale, double ema_keep, OptT skip) {
+  need_gpu(p, "p");
+  need_gpu(g, "g");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 arena expected");
+  const long long n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "arena size mismatch");
+  check(ds2_adam_ema(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                     ptr_or_null<float>(ema, "ema"), ptr_or_null<void>(p16, "p16"), n, (float)lr_t, (float)b1,
+                     (float)b2, (float)eps, (float)gscale, (float)ema_keep, ptr_or_null<const int>(skip, "skip"),
+                     cur_stream()),
+        "adam_ema");
+}
+
+int64_t grad_norm_blocks(int64_t n) { return ds2_grad_norm_blocks(n); }
+
+void grad_norm(at::Tensor g, double gscale, at::Tensor part, at::Tensor bad) {
+  need_gpu(g, "g");
+  check(ds2_grad_norm(g.data_ptr<float>(), g.numel(), (float)gscale, part.data_ptr<float>(), (int)part.numel(),
+                      bad.data_ptr<int>(), cur_stream()),
+        "grad_norm");
+}
+
+void cast_bf16(at::Tensor x, at::Tensor y) {
+  need_gpu(x, "x");
+  need_gpu(y, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "size mismatch");
+  check(ds2_cast_bf16(x.data_ptr<float>(), y.data_ptr(), x.numel(), cur_stream()), "cast_bf16");
+}
+
+// --------------------------------------------------------------------------- device info
+py::dict device_info(int64_t dev) {
+  hipDeviceProp_t prop;
+  TORCH_CHECK(hipGetDeviceProperties(&prop, (int)dev) == hipSuccess, "hipGetDeviceProperties failed");
+  py::dict d;
+  d["name"] = std::string(prop.name);
+  d["gcn_arch"] = std::string(prop.gcnArchName);
+  d["cus"] = prop.multiProcessorCount;
+  d["lds_per_block"] = (int64_t)prop.sharedMemPerBlock;
+  d["clock_khz"] = prop.clockRate;
+  d["total_mem"] = (int64_t)prop.totalGlobalMem;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "deepspeech_amd gfx950 kernels";
+  m.def("rnn_fwd", &rnn_fwd);
+  m.def("rnn_bwd", &rnn_bwd);
+  m.def("rnn_kpw", &rnn_kpw);
+  m.def("ctc_fused", &ctc_fused);
+  m.def("bn_chunks", &bn_chunks);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("adam_ema", &adam_ema);
+  m.def("grad_norm_blocks", &grad_norm_blocks);
+  m.def("grad_norm", &grad_norm);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("device_info", &device_info);
+}

@@ -1,0 +1,268 @@
+"""DeepSpeech2 network: 2-D conv front-end -> stacked (bi)directional RNN/GRU -> FC.
+
+Reference graph: src/deepSpeech_NCHW.py:81-201 (NCHW default) and src/deepSpeech.py:81-203.
+
+  conv1  [20x5] stride (2,2) VALID, 1 -> C,  bias -0.05, BN(eps 1e-3), clipped ReLU(20)
+  conv2  [10x5] stride (2,1) VALID, C -> C,  bias -0.05, BN(eps 1e-3), clipped ReLU(20)
+  [N,C,T2,F2] -> time-major [T2, N, C*F2]        (src/deepSpeech_NCHW.py:166-168)
+  L x recurrent layer (cell: rnn_relu | gru), directions summed (Q2)
+  FC H -> 29 classes, time-major logits            (src/deepSpeech_NCHW.py:188-198)
+
+Two engines share these parameters:
+  * ``ref`` — pure PyTorch (CPU golden model, any device);
+  * ``hip`` — gfx950 kernels: fused BN+clip(+time-major store), persistent
+    bidirectional recurrence, fused CTC (see deepspeech_amd/ops).
+
+Reference quirks handled explicitly:
+  Q1 stack_fix, Q2 sum of directions, Q3 seq_bn='frozen', Q4 proper BN train/eval,
+  Q7 dynamic batch sizes.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import FREQ_BINS, NUM_CLASSES
+from ..ops import reference as R
+
+CONV_BN_EPS = 1e-3
+GATES = {"rnn_relu": 1, "gru": 3}
+
+
+def tf_fans(shape) -> Tuple[int, int]:
+    """Fan computation of TF's variance_scaling / glorot initialisers for a TF shape."""
+    if len(shape) == 2:
+        return shape[0], shape[1]
+    receptive = 1
+    for d in shape[:-2]:
+        receptive *= d
+    return shape[-2] * receptive, shape[-1] * receptive
+
+
+def he_trunc_normal_(t: torch.Tensor, tf_shape) -> torch.Tensor:
+    """variance_scaling_initializer(factor=2, FAN_IN, uniform=False) of TF 1.x contrib:
+    truncated normal with stddev sqrt(1.3*factor/fan_in) (src/helper_routines.py:65-72)."""
+    fan_in, _ = tf_fans(tf_shape)
+    std = math.sqrt(1.3 * 2.0 / fan_in)
+    with torch.no_grad():
+        nn.init.trunc_normal_(t, mean=0.0, std=std, a=-2 * std, b=2 * std)
+    return t
+
+
+def glorot_uniform_(t: torch.Tensor, tf_shape) -> torch.Tensor:
+    """TF's default get_variable initializer (glorot_uniform) for the RNN W/U."""
+    fan_in, fan_out = tf_fans(tf_shape)
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    with torch.no_grad():
+        t.uniform_(-lim, lim)
+    return t
+
+
+def conv_out_len(T: int) -> Tuple[int, int]:
+    t1 = (T - 20) // 2 + 1
+    t2 = (t1 - 10) // 2 + 1
+    return t1, t2
+
+
+def freq_out(F_in: int = FREQ_BINS) -> Tuple[int, int]:
+    f1 = (F_in - 5) // 2 + 1
+    f2 = f1 - 5 + 1
+    return f1, f2
+
+
+class ConvBlock(nn.Module):
+    """conv + bias + BatchNorm + clipped ReLU (src/deepSpeech_NCHW.py:110-158)."""
+
+    def __init__(self, cin: int, cout: int, kernel: Tuple[int, int], stride: Tuple[int, int]):
+        super().__init__()
+        self.stride = stride
+        self.weight = nn.Parameter(torch.empty(cout, cin, *kernel))
+        self.bias = nn.Parameter(torch.full((cout,), -0.05))
+        self.bn_gamma = nn.Parameter(torch.ones(cout))
+        self.bn_beta = nn.Parameter(torch.zeros(cout))
+        self.register_buffer("running_mean", torch.zeros(cout))
+        self.register_buffer("running_var", torch.ones(cout))
+        # TF HWIO shape for initialisation parity
+        he_trunc_normal_(self.weight, [kernel[0], kernel[1], cin, cout])
+
+    def forward_ref(self, x: torch.Tensor) -> torch.Tensor:
+        y = F.conv2d(x, self.weight.to(x.dtype), self.bias.to(x.dtype), stride=self.stride)
+        y = F.batch_norm(y, self.running_mean, self.running_var, self.bn_gamma.to(y.dtype),
+                         self.bn_beta.to(y.dtype), training=self.training, momentum=0.01,
+                         eps=CONV_BN_EPS)
+        return R.clipped_relu(y)
+
+
+class RecurrentDirection(nn.Module):
+    """Parameters of one direction of one recurrent layer.
+
+    rnn_relu: W [H,in], U [H,H], b [H] — names follow CustomRNNCell2 (src/custom_ops.py:56-70).
+    gru     : W [3H,in], U [3H,H], b [3H] (input bias, gates r,z,n), b_h [3H] (recurrent bias).
+    The sequence-BN moving stats are buffers (non-trainable, like the reference's sbn vars).
+    """
+
+    def __init__(self, in_dim: int, hidden: int, cell: str):
+        super().__init__()
+        G = GATES[cell]
+        self.cell = cell
+        self.hidden = hidden
+        self.W = nn.Parameter(torch.empty(G * hidden, in_dim))
+        self.U = nn.Parameter(torch.empty(G * hidden, hidden))
+        self.b = nn.Parameter(torch.zeros(G * hidden))
+        if cell == "gru":
+            self.b_h = nn.Parameter(torch.zeros(G * hidden))
+        else:
+            self.register_parameter("b_h", None)
+        self.register_buffer("sbn_mean", torch.zeros(G * hidden))
+        self.register_buffer("sbn_var", torch.ones(G * hidden))
+        glorot_uniform_(self.W, [G * hidden, in_dim])
+        glorot_uniform_(self.U, [G * hidden, hidden])
+
+
+class RecurrentLayer(nn.Module):
+    def __init__(self, in_dim: int, hidden: int, cell: str, bidirectional: bool, seq_bn: str):
+        super().__init__()
+        self.cell = cell
+        self.hidden = hidden
+        self.bidirectional = bidirectional
+        self.seq_bn = seq_bn
+        self.fw = RecurrentDirection(in_dim, hidden, cell)
+        self.bw = RecurrentDirection(in_dim, hidden, cell) if bidirectional else None
+
+    def directions(self) -> List[RecurrentDirection]:
+        return [self.fw] + ([self.bw] if self.bw is not None else [])
+
+    def input_projection_ref(self, x: torch.Tensor, d: RecurrentDirection, lens) -> torch.Tensor:
+        y = x @ d.W.to(x.dtype).t()
+        y = R.seq_batch_norm(y, lens, self.seq_bn, d.sbn_mean, d.sbn_var, self.training)
+        return y + d.b.to(y.dtype)
+
+    def forward_ref(self, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+        gx_f = self.input_projection_ref(x, self.fw, lens)
+        gx_b = self.input_projection_ref(x, self.bw, lens) if self.bw is not None else None
+        bh = lambda d: None if d is None or d.b_h is None else d.b_h.to(x.dtype)
+        return R.birnn_ref(self.cell, gx_f, gx_b, self.fw.U.to(x.dtype),
+                           None if self.bw is None else self.bw.U.to(x.dtype),
+                           bh(self.fw), bh(self.bw), lens)
+
+
+class DeepSpeech2(nn.Module):
+    def __init__(self, num_filters: int = 32, num_hidden: int = 1024, num_rnn_layers: int = 2,
+                 cell: str = "rnn_relu", bidirectional: bool = True, stack_fix: bool = True,
+                 seq_bn: str = "frozen", num_classes: int = NUM_CLASSES,
+                 freq_bins: int = FREQ_BINS):
+        super().__init__()
+        if cell not in GATES:
+            raise ValueError("cell must be one of %s" % list(GATES))
+        self.num_filters = num_filters
+        self.num_hidden = num_hidden
+        self.num_rnn_layers = num_rnn_layers
+        self.cell = cell
+        self.bidirectional = bidirectional
+        self.stack_fix = stack_fix
+        self.seq_bn = seq_bn
+        self.num_classes = num_classes
+        self.freq_bins = freq_bins
+        _, f2 = freq_out(freq_bins)
+        self.rnn_in = f2 * num_filters                     # 75*C = 2400 for 161 bins
+        self.conv1 = ConvBlock(1, num_filters, (20, 5), (2, 2))
+        self.conv2 = ConvBlock(num_filters, num_filters, (10, 5), (2, 1))
+        layers = []
+        for i in range(num_rnn_layers):
+            # Q1: with stack_fix=False every layer consumes the conv output.
+            in_dim = self.rnn_in if (i == 0 or not stack_fix) else num_hidden
+            layers.append(RecurrentLayer(in_dim, num_hidden, cell, bidirectional, seq_bn))
+        self.rnn = nn.ModuleList(layers)
+        self.fc_weight = nn.Parameter(torch.empty(num_classes, num_hidden))
+        self.fc_bias = nn.Parameter(torch.zeros(num_classes))
+        he_trunc_normal_(self.fc_weight, [num_classes, num_hidden])
+        self.engine = "ref"
+        self.compute_dtype = torch.float32
+
+    # ------------------------------------------------------------------ config
+    def set_engine(self, engine: str, compute_dtype: torch.dtype = torch.float32) -> "DeepSpeech2":
+        if engine not in ("ref", "hip"):
+            raise ValueError(engine)
+        self.engine = engine
+        self.compute_dtype = compute_dtype
+        return self
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def flops_per_step(self, N: int, T: int) -> float:
+        """Analytic training FLOPs (fwd + 2x bwd) for a [N, T] batch."""
+        t1, t2 = conv_out_len(T)
+        f1, f2 = freq_out(self.freq_bins)
+        C, H, G = self.num_filters, self.num_hidden, GATES[self.cell]
+        dirs = 2 if self.bidirectional else 1
+        fwd = 2.0 * N * t1 * f1 * C * 100                     # conv1
+        fwd += 2.0 * N * t2 * f2 * C * C * 50                  # conv2
+        for i, layer in enumerate(self.rnn):
+            in_dim = layer.fw.W.shape[1]
+            fwd += dirs * 2.0 * N * t2 * G * H * (in_dim + H)
+        fwd += 2.0 * N * t2 * H * self.num_classes
+        return 3.0 * fwd
+
+    # ------------------------------------------------------------------ forward
+    def frontend(self, feats: torch.Tensor) -> torch.Tensor:
+        """feats [N, T, F] -> time-major rnn input [T2, N, C*F2]."""
+        if self.engine == "hip":
+            from ..ops import frontend as FE
+            return FE.frontend_hip(self, feats)
+        x = feats.unsqueeze(1)
+        x = self.conv1.forward_ref(x)
+        x = self.conv2.forward_ref(x)
+        N, C, T2, F2 = x.shape
+        return x.permute(2, 0, 1, 3).reshape(T2, N, C * F2)
+
+    def recurrent(self, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+        inp = x
+        out = x
+        for layer in self.rnn:
+            if self.engine == "hip":
+                from ..ops import rnn as RNN
+                out = RNN.recurrent_layer_hip(layer, inp, lens)
+            else:
+                out = layer.forward_ref(inp, lens)
+            inp = out if self.stack_fix else x
+        return out
+
+    def head(self, h: torch.Tensor) -> torch.Tensor:
+        T, N, H = h.shape
+        w = self.fc_weight.to(h.dtype)
+        b = self.fc_bias.to(h.dtype)
+        return torch.addmm(b, h.reshape(T * N, H), w.t()).view(T, N, -1)
+
+    def forward(self, feats: torch.Tensor, seq_lens: torch.Tensor
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Returns (logits [T2, N, K] time-major, rnn lengths [N] int32)."""
+        lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
+        if self.engine == "ref" and feats.device.type == "cuda" and self.compute_dtype != torch.float32:
+            with torch.autocast("cuda", dtype=self.compute_dtype):
+                x = self.frontend(feats)
+                h = self.recurrent(x, lens)
+                logits = self.head(h)
+            return logits.float(), lens
+        if self.engine == "hip":
+            feats = feats.to(self.compute_dtype)
+        x = self.frontend(feats)
+        h = self.recurrent(x, lens.to(x.device))
+        return self.head(h), lens
+
+    # ------------------------------------------------------------------ loss
+    def loss(self, logits: torch.Tensor, lens: torch.Tensor, targets: torch.Tensor,
+             target_lens: torch.Tensor) -> torch.Tensor:
+        """Mean CTC loss over the batch (src/deepSpeech_NCHW.py:204-228)."""
+        if self.engine == "hip":
+            from ..ops import ctc as CTC
+            return CTC.ctc_loss_hip(logits, lens, targets, target_lens).mean()
+        return R.ctc_loss_ref(logits, targets, lens, target_lens).mean()
+
+
+def build_model(**kw) -> DeepSpeech2:
+    return DeepSpeech2(**kw)

@@ -1,0 +1,84 @@
+"""Process-group setup for one-process-per-GPU data parallelism.
+
+The reference is single-process (src/deepSpeech_train.py:425 pins everything to /cpu;
+its multi-tower ``average_gradients`` at :193-228 is dead code). Here each rank drives
+one MI355X; ``torch.distributed`` with backend "nccl" is RCCL over xGMI on ROCm, "gloo"
+is used for CPU tests. Rendezvous is env:// (torchrun sets RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    local_rank: int = 0
+    world_size: int = 1
+    backend: Optional[str] = None
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def enabled(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    def barrier(self) -> None:
+        if self.enabled:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def all_reduce_max(self, x: float) -> float:
+        if not self.enabled:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_reduce_sum(self, x: float) -> float:
+        if not self.enabled:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        return float(t.item())
+
+
+def init_distributed(device_pref: str = "auto", timeout_s: int = 600) -> DistContext:
+    """Initialise from torchrun env vars; a no-op single-process context otherwise."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = (device_pref in ("auto", "cuda")) and torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    ctx = DistContext(rank=rank, local_rank=local, world_size=world, device=device)
+    if world > 1:
+        backend = "nccl" if use_cuda else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if use_cuda:
+            kw["device_id"] = device
+        if not dist.is_initialized():
+            dist.init_process_group(**kw)
+        ctx.backend = backend
+    return ctx
+
+
+def shutdown(ctx: DistContext) -> None:
+    if ctx.enabled and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,121 @@
+"""Bucketed gradient all-reduce overlapped with backward.
+
+MI355X-first choices:
+  * gradients already live in one flat fp32 arena (ops/optim.py), laid out in the order
+    backward produces them, so a bucket is a contiguous slice: no pack/unpack copies;
+  * a bucket is launched (async RCCL all-reduce) from a post-accumulate-grad hook the
+    moment its last parameter's gradient lands, while BPTT of earlier layers continues.
+    The recurrent layers finish their weight gradients one layer at a time, so bucket
+    boundaries are snapped to layer (parameter) boundaries;
+  * default bucket size 32 MB: each all-reduce is long enough to run at xGMI link rate
+    (ring algorithms are per-link bound on the point-to-point mesh) but small enough that
+    the last bucket (conv layers, ~0.1 MB) adds almost nothing after backward ends;
+  * optional bf16 compression halves bytes on the links (sum in bf16, scaled in fp32
+    afterwards by the optimizer's gscale = 1/world).
+The SUM is averaged by the optimizer (``gscale``), so no extra division kernel runs.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+class GradBucketer:
+    def __init__(self, arena, bucket_mb: float = 32.0, compress_bf16: bool = False,
+                 process_group=None):
+        self.arena = arena
+        self.pg = process_group
+        self.compress = compress_bf16
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        limit = int(bucket_mb * 1024 * 1024 / 4)
+        # snap buckets to parameter boundaries, in arena (= gradient production) order
+        self.buckets: List[Tuple[int, int, List[int]]] = []
+        cur: List[int] = []
+        start = None
+        for i, (off, n) in enumerate(arena.offsets):
+            if start is None:
+                start = off
+            cur.append(i)
+            end = off + n
+            if end - start >= limit:
+                self.buckets.append((start, arena.offsets[cur[-1]][0] + arena.offsets[cur[-1]][1], cur))
+                cur, start = [], None
+        if cur:
+            self.buckets.append((start, arena.offsets[cur[-1]][0] + arena.offsets[cur[-1]][1], cur))
+        # extend each bucket to the next bucket's start so alignment padding is covered too
+        fixed = []
+        for bi, (s, e, idx) in enumerate(self.buckets):
+            e2 = self.buckets[bi + 1][0] if bi + 1 < len(self.buckets) else arena.numel
+            fixed.append((s, e2, idx))
+        self.buckets = fixed
+        self.param_bucket = {}
+        for bi, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self.param_bucket[i] = bi
+        self._pending: List[int] = []
+        self._launched: List[bool] = []
+        self._works = []
+        self._shadow: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
+        self._handles = []
+        self.enabled = self.world > 1
+        if self.enabled:
+            for i, p in enumerate(arena.params):
+                self._handles.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.prepare()
+
+    def _make_hook(self, i: int):
+        def hook(_p):
+            b = self.param_bucket[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._launch(b)
+        return hook
+
+    def prepare(self) -> None:
+        self._pending = [len(idx) for (_, _, idx) in self.buckets]
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+
+    def _launch(self, b: int) -> None:
+        if self._launched[b]:
+            return
+        self._launched[b] = True
+        s, e, _ = self.buckets[b]
+        g = self.arena.grad[s:e]
+        if self.compress:
+            sh = self._shadow[b]
+            if sh is None or sh.numel() != g.numel():
+                sh = torch.empty(g.numel(), device=g.device, dtype=torch.bfloat16)
+                self._shadow[b] = sh
+            sh.copy_(g)
+            self._works.append((b, dist.all_reduce(sh, group=self.pg, async_op=True)))
+        else:
+            self._works.append((b, dist.all_reduce(g, group=self.pg, async_op=True)))
+
+    def finish(self) -> None:
+        """Launch buckets whose params got no gradient (in index order on every rank),
+        then wait for all all-reduces of this step."""
+        if not self.enabled:
+            return
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:
+                self._launch(b)
+        for b, w in self._works:
+            w.wait()
+            if self.compress:
+                s, e, _ = self.buckets[b]
+                self.arena.grad[s:e].copy_(self._shadow[b])
+        self.prepare()
+
+    def remove(self) -> None:
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+
+def broadcast_params(arena, src: int = 0, process_group=None) -> None:
+    """Make every rank start from rank 0's weights (one collective on the flat arena)."""
+    if dist.is_initialized() and dist.get_world_size(process_group) > 1:
+        dist.broadcast(arena.flat, src=src, group=process_group)

@@ -1,0 +1,103 @@
+"""One training step, shared by the CLI driver (train.py) and bench.py.
+
+Reference step (src/deepSpeech_train.py:292-380 + :419-496): forward, mean CTC loss,
+backward, Adam with staircase-decayed LR, weight EMA (0.9999, num_updates=global_step),
+loss EMA (0.9), NaN assert.
+
+MI355X step:
+  arena.zero_grad()                       one memset over the flat gradient arena
+  logits = model(feats)                   conv (bf16) + fused BN/clip -> persistent RNN
+                                          layers -> FC GEMM
+  loss = fused CTC(logits)                loss and dlogits in one kernel
+  loss.backward()                         RCCL bucket all-reduces launch from grad hooks
+  bucketer.finish()                       wait for the in-flight buckets
+  optimizer.step()                        fused Adam + EMA, one kernel over the arena
+No host synchronisation happens inside the step; the loss is returned as a device tensor.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from .models import DeepSpeech2
+from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
+from .parallel.grad_sync import GradBucketer, broadcast_params
+
+
+@dataclass
+class LRSchedule:
+    initial_lr: float
+    decay_steps: int
+    decay_rate: float
+    staircase: bool = True
+
+    def __call__(self, step: int) -> float:
+        return exponential_decay(self.initial_lr, step, self.decay_steps, self.decay_rate, self.staircase)
+
+
+def lr_schedule_from_args(args, steps_per_epoch: int) -> LRSchedule:
+    """decay_steps = batches_per_epoch * num_epochs_per_decay (src/deepSpeech_train.py:239-241),
+    with the epoch size taken from the ACTIVE dataset (quirk Q14)."""
+    return LRSchedule(args.initial_lr, max(1, int(steps_per_epoch * args.num_epochs_per_decay)),
+                      args.lr_decay_factor)
+
+
+class Trainer:
+    def __init__(self, model: DeepSpeech2, lr_schedule: LRSchedule, moving_avg_decay: Optional[float] = 0.9999,
+                 world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
+                 nan_policy: str = "abort", collapse_repeated: bool = False):
+        self.model = model
+        self.arena = ParamArena(model)
+        self.opt = FusedAdamEMA(self.arena, lr=lr_schedule.initial_lr, ema_decay=moving_avg_decay)
+        self.lr_schedule = lr_schedule
+        self.world = world_size
+        self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb, compress_bf16=allreduce_bf16)
+        if world_size > 1:
+            broadcast_params(self.arena)
+            if self.opt.ema is not None:
+                self.opt.ema.copy_(self.arena.flat)
+        self.global_step = 0
+        self.nan_policy = nan_policy
+        self.collapse_repeated = collapse_repeated
+        self.loss_ema: Optional[float] = None
+        self.last_skip: Optional[torch.Tensor] = None
+
+    @property
+    def lr(self) -> float:
+        return self.lr_schedule(self.global_step)
+
+    def step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
+        model = self.model
+        model.train()
+        self.arena.zero_grad()
+        logits, lens = model(batch["feats"], batch["seq_lens"])
+        loss = model.loss(logits, lens, batch["labels"], batch["label_lens"])
+        loss.backward()
+        self.bucketer.finish()
+        gscale = 1.0 / self.world
+        skip = None
+        if self.nan_policy == "skip":
+            _, skip = self.opt.grad_norm_and_finite(gscale)
+            self.last_skip = skip
+        self.opt.step(self.lr, self.global_step, gscale=gscale, skip_flag=skip)
+        self.global_step += 1
+        return loss.detach()
+
+    def update_loss_ema(self, loss_value: float, decay: float = 0.9) -> float:
+        """tf.train.ExponentialMovingAverage(0.9) of the loss (src/deepSpeech_train.py:175-188)."""
+        if self.loss_ema is None:
+            self.loss_ema = loss_value
+        else:
+            self.loss_ema = decay * self.loss_ema + (1 - decay) * loss_value
+        return self.loss_ema
+
+    # ---- EMA weights for eval (reference evaluates the shadow variables) -------------
+    def swap_ema(self) -> None:
+        if self.opt.ema is None:
+            return
+        tmp = self.arena.flat.clone()
+        self.arena.flat.copy_(self.opt.ema)
+        self.opt.ema.copy_(tmp)

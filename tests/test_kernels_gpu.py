@@ -1,0 +1,201 @@
+"""Numerics of every gfx950 kernel against a plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deepspeech_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+# --------------------------------------------------------------------------- recurrence
+def _rnn_case(cuda, cell, N, H, T, ndir, mode, seed=0, din=None):
+    import os
+    from deepspeech_amd.ops import rnn as RNN
+    torch.manual_seed(seed)
+    G = RNN.GATES[cell]
+    lens = torch.randint(max(1, T // 2), T + 1, (N,), dtype=torch.int32)
+    lens[0] = T
+    scale = 0.5 if cell == "gru" else 0.2
+    gx = (torch.randn(T, N, ndir * G * H) * scale).bfloat16().to(cuda)
+    for b in range(N):
+        gx[int(lens[b]):, b] = 0
+    Us = [(torch.randn(G * H, H) / math.sqrt(H)).bfloat16().to(cuda) for _ in range(ndir)]
+    bhs = [(torch.randn(G * H) * 0.1).to(cuda) if cell == "gru" else None for _ in range(ndir)]
+    old = os.environ.get("DS2_RNN_MODE")
+    os.environ["DS2_RNN_MODE"] = mode
+    try:
+        RNN._plan_cache.clear()
+        plan = RNN.plan_for(N, H, cell, ndir, cuda)
+    finally:
+        if old is None:
+            os.environ.pop("DS2_RNN_MODE")
+        else:
+            os.environ["DS2_RNN_MODE"] = old
+    # HIP
+    gx_h = gx.clone().requires_grad_(True)
+    U_h = [u.clone().requires_grad_(True) for u in Us]
+    b_h = [b.clone().requires_grad_(True) if b is not None else None for b in bhs]
+    y = RNN.BiRecurrence.apply(gx_h, lens.to(cuda), U_h[0], U_h[1] if ndir == 2 else None,
+                               b_h[0], b_h[1] if ndir == 2 else None, plan)
+    dy = torch.randn(T, N, H, device=cuda).bfloat16()
+    for b in range(N):
+        dy[int(lens[b]):, b] = 0
+    y.backward(dy)
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    # fp32 reference
+    gx_r = gx.float().clone().requires_grad_(True)
+    U_r = [u.float().clone().requires_grad_(True) for u in Us]
+    b_r = [b.clone().requires_grad_(True) if b is not None else None for b in bhs]
+    GH = G * H
+    yr = R.birnn_ref(cell, gx_r[..., :GH], gx_r[..., GH:] if ndir == 2 else None, U_r[0],
+                     U_r[1] if ndir == 2 else None, b_r[0], b_r[1] if ndir == 2 else None,
+                     lens.to(cuda))
+    yr.backward(dy.float())
+    assert _rel(y, yr) < 2e-2, ("y", _rel(y, yr))
+    assert _rel(gx_h.grad, gx_r.grad) < 3e-2, ("dgx", _rel(gx_h.grad, gx_r.grad))
+    for d in range(ndir):
+        assert _rel(U_h[d].grad, U_r[d].grad) < 3e-2, ("dU", d, _rel(U_h[d].grad, U_r[d].grad))
+        if cell == "gru":
+            assert _rel(b_h[d].grad, b_r[d].grad) < 3e-2, ("dbh", d)
+    # padding positions must be exactly zero
+    for b in range(N):
+        L = int(lens[b])
+        assert float(y[L:, b].abs().max() if L < T else 0) == 0.0
+        assert float(gx_h.grad[L:, b].abs().max() if L < T else 0) == 0.0
+
+
+@pytest.mark.parametrize("cell", ["rnn_relu", "gru"])
+@pytest.mark.parametrize("mode", ["auto", "step"])
+def test_birnn_small(cuda, cell, mode):
+    _rnn_case(cuda, cell, N=5, H=64, T=23, ndir=2, mode=mode)
+
+
+@pytest.mark.parametrize("cell", ["rnn_relu", "gru"])
+def test_birnn_ds2_shape(cuda, cell):
+    # the flagship geometry: batch 32, H=800 (two batch groups, 50 slices per direction)
+    _rnn_case(cuda, cell, N=32, H=800, T=61, ndir=2, mode="auto", seed=3)
+
+
+def test_unirnn_gru(cuda):
+    _rnn_case(cuda, "gru", N=17, H=256, T=40, ndir=1, mode="auto", seed=5)
+
+
+def test_birnn_mt2(cuda):
+    # batch 96 with H=1280 forces two 16-row tiles per workgroup
+    _rnn_case(cuda, "gru", N=96, H=1280, T=12, ndir=2, mode="auto", seed=7)
+
+
+# --------------------------------------------------------------------------- CTC
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ctc_fused(cuda, dtype):
+    from deepspeech_amd.ops import ctc as CTC
+    torch.manual_seed(0)
+    T, N, K = 50, 6, 29
+    logits = (torch.randn(T, N, K) * 2).to(dtype).to(cuda)
+    lens = torch.tensor([50, 45, 30, 50, 12, 40], dtype=torch.int32)
+    Ls = [20, 10, 14, 1, 5, 19]
+    labels = torch.zeros(N, max(Ls), dtype=torch.int32)
+    for b, L in enumerate(Ls):
+        labels[b, :L] = torch.randint(0, K - 1, (L,))
+    labels[0, 3] = labels[0, 4]          # a repeat (needs a blank between)
+    lab_lens = torch.tensor(Ls, dtype=torch.int32)
+    x = logits.clone().requires_grad_(True)
+    loss = CTC.ctc_loss_hip(x, lens.to(cuda), labels.to(cuda), lab_lens.to(cuda))
+    loss.mean().backward()
+    xr = logits.float().clone().requires_grad_(True)
+    lr = R.ctc_loss_ref(xr, labels.to(cuda), lens.to(cuda), lab_lens.to(cuda))
+    lr.mean().backward()
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert torch.allclose(loss, lr, rtol=tol, atol=tol), (loss, lr)
+    assert _rel(x.grad, xr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+def test_ctc_infeasible_zero(cuda):
+    from deepspeech_amd.ops import ctc as CTC
+    T, N, K = 4, 1, 29
+    logits = torch.randn(T, N, K, device=cuda, requires_grad=True)
+    labels = torch.tensor([[1, 1, 1, 1]], dtype=torch.int32, device=cuda)
+    loss = CTC.ctc_loss_hip(logits, torch.tensor([4], dtype=torch.int32, device=cuda), labels,
+                            torch.tensor([4], dtype=torch.int32, device=cuda))
+    loss.sum().backward()
+    assert float(loss) == 0.0 and float(logits.grad.abs().sum()) == 0.0
+
+
+# --------------------------------------------------------------------------- BN + clip
+@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_clip(cuda, layout, dtype):
+    from deepspeech_amd.ops.frontend import BNClip, BN_EPS
+    torch.manual_seed(0)
+    N, C, T, Fd = 3, 8, 37, 11
+    y = (torch.randn(N, C, T, Fd) * 3 + 1).to(dtype).to(cuda)
+    gamma = (torch.rand(C) + 0.5).to(cuda)
+    beta = (torch.randn(C) * 0.5).to(cuda)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    yh = y.clone().requires_grad_(True)
+    gh, bh = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    out = BNClip.apply(yh, gh, bh, rm, rv, True, layout, dtype)
+    yr = y.float().clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    ref = R.clipped_relu(F.batch_norm(yr, None, None, gr, br, training=True, eps=BN_EPS))
+    if layout == 1:
+        ref = ref.permute(2, 0, 1, 3).reshape(T, N, C * Fd)
+    dout = torch.randn_like(ref)
+    out.backward(dout.to(dtype))
+    ref.backward(dout)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert _rel(out, ref) < tol
+    assert _rel(yh.grad, yr.grad) < tol * 3
+    assert _rel(gh.grad, gr.grad) < tol * 3
+    assert _rel(bh.grad, br.grad) < tol * 3
+    # running stats updated with unbiased variance
+    m = y.float().mean(dim=(0, 2, 3))
+    assert torch.allclose(rm, 0.01 * m, atol=1e-3)
+
+
+# --------------------------------------------------------------------------- optimizer
+def test_adam_ema_matches_torch(cuda):
+    from deepspeech_amd.ops.optim import ParamArena, FusedAdamEMA
+    torch.manual_seed(0)
+
+    def make(dev):
+        torch.manual_seed(1)
+        return torch.nn.Sequential(torch.nn.Linear(13, 7), torch.nn.Linear(7, 3)).to(dev)
+
+    outs = []
+    for dev in (torch.device("cpu"), cuda):
+        m = make(dev)
+        arena = ParamArena(m)
+        opt = FusedAdamEMA(arena, ema_decay=0.99)
+        g = torch.Generator().manual_seed(2)
+        for step in range(5):
+            arena.zero_grad()
+            x = torch.randn(4, 13, generator=g).to(dev)
+            m(x).pow(2).sum().backward()
+            opt.step(lr=1e-2, global_step=step)
+        outs.append((arena.flat.cpu(), opt.ema.cpu()))
+    assert torch.allclose(outs[0][0], outs[1][0], atol=1e-5)
+    assert torch.allclose(outs[0][1], outs[1][1], atol=1e-5)
+
+
+def test_grad_norm(cuda):
+    from deepspeech_amd.ops.optim import ParamArena, FusedAdamEMA
+    m = torch.nn.Linear(100, 50).to(cuda)
+    arena = ParamArena(m)
+    arena.grad.normal_()
+    opt = FusedAdamEMA(arena)
+    n, bad = opt.grad_norm_and_finite(0.5)
+    assert abs(float(n) - float(arena.grad.norm() * 0.5)) < 1e-3
+    assert int(bad) == 0
+    arena.grad[3] = float("nan")
+    n, bad = opt.grad_norm_and_finite(1.0)
+    assert int(bad) == 1
