@@ -227,13 +227,16 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
           red[wave][m * 16 + (lane >> 4) * 4 + j][g * 16 + (lane & 15)] = acc[m][g][j];
     __syncthreads();
 
-    // (5) cell epilogue
+    // (5) cell epilogue: only the bf16 exchange copy is written before the publish
+    float hout[EPT];
+    float4 gsv[EPT];
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
       const int e = tid + i * NT;
+      hout[i] = 0.f;
+      gsv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (e < NE) {
         const int row = e >> 4, c = e & 15;
-        const int b = r0 + row, u = u0 + c;
         float pre[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -244,7 +247,6 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
         }
         const bool act = s < lenr[i];
         float hn;
-        float4 gsv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (CELL == CELL_GRU) {
           const float ghr = pre[0] + bhv[i][0];
           const float ghz = pre[1] + bhv[i][1];
@@ -253,21 +255,14 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
           const float z = sigmoidf_(gxv[i][1] + ghz);
           const float n = tanhf_(gxv[i][2] + r * ghn);
           hn = (1.f - z) * n + z * hreg[i];
-          gsv = make_float4(r, z, n, ghn);
+          if (act) gsv[i] = make_float4(r, z, n, ghn);
         } else {
           hn = fminf(fmaxf(gxv[i][0] + pre[0], 0.f), RELU_CAP);
         }
         const float hnew = act ? hn : hreg[i];
         hreg[i] = hnew;
+        hout[i] = act ? hn : 0.f;
         stage[row][c] = f2bf(hnew);
-        a.hsave[dir][((size_t)(s + 1) * NP + b) * H + u] = hnew;
-        if (CELL == CELL_GRU) {
-          reinterpret_cast<float4*>(a.gates[dir])[((size_t)s * NP + b) * H + u] = act ? gsv : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        if (b < N) {
-          const int t = act ? ((dir == 0) ? s : (lenr[i] - 1 - s)) : s;
-          a.y[dir][((size_t)t * N + b) * H + u] = act ? f2bf(hn) : (bf16_t)0;
-        }
       }
     }
     __syncthreads();
@@ -282,6 +277,23 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) st_flag(a.flags + grp * S + slice, (unsigned)(s - a.s_begin + 1));
+    }
+
+    // (7) off-critical-path stores: fp32 state, gates, time-indexed output
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NT;
+      if (e < NE) {
+        const int row = e >> 4, c = e & 15;
+        const int b = r0 + row, u = u0 + c;
+        const bool act = s < lenr[i];
+        a.hsave[dir][((size_t)(s + 1) * NP + b) * H + u] = hreg[i];
+        if (CELL == CELL_GRU) reinterpret_cast<float4*>(a.gates[dir])[((size_t)s * NP + b) * H + u] = gsv[i];
+        if (b < N) {
+          const int t = act ? ((dir == 0) ? s : (lenr[i] - 1 - s)) : s;
+          a.y[dir][((size_t)t * N + b) * H + u] = f2bf(hout[i]);
+        }
+      }
     }
   }
 }
@@ -413,19 +425,21 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
       for (int j = 0; j < 4; ++j) red[wave][m * 16 + (lane >> 4) * 4 + j][lane & 15] = acc[m][j];
     __syncthreads();
 
-    // (4) cell backward epilogue
+    // (4) cell backward epilogue (exchange copy first; dgx stores after the publish)
+    float gxs[EPT][G];
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
       const int e = tid + i * NT;
+#pragma unroll
+      for (int g = 0; g < G; ++g) gxs[i][g] = 0.f;
       if (e < NE) {
         const int row = e >> 4, c = e & 15;
-        const int b = r0 + row, u = u0 + c;
         float dhrec = 0.f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) dhrec += red[w][row][c];
         const bool act = s < lenr[i];
         const float dh = dyv[i] + carry[i] + dhrec;
-        float ghv[G], gxg[G];
+        float ghv[G];
         float cnew = 0.f;
         if (CELL == CELL_GRU) {
           const float r = gsv[i].x, z = gsv[i].y, n = gsv[i].z, ghn = gsv[i].w;
@@ -438,27 +452,21 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
           const float daz = dz * z * (1.f - z);
           const float dar = dr * r * (1.f - r);
           ghv[0] = dar; ghv[1] = daz; ghv[2] = dghn;
-          gxg[0] = dar; gxg[1] = daz; gxg[2] = dan;
+          gxs[i][0] = dar; gxs[i][1] = daz; gxs[i][2] = dan;
         } else {
           const float h = hp[i];
           const float da = (h > 0.f && h < RELU_CAP) ? dh : 0.f;
           ghv[0] = da;
-          gxg[0] = da;
+          gxs[i][0] = da;
         }
         if (!act) {
           cnew = 0.f;
 #pragma unroll
-          for (int g = 0; g < G; ++g) { ghv[g] = 0.f; gxg[g] = 0.f; }
+          for (int g = 0; g < G; ++g) { ghv[g] = 0.f; gxs[i][g] = 0.f; }
         }
         carry[i] = cnew;
 #pragma unroll
         for (int g = 0; g < G; ++g) stage[row][g * 16 + c] = f2bf(ghv[g]);
-        if (b < N) {
-          const int t = act ? ((dir == 0) ? s : (lenr[i] - 1 - s)) : s;
-          bf16_t* dst = a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + u;
-#pragma unroll
-          for (int g = 0; g < G; ++g) dst[g * H] = f2bf(gxg[g]);
-        }
       }
     }
     __syncthreads();
@@ -474,6 +482,23 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) st_flag(a.flags + grp * S + slice, (unsigned)(it + 1));
+    }
+
+    // (6) time-indexed input-projection gradient (off the critical path)
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NT;
+      if (e < NE) {
+        const int row = e >> 4, c = e & 15;
+        const int b = r0 + row, u = u0 + c;
+        if (b < N) {
+          const bool act = s < lenr[i];
+          const int t = act ? ((dir == 0) ? s : (lenr[i] - 1 - s)) : s;
+          bf16_t* dst = a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + u;
+#pragma unroll
+          for (int g = 0; g < G; ++g) dst[g * H] = f2bf(gxs[i][g]);
+        }
+      }
     }
   }
 

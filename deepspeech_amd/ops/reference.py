@@ -94,8 +94,14 @@ def seq_batch_norm(y: torch.Tensor, lens: torch.Tensor, mode: str,
 # ---------------------------------------------------------------------------------
 # single-direction recurrences over a precomputed input projection gx[T, N, G*H]
 # ---------------------------------------------------------------------------------
+def _mm_in(h: torch.Tensor, mm_dtype) -> torch.Tensor:
+    """Operand rounding of the recurrent product (the HIP kernels feed h to MFMA in bf16
+    while keeping the state itself in fp32); identity when mm_dtype is None."""
+    return h if mm_dtype is None else h.to(mm_dtype).to(h.dtype)
+
+
 def rnn_relu_scan(gx: torch.Tensor, U: torch.Tensor, lens: torch.Tensor,
-                  h0: Optional[torch.Tensor] = None, cap: float = RELU_CLIP
+                  h0: Optional[torch.Tensor] = None, cap: float = RELU_CLIP, mm_dtype=None
                   ) -> Tuple[torch.Tensor, torch.Tensor]:
     """h_t = min(relu(gx_t + U h_{t-1}), cap); gx already holds SBN(Wx) + B.
 
@@ -106,7 +112,7 @@ def rnn_relu_scan(gx: torch.Tensor, U: torch.Tensor, lens: torch.Tensor,
     outs = []
     Ut = U.t()
     for t in range(T):
-        hn = torch.clamp(gx[t] + h @ Ut, 0.0, cap)
+        hn = torch.clamp(gx[t] + _mm_in(h, mm_dtype) @ Ut, 0.0, cap)
         m = mask[t]
         outs.append(torch.where(m, hn, torch.zeros_like(hn)))
         h = torch.where(m, hn, h)
@@ -114,7 +120,7 @@ def rnn_relu_scan(gx: torch.Tensor, U: torch.Tensor, lens: torch.Tensor,
 
 
 def gru_scan(gx: torch.Tensor, U: torch.Tensor, b_h: torch.Tensor, lens: torch.Tensor,
-             h0: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+             h0: Optional[torch.Tensor] = None, mm_dtype=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Reset-after GRU over gx[T,N,3H] (gate order r, z, n)."""
     T, N, G3 = gx.shape
     H = G3 // 3
@@ -123,7 +129,7 @@ def gru_scan(gx: torch.Tensor, U: torch.Tensor, b_h: torch.Tensor, lens: torch.T
     outs = []
     Ut = U.t()
     for t in range(T):
-        gh = h @ Ut + b_h
+        gh = _mm_in(h, mm_dtype) @ Ut + b_h
         r = torch.sigmoid(gx[t, :, :H] + gh[:, :H])
         z = torch.sigmoid(gx[t, :, H:2 * H] + gh[:, H:2 * H])
         n = torch.tanh(gx[t, :, 2 * H:] + r * gh[:, 2 * H:])
@@ -134,21 +140,21 @@ def gru_scan(gx: torch.Tensor, U: torch.Tensor, b_h: torch.Tensor, lens: torch.T
     return torch.stack(outs, 0), h
 
 
-def recurrent_scan(cell: str, gx, U, b_h, lens, h0=None):
+def recurrent_scan(cell: str, gx, U, b_h, lens, h0=None, mm_dtype=None):
     if cell == "rnn_relu":
-        return rnn_relu_scan(gx, U, lens, h0)
+        return rnn_relu_scan(gx, U, lens, h0, mm_dtype=mm_dtype)
     if cell == "gru":
-        return gru_scan(gx, U, b_h, lens, h0)
+        return gru_scan(gx, U, b_h, lens, h0, mm_dtype=mm_dtype)
     raise ValueError(cell)
 
 
 def birnn_ref(cell: str, gx_f: torch.Tensor, gx_b: Optional[torch.Tensor],
-              U_f, U_b, bh_f, bh_b, lens: torch.Tensor) -> torch.Tensor:
+              U_f, U_b, bh_f, bh_b, lens: torch.Tensor, mm_dtype=None) -> torch.Tensor:
     """Bidirectional layer over precomputed projections; returns fw + bw (Q2)."""
-    y_f, _ = recurrent_scan(cell, gx_f, U_f, bh_f, lens)
+    y_f, _ = recurrent_scan(cell, gx_f, U_f, bh_f, lens, mm_dtype=mm_dtype)
     if gx_b is None:
         return y_f
-    y_b_rev, _ = recurrent_scan(cell, reverse_sequence(gx_b, lens), U_b, bh_b, lens)
+    y_b_rev, _ = recurrent_scan(cell, reverse_sequence(gx_b, lens), U_b, bh_b, lens, mm_dtype=mm_dtype)
     return y_f + reverse_sequence(y_b_rev, lens)
 
 

@@ -48,8 +48,16 @@ class RnnPlan:
     ndir: int
 
 
-def _vgpr_est(kpw: int, tiles: int, mt: int) -> int:
-    return 60 + 4 * kpw * (tiles + mt)
+# Largest KPW (k-steps per wave) that compiles WITHOUT register spills, per
+# (cell, direction, waves per workgroup, row tiles) — from hipcc -Rpass-analysis on gfx950.
+_MAX_KPW = {
+    ("gru", "fwd", 4, 1): 24, ("gru", "fwd", 4, 2): 16, ("gru", "fwd", 8, 1): 8, ("gru", "fwd", 8, 2): 8,
+    ("rnn_relu", "fwd", 4, 1): 32, ("rnn_relu", "fwd", 4, 2): 32,
+    ("rnn_relu", "fwd", 8, 1): 16, ("rnn_relu", "fwd", 8, 2): 16,
+    ("gru", "bwd", 4, 1): 32, ("gru", "bwd", 4, 2): 32, ("gru", "bwd", 8, 1): 16, ("gru", "bwd", 8, 2): 12,
+    ("rnn_relu", "bwd", 4, 1): 32, ("rnn_relu", "bwd", 4, 2): 32,
+    ("rnn_relu", "bwd", 8, 1): 24, ("rnn_relu", "bwd", 8, 2): 12,
+}
 
 
 def _kpw(H: int, G: int, nw: int, fwd: bool) -> int:
@@ -59,6 +67,12 @@ def _kpw(H: int, G: int, nw: int, fwd: bool) -> int:
         if k >= need:
             return k
     return -1
+
+
+def _fits(cell: str, H: int, nw: int, mt: int) -> bool:
+    G = GATES[cell]
+    kf, kb = _kpw(H, G, nw, True), _kpw(H, G, nw, False)
+    return (0 < kf <= _MAX_KPW[(cell, "fwd", nw, mt)]) and (0 < kb <= _MAX_KPW[(cell, "bwd", nw, mt)])
 
 
 def make_plan(N: int, H: int, cell: str, ndir: int, cus: int, mode: Optional[str] = None) -> RnnPlan:
@@ -85,9 +99,7 @@ def make_plan(N: int, H: int, cell: str, ndir: int, cus: int, mode: Optional[str
     nw_opts = [force_nw] if force_nw else [8, 4]
     nw = None
     for cand in nw_opts:
-        kf, kb = _kpw(H, G, cand, True), _kpw(H, G, cand, False)
-        lim = 240 if cand == 8 else 256
-        if kf > 0 and kb > 0 and _vgpr_est(kf, G, mt) <= lim and _vgpr_est(kb, 1, mt) <= lim:
+        if _fits(cell, H, cand, mt):
             nw = cand
             break
     if nw is None:

@@ -58,7 +58,7 @@ def _rnn_case(cuda, cell, N, H, T, ndir, mode, seed=0, din=None):
     GH = G * H
     yr = R.birnn_ref(cell, gx_r[..., :GH], gx_r[..., GH:] if ndir == 2 else None, U_r[0],
                      U_r[1] if ndir == 2 else None, b_r[0], b_r[1] if ndir == 2 else None,
-                     lens.to(cuda))
+                     lens.to(cuda), mm_dtype=torch.bfloat16)
     yr.backward(dy.float())
     assert _rel(y, yr) < 2e-2, ("y", _rel(y, yr))
     assert _rel(gx_h.grad, gx_r.grad) < 3e-2, ("dgx", _rel(gx_h.grad, gx_r.grad))
