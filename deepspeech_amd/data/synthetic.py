@@ -54,11 +54,17 @@ def random_labels(rng: np.random.Generator, n: int, length: int) -> np.ndarray:
     return rng.integers(0, NUM_CLASSES - 1, size=(n, length), dtype=np.int32)
 
 
-def feasible_label_len(frames: int, want: int) -> int:
-    """Cap a label length so that CTC has a path (README.md:63-65, quirk Q15):
-    worst case every label repeats and needs a blank in between -> 2L-1 <= T2."""
+def feasible_label_len(frames: int, want: int, labels: Optional[np.ndarray] = None) -> int:
+    """Largest L <= want such that CTC has a path (README.md:63-65, quirk Q15): the
+    label plus one blank between each repeated pair must fit in T2 frames. Without the
+    concrete labels the worst case (all repeats: 2L-1 <= T2) is assumed."""
     t2 = get_rnn_seqlen_py(frames)
-    return max(1, min(want, (t2 + 1) // 2))
+    if labels is None:
+        return max(1, min(want, (t2 + 1) // 2))
+    L = max(1, min(want, len(labels), t2))
+    while L > 1 and L + int(np.sum(labels[1:L] == labels[:L - 1])) > t2:
+        L -= 1
+    return L
 
 
 class DummyBucketWalk:
@@ -96,10 +102,11 @@ class DummyBucketWalk:
             self.remaining[i] = 0
             self.current += 1
         T = UTT_LENGTHS[i]
-        L = feasible_label_len(T, LABEL_LENGTHS[i])
         start = int(self.rng.integers(0, EXTRA + B * (UTT_LENGTHS[-1] - T)))
         feats = self.buffer[start: start + T * n].reshape(n, T, FREQ_BINS)
-        label = random_labels(self.rng, 1, L)
+        label = random_labels(self.rng, 1, LABEL_LENGTHS[i])
+        L = feasible_label_len(T, LABEL_LENGTHS[i], label[0])
+        label = label[:, :L]
         labels = np.repeat(label, n, axis=0)     # reference replicates one label per batch
         return Batch(feats=np.ascontiguousarray(feats), seq_lens=np.full(n, T, np.int32),
                      labels=labels, label_lens=np.full(n, L, np.int32))
@@ -127,11 +134,12 @@ class FixedShapeBatches:
                 lens[0] = max_frames          # the batch is padded to its longest utterance
             else:
                 lens = np.full(batch_size, max_frames, np.int32)
-            want = [int(round(chars_per_sec * l / 100.0)) for l in lens]
-            L = np.array([feasible_label_len(int(l), w) for l, w in zip(lens, want)], np.int32)
+            want = [max(1, int(round(chars_per_sec * l / 100.0))) for l in lens]
+            rows = [self.rng.integers(0, NUM_CLASSES - 1, size=w).astype(np.int32) for w in want]
+            L = np.array([feasible_label_len(int(l), w, r) for l, w, r in zip(lens, want, rows)], np.int32)
             labels = np.full((batch_size, int(L.max())), -1, np.int32)
             for b in range(batch_size):
-                labels[b, : L[b]] = self.rng.integers(0, NUM_CLASSES - 1, size=L[b])
+                labels[b, : L[b]] = rows[b][: L[b]]
                 feats[b, lens[b]:] = 0.0
             self.batches.append(Batch(feats, lens, labels, L))
         self.i = 0

@@ -1,0 +1,210 @@
+"""Training driver, CLI-compatible with the reference's deepSpeech_train.py.
+
+  python -m deepspeech_amd.train --batch_size 32 --no-shuffle --max_steps 40000 \
+      --num_rnn_layers 7 --num_hidden 1760 --num_filters 32 --initial_lr 1e-4 \
+      --train_dir ../models/librispeech/train --data_dir ../data/LibriSpeech/processed/ \
+      [--dummy True] [--cell gru] [--engine hip]
+  multi-GPU: python -m torch.distributed.run --nproc-per-node 8 -m deepspeech_amd.train ...
+
+Reference flow (src/deepSpeech_train.py:419-528): wipe/create train_dir, dump the flags to
+deepSpeech_parameters.json, build graph, Adam + staircase LR + weight EMA, restore or
+init, loop: step, NaN check, throughput line every 10 steps (after step 10), summaries
+every 50 steps, checkpoint every 10 steps + last, --debug traces at step 20.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import sys
+import time
+from datetime import datetime
+
+import numpy as np
+import torch
+
+from . import config as C
+from .data.synthetic import DummyBucketWalk, FixedShapeBatches, to_device
+from .models import DeepSpeech2
+from .ops import reference as R
+from .parallel.dist import init_distributed, shutdown
+from .trainer import Trainer, lr_schedule_from_args
+from .utils import checkpoint as CK
+from .utils.summary import EventWriter, JsonlWriter
+
+OUR_FILES = ("model.ckpt-*", "checkpoint", "events.out.tfevents.*", "deepSpeech_parameters.json",
+             "metrics.jsonl", "profiling.json", "profile_*.txt")
+
+
+def clean_train_dir(path: str) -> None:
+    """The reference deletes train_dir unless it is the --checkpoint dir
+    (src/deepSpeech_train.py:504-507). We remove only the files this driver writes."""
+    os.makedirs(path, exist_ok=True)
+    for pat in OUR_FILES:
+        for f in glob.glob(os.path.join(path, pat)):
+            if os.path.isfile(f):
+                os.remove(f)
+
+
+def collapse_batch_labels(batch):
+    """preprocess_collapse_repeated=True (src/deepSpeech_NCHW.py:225), applied on the host."""
+    labs = batch.labels.copy()
+    lens = batch.label_lens.copy()
+    for i in range(labs.shape[0]):
+        c = R.collapse_repeated(labs[i, : lens[i]].tolist())
+        labs[i, :] = -1
+        labs[i, : len(c)] = c
+        lens[i] = len(c)
+    batch.labels, batch.label_lens = labs, lens
+    return batch
+
+
+def build_data(args, ctx, train_dir):
+    """Returns (source with .next(), steps_per_epoch)."""
+    if args.dummy:
+        src = DummyBucketWalk(args.batch_size, seed=args.seed + ctx.rank)
+        return src, src.steps_per_epoch()
+    from .data.store import StoreBatches, find_partition_files, find_store, tfrecords_to_store
+    if not args.data_dir:
+        raise ValueError("Please supply a data_dir (or --dummy True)")
+    prefix = find_store(args.data_dir, "train")
+    if prefix is None:
+        files = find_partition_files(args.data_dir, "train")
+        if not files:
+            raise ValueError("no training data (store or TFRecords) under %s" % args.data_dir)
+        prefix = os.path.join(train_dir, "cache", "train")
+        if ctx.is_main and not os.path.exists(prefix + ".index.npz"):
+            tfrecords_to_store(files, prefix)
+        ctx.barrier()
+    src = StoreBatches(prefix, args.batch_size, rank=ctx.rank, world=ctx.world_size,
+                       max_frames=args.max_frames, sortagrad_epochs=args.sortagrad_epochs if not args.shuffle else 0,
+                       shuffle=True, seed=args.seed)
+    return src, src.steps_per_epoch()
+
+
+def main(argv=None) -> int:
+    args = C.parse_train_args(argv)
+    ctx = init_distributed(args.device)
+    dev = ctx.device
+    engine = C.resolve_engine(args.engine, dev)
+    dtype = C.resolve_dtype(args.dtype, args.use_fp16, dev)
+    torch.manual_seed(args.seed)
+    np.random.seed(args.seed + ctx.rank)
+    if ctx.is_main:
+        print("debug: ", args.debug)
+        print("nchw: ", args.nchw)
+        print("dummy: ", args.dummy)
+        print("engine: ", args.engine, "->", engine, "| dtype:", dtype, "| world:", ctx.world_size)
+        if args.train_dir != args.checkpoint:
+            clean_train_dir(args.train_dir)
+        C.dump_param_json(args, args.train_dir)
+        print("Running on platform: ", args.platform)
+    ctx.barrier()
+
+    model = DeepSpeech2(**C.model_kwargs_from_args(args)).to(dev)
+    model.set_engine(engine, dtype)
+    data, steps_per_epoch = build_data(args, ctx, args.train_dir)
+    trainer = Trainer(model, lr_schedule_from_args(args, steps_per_epoch), args.moving_avg_decay,
+                      world_size=ctx.world_size, bucket_mb=args.bucket_mb,
+                      allreduce_bf16=args.allreduce_dtype == "bf16", nan_policy=args.nan_policy)
+    start = 0
+    if args.checkpoint is not None:
+        print("has checkpoint")
+        step = CK.restore(trainer, args.checkpoint)
+        if step is not None:
+            start = trainer.global_step
+    else:
+        print("does not have checkpoint")
+    if ctx.is_main:
+        for n, p in model.named_parameters():
+            print("Variable: ", n, tuple(p.shape))
+        print("parameters: %d" % model.num_params())
+
+    ckpt = CK.CheckpointManager(args.train_dir, args.max_to_keep, args.async_checkpoint) if ctx.is_main else None
+    events = EventWriter(args.train_dir) if ctx.is_main else None
+    metrics = JsonlWriter(os.path.join(args.train_dir, "metrics.jsonl")) if ctx.is_main else None
+    durations = []
+    audio_hist = []
+    t_last = time.time()
+    steps_since = 0
+    audio_since = 0.0
+    loss = None
+    prof = None
+    for step in range(start, args.max_steps):
+        t0 = time.time()
+        hb = data.next()
+        if args.ctc_collapse_repeated:
+            hb = collapse_batch_labels(hb)
+        data_time = time.time() - t0
+        if args.debug and step == 20:
+            from torch.profiler import ProfilerActivity, profile
+            prof = profile(activities=[ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if dev.type == "cuda" else []),
+                           record_shapes=False)
+            prof.__enter__()
+        batch = to_device(hb, dev)
+        loss = trainer.step(batch)
+        if args.fault_inject_step == step and ctx.rank == args.fault_inject_rank:
+            print("fault injection at step %d on rank %d" % (step, ctx.rank), flush=True)
+            os._exit(17)
+        steps_since += 1
+        audio_since += hb.audio_seconds
+        if prof is not None:
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            prof.__exit__(None, None, None)
+            if ctx.is_main:
+                prof.export_chrome_trace(os.path.join(args.train_dir, "profiling.json"))
+                with open(os.path.join(args.train_dir, "profile_ops.txt"), "w") as f:
+                    f.write(prof.key_averages().table(sort_by="self_cuda_time_total" if dev.type == "cuda"
+                                                      else "self_cpu_time_total", row_limit=80))
+            prof = None
+        do_log = (step > 10 and step % args.log_every == 0) or step + 1 == args.max_steps
+        do_sum = ctx.is_main and step % args.summary_every == 0
+        do_ckpt = ctx.is_main and (step % args.checkpoint_every == 0 or step + 1 == args.max_steps)
+        if do_log or do_sum or do_ckpt:
+            lv = float(loss.item())          # host sync point
+            if engine == "hip":
+                from .ops import rnn as RNN
+                RNN.check_errors()
+            if lv != lv or lv in (float("inf"), float("-inf")):
+                if args.nan_policy == "abort":
+                    raise FloatingPointError("Model diverged with loss = NaN (step %d)" % step)
+            now = time.time()
+            dur = (now - t_last) / max(1, steps_since)
+            if step >= 10:
+                durations.append(dur)
+                audio_hist.append(audio_since / max(1e-9, now - t_last))
+            t_last, steps_since, audio_since = now, 0, 0.0
+            ema = trainer.update_loss_ema(lv)
+            if do_log and ctx.is_main and durations:
+                sec_batch = float(np.mean(durations))
+                ex_sec = args.batch_size * ctx.world_size / sec_batch
+                aps = float(np.mean(audio_hist)) * ctx.world_size
+                if args.dummy:
+                    print("%s: step %d, loss = %.2f (%.1f examples/sec; %.3f sec/batch; %.3f dummy sec/batch; "
+                          "%.1f audio-sec/sec)" % (datetime.now(), step, lv, ex_sec, sec_batch, data_time, aps),
+                          flush=True)
+                else:
+                    print("%s: step %d, loss = %.2f (%.1f examples/sec; %.3f sec/batch; %.1f audio-sec/sec)"
+                          % (datetime.now(), step, lv, ex_sec, sec_batch, aps), flush=True)
+            if ctx.is_main:
+                metrics.write(step, loss=lv, loss_ema=ema, lr=trainer.lr)
+            if do_sum:
+                events.scalars(step, {"ctc_loss(raw)": lv, "ctc_loss": ema, "learning_rate": trainer.lr})
+                if not args.dummy:
+                    for n, p in model.named_parameters():
+                        events.histogram(step, n, p.detach().float().cpu().numpy())
+                events.flush()
+            if do_ckpt:
+                ckpt.save(trainer, step)
+    if ckpt is not None:
+        ckpt.wait()
+    if events is not None:
+        events.close()
+    if hasattr(data, "close"):
+        data.close()
+    shutdown(ctx)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,256 @@
+"""Checkpoint / resume with the reference's directory contract.
+
+Reference (src/deepSpeech_train.py:354-356, :383-398, :471, :504-513):
+  train_dir/deepSpeech_parameters.json      json.dump(vars(ARGS))
+  train_dir/model.ckpt-<step>               saver.save(..., global_step=step), max_to_keep=100
+  train_dir/checkpoint                      TF state file naming the latest checkpoint
+Saved set: model variables, Adam slots, global_step, weight-EMA shadows (eval restores
+them: src/deepSpeech_test.py:217-220), BN moving stats.
+
+Here every entry is keyed by its TF variable name and stored in TF orientation (conv
+kernels HWIO), so checkpoints map 1:1 onto the reference graph's variables
+(SURVEY.md §5.4). Files are plain ``torch.save`` dicts of tensors/ints/strings that load
+with ``torch.load(weights_only=True)``. Saving is asynchronous: tensors are copied to
+host on the caller's thread (one device sync), the file write runs on a side thread.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import re
+import threading
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from ..models.deepspeech2 import DeepSpeech2
+
+EMA_SUFFIX = "/ExponentialMovingAverage"
+ADAM_M = "/Adam"
+ADAM_V = "/Adam_1"
+
+
+def _conv_to_tf(w: torch.Tensor) -> torch.Tensor:      # [O, I, H, W] -> [H, W, I, O]
+    return w.permute(2, 3, 1, 0).contiguous()
+
+
+def _conv_from_tf(w: torch.Tensor) -> torch.Tensor:    # [H, W, I, O] -> [O, I, H, W]
+    return w.permute(3, 2, 0, 1).contiguous()
+
+
+def tf_name_map(model: DeepSpeech2) -> List[Tuple[str, str, Callable, Callable]]:
+    """[(tf_name, torch_name, to_tf, from_tf)] for every parameter and buffer."""
+    ident = lambda t: t  # noqa: E731
+    out = []
+    for blk in ("conv1", "conv2"):
+        out += [
+            ("%s/weights" % blk, "%s.weight" % blk, _conv_to_tf, _conv_from_tf),
+            ("%s/biases" % blk, "%s.bias" % blk, ident, ident),
+            ("%s/bn2/beta" % blk, "%s.bn_beta" % blk, ident, ident),
+            ("%s/bn2/gamma" % blk, "%s.bn_gamma" % blk, ident, ident),
+            ("%s/bn2/moving_mean" % blk, "%s.running_mean" % blk, ident, ident),
+            ("%s/bn2/moving_variance" % blk, "%s.running_var" % blk, ident, ident),
+        ]
+    cell_scope = "CustomRNNCell2" if model.cell == "rnn_relu" else "GRUCell"
+    for i, layer in enumerate(model.rnn):
+        for dname in (["fw", "bw"] if layer.bw is not None else ["fw"]):
+            if layer.bw is not None:
+                scope = "rnn/brnn-%d/bidirectional_rnn/%s/%s" % (i, dname, cell_scope)
+            else:
+                scope = "rnn/rnn-%d/%s" % (i, cell_scope)
+            tp = "rnn.%d.%s" % (i, dname)
+            out += [("%s/W" % scope, tp + ".W", ident, ident),
+                    ("%s/U" % scope, tp + ".U", ident, ident),
+                    ("%s/%s" % (scope, "B" if model.cell == "rnn_relu" else "b_i"), tp + ".b", ident, ident),
+                    ("%s/sbn/moving_mean" % scope, tp + ".sbn_mean", ident, ident),
+                    ("%s/sbn/moving_variance" % scope, tp + ".sbn_var", ident, ident)]
+            if model.cell == "gru":
+                out.append(("%s/b_h" % scope, tp + ".b_h", ident, ident))
+    out += [("softmax_linear/weights", "fc_weight", ident, ident),
+            ("softmax_linear/biases", "fc_bias", ident, ident)]
+    return out
+
+
+def model_to_tf(model: DeepSpeech2) -> Dict[str, torch.Tensor]:
+    sd = dict(model.named_parameters())
+    sd.update(dict(model.named_buffers()))
+    return {tf: to_tf(sd[tn].detach()) for tf, tn, to_tf, _ in tf_name_map(model)}
+
+
+def load_model_from_tf(model: DeepSpeech2, tensors: Dict[str, torch.Tensor], strict: bool = True,
+                       use_ema: bool = False) -> List[str]:
+    """Copy TF-named tensors into the model; with use_ema, prefer '<name>/ExponentialMovingAverage'."""
+    sd = dict(model.named_parameters())
+    sd.update(dict(model.named_buffers()))
+    missing = []
+    with torch.no_grad():
+        for tf, tn, _, from_tf in tf_name_map(model):
+            key = tf + EMA_SUFFIX if (use_ema and (tf + EMA_SUFFIX) in tensors) else tf
+            if key not in tensors:
+                missing.append(tf)
+                continue
+            src = from_tf(tensors[key].to(torch.float32))
+            dst = sd[tn]
+            if tuple(src.shape) != tuple(dst.shape):
+                raise ValueError("shape mismatch for %s: %s vs %s" % (tf, tuple(src.shape), tuple(dst.shape)))
+            dst.copy_(src.to(dst.dtype))
+    if strict and missing:
+        raise KeyError("checkpoint lacks %s" % missing[:5])
+    return missing
+
+
+def _arena_slots(trainer) -> Dict[str, torch.Tensor]:
+    """Adam m/v and EMA shadows keyed by TF slot names."""
+    out = {}
+    model = trainer.model
+    names = {tn: (tf, to_tf) for tf, tn, to_tf, _ in tf_name_map(model)}
+    arena, opt = trainer.arena, trainer.opt
+    vm, vv = arena.views(opt.m), arena.views(opt.v)
+    ve = arena.views(opt.ema) if opt.ema is not None else None
+    for tn in arena.names:
+        tf, to_tf = names[tn]
+        out[tf + ADAM_M] = to_tf(vm[tn])
+        out[tf + ADAM_V] = to_tf(vv[tn])
+        if ve is not None:
+            out[tf + EMA_SUFFIX] = to_tf(ve[tn])
+    return out
+
+
+def _load_arena_slots(trainer, tensors: Dict[str, torch.Tensor]) -> None:
+    model = trainer.model
+    names = {tn: (tf, from_tf) for tf, tn, _, from_tf in tf_name_map(model)}
+    arena, opt = trainer.arena, trainer.opt
+    vm, vv = arena.views(opt.m), arena.views(opt.v)
+    ve = arena.views(opt.ema) if opt.ema is not None else None
+    with torch.no_grad():
+        for tn in arena.names:
+            tf, from_tf = names[tn]
+            if tf + ADAM_M in tensors:
+                vm[tn].copy_(from_tf(tensors[tf + ADAM_M]))
+                vv[tn].copy_(from_tf(tensors[tf + ADAM_V]))
+            if ve is not None and tf + EMA_SUFFIX in tensors:
+                ve[tn].copy_(from_tf(tensors[tf + EMA_SUFFIX]))
+
+
+def write_state_file(directory: str, latest: str, all_paths: List[str]) -> None:
+    """TF's `checkpoint` text-proto state file."""
+    lines = ['model_checkpoint_path: "%s"' % latest]
+    lines += ['all_model_checkpoint_paths: "%s"' % p for p in all_paths]
+    tmp = os.path.join(directory, "checkpoint.tmp")
+    with open(tmp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    os.replace(tmp, os.path.join(directory, "checkpoint"))
+
+
+def latest_checkpoint(directory: str) -> Optional[str]:
+    """tf.train.get_checkpoint_state(dir).model_checkpoint_path equivalent."""
+    state = os.path.join(directory, "checkpoint")
+    if os.path.exists(state):
+        with open(state) as f:
+            for line in f:
+                m = re.match(r'\s*model_checkpoint_path:\s*"(.*)"', line)
+                if m:
+                    p = m.group(1)
+                    return p if os.path.isabs(p) else os.path.join(directory, p)
+    cands = glob.glob(os.path.join(directory, "model.ckpt-*"))
+    if not cands:
+        return None
+    return max(cands, key=lambda p: int(re.findall(r"-(\d+)$", p)[0]) if re.findall(r"-(\d+)$", p) else -1)
+
+
+def step_from_path(path: str) -> int:
+    """global_step parsed from the file name (src/deepSpeech_train.py:393-397)."""
+    return int(path.split("/")[-1].split("-")[-1])
+
+
+class CheckpointManager:
+    def __init__(self, directory: str, max_to_keep: int = 100, async_save: bool = True):
+        self.dir = directory
+        self.max_to_keep = max_to_keep
+        self.async_save = async_save
+        self._thread: Optional[threading.Thread] = None
+        self._error: Optional[BaseException] = None
+        os.makedirs(directory, exist_ok=True)
+        self.kept: List[str] = []
+        state = os.path.join(directory, "checkpoint")
+        if os.path.exists(state):
+            with open(state) as f:
+                self.kept = [m.group(1) for m in (re.match(r'\s*all_model_checkpoint_paths:\s*"(.*)"', l) for l in f) if m]
+
+    def snapshot(self, trainer) -> Dict[str, object]:
+        out: Dict[str, object] = {}
+        for k, v in model_to_tf(trainer.model).items():
+            out[k] = v.detach().to("cpu", copy=True)
+        for k, v in _arena_slots(trainer).items():
+            out[k] = v.detach().to("cpu", copy=True)
+        out["global_step"] = int(trainer.global_step)
+        out["beta1_power"] = float(trainer.opt.b1 ** trainer.opt.t)
+        out["beta2_power"] = float(trainer.opt.b2 ** trainer.opt.t)
+        out["adam_t"] = int(trainer.opt.t)
+        out["format"] = "deepspeech_amd/tfnames/v1"
+        return out
+
+    def save(self, trainer, step: int) -> str:
+        self.wait()
+        snap = self.snapshot(trainer)
+        name = "model.ckpt-%d" % step
+        path = os.path.join(self.dir, name)
+
+        def write():
+            try:
+                tmp = path + ".tmp"
+                torch.save(snap, tmp)
+                os.replace(tmp, path)
+                if name in self.kept:
+                    self.kept.remove(name)
+                self.kept.append(name)
+                while len(self.kept) > self.max_to_keep:
+                    old = self.kept.pop(0)
+                    try:
+                        os.remove(os.path.join(self.dir, old))
+                    except FileNotFoundError:
+                        pass
+                write_state_file(self.dir, name, self.kept)
+            except BaseException as e:  # surfaced by wait()
+                self._error = e
+
+        if self.async_save:
+            self._thread = threading.Thread(target=write, daemon=True)
+            self._thread.start()
+        else:
+            write()
+            self._raise()
+        return path
+
+    def _raise(self):
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise e
+
+    def wait(self) -> None:
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        self._raise()
+
+
+def load_checkpoint_file(path: str) -> Dict[str, object]:
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def restore(trainer, directory_or_file: str) -> Optional[int]:
+    """Restore model + Adam slots + EMA + step; returns the global step (or None)."""
+    path = directory_or_file
+    if os.path.isdir(path):
+        path = latest_checkpoint(path)
+        if path is None:
+            print("No checkpoint file found")
+            return None
+    data = load_checkpoint_file(path)
+    tensors = {k: v for k, v in data.items() if isinstance(v, torch.Tensor)}
+    load_model_from_tf(trainer.model, tensors, strict=True)
+    _load_arena_slots(trainer, tensors)
+    step = int(data.get("global_step", step_from_path(path)))
+    trainer.global_step = step + 1 if data.get("format") else step
+    trainer.opt.t = int(data.get("adam_t", step + 1))
+    return step

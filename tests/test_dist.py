@@ -1,0 +1,135 @@
+"""Data parallelism without a cluster: gloo process groups on CPU (world size 2)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batches(n=2):
+    from deepspeech_amd.data.synthetic import FixedShapeBatches
+    return [FixedShapeBatches(2, max_frames=140, seed=10 + i, pool=1).next() for i in range(n)]
+
+
+def _make_trainer(world, bucket_mb):
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="gru")
+    # BN batch statistics are per rank (parity with the single-device reference); freeze
+    # them in eval mode here so that DP == one big batch exactly
+    return Trainer(m, LRSchedule(1e-2, 10 ** 6, 0.9), moving_avg_decay=0.99, world_size=world,
+                   bucket_mb=bucket_mb)
+
+
+def _eval_mode_step(tr, batch, update=True):
+    tr.model.eval()
+    tr.arena.zero_grad()
+    logits, lens = tr.model(batch["feats"], batch["seq_lens"])
+    loss = tr.model.loss(logits, lens, batch["labels"], batch["label_lens"])
+    loss.backward()
+    tr.bucketer.finish()
+    if update:
+        tr.opt.step(tr.lr, tr.global_step, gscale=1.0 / tr.world)
+        tr.global_step += 1
+
+
+def _worker(rank, world, port, bucket_mb, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from deepspeech_amd.data.synthetic import to_device
+    from deepspeech_amd.parallel.dist import init_distributed, shutdown
+    ctx = init_distributed("cpu")
+    tr = _make_trainer(world, bucket_mb)
+    assert len(tr.bucketer.buckets) >= (2 if bucket_mb < 0.01 else 1)
+    b = _batches()[rank]
+    _eval_mode_step(tr, to_device(b, torch.device("cpu")), update=False)
+    g = tr.arena.grad.clone() / world
+    tr.opt.step(tr.lr, 0, gscale=1.0 / world)
+    if rank == 0:
+        torch.save({"w": tr.arena.flat.clone(), "g": g}, out)
+    shutdown(ctx)
+
+
+@pytest.mark.parametrize("bucket_mb", [0.001, 32.0])
+def test_dp2_equals_single_process_big_batch(tmp_path, bucket_mb):
+    from deepspeech_amd.data.synthetic import Batch, to_device
+    import numpy as np
+    out = str(tmp_path / "dp.pt")
+    mp.spawn(_worker, args=(2, _free_port(), bucket_mb, out), nprocs=2, join=True)
+    res = torch.load(out, weights_only=True)
+    # single process: the mean CTC over the concatenated 4-utterance batch equals the
+    # average of the two ranks' per-batch means (equal batch sizes)
+    b0, b1 = _batches()
+    T = max(b0.feats.shape[1], b1.feats.shape[1])
+
+    def pad(a, T):
+        o = np.zeros((a.shape[0], T, a.shape[2]), np.float32)
+        o[:, : a.shape[1]] = a
+        return o
+
+    L = max(b0.labels.shape[1], b1.labels.shape[1])
+
+    def padl(a):
+        o = np.full((a.shape[0], L), -1, np.int32)
+        o[:, : a.shape[1]] = a
+        return o
+
+    big = Batch(np.concatenate([pad(b0.feats, T), pad(b1.feats, T)]), np.concatenate([b0.seq_lens, b1.seq_lens]),
+                np.concatenate([padl(b0.labels), padl(b1.labels)]), np.concatenate([b0.label_lens, b1.label_lens]))
+    tr = _make_trainer(1, 32.0)
+    _eval_mode_step(tr, to_device(big, torch.device("cpu")), update=False)
+    gr = tr.arena.grad.clone()
+    tr.opt.step(tr.lr, 0)
+    # the all-reduced mean gradient, then one Adam step from identical starts
+    # (Adam divides by sqrt(v): elements with |g| ~ eps amplify float-order noise)
+    assert torch.allclose(res["w"], tr.arena.flat, atol=2e-3), (res["w"] - tr.arena.flat).abs().max()
+    g = res["g"]
+    assert ((g - gr).norm() / gr.norm()) < 1e-5
+
+
+def test_fault_injection_and_resume(tmp_path):
+    """Kill the job at step 7, resume from the last checkpoint (step 5) and finish."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    common = [sys.executable, "-m", "deepspeech_amd.train", "--dummy", "True", "--batch_size", "2",
+              "--num_hidden", "16", "--num_rnn_layers", "1", "--num_filters", "4", "--device", "cpu",
+              "--checkpoint_every", "5", "--log_every", "1000"]
+    d = str(tmp_path / "run")
+    r = subprocess.run(common + ["--train_dir", d, "--max_steps", "20", "--fault_inject_step", "7"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 17, r.stdout + r.stderr
+    from deepspeech_amd.utils import checkpoint as CK
+    assert CK.latest_checkpoint(d).endswith("model.ckpt-5")
+    r = subprocess.run(common + ["--train_dir", d, "--checkpoint", d, "--max_steps", "12"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert CK.latest_checkpoint(d).endswith("model.ckpt-11")
+    assert "has checkpoint" in r.stdout
+
+
+def test_torchrun_gloo_two_ranks(tmp_path):
+    """The real launcher path: torch.distributed.run with 2 CPU ranks over gloo."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "deepspeech_amd.train",
+           "--dummy", "True", "--batch_size", "2", "--num_hidden", "16", "--num_rnn_layers", "1",
+           "--num_filters", "4", "--device", "cpu", "--max_steps", "13", "--train_dir", str(tmp_path / "tr"),
+           "--log_every", "12"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "step 12" in r.stdout

@@ -1,0 +1,129 @@
+"""Model-level semantics of the reference graph (CPU, engine=ref)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from deepspeech_amd import NUM_CLASSES
+from deepspeech_amd.config import get_rnn_seqlen_py
+from deepspeech_amd.models import DeepSpeech2, conv_out_len, freq_out
+from deepspeech_amd.ops import reference as R
+
+
+def test_get_rnn_seqlen_matches_conv_output():
+    # T2 = ceil((ceil((T-19)/2)-9)/2) equals the VALID conv output length
+    for T in [39, 40, 100, 101, 999, 1000, 1500, 1800]:
+        t1, t2 = conv_out_len(T)
+        assert int(R.get_rnn_seqlen(torch.tensor([T]))[0]) == t2 == get_rnn_seqlen_py(T)
+    assert conv_out_len(1000) == (491, 241)
+    assert conv_out_len(1500) == (741, 366)
+    assert freq_out(161) == (79, 75)
+
+
+@pytest.mark.parametrize("cell", ["rnn_relu", "gru"])
+def test_forward_shapes(cell):
+    m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=3, cell=cell)
+    x = torch.randn(3, 120, 161)
+    logits, lens = m(x, torch.tensor([120, 100, 80], dtype=torch.int32))
+    assert logits.shape == (conv_out_len(120)[1], 3, NUM_CLASSES)
+    assert lens.tolist() == [get_rnn_seqlen_py(t) for t in (120, 100, 80)]
+
+
+def test_param_shapes_follow_reference():
+    m = DeepSpeech2(num_filters=32, num_hidden=64, num_rnn_layers=2, cell="rnn_relu")
+    assert tuple(m.conv1.weight.shape) == (32, 1, 20, 5)
+    assert tuple(m.conv2.weight.shape) == (32, 32, 10, 5)
+    assert torch.allclose(m.conv1.bias, torch.full((32,), -0.05))
+    assert tuple(m.rnn[0].fw.W.shape) == (64, 2400)      # W [H, 75*C]
+    assert tuple(m.rnn[1].fw.W.shape) == (64, 64)        # correctly stacked (Q1 fix)
+    assert tuple(m.fc_weight.shape) == (NUM_CLASSES, 64)
+    # quirk Q1 reproduction: every layer consumes the conv output
+    q = DeepSpeech2(num_filters=32, num_hidden=64, num_rnn_layers=2, stack_fix=False)
+    assert tuple(q.rnn[1].fw.W.shape) == (64, 2400)
+
+
+def test_reverse_sequence_semantics():
+    x = torch.arange(5).view(5, 1, 1).repeat(1, 2, 1).float()
+    y = R.reverse_sequence(x, torch.tensor([3, 5]))
+    assert y[:, 0, 0].tolist() == [2, 1, 0, 3, 4]       # reversed within length, tail kept
+    assert y[:, 1, 0].tolist() == [4, 3, 2, 1, 0]
+
+
+def test_outputs_zero_past_length_and_bw_direction():
+    torch.manual_seed(0)
+    T, N, H = 6, 2, 4
+    gx = torch.randn(T, N, H)
+    U = torch.randn(H, H) * 0.3
+    lens = torch.tensor([4, 6])
+    y, _ = R.rnn_relu_scan(gx, U, lens)
+    assert float(y[4:, 0].abs().sum()) == 0.0
+    # bw direction of a length-4 utterance == fw scan of its time-reversed prefix
+    yb = R.birnn_ref("rnn_relu", torch.zeros_like(gx), gx, torch.zeros(H, H), U, None, None, lens)
+    ref, _ = R.rnn_relu_scan(gx[:4, :1].flip(0), U, torch.tensor([4]))
+    y_f0, _ = R.rnn_relu_scan(torch.zeros(T, N, H), torch.zeros(H, H), lens)
+    assert torch.allclose(yb[:4, 0] - y_f0[:4, 0], ref.flip(0)[:, 0], atol=1e-6)
+
+
+def test_clipped_relu_cap():
+    x = torch.tensor([-1.0, 0.5, 25.0])
+    assert R.clipped_relu(x).tolist() == [0.0, 0.5, 20.0]
+
+
+def test_frozen_seq_bn_is_constant_scale():
+    y = torch.randn(5, 3, 7)
+    out = R.seq_batch_norm(y, torch.tensor([5, 5, 5]), "frozen", torch.zeros(7), torch.ones(7))
+    assert torch.allclose(out, y / math.sqrt(1 + 1e-5))
+
+
+def test_batch_seq_bn_uses_valid_positions_only():
+    y = torch.randn(4, 2, 3)
+    lens = torch.tensor([4, 2])
+    y[2:, 1] = 1000.0            # padding garbage must not affect the statistics
+    out = R.seq_batch_norm(y, lens, "batch", torch.zeros(3), torch.ones(3), training=True)
+    valid = torch.cat([y[:, 0], y[:2, 1]], 0)
+    ref = (valid - valid.mean(0)) / torch.sqrt(valid.var(0, unbiased=False) + 1e-5)
+    assert torch.allclose(torch.cat([out[:, 0], out[:2, 1]], 0), ref, atol=1e-5)
+
+
+def test_gru_matches_torch_gru_cell():
+    torch.manual_seed(0)
+    H, I, N, T = 8, 5, 3, 4
+    cell = torch.nn.GRUCell(I, H)
+    x = torch.randn(T, N, I)
+    gx = x @ cell.weight_ih.t() + cell.bias_ih
+    y, _ = R.gru_scan(gx, cell.weight_hh, cell.bias_hh, torch.tensor([T] * N))
+    h = torch.zeros(N, H)
+    for t in range(T):
+        h = cell(x[t], h)
+    assert torch.allclose(y[-1], h, atol=1e-5)
+
+
+def test_ctc_ref_mean_over_batch_not_normalised_by_label_length():
+    torch.manual_seed(0)
+    logits = torch.randn(20, 2, NUM_CLASSES)
+    labels = torch.tensor([[1, 2, 3], [4, 5, 0]], dtype=torch.int32)
+    per = R.ctc_loss_ref(logits, labels, torch.tensor([20, 15]), torch.tensor([3, 2]))
+    m = DeepSpeech2(num_filters=4, num_hidden=8, num_rnn_layers=1)
+    mean = m.loss(logits, torch.tensor([20, 15], dtype=torch.int32), labels, torch.tensor([3, 2]))
+    assert torch.allclose(mean, per.mean())
+
+
+@pytest.mark.parametrize("cell", ["rnn_relu", "gru"])
+def test_overfits_one_batch(cell):
+    from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=4, num_hidden=32, num_rnn_layers=1, cell=cell)
+    tr = Trainer(m, LRSchedule(3e-3, 10 ** 6, 0.9), moving_avg_decay=0.9999)
+    b = to_device(FixedShapeBatches(2, max_frames=160, seed=0, pool=1, chars_per_sec=5).next(), torch.device("cpu"))
+    first = float(tr.step(b))
+    for _ in range(25):
+        last = float(tr.step(b))
+    assert last < first * 0.8, (first, last)
+
+
+def test_flops_positive_and_gru_heavier():
+    a = DeepSpeech2(num_filters=32, num_hidden=800, num_rnn_layers=5, cell="gru").flops_per_step(32, 1000)
+    b = DeepSpeech2(num_filters=32, num_hidden=800, num_rnn_layers=5, cell="rnn_relu").flops_per_step(32, 1000)
+    assert a > b > 0
