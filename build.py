@@ -77,7 +77,9 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         for f in os.listdir(BUILD):
             if f.endswith(".o"):
                 os.remove(os.path.join(BUILD, f))
-    headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+    # every TU may #include any other csrc file (e.g. the stamps build includes the kernel
+    # source), so all of csrc is a dependency of every object
+    headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip")))
     hip_srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
     common = ["-O3", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-I" + CSRC]
     hip_flags = [HIPCC, "--offload-arch=" + ARCH, "-fno-gpu-rdc", "-munsafe-fp-atomics"] + common

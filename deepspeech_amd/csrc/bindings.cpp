@@ -25,6 +25,7 @@ struct DS2RnnFwd {
   unsigned* flags;
   unsigned* err;
   long long timeout;
+  unsigned long long* stamps;
 };
 struct DS2RnnBwd {
   int T, N, NP, H, S, BG, steps, gstride, ndir, cell, nw, mt, persistent;
@@ -39,9 +40,12 @@ struct DS2RnnBwd {
   unsigned* flags;
   unsigned* err;
   long long timeout;
+  unsigned long long* stamps;
 };
 int ds2_rnn_fwd(const DS2RnnFwd* d, hipStream_t st);
 int ds2_rnn_bwd(const DS2RnnBwd* d, hipStream_t st);
+int ds2_rnn_fwd_stamps(const DS2RnnFwd* d, hipStream_t st);
+int ds2_rnn_bwd_stamps(const DS2RnnBwd* d, hipStream_t st);
 int ds2_rnn_kpw(int H, int G, int nw, int fwd);
 int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const int* labels, const int* label_lens,
                   float* loss, void* grad, float* lp_ws, float* alpha_ws, int T, int N, int K, int Lmax, int blank,
@@ -93,7 +97,8 @@ int is_bf16(const at::Tensor& t) {
 void rnn_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_f, OptT bh_b, at::Tensor y_f,
              OptT y_b, at::Tensor hx_f, OptT hx_b, at::Tensor hs_f, OptT hs_b, OptT gates_f, OptT gates_b,
              at::Tensor flags, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t steps,
-             int64_t gstride, int64_t ndir, int64_t cell, int64_t nw, int64_t mt, bool persistent, int64_t timeout) {
+             int64_t gstride, int64_t ndir, int64_t cell, int64_t nw, int64_t mt, bool persistent, int64_t timeout,
+             OptT stamps) {
   need_gpu(gx, "gx");
   TORCH_CHECK(gx.scalar_type() == at::kBFloat16, "gx must be bf16");
   TORCH_CHECK(lens.scalar_type() == at::kInt, "lens must be int32");
@@ -123,13 +128,15 @@ void rnn_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_f
   d.flags = reinterpret_cast<unsigned*>(flags.data_ptr<int>());
   d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
   d.timeout = timeout;
-  check(ds2_rnn_fwd(&d, cur_stream()), "rnn_fwd");
+  d.stamps = ptr_or_null<unsigned long long>(stamps, "stamps");
+  check(d.stamps ? ds2_rnn_fwd_stamps(&d, cur_stream()) : ds2_rnn_fwd(&d, cur_stream()), "rnn_fwd");
 }
 
 void rnn_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tensor hs_f, OptT hs_b, OptT gates_f,
              OptT gates_b, at::Tensor dgh_f, OptT dgh_b, at::Tensor dgx, OptT carry_f, OptT carry_b,
              at::Tensor flags, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t steps,
-             int64_t gstride, int64_t ndir, int64_t cell, int64_t nw, int64_t mt, bool persistent, int64_t timeout) {
+             int64_t gstride, int64_t ndir, int64_t cell, int64_t nw, int64_t mt, bool persistent, int64_t timeout,
+             OptT stamps) {
   need_gpu(dy, "dy");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dgx.scalar_type() == at::kBFloat16, "dy/dgx must be bf16");
   TORCH_CHECK(dgx.numel() >= T * N * gstride, "dgx too small");
@@ -155,7 +162,8 @@ void rnn_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tenso
   d.flags = reinterpret_cast<unsigned*>(flags.data_ptr<int>());
   d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
   d.timeout = timeout;
-  check(ds2_rnn_bwd(&d, cur_stream()), "rnn_bwd");
+  d.stamps = ptr_or_null<unsigned long long>(stamps, "stamps");
+  check(d.stamps ? ds2_rnn_bwd_stamps(&d, cur_stream()) : ds2_rnn_bwd(&d, cur_stream()), "rnn_bwd");
 }
 
 int64_t rnn_kpw(int64_t H, int64_t G, int64_t nw, bool fwd) { return ds2_rnn_kpw((int)H, (int)G, (int)nw, fwd ? 1 : 0); }
@@ -269,8 +277,18 @@ py::dict device_info(int64_t dev) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "deepspeech_amd gfx950 kernels";
-  m.def("rnn_fwd", &rnn_fwd);
-  m.def("rnn_bwd", &rnn_bwd);
+  m.def("rnn_fwd", &rnn_fwd, py::arg("gx"), py::arg("lens"), py::arg("U_f"), py::arg("U_b"), py::arg("bh_f"),
+        py::arg("bh_b"), py::arg("y_f"), py::arg("y_b"), py::arg("hx_f"), py::arg("hx_b"), py::arg("hs_f"),
+        py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("flags"), py::arg("err"), py::arg("T"),
+        py::arg("N"), py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("steps"), py::arg("gstride"),
+        py::arg("ndir"), py::arg("cell"), py::arg("nw"), py::arg("mt"), py::arg("persistent"), py::arg("timeout"),
+        py::arg("stamps") = py::none());
+  m.def("rnn_bwd", &rnn_bwd, py::arg("dy"), py::arg("lens"), py::arg("U_f"), py::arg("U_b"), py::arg("hs_f"),
+        py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("dgh_f"), py::arg("dgh_b"), py::arg("dgx"),
+        py::arg("carry_f"), py::arg("carry_b"), py::arg("flags"), py::arg("err"), py::arg("T"), py::arg("N"),
+        py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("steps"), py::arg("gstride"), py::arg("ndir"),
+        py::arg("cell"), py::arg("nw"), py::arg("mt"), py::arg("persistent"), py::arg("timeout"),
+        py::arg("stamps") = py::none());
   m.def("rnn_kpw", &rnn_kpw);
   m.def("ctc_fused", &ctc_fused);
   m.def("bn_chunks", &bn_chunks);

@@ -55,6 +55,7 @@ struct FwdArgs {
   unsigned* flags;
   unsigned* err;
   long long timeout;
+  unsigned long long* stamps;
 };
 
 struct BwdArgs {
@@ -70,7 +71,35 @@ struct BwdArgs {
   unsigned* flags;
   unsigned* err;
   long long timeout;
+  unsigned long long* stamps;
 };
+
+// Diagnostic build (rnn_persistent_stamps.hip): per-phase s_memtime cycle sums per
+// workgroup, recorded by wave 0 (cdna_hip_programming.md §7 "In-kernel stamps"). The
+// production build compiles every STAMP away.
+#ifdef DS2_RNN_STAMPS
+#define DS2_STAMP_DECL unsigned long long st_prev = 0, st_acc[6] = {0, 0, 0, 0, 0, 0};
+#define DS2_STAMP(i)                                                                      \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    unsigned long long _t;                                                                \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if (st_prev) st_acc[i] += _t - st_prev;                                               \
+    st_prev = _t;                                                                         \
+  } while (0)
+#define DS2_STAMP_STORE(a)                                                                \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && (a).stamps)                                                   \
+      for (int _k = 0; _k < 6; ++_k) (a).stamps[blockIdx.x * 8 + _k] = st_acc[_k];        \
+  } while (0)
+#define DS2_EXPORT(name) name##_stamps
+#else
+#define DS2_STAMP_DECL
+#define DS2_STAMP(i)
+#define DS2_STAMP_STORE(a)
+#define DS2_EXPORT(name) name
+#endif
 
 // Wait until every workgroup of the group published iteration `need`-1.
 // Returns false on timeout (error word set).  Executed by wave 0 only.
@@ -156,8 +185,10 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(a.hx[dir], hx_bytes);
   const unsigned* gflags = a.flags + grp * S;
   __syncthreads();
+  DS2_STAMP_DECL
 
   for (int s = a.s_begin; s < a.s_end; ++s) {
+    DS2_STAMP(5);
     // (1) prefetch this step's input projection (independent of the recurrence)
     float gxv[EPT][G];
 #pragma unroll
@@ -183,6 +214,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
       __syncthreads();
       if (abort_flag) break;
     }
+    DS2_STAMP(0);
 
     // (3) gh = h_{s-1} . U^T over this wave's k-steps
     f32x4 acc[MT][G];
@@ -217,6 +249,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
       }
     }
 
+    DS2_STAMP(1);
     // (4) cross-wave reduction through LDS
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -227,6 +260,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
           red[wave][m * 16 + (lane >> 4) * 4 + j][g * 16 + (lane & 15)] = acc[m][g][j];
     __syncthreads();
 
+    DS2_STAMP(2);
     // (5) cell epilogue: only the bf16 exchange copy is written before the publish
     float hout[EPT];
     float4 gsv[EPT];
@@ -266,6 +300,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
       }
     }
     __syncthreads();
+    DS2_STAMP(3);
 
     // (6) publish h_s: write-through 16-B stores, drain, one flag per workgroup
     if (wave == 0) {
@@ -279,6 +314,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
       if (lane == 0) st_flag(a.flags + grp * S + slice, (unsigned)(s - a.s_begin + 1));
     }
 
+    DS2_STAMP(4);
     // (7) off-critical-path stores: fp32 state, gates, time-indexed output
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
@@ -296,6 +332,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_fwd_kernel(FwdArgs a) {
       }
     }
   }
+  DS2_STAMP_STORE(a);
 }
 
 template <int CELL, int NW, int MT, int KPW>
@@ -356,9 +393,11 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
   const __amdgpu_buffer_rsrc_t rs_dgh = make_rsrc(a.dgh[dir], dgh_bytes);
   const unsigned* gflags = a.flags + grp * S;
   __syncthreads();
+  DS2_STAMP_DECL
 
   for (int s = a.s_end - 1; s >= a.s_begin; --s) {
     const int it = a.s_end - 1 - s;
+    DS2_STAMP(5);
     // (1) prefetch everything that does not depend on the recurrence
     float dyv[EPT];
     float4 gsv[EPT];
@@ -390,6 +429,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
       __syncthreads();
       if (abort_flag) break;
     }
+    DS2_STAMP(0);
 
     // (3) dh_rec = dgh_{s+1} . U[:, slice]
     f32x4 acc[MT];
@@ -419,12 +459,14 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
         }
       }
     }
+    DS2_STAMP(1);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int j = 0; j < 4; ++j) red[wave][m * 16 + (lane >> 4) * 4 + j][lane & 15] = acc[m][j];
     __syncthreads();
 
+    DS2_STAMP(2);
     // (4) cell backward epilogue (exchange copy first; dgx stores after the publish)
     float gxs[EPT][G];
 #pragma unroll
@@ -470,6 +512,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
       }
     }
     __syncthreads();
+    DS2_STAMP(3);
 
     // (5) publish dgh_s
     if (wave == 0) {
@@ -484,6 +527,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
       if (lane == 0) st_flag(a.flags + grp * S + slice, (unsigned)(it + 1));
     }
 
+    DS2_STAMP(4);
     // (6) time-indexed input-projection gradient (off the critical path)
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
@@ -502,6 +546,7 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
     }
   }
 
+  DS2_STAMP_STORE(a);
   // step-mode carry hand-over
   if (a.carry[dir] != nullptr && a.s_begin > 0) {
 #pragma unroll
@@ -574,6 +619,7 @@ struct DS2RnnFwd {
   unsigned* flags;
   unsigned* err;
   long long timeout;
+  unsigned long long* stamps;
 };
 
 struct DS2RnnBwd {
@@ -589,17 +635,18 @@ struct DS2RnnBwd {
   unsigned* flags;
   unsigned* err;
   long long timeout;
+  unsigned long long* stamps;
 };
 
-int ds2_rnn_kpw(int H, int G, int nw, int fwd) {
+int DS2_EXPORT(ds2_rnn_kpw)(int H, int G, int nw, int fwd) {
   const int ks = fwd ? H / 32 : G * H / 32;
   return pick_kpw((ks + nw - 1) / nw);
 }
 
-int ds2_rnn_fwd(const DS2RnnFwd* d, hipStream_t st) {
+int DS2_EXPORT(ds2_rnn_fwd)(const DS2RnnFwd* d, hipStream_t st) {
   if (d->H % 32 != 0 || d->NP % (16 * d->mt) != 0) return -10;
   const int G = d->cell == CELL_GRU ? 3 : 1;
-  const int kpw = ds2_rnn_kpw(d->H, G, d->nw, 1);
+  const int kpw = DS2_EXPORT(ds2_rnn_kpw)(d->H, G, d->nw, 1);
   if (kpw < 0) return -11;
   FwdArgs a;
   a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.S = d->S; a.BG = d->BG;
@@ -609,7 +656,7 @@ int ds2_rnn_fwd(const DS2RnnFwd* d, hipStream_t st) {
     a.U[i] = (const bf16_t*)d->U[i]; a.bh[i] = d->bh[i]; a.y[i] = (bf16_t*)d->y[i];
     a.hx[i] = (bf16_t*)d->hx[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
   }
-  a.flags = d->flags; a.err = d->err; a.timeout = d->timeout;
+  a.flags = d->flags; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   const int grid = d->ndir * d->BG * d->S;
   auto run = [&](int s0, int s1) -> int {
     a.s_begin = s0; a.s_end = s1;
@@ -637,10 +684,10 @@ int ds2_rnn_fwd(const DS2RnnFwd* d, hipStream_t st) {
   return 0;
 }
 
-int ds2_rnn_bwd(const DS2RnnBwd* d, hipStream_t st) {
+int DS2_EXPORT(ds2_rnn_bwd)(const DS2RnnBwd* d, hipStream_t st) {
   if (d->H % 32 != 0 || d->NP % (16 * d->mt) != 0) return -10;
   const int G = d->cell == CELL_GRU ? 3 : 1;
-  const int kpw = ds2_rnn_kpw(d->H, G, d->nw, 0);
+  const int kpw = DS2_EXPORT(ds2_rnn_kpw)(d->H, G, d->nw, 0);
   if (kpw < 0) return -11;
   BwdArgs a;
   a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.S = d->S; a.BG = d->BG;
@@ -650,7 +697,7 @@ int ds2_rnn_bwd(const DS2RnnBwd* d, hipStream_t st) {
     a.U[i] = (const bf16_t*)d->U[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
     a.dgh[i] = (bf16_t*)d->dgh[i]; a.carry[i] = d->carry[i];
   }
-  a.flags = d->flags; a.err = d->err; a.timeout = d->timeout;
+  a.flags = d->flags; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   const int grid = d->ndir * d->BG * d->S;
   auto run = [&](int s0, int s1) -> int {
     a.s_begin = s0; a.s_end = s1;

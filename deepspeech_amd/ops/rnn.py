@@ -30,8 +30,10 @@ from . import reference as R
 CELL_CODE = {"rnn_relu": 0, "gru": 1}
 GATES = {"rnn_relu": 1, "gru": 3}
 TIMEOUT_TICKS = int(float(os.environ.get("DS2_RNN_TIMEOUT_S", "20")) * 1e8)   # s_memrealtime = 100 MHz
-
 _pending_errors: List[torch.Tensor] = []
+# diagnostic: when set to a list, each kernel launch appends (kind, plan, stamps[grid, 8])
+# recorded by the s_memtime build (csrc/rnn_persistent_stamps.hip)
+STAMP_LOG: Optional[list] = None
 
 
 @dataclass(frozen=True)
@@ -103,7 +105,10 @@ def make_plan(N: int, H: int, cell: str, ndir: int, cus: int, mode: Optional[str
             nw = cand
             break
     if nw is None:
-        raise ValueError("no register-feasible tile for H=%d cell=%s" % (H, cell))
+        # no spill-free instantiation: take the 4-wave one (correct, some register spills)
+        if _kpw(H, G, 4, True) < 0 or _kpw(H, G, 4, False) < 0:
+            raise ValueError("no tile for H=%d cell=%s" % (H, cell))
+        nw = 4
     return RnnPlan(N=N, NP=BG * 16 * mt, BG=BG, mt=mt, nw=nw, persistent=persistent, H=H, S=S,
                    cell=cell, ndir=ndir)
 
@@ -119,6 +124,14 @@ def check_errors(clear: bool = True) -> None:
         if int(e.item()) != 0:
             raise RuntimeError("persistent recurrence kernel timed out waiting for its peers "
                                "(grid not co-resident?) — rerun with DS2_RNN_MODE=step")
+
+
+def _stamps(kind: str, plan: "RnnPlan", grid: int, dev) -> Optional[torch.Tensor]:
+    if STAMP_LOG is None:
+        return None
+    t = torch.zeros(grid, 8, device=dev, dtype=torch.int64)
+    STAMP_LOG.append((kind, plan, t))
+    return t
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -145,7 +158,7 @@ class BiRecurrence(torch.autograd.Function):
         bf16 = torch.bfloat16
         y2 = torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
         hx = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=bf16)
-        hx[:, 0].zero_()
+        hx[:, 0].zero_()                         # h0
         hs = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=torch.float32)
         hs[:, 0].zero_()
         gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
@@ -161,7 +174,8 @@ class BiRecurrence(torch.autograd.Function):
                   gates[0] if gates is not None else None,
                   gates[1] if (gates is not None and d1) else None,
                   flags, err, T, N, plan.NP, H, plan.BG, steps, gstride, ndir,
-                  CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS)
+                  CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS,
+                  _stamps("fwd", plan, flags.numel(), dev))
         _pending_errors.append(err)
         y = y2[0] + y2[1] if d1 else y2[0]
         ctx.save_for_backward(lens, U_f, U_b if U_b is not None else torch.empty(0, device=dev),
@@ -193,7 +207,8 @@ class BiRecurrence(torch.autograd.Function):
                   carry[0] if carry is not None else None,
                   carry[1] if (carry is not None and d1) else None,
                   flags, err, T, N, plan.NP, H, plan.BG, steps, gstride, ndir,
-                  CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS)
+                  CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS,
+                  _stamps("bwd", plan, flags.numel(), dev))
         _pending_errors.append(err)
         grads_U, grads_b = [], []
         for d in range(ndir):

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Micro-benchmark + phase breakdown of the persistent recurrence kernels.
+
+  python tools/bench_rnn.py [--cell gru] [--H 800] [--N 32] [--T 241] [--stamps]
+
+Times forward and backward of ONE bidirectional layer (the recurrence only) with HIP
+events, interleaving the variants in one process (cdna_hip_programming.md §5.4 rule 24).
+With --stamps, re-runs the s_memtime diagnostic build and prints the average cycles per
+step in each phase (wait / load+MFMA / reduce / epilogue / publish / rest) over all
+workgroups — read the SHARES, not the absolute time, of that build.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+PHASES = ["wait", "load+mfma", "reduce", "epilogue", "publish", "rest(stores+prefetch)"]
+
+
+def run(cell, N, H, T, ndir, nw, mode, iters, stamps=False):
+    from deepspeech_amd.ops import rnn as RNN
+    dev = torch.device("cuda")
+    os.environ["DS2_RNN_NW"] = str(nw) if nw else ""
+    if not nw:
+        os.environ.pop("DS2_RNN_NW")
+    os.environ["DS2_RNN_MODE"] = mode
+    RNN._plan_cache.clear()
+    plan = RNN.plan_for(N, H, cell, ndir, dev)
+    G = RNN.GATES[cell]
+    torch.manual_seed(0)
+    gx = (torch.randn(T, N, ndir * G * H, device=dev) * 0.5).bfloat16().requires_grad_(True)
+    Us = [(torch.randn(G * H, H, device=dev) / H ** 0.5).bfloat16().requires_grad_(True) for _ in range(ndir)]
+    bh = [torch.zeros(G * H, device=dev, requires_grad=True) if cell == "gru" else None for _ in range(ndir)]
+    lens = torch.full((N,), T, dtype=torch.int32, device=dev)
+    dy = torch.randn(T, N, H, device=dev).bfloat16()
+
+    def fwd():
+        return RNN.BiRecurrence.apply(gx, lens, Us[0], Us[1] if ndir == 2 else None, bh[0],
+                                      bh[1] if ndir == 2 else None, plan)
+
+    if stamps:
+        RNN.STAMP_LOG = []
+    y = fwd()
+    y.backward(dy)
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    res = {"plan": plan.__dict__}
+    if stamps:
+        log = RNN.STAMP_LOG
+        RNN.STAMP_LOG = None
+        for kind, p, t in log:
+            w = t[:, :6].double() / T
+            active = w.sum(1) > 0
+            w = w[active]
+            res[kind + "_cycles_per_step"] = {ph: [round(float(w[:, i].mean()), 0), round(float(w[:, i].min()), 0),
+                                                   round(float(w[:, i].max()), 0)] for i, ph in enumerate(PHASES)}
+            res[kind + "_busy_(non-wait)_max"] = round(float((w.sum(1) - w[:, 0]).max()), 0)
+        return res
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    tf, tb = [], []
+    for _ in range(iters):
+        ev[0].record()
+        y = fwd()
+        ev[1].record()
+        ev[2].record()
+        y.backward(dy)
+        ev[3].record()
+        torch.cuda.synchronize()
+        tf.append(ev[0].elapsed_time(ev[1]))
+        tb.append(ev[2].elapsed_time(ev[3]))
+    RNN.check_errors()
+    tf.sort(), tb.sort()
+    res.update(fwd_ms=tf[len(tf) // 2], bwd_ms=tb[len(tb) // 2],
+               fwd_us_per_step=1000 * tf[len(tf) // 2] / T, bwd_us_per_step=1000 * tb[len(tb) // 2] / T)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cell", default="gru")
+    ap.add_argument("--H", type=int, default=800)
+    ap.add_argument("--N", type=int, default=32)
+    ap.add_argument("--T", type=int, default=241)
+    ap.add_argument("--ndir", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--nw", type=str, default="0,4,8")
+    ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--protos", type=str, default="flag")
+    a = ap.parse_args()
+    for proto in a.protos.split(","):
+      os.environ["DS2_RNN_PROTO"] = proto
+      for nw in [int(x) for x in a.nw.split(",")]:
+        for mode in ("auto",):
+            try:
+                r = run(a.cell, a.N, a.H, a.T, a.ndir, nw, mode, a.iters)
+                print(json.dumps({"proto": proto, "nw": nw, "mode": mode,
+                                  **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}}), flush=True)
+            except Exception as e:  # noqa: BLE001
+                print(json.dumps({"proto": proto, "nw": nw, "mode": mode, "error": str(e)[:200]}), flush=True)
+      if a.stamps:
+        r = run(a.cell, a.N, a.H, a.T, a.ndir, 0, "auto", 1, stamps=True)
+        print(json.dumps({"proto": proto, "stamps [mean,min,max] cycles/step": r}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
