@@ -37,6 +37,9 @@ struct DS2RnnBwd {
   void* dgh[2];
   void* dgx;
   float* carry[2];
+  float* dbx_part[2];
+  float* dbh_part[2];
+  float dgx_scale;
   unsigned* flags;
   unsigned* err;
   long long timeout;
@@ -48,8 +51,9 @@ int ds2_rnn_fwd_stamps(const DS2RnnFwd* d, hipStream_t st);
 int ds2_rnn_bwd_stamps(const DS2RnnBwd* d, hipStream_t st);
 int ds2_rnn_kpw(int H, int G, int nw, int fwd);
 int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const int* labels, const int* label_lens,
-                  float* loss, void* grad, float* lp_ws, float* alpha_ws, int T, int N, int K, int Lmax, int blank,
-                  int zero_inf, hipStream_t st);
+                  float* loss, void* grad, float* ws, int T, int N, int K, int Lmax, int blank, int zero_inf,
+                  hipStream_t st);
+long long ds2_ctc_ws_floats(int T, int N, int Lmax);
 int ds2_bn_stats(const void* y, int y_bf16, int N, int C, int T, int F, float* part, int nb, float eps, float* mean,
                  float* invstd, float* run_mean, float* run_var, float momentum, hipStream_t st);
 int ds2_bn_chunks(int N, int T, int F);
@@ -136,7 +140,7 @@ void rnn_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tenso
              OptT gates_b, at::Tensor dgh_f, OptT dgh_b, at::Tensor dgx, OptT carry_f, OptT carry_b,
              at::Tensor flags, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t steps,
              int64_t gstride, int64_t ndir, int64_t cell, int64_t nw, int64_t mt, bool persistent, int64_t timeout,
-             OptT stamps) {
+             OptT stamps, OptT dbx_part, OptT dbh_part, double dgx_scale) {
   need_gpu(dy, "dy");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dgx.scalar_type() == at::kBFloat16, "dy/dgx must be bf16");
   TORCH_CHECK(dgx.numel() >= T * N * gstride, "dgx too small");
@@ -158,6 +162,16 @@ void rnn_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tenso
   d.dgx = dgx.data_ptr();
   d.carry[0] = ptr_or_null<float>(carry_f, "carry_f");
   d.carry[1] = ptr_or_null<float>(carry_b, "carry_b");
+  const int G = cell == 1 ? 3 : 1;
+  float* bx = ptr_or_null<float>(dbx_part, "dbx_part");
+  float* bh = ptr_or_null<float>(dbh_part, "dbh_part");
+  if (bx) TORCH_CHECK(dbx_part->numel() == ndir * BG * G * H && dbx_part->scalar_type() == at::kFloat, "dbx_part must be fp32 [ndir, BG, G*H]");
+  if (bh) TORCH_CHECK(dbh_part->numel() == ndir * BG * G * H && dbh_part->scalar_type() == at::kFloat, "dbh_part must be fp32 [ndir, BG, G*H]");
+  for (int i = 0; i < 2; ++i) {
+    d.dbx_part[i] = (bx && i < ndir) ? bx + (size_t)i * BG * G * H : nullptr;
+    d.dbh_part[i] = (bh && i < ndir) ? bh + (size_t)i * BG * G * H : nullptr;
+  }
+  d.dgx_scale = (float)dgx_scale;
   TORCH_CHECK(ndir == 1 || (d.U[1] && d.hsave[1] && d.dgh[1]), "backward-direction buffers missing");
   d.flags = reinterpret_cast<unsigned*>(flags.data_ptr<int>());
   d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
@@ -169,20 +183,22 @@ void rnn_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tenso
 int64_t rnn_kpw(int64_t H, int64_t G, int64_t nw, bool fwd) { return ds2_rnn_kpw((int)H, (int)G, (int)nw, fwd ? 1 : 0); }
 
 // --------------------------------------------------------------------------- CTC
+int64_t ctc_ws_floats(int64_t T, int64_t N, int64_t Lmax) { return ds2_ctc_ws_floats((int)T, (int)N, (int)Lmax); }
+
 void ctc_fused(at::Tensor logits, at::Tensor lens, at::Tensor labels, at::Tensor label_lens, at::Tensor loss,
-               at::Tensor grad, at::Tensor lp_ws, at::Tensor alpha_ws, int64_t blank, bool zero_inf) {
+               at::Tensor grad, at::Tensor ws, int64_t blank, bool zero_inf) {
   need_gpu(logits, "logits");
   need_gpu(labels, "labels");
+  need_gpu(ws, "ws");
   TORCH_CHECK(logits.dim() == 3, "logits must be [T, N, K]");
   TORCH_CHECK(grad.scalar_type() == logits.scalar_type() && grad.sizes() == logits.sizes(), "grad mismatch");
   const int T = (int)logits.size(0), N = (int)logits.size(1), K = (int)logits.size(2);
   const int Lmax = (int)labels.size(1);
   TORCH_CHECK(labels.size(0) == N && lens.numel() == N && label_lens.numel() == N, "batch mismatch");
-  TORCH_CHECK(lp_ws.numel() >= (int64_t)N * T * 32, "lp workspace too small");
-  TORCH_CHECK(alpha_ws.numel() >= (int64_t)N * T * (2 * Lmax + 1), "alpha workspace too small");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= ds2_ctc_ws_floats(T, N, Lmax), "CTC workspace too small");
   check(ds2_ctc_fused(logits.data_ptr(), is_bf16(logits), lens.data_ptr<int>(), labels.data_ptr<int>(),
-                      label_lens.data_ptr<int>(), loss.data_ptr<float>(), grad.data_ptr(), lp_ws.data_ptr<float>(),
-                      alpha_ws.data_ptr<float>(), T, N, K, Lmax, (int)blank, zero_inf ? 1 : 0, cur_stream()),
+                      label_lens.data_ptr<int>(), loss.data_ptr<float>(), grad.data_ptr(), ws.data_ptr<float>(), T,
+                      N, K, Lmax, (int)blank, zero_inf ? 1 : 0, cur_stream()),
         "ctc_fused");
 }
 
@@ -288,9 +304,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("carry_f"), py::arg("carry_b"), py::arg("flags"), py::arg("err"), py::arg("T"), py::arg("N"),
         py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("steps"), py::arg("gstride"), py::arg("ndir"),
         py::arg("cell"), py::arg("nw"), py::arg("mt"), py::arg("persistent"), py::arg("timeout"),
-        py::arg("stamps") = py::none());
+        py::arg("stamps") = py::none(), py::arg("dbx_part") = py::none(), py::arg("dbh_part") = py::none(),
+        py::arg("dgx_scale") = 1.0);
   m.def("rnn_kpw", &rnn_kpw);
   m.def("ctc_fused", &ctc_fused);
+  m.def("ctc_ws_floats", &ctc_ws_floats);
   m.def("bn_chunks", &bn_chunks);
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);

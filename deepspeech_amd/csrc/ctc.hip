@@ -1,15 +1,20 @@
 // Fused CTC loss + gradient for gfx950 (reference: tf.nn.ctc_loss at
 // src/deepSpeech_NCHW.py:225, blank = last class, time-major logits).
 //
-// One workgroup per utterance:
-//   phase 0  log-softmax of every frame t < len into a small global scratch lp[T][32]
-//            (one wave per frame, 64-lane reductions);
-//   phase 1  alpha recursion over the extended label lattice (2L+1 states), two LDS
-//            rows, one barrier per frame; alpha rows spill to global for phase 2;
-//   phase 2  beta recursion fused with the gradient: at frame t each state adds its
-//            occupancy exp(alpha+beta-lp-logP) into a per-class LDS accumulator with an
-//            LDS float atomic, then grad[t][k] = softmax_t(k) - occ_k(t). Frames past
-//            the utterance length get a zero gradient.
+// Three launches, each shaped for what it does:
+//   1. ctc_lsm_kernel     log-softmax of every valid frame -> lp[N][T][32]. Fully parallel
+//                         (one wave per (t, b) frame, 64-lane shuffle reductions).
+//   2. ctc_recur_kernel   the two serial recursions, alpha (blockIdx.y = 0) and beta
+//                         (blockIdx.y = 1) of every utterance CONCURRENTLY, ONE WAVE each:
+//                         lane l owns lattice states [l*SPL, l*SPL+SPL) in registers, the
+//                         s-1/s-2 (s+1/s+2) neighbours crossing a lane boundary come from a
+//                         cross-lane shuffle, so a frame costs no barrier and no LDS round
+//                         trip; the next frame's lp row is prefetched one frame ahead.
+//                         alpha/beta rows are streamed to ab_ws[2][N][T][SPmax].
+//   3. ctc_grad_kernel    fully parallel over frames (one wave per (t, b)): occupancy
+//                         gamma_t(s) = alpha+beta-lp-logP, blank states summed with a wave
+//                         reduction, label states with per-wave LDS atomics, then
+//                         grad[t][k] = softmax_t(k) - occ_t(k). Frames past the length get 0.
 // Infeasible utterances (logP = -inf) get loss 0 and zero gradient when zero_inf != 0.
 #include "common.h"
 
@@ -17,7 +22,6 @@ using namespace ds2;
 
 namespace {
 
-constexpr int CTC_THREADS = 256;
 constexpr int KPAD = 32;
 constexpr float NEG_INF = -INFINITY;
 
@@ -46,153 +50,242 @@ __device__ __forceinline__ void st_grad<float>(float* p, float v) { *p = v; }
 template <>
 __device__ __forceinline__ void st_grad<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
 
-template <typename LT>
-__global__ __launch_bounds__(CTC_THREADS) void ctc_fused_kernel(
-    const LT* __restrict__ logits,      // [T, N, K]
-    const int* __restrict__ lens,       // [N]
-    const int* __restrict__ labels,     // [N, Lmax]
-    const int* __restrict__ label_lens, // [N]
-    float* __restrict__ loss,           // [N]
-    LT* __restrict__ grad,              // [T, N, K]
-    float* __restrict__ lp_ws,          // [N, T, KPAD]
-    float* __restrict__ alpha_ws,       // [N, T, SPmax]
-    int T, int N, int K, int Lmax, int SPmax, int blank, int zero_inf) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* arow = reinterpret_cast<float*>(smem);                 // [2][SPmax]
-  int* lab = reinterpret_cast<int*>(arow + 2 * SPmax);          // [SPmax] class of state
-  float* occ = reinterpret_cast<float*>(lab + SPmax);           // [2][KPAD]
-  __shared__ float s_logp;
+__device__ __forceinline__ int state_class(const int* labels, int b, int Lmax, int s, int blank) {
+  return (s & 1) ? labels[(size_t)b * Lmax + (s >> 1)] : blank;
+}
 
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int NWAVE = CTC_THREADS / 64;
+// ---------------------------------------------------------------- 1. log-softmax
+template <typename LT>
+__global__ __launch_bounds__(256) void ctc_lsm_kernel(const LT* __restrict__ logits, const int* __restrict__ lens,
+                                                      float* __restrict__ lp_ws, int T, int N, int K) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= T * N) return;
+  const int t = w / N, b = w % N;
+  if (t >= lens[b]) return;
+  const float x = (lane < K) ? ld_logit<LT>(logits + (size_t)w * K + lane) : NEG_INF;
+  const float m = wave_max(x);
+  const float sum = wave_sum((lane < K) ? __expf(x - m) : 0.f);
+  if (lane < KPAD) lp_ws[((size_t)b * T + t) * KPAD + lane] = (lane < K) ? (x - m - __logf(sum)) : NEG_INF;
+}
+
+// ---------------------------------------------------------------- 2. alpha / beta
+template <int SPL>
+__global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ lens, const int* __restrict__ labels,
+                                                       const int* __restrict__ label_lens,
+                                                       const float* __restrict__ lp_ws, float* __restrict__ ab_ws,
+                                                       float* __restrict__ logp_out, int T, int N, int Lmax,
+                                                       int SPmax, int blank) {
+  const int b = blockIdx.x, beta = blockIdx.y, lane = threadIdx.x;
   const int len = min(lens[b], T);
   const int L = label_lens[b];
   const int SP = 2 * L + 1;
-  float* lp = lp_ws + (size_t)b * T * KPAD;
-  float* al = alpha_ws + (size_t)b * T * SPmax;
-
-  for (int s = tid; s < SP; s += CTC_THREADS) lab[s] = (s & 1) ? labels[(size_t)b * Lmax + (s >> 1)] : blank;
-  if (tid < 2 * KPAD) occ[tid] = 0.f;
-
-  // phase 0: log-softmax of each valid frame
-  for (int t = wave; t < len; t += NWAVE) {
-    const float x = (lane < K) ? ld_logit<LT>(logits + ((size_t)t * N + b) * K + lane) : NEG_INF;
-    const float m = wave_max(x);
-    const float e = (lane < K) ? __expf(x - m) : 0.f;
-    const float sum = wave_sum(e);
-    if (lane < KPAD) lp[(size_t)t * KPAD + lane] = (lane < K) ? (x - m - __logf(sum)) : NEG_INF;
-  }
-  // zero gradient past the utterance
-  for (size_t i = (size_t)len * K + tid; i < (size_t)T * K; i += CTC_THREADS) {
-    const size_t t = i / K, k = i % K;
-    st_grad<LT>(grad + (t * N + b) * K + k, 0.f);
-  }
-  __syncthreads();
-
-  if (len <= 0 || L > len) {   // nothing feasible (also covers empty frames)
-    if (tid == 0) loss[b] = zero_inf ? 0.f : INFINITY;
-    for (size_t i = tid; i < (size_t)len * K; i += CTC_THREADS) {
-      const size_t t = i / K, k = i % K;
-      st_grad<LT>(grad + (t * N + b) * K + k, 0.f);
-    }
+  if (len <= 0 || L > len) {
+    if (!beta && lane == 0) logp_out[b] = NEG_INF;
     return;
   }
-
-  // phase 1: alpha
-  for (int s = tid; s < SP; s += CTC_THREADS) {
-    float v = NEG_INF;
-    if (s == 0) v = lp[blank];
-    else if (s == 1) v = lp[lab[1]];
-    arow[s] = v;
-    al[s] = v;
-  }
-  __syncthreads();
-  for (int t = 1; t < len; ++t) {
-    const float* prev = arow + ((t - 1) & 1) * SPmax;
-    float* cur = arow + (t & 1) * SPmax;
-    const float* lpt = lp + (size_t)t * KPAD;
-    for (int s = tid; s < SP; s += CTC_THREADS) {
-      const int c = lab[s];
-      float a = prev[s];
-      float b1 = (s >= 1) ? prev[s - 1] : NEG_INF;
-      float b2 = (s >= 2 && c != blank && c != lab[s - 2]) ? prev[s - 2] : NEG_INF;
-      const float v = lse3(a, b1, b2) + lpt[c];
-      cur[s] = v;
-      al[(size_t)t * SPmax + s] = v;
+  const int s0 = lane * SPL;
+  int cls[SPL];
+  unsigned skip = 0;   // bit j: the s-2 (alpha) / s+2 (beta) transition into/out of state s0+j exists
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) {
+    const int s = s0 + j;
+    cls[j] = (s < SP) ? state_class(labels, b, Lmax, s, blank) : blank;
+    bool ok = false;
+    if (s < SP && cls[j] != blank) {
+      if (!beta) ok = s >= 2 && cls[j] != state_class(labels, b, Lmax, s - 2, blank);
+      else ok = s + 2 < SP && cls[j] != state_class(labels, b, Lmax, s + 2, blank);
     }
-    __syncthreads();
+    skip |= (ok ? 1u : 0u) << j;
   }
-  if (tid == 0) {
-    const float* last = arow + ((len - 1) & 1) * SPmax;
-    s_logp = lse2(last[SP - 1], SP >= 2 ? last[SP - 2] : NEG_INF);
-  }
-  __syncthreads();
-  const float logp = s_logp;
-  const bool infeasible = !(logp > NEG_INF);
-  if (tid == 0) loss[b] = infeasible ? (zero_inf ? 0.f : INFINITY) : -logp;
-  if (infeasible) {
-    for (size_t i = tid; i < (size_t)len * K; i += CTC_THREADS) {
-      const size_t t = i / K, k = i % K;
-      st_grad<LT>(grad + (t * N + b) * K + k, 0.f);
-    }
-    return;
-  }
-
-  // phase 2: beta + gradient
-  for (int t = len - 1; t >= 0; --t) {
-    const float* nxt = arow + ((t + 1) & 1) * SPmax;
-    float* cur = arow + (t & 1) * SPmax;
-    const float* lpt = lp + (size_t)t * KPAD;
-    float* oc = occ + (t & 1) * KPAD;
-    for (int s = tid; s < SP; s += CTC_THREADS) {
-      const int c = lab[s];
-      float v;
-      if (t == len - 1) {
-        v = (s == SP - 1 || s == SP - 2) ? lpt[c] : NEG_INF;
-      } else {
-        const float a = nxt[s];
-        const float b1 = (s + 1 < SP) ? nxt[s + 1] : NEG_INF;
-        const float b2 = (s + 2 < SP && c != blank && c != lab[s + 2]) ? nxt[s + 2] : NEG_INF;
-        v = lse3(a, b1, b2) + lpt[c];
+  const float* lp = lp_ws + (size_t)b * T * KPAD;
+  float* out = ab_ws + ((size_t)beta * N + b) * (size_t)T * SPmax;
+  // lp rows are staged through LDS in chunks of 64 frames (one 128-B row per lane), so
+  // the per-frame gathers are LDS reads: a global load in the frame loop would make the
+  // wave wait (vmcnt) behind its own streaming alpha/beta stores every frame.
+  __shared__ float lps[64][KPAD + 1];
+  const int dt = beta ? -1 : 1;
+  const int t0 = beta ? len - 1 : 0;
+  auto stage = [&](int c0) {   // frames c0 .. c0+63 (forward) or c0 .. c0-63 (backward)
+    const int t = c0 + dt * lane;
+    __builtin_amdgcn_wave_barrier();
+    if (t >= 0 && t < len) {
+      const float4* src = reinterpret_cast<const float4*>(lp + (size_t)t * KPAD);
+#pragma unroll
+      for (int q = 0; q < KPAD / 4; ++q) {
+        const float4 v4 = src[q];
+        lps[lane][4 * q + 0] = v4.x; lps[lane][4 * q + 1] = v4.y;
+        lps[lane][4 * q + 2] = v4.z; lps[lane][4 * q + 3] = v4.w;
       }
-      cur[s] = v;
-      const float ab = al[(size_t)t * SPmax + s] + v - lpt[c] - logp;
-      if (ab > -80.f) atomicAdd(&oc[c], __expf(ab));
     }
-    __syncthreads();
-    if (tid < K) {
-      const float g = __expf(lpt[tid]) - oc[tid];
-      st_grad<LT>(grad + ((size_t)t * N + b) * K + tid, g);
-      oc[tid] = 0.f;
-    }
-    // the next frame accumulates into the other occ buffer; its reset above is ordered
-    // before that buffer's reuse by the barrier at the end of the next iteration
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  float v[SPL];
+  stage(t0);
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) {
+    const int s = s0 + j;
+    const float l = lps[0][cls[j]];
+    if (!beta) v[j] = (s == 0 || s == 1) && s < SP ? l : NEG_INF;
+    else v[j] = (s == SP - 1 || s == SP - 2) ? l : NEG_INF;
   }
+#pragma unroll
+  for (int j = 0; j < SPL; ++j)
+    if (s0 + j < SPmax) out[(size_t)t0 * SPmax + s0 + j] = v[j];
+
+  for (int step = 1; step < len; ++step) {
+    const int t = t0 + dt * step;
+    if ((step & 63) == 0) stage(t);
+    float lcur[SPL];
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) lcur[j] = lps[step & 63][cls[j]];
+    float nv[SPL];
+    if (!beta) {
+      // neighbours s-1, s-2 of this lane's first two states live in the previous lane
+      float p1 = __shfl_up(v[SPL - 1], 1, 64);
+      float p2 = __shfl_up(v[SPL - 2], 1, 64);
+      if (lane == 0) { p1 = NEG_INF; p2 = NEG_INF; }
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        const float a1 = (j >= 1) ? v[j - 1] : p1;
+        const float a2 = (j >= 2) ? v[j - 2] : (j == 1 ? p1 : p2);
+        const float r = lse3(v[j], a1, ((skip >> j) & 1u) ? a2 : NEG_INF);
+        nv[j] = (s0 + j < SP) ? r + lcur[j] : NEG_INF;
+      }
+    } else {
+      float n1 = __shfl_down(v[0], 1, 64);
+      float n2 = __shfl_down(v[1], 1, 64);
+      if (lane == 63) { n1 = NEG_INF; n2 = NEG_INF; }
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        const float b1 = (j + 1 < SPL) ? v[j + 1] : n1;
+        const float b2 = (j + 2 < SPL) ? v[j + 2] : (j + 1 < SPL ? n1 : n2);
+        const float r = lse3(v[j], b1, ((skip >> j) & 1u) ? b2 : NEG_INF);
+        nv[j] = (s0 + j < SP) ? r + lcur[j] : NEG_INF;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+      v[j] = nv[j];
+      if (s0 + j < SPmax) out[(size_t)t * SPmax + s0 + j] = v[j];
+    }
+  }
+  if (!beta) {
+    // logP = lse(alpha_{len-1}(SP-1), alpha_{len-1}(SP-2))
+    float mine = NEG_INF;
+#pragma unroll
+    for (int j = 0; j < SPL; ++j)
+      if (s0 + j == SP - 1 || s0 + j == SP - 2) mine = lse2(mine, v[j]);
+    // at most two lanes hold a term: combine with a max-shifted wave reduction
+    const float m = wave_max(mine);
+    float e = (m == NEG_INF) ? 0.f : __expf(mine - m);
+    e = wave_sum(e);
+    if (lane == 0) logp_out[b] = (m == NEG_INF) ? NEG_INF : m + __logf(e);
+  }
+}
+
+// ---------------------------------------------------------------- 3. gradient
+template <typename LT>
+__global__ __launch_bounds__(256) void ctc_grad_kernel(const LT* __restrict__ logits, const int* __restrict__ lens,
+                                                       const int* __restrict__ labels,
+                                                       const int* __restrict__ label_lens,
+                                                       const float* __restrict__ ab_ws,
+                                                       const float* __restrict__ logp_in, float* __restrict__ loss,
+                                                       LT* __restrict__ grad, int T, int N, int K, int Lmax, int SPmax,
+                                                       int blank, int zero_inf) {
+  __shared__ float occ_s[4][KPAD];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + wv;
+  if (w >= T * N) return;
+  const int t = w / N, b = w % N;
+  const int len = min(lens[b], T);
+  const int L = label_lens[b];
+  const float logp = (len > 0 && L <= len) ? logp_in[b] : NEG_INF;
+  const bool feasible = logp > NEG_INF;
+  if (t == 0 && lane == 0) loss[b] = feasible ? -logp : (zero_inf ? 0.f : INFINITY);
+  LT* g = grad + (size_t)w * K;
+  if (t >= len || !feasible) {
+    if (lane < K) st_grad<LT>(g + lane, 0.f);
+    return;
+  }
+  float* occ = occ_s[wv];
+  if (lane < KPAD) occ[lane] = 0.f;
+  const float x = (lane < K) ? ld_logit<LT>(logits + (size_t)w * K + lane) : NEG_INF;
+  const float m = wave_max(x);
+  const float sum = wave_sum((lane < K) ? __expf(x - m) : 0.f);
+  const float lpk = (lane < K) ? (x - m - __logf(sum)) : NEG_INF;    // lane k holds lp_t(k)
+  const int SP = 2 * L + 1;
+  const float* A = ab_ws + ((size_t)b * T + t) * SPmax;
+  const float* B = ab_ws + ((size_t)(N + b) * T + t) * SPmax;
+  float blank_acc = 0.f;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  for (int base = 0; base < SP; base += 64) {       // wave-uniform trip count (shuffles below)
+    const int s = base + lane;
+    const bool in = s < SP;
+    const int c = in ? state_class(labels, b, Lmax, s, blank) : blank;
+    const float lc = __shfl(lpk, c, 64);
+    float e = 0.f;
+    if (in) {
+      const float ga = A[s] + B[s] - lc - logp;
+      e = (ga > -80.f) ? __expf(ga) : 0.f;
+    }
+    if (in && c != blank) atomicAdd(&occ[c], e);
+    else blank_acc += e;
+  }
+  blank_acc = wave_sum(blank_acc);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // this wave's LDS atomics have landed
+  if (lane < K) {
+    const float p = __expf(lpk);
+    const float o = (lane == blank) ? blank_acc : occ[lane];
+    st_grad<LT>(g + lane, p - o);
+  }
+}
+
+template <int SPL>
+static void launch_recur(const int* lens, const int* labels, const int* label_lens, const float* lp_ws, float* ab_ws,
+                         float* logp, int T, int N, int Lmax, int SPmax, int blank, hipStream_t st) {
+  hipLaunchKernelGGL(ctc_recur_kernel<SPL>, dim3(N, 2), dim3(64), 0, st, lens, labels, label_lens, lp_ws, ab_ws, logp,
+                     T, N, Lmax, SPmax, blank);
 }
 
 }  // namespace
 
 extern "C" {
 
-size_t ds2_ctc_smem_bytes(int SPmax) { return (size_t)(2 * SPmax) * 4 + (size_t)SPmax * 4 + 2 * KPAD * 4; }
+// workspace floats: lp [N][T][32] + alpha/beta [2][N][T][SPmax] + logP [N]
+long long ds2_ctc_ws_floats(int T, int N, int Lmax) {
+  const long long SPmax = 2LL * Lmax + 1;
+  return (long long)N * T * KPAD + 2LL * N * T * SPmax + N;
+}
 
 int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const int* labels,
-                  const int* label_lens, float* loss, void* grad, float* lp_ws, float* alpha_ws,
-                  int T, int N, int K, int Lmax, int blank, int zero_inf, hipStream_t st) {
+                  const int* label_lens, float* loss, void* grad, float* ws, int T, int N, int K, int Lmax, int blank,
+                  int zero_inf, hipStream_t st) {
   if (K > 64 || K > KPAD) return -20;
   const int SPmax = 2 * Lmax + 1;
-  const size_t smem = ds2_ctc_smem_bytes(SPmax);
-  if (smem > 160 * 1024) return -21;
-  if (logits_bf16) {
-    hipLaunchKernelGGL(ctc_fused_kernel<bf16_t>, dim3(N), dim3(CTC_THREADS), smem, st,
-                       (const bf16_t*)logits, lens, labels, label_lens, loss, (bf16_t*)grad, lp_ws,
-                       alpha_ws, T, N, K, Lmax, SPmax, blank, zero_inf);
-  } else {
-    hipLaunchKernelGGL(ctc_fused_kernel<float>, dim3(N), dim3(CTC_THREADS), smem, st,
-                       (const float*)logits, lens, labels, label_lens, loss, (float*)grad, lp_ws,
-                       alpha_ws, T, N, K, Lmax, SPmax, blank, zero_inf);
-  }
+  if (SPmax > 64 * 32) return -21;    // > 1023 labels per utterance
+  float* lp_ws = ws;
+  float* ab_ws = lp_ws + (size_t)N * T * KPAD;
+  float* logp = ab_ws + 2 * (size_t)N * T * SPmax;
+  const int nw = T * N;
+  const dim3 g4((nw + 3) / 4);
+  if (logits_bf16)
+    hipLaunchKernelGGL(ctc_lsm_kernel<bf16_t>, g4, dim3(256), 0, st, (const bf16_t*)logits, lens, lp_ws, T, N, K);
+  else
+    hipLaunchKernelGGL(ctc_lsm_kernel<float>, g4, dim3(256), 0, st, (const float*)logits, lens, lp_ws, T, N, K);
+  const int need = (SPmax + 63) / 64;
+  if (need <= 2) launch_recur<2>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else if (need <= 4) launch_recur<4>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else if (need <= 8) launch_recur<8>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else if (need <= 16) launch_recur<16>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else launch_recur<32>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  if (logits_bf16)
+    hipLaunchKernelGGL(ctc_grad_kernel<bf16_t>, g4, dim3(256), 0, st, (const bf16_t*)logits, lens, labels, label_lens,
+                       ab_ws, logp, loss, (bf16_t*)grad, T, N, K, Lmax, SPmax, blank, zero_inf);
+  else
+    hipLaunchKernelGGL(ctc_grad_kernel<float>, g4, dim3(256), 0, st, (const float*)logits, lens, labels, label_lens,
+                       ab_ws, logp, loss, (float*)grad, T, N, K, Lmax, SPmax, blank, zero_inf);
   return (int)hipGetLastError();
 }
 

@@ -68,6 +68,9 @@ struct BwdArgs {
   bf16_t* dgh[2];
   bf16_t* dgx;
   float* carry[2];
+  float* dbx_part[2];   // [BG, G*H] per direction: sum of dgx over steps and rows (input bias grad)
+  float* dbh_part[2];   // [BG, G*H] per direction: sum of dgh (GRU recurrent bias grad)
+  float dgx_scale;      // dgx is stored pre-multiplied (frozen sequence-BN scale folded in)
   unsigned* flags;
   unsigned* err;
   long long timeout;
@@ -376,12 +379,17 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
 
   float carry[EPT];
   int lenr[EPT];
+  float sbx[EPT][G];      // per-element bias-gradient sums over this launch's steps
+  float sbh[EPT];         // GRU: sum of d(U_n h + b_hn) (the only gate where dgh != dgx)
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = tid + i * NT;
     const int row = e >> 4, c = e & 15;
     const int b = r0 + row, u = u0 + c;
     carry[i] = 0.f;
+    sbh[i] = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) sbx[i][g] = 0.f;
     lenr[i] = 0;
     if (e < NE) {
       lenr[i] = (b < N) ? a.lens[b] : 0;
@@ -508,7 +516,11 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
         }
         carry[i] = cnew;
 #pragma unroll
-        for (int g = 0; g < G; ++g) stage[row][g * 16 + c] = f2bf(ghv[g]);
+        for (int g = 0; g < G; ++g) {
+          stage[row][g * 16 + c] = f2bf(ghv[g]);
+          sbx[i][g] += gxs[i][g];
+        }
+        if (CELL == CELL_GRU) sbh[i] += ghv[G - 1];
       }
     }
     __syncthreads();
@@ -540,13 +552,46 @@ __global__ __launch_bounds__(NW * 64) void rnn_bwd_kernel(BwdArgs a) {
           const int t = act ? ((dir == 0) ? s : (lenr[i] - 1 - s)) : s;
           bf16_t* dst = a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + u;
 #pragma unroll
-          for (int g = 0; g < G; ++g) dst[g * H] = f2bf(gxs[i][g]);
+          for (int g = 0; g < G; ++g) dst[g * H] = f2bf(gxs[i][g] * a.dgx_scale);
         }
       }
     }
   }
 
   DS2_STAMP_STORE(a);
+  // bias gradients: reduce this workgroup's rows through LDS, then one read-modify-write
+  // per (gate, unit) of the workgroup's own [bg] partial row (no atomics: every element
+  // has exactly one writer per launch; step-mode launches are stream-ordered)
+  if (a.dbx_part[dir] != nullptr) {
+    constexpr int BW = (G + 1) * 16;
+    static_assert(NW * ROWS * 16 >= ROWS * BW, "bias reduction does not fit the LDS scratch");
+    float* bred = &red[0][0][0];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int e = tid + i * NT;
+      if (e < NE) {
+        const int row = e >> 4, c = e & 15;
+#pragma unroll
+        for (int g = 0; g < G; ++g) bred[row * BW + g * 16 + c] = sbx[i][g];
+        bred[row * BW + G * 16 + c] = sbh[i];
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < BW; q += NT) {
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) sum += bred[r * BW + q];
+      const int g = q >> 4, c = q & 15;
+      const size_t base = (size_t)bg * GH + u0 + c;
+      if (g < G) {
+        a.dbx_part[dir][base + (size_t)g * H] += sum;
+        if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr && g < G - 1) a.dbh_part[dir][base + (size_t)g * H] += sum;
+      } else if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr) {
+        a.dbh_part[dir][base + (size_t)(G - 1) * H] += sum;
+      }
+    }
+  }
   // step-mode carry hand-over
   if (a.carry[dir] != nullptr && a.s_begin > 0) {
 #pragma unroll
@@ -632,6 +677,9 @@ struct DS2RnnBwd {
   void* dgh[2];
   void* dgx;
   float* carry[2];
+  float* dbx_part[2];
+  float* dbh_part[2];
+  float dgx_scale;
   unsigned* flags;
   unsigned* err;
   long long timeout;
@@ -696,7 +744,9 @@ int DS2_EXPORT(ds2_rnn_bwd)(const DS2RnnBwd* d, hipStream_t st) {
   for (int i = 0; i < 2; ++i) {
     a.U[i] = (const bf16_t*)d->U[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
     a.dgh[i] = (bf16_t*)d->dgh[i]; a.carry[i] = d->carry[i];
+    a.dbx_part[i] = d->dbx_part[i]; a.dbh_part[i] = d->dbh_part[i];
   }
+  a.dgx_scale = d->dgx_scale;
   a.flags = d->flags; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   const int grid = d->ndir * d->BG * d->S;
   auto run = [&](int s0, int s1) -> int {

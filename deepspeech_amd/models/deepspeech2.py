@@ -232,7 +232,31 @@ class DeepSpeech2(nn.Module):
             inp = out if self.stack_fix else x
         return out
 
+    def arena_groups(self):
+        """Parameter layout for ops.optim.ParamArena: gradient-production order (FC first,
+        conv1 last) and, per recurrent layer, [W_fw; W_bw] and [b_fw; b_bw] packed back to
+        back so the fused layer reads/writes both directions as one matrix."""
+        groups = [[("fc_bias", self.fc_bias)], [("fc_weight", self.fc_weight)]]
+        for i in reversed(range(len(self.rnn))):
+            layer = self.rnn[i]
+            pre = "rnn.%d." % i
+            dirs = [("fw", layer.fw)] + ([("bw", layer.bw)] if layer.bw is not None else [])
+            groups.append([(pre + n + ".W", d.W) for n, d in dirs])
+            groups.append([(pre + n + ".b", d.b) for n, d in dirs])
+            for n, d in dirs:
+                groups.append([(pre + n + ".U", d.U)])
+                if d.b_h is not None:
+                    groups.append([(pre + n + ".b_h", d.b_h)])
+        for cname in ("conv2", "conv1"):
+            blk = getattr(self, cname)
+            for pn in ("bn_beta", "bn_gamma", "bias", "weight"):
+                groups.append([("%s.%s" % (cname, pn), getattr(blk, pn))])
+        return groups
+
     def head(self, h: torch.Tensor) -> torch.Tensor:
+        if self.engine == "hip":
+            from ..ops.frontend import FusedHead
+            return FusedHead.apply(h, self.fc_weight, self.fc_bias)
         T, N, H = h.shape
         w = self.fc_weight.to(h.dtype)
         b = self.fc_bias.to(h.dtype)

@@ -30,9 +30,8 @@ class CTCLossFused(torch.autograd.Function):
         label_lens = label_lens.to(device=dev, dtype=torch.int32).contiguous()
         loss = torch.empty(N, device=dev, dtype=torch.float32)
         grad = torch.empty_like(logits)
-        lp_ws = torch.empty(N, T, 32, device=dev, dtype=torch.float32)
-        alpha_ws = torch.empty(N, T, 2 * Lmax + 1, device=dev, dtype=torch.float32)
-        C.ctc_fused(logits, lens, labels, label_lens, loss, grad, lp_ws, alpha_ws, blank, zero_infinity)
+        ws = torch.empty(int(C.ctc_ws_floats(T, N, labels.shape[1])), device=dev, dtype=torch.float32)
+        C.ctc_fused(logits, lens, labels, label_lens, loss, grad, ws, blank, zero_infinity)
         ctx.save_for_backward(grad)
         ctx.in_dtype = logits.dtype
         return loss

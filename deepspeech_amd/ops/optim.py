@@ -24,32 +24,114 @@ from . import _ext
 
 
 class ParamArena:
-    def __init__(self, model: nn.Module, align: int = 64):
-        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
-        named = list(reversed(named))
-        self.names: List[str] = [n for n, _ in named]
-        self.params: List[nn.Parameter] = [p for _, p in named]
+    """Flat fp32 master weights + fp32 gradients (+ optional bf16 compute shadows).
+
+    Layout: ``groups`` (default: the model's ``arena_groups()`` if it has one, otherwise
+    one group per parameter in reverse registration order). Members of a group are
+    packed back to back with NO padding, so e.g. ``[W_fw; W_bw]`` of a bidirectional
+    layer is one contiguous ``[2*G*H, in]`` matrix in all three buffers (the input
+    projection of both directions is then ONE GEMM with no concat); groups start on
+    ``align``-element (256 B) boundaries.
+
+    Fused HIP ops write weight gradients straight into ``p.main_grad`` (a view of
+    ``grad``) in fp32 and report them with :meth:`grad_done` — no bf16->fp32 casts, no
+    autograd accumulation kernels — and read the weights from ``p.bf16`` (a view of the
+    shadow that the fused optimizer rewrites after every update).
+    """
+
+    def __init__(self, model: nn.Module, align: int = 64, groups=None, bf16_shadow: bool = False):
+        if groups is None and hasattr(model, "arena_groups"):
+            groups = model.arena_groups()
+        if groups is None:
+            named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+            groups = [[np_] for np_ in reversed(named)]
+        groups = [[(n, p) for n, p in g if p.requires_grad] for g in groups]
+        groups = [g for g in groups if g]
+        seen = {id(p) for g in groups for _, p in g}
+        want = {id(p) for _, p in model.named_parameters() if p.requires_grad}
+        if seen != want or sum(len(g) for g in groups) != len(want):
+            raise ValueError("arena groups must cover every trainable parameter exactly once")
+        self.names: List[str] = [n for g in groups for n, _ in g]
+        self.params: List[nn.Parameter] = [p for g in groups for _, p in g]
         dev = self.params[0].device
         self.offsets: List[Tuple[int, int]] = []
         off = 0
-        for p in self.params:
-            n = p.numel()
-            self.offsets.append((off, n))
-            off += -(-n // align) * align           # 256-B aligned views
+        for g in groups:
+            for _, p in g:
+                self.offsets.append((off, p.numel()))
+                off += p.numel()
+            off = -(-off // align) * align
         self.numel = off
         self.flat = torch.zeros(off, device=dev, dtype=torch.float32)
         self.grad = torch.zeros(off, device=dev, dtype=torch.float32)
-        for p, (o, n) in zip(self.params, self.offsets):
+        self.p16 = torch.zeros(off, device=dev, dtype=torch.bfloat16) if bf16_shadow else None
+        self._index = {}
+        self._ready_cbs = []
+        self._written = set()
+        for i, (p, (o, n)) in enumerate(zip(self.params, self.offsets)):
             self.flat[o:o + n].copy_(p.data.reshape(-1).float())
             p.data = self.flat[o:o + n].view_as(p)
             p.grad = self.grad[o:o + n].view_as(p)
+            self._index[id(p)] = i
+            if bf16_shadow:
+                p.main_grad = self.grad[o:o + n].view_as(p)
+                p.bf16 = self.p16[o:o + n].view_as(p)
+                p._ds2_arena = self
+        self._dirty = True
+        self.ensure_bf16()
 
+    # ---- bf16 shadow ------------------------------------------------------------
+    def mark_dirty(self) -> None:
+        """Call after changing master weights outside the fused optimizer (restore, EMA swap)."""
+        self._dirty = True
+
+    def ensure_bf16(self) -> None:
+        if self.p16 is not None and self._dirty:
+            self.p16.copy_(self.flat)
+        self._dirty = False
+
+    def group_view(self, params, buf: str = "p16") -> Optional[torch.Tensor]:
+        """Contiguous 1-D view of ``buf`` spanning ``params`` if they are packed back to back
+        in this order, else None."""
+        idx = [self._index.get(id(p)) for p in params]
+        if any(i is None for i in idx):
+            return None
+        start = self.offsets[idx[0]][0]
+        pos = start
+        for i in idx:
+            o, n = self.offsets[i]
+            if o != pos:
+                return None
+            pos = o + n
+        b = {"p16": self.p16, "grad": self.grad, "flat": self.flat}[buf]
+        return None if b is None else b[start:pos]
+
+    # ---- gradients ----------------------------------------------------------------
     def zero_grad(self) -> None:
         self.grad.zero_()
+        self._written.clear()
         # re-attach in case an op replaced a .grad (e.g. set_to_none elsewhere)
         for p, (o, n) in zip(self.params, self.offsets):
             if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
                 p.grad = self.grad[o:o + n].view_as(p)
+
+    def first_write(self, p) -> bool:
+        """True if ``p``'s gradient has not been written yet this step (fused ops then
+        overwrite instead of accumulate)."""
+        return id(p) not in self._written
+
+    def grad_done(self, *params) -> None:
+        """Report gradients written straight into ``main_grad`` (fires bucket hooks)."""
+        for p in params:
+            if p is None:
+                continue
+            self._written.add(id(p))
+            i = self._index[id(p)]
+            for cb in self._ready_cbs:
+                cb(i)
+
+    def on_grad_ready(self, cb) -> None:
+        self._ready_cbs.append(cb)
 
     def views(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
         return {n: buf[o:o + c].view_as(p) for n, p, (o, c) in zip(self.names, self.params, self.offsets)}
@@ -57,6 +139,53 @@ class ParamArena:
     def param_range(self, name: str) -> Tuple[int, int]:
         i = self.names.index(name)
         return self.offsets[i]
+
+
+def arena_of(p) -> Optional["ParamArena"]:
+    return getattr(p, "_ds2_arena", None) if p is not None else None
+
+
+def emit_grad(p, g: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Deliver gradient ``g`` of parameter ``p`` from a fused op's backward.
+
+    Arena-managed parameter: written (first producer this step) or accumulated into
+    ``p.main_grad`` in fp32, reported ready, and None is returned to autograd.
+    Otherwise ``g`` is returned for autograd to accumulate as usual."""
+    if g is None or p is None:
+        return None
+    a = arena_of(p)
+    if a is None:
+        return g.to(p.dtype) if g.dtype != p.dtype else g
+    mg = p.main_grad
+    if a.first_write(p):
+        mg.copy_(g.view_as(mg))
+    else:
+        mg.add_(g.view_as(mg))
+    a.grad_done(p)
+    return None
+
+
+def mm_into(p, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Weight gradient ``a @ b`` (bf16 operands, fp32 accumulation) for parameter ``p``.
+
+    Arena-managed: the GEMM writes fp32 straight into ``p.main_grad`` (``out`` may name a
+    larger group view of the gradient arena covering several packed parameters) and
+    returns None; otherwise returns the fp32 product."""
+    arena = arena_of(p)
+    if arena is None:
+        try:
+            return torch.mm(a, b, out_dtype=torch.float32)
+        except (RuntimeError, TypeError):
+            return torch.mm(a.float(), b.float())
+    dst = out if out is not None else p.main_grad.view(a.shape[0], b.shape[1])
+    if arena.first_write(p):
+        try:
+            torch.mm(a, b, out_dtype=torch.float32, out=dst)
+        except (RuntimeError, TypeError):
+            dst.copy_(torch.mm(a.float(), b.float()))
+    else:
+        dst.add_(torch.mm(a.float(), b.float()))
+    return None
 
 
 def exponential_decay(initial_lr: float, step: int, decay_steps: int, decay_rate: float,
@@ -82,10 +211,11 @@ class FusedAdamEMA:
         self.m = torch.zeros_like(arena.flat)
         self.v = torch.zeros_like(arena.flat)
         self.ema = arena.flat.clone() if ema_decay is not None else None
-        self.p16 = (torch.empty(arena.numel, device=dev, dtype=torch.bfloat16) if bf16_copy else None)
+        self.p16 = arena.p16 if arena.p16 is not None else (
+            torch.empty(arena.numel, device=dev, dtype=torch.bfloat16) if bf16_copy else None)
         self.t = 0          # number of applied updates (Adam bias-correction power)
         self.use_hip = dev.type == "cuda"
-        if self.p16 is not None and self.use_hip:
+        if self.p16 is not None and self.use_hip and arena.p16 is None:
             _ext.ext().cast_bf16(arena.flat, self.p16)
         self._norm_part = None
         self._bad = None

@@ -26,6 +26,7 @@ import torch
 
 from . import _ext
 from . import reference as R
+from .optim import arena_of, emit_grad, mm_into
 
 CELL_CODE = {"rnn_relu": 0, "gru": 1}
 GATES = {"rnn_relu": 1, "gru": 3}
@@ -141,84 +142,219 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return torch.mm(a, b).float()
 
 
+def _run_fwd(gx, lens, U, bh, plan: RnnPlan):
+    """Launch the persistent forward recurrence over gx [T, N, ndir*G*H] (bf16).
+    U / bh: per-direction lists (bf16 [G*H, H] / fp32 [G*H] or None).
+    Returns (y [T, N, H] bf16 = sum of directions, saved-state tuple)."""
+    C = _ext.ext()
+    T, N, gstride = gx.shape
+    H, ndir = plan.H, plan.ndir
+    steps = T
+    dev = gx.device
+    d1 = ndir == 2
+    bf16 = torch.bfloat16
+    y2 = torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
+    hx = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=bf16)
+    hx[:, 0].zero_()                         # h0
+    hs = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=torch.float32)
+    hs[:, 0].zero_()
+    gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
+             if plan.cell == "gru" else None)
+    flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
+    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    C.rnn_fwd(gx, lens, U[0], U[1] if d1 else None,
+              bh[0], bh[1] if d1 else None,
+              y2[0], y2[1] if d1 else None, hx[0], hx[1] if d1 else None,
+              hs[0], hs[1] if d1 else None,
+              gates[0] if gates is not None else None,
+              gates[1] if (gates is not None and d1) else None,
+              flags, err, T, N, plan.NP, H, plan.BG, steps, gstride, ndir,
+              CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS,
+              _stamps("fwd", plan, flags.numel(), dev))
+    _pending_errors.append(err)
+    y = torch.add(y2[0], y2[1]) if d1 else y2[0]
+    return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
+
+
+def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale: float = 1.0,
+             want_bias: bool = True):
+    """Launch BPTT. Returns (dgx [T, N, gstride] bf16 (x dgx_scale), dgh [ndir, steps, NP, G*H],
+    parts [k, ndir, BG, G*H] fp32 in-kernel bias-gradient partials: k=0 input bias, k=1 GRU
+    recurrent bias; None if want_bias is False)."""
+    C = _ext.ext()
+    T, N, H = dy.shape
+    ndir, G = plan.ndir, GATES[plan.cell]
+    steps = T
+    dev = dy.device
+    d1 = ndir == 2
+    dy = dy.to(torch.bfloat16).contiguous()
+    dgh = torch.empty(ndir, steps, plan.NP, G * H, device=dev, dtype=torch.bfloat16)
+    dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
+    carry = None if plan.persistent else torch.zeros(ndir, plan.NP, H, device=dev, dtype=torch.float32)
+    flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
+    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    parts = torch.zeros(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
+                        dtype=torch.float32) if want_bias else None
+    has_g = gates.numel() > 0
+    C.rnn_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
+              gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
+              dgh[0], dgh[1] if d1 else None, dgx,
+              carry[0] if carry is not None else None,
+              carry[1] if (carry is not None and d1) else None,
+              flags, err, T, N, plan.NP, H, plan.BG, steps, gstride, ndir,
+              CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS,
+              _stamps("bwd", plan, flags.numel(), dev),
+              parts[0] if parts is not None else None,
+              parts[1] if (parts is not None and plan.cell == "gru") else None,
+              float(dgx_scale))
+    _pending_errors.append(err)
+    return dgx, dgh, parts
+
+
+def _dU(dgh, hx, d: int, plan: RnnPlan, p_U):
+    steps = dgh.shape[1]
+    G = GATES[plan.cell]
+    g2 = dgh[d].view(steps * plan.NP, G * plan.H)
+    h2 = hx[d, :steps].reshape(steps * plan.NP, plan.H)
+    return mm_into(p_U, g2.t(), h2)
+
+
 class BiRecurrence(torch.autograd.Function):
-    """y = sum_d recurrence_d(gx[..., d]) over a [T, N, ndir*G*H] bf16 projection."""
+    """y = sum_d recurrence_d(gx[..., d]) over a [T, N, ndir*G*H] bf16 projection.
+    Used when the projection needs autograd of its own (sequence-BN in batch mode)."""
 
     @staticmethod
     def forward(ctx, gx, lens, U_f, U_b, bh_f, bh_b, plan: RnnPlan):
-        C = _ext.ext()
-        T, N, gstride = gx.shape
-        H, ndir, G = plan.H, plan.ndir, GATES[plan.cell]
-        steps = T
-        dev = gx.device
         gx = gx.contiguous()
-        lens = lens.to(device=dev, dtype=torch.int32).contiguous()
-        U_f = U_f.contiguous()
-        U_b = U_b.contiguous() if U_b is not None else None
-        bf16 = torch.bfloat16
-        y2 = torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
-        hx = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=bf16)
-        hx[:, 0].zero_()                         # h0
-        hs = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=torch.float32)
-        hs[:, 0].zero_()
-        gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
-                 if plan.cell == "gru" else None)
-        flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
-        err = torch.zeros(1, device=dev, dtype=torch.int32)
-        d1 = ndir == 2
-        C.rnn_fwd(gx, lens, U_f, U_b if d1 else None,
-                  bh_f.contiguous().float() if bh_f is not None else None,
-                  bh_b.contiguous().float() if (bh_b is not None and d1) else None,
-                  y2[0], y2[1] if d1 else None, hx[0], hx[1] if d1 else None,
-                  hs[0], hs[1] if d1 else None,
-                  gates[0] if gates is not None else None,
-                  gates[1] if (gates is not None and d1) else None,
-                  flags, err, T, N, plan.NP, H, plan.BG, steps, gstride, ndir,
-                  CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS,
-                  _stamps("fwd", plan, flags.numel(), dev))
-        _pending_errors.append(err)
-        y = y2[0] + y2[1] if d1 else y2[0]
-        ctx.save_for_backward(lens, U_f, U_b if U_b is not None else torch.empty(0, device=dev),
-                              hx, hs, gates if gates is not None else torch.empty(0, device=dev))
+        lens = lens.to(device=gx.device, dtype=torch.int32).contiguous()
+        U = [U_f.contiguous(), U_b.contiguous() if U_b is not None else None]
+        bh = [b.contiguous().float() if b is not None else None for b in (bh_f, bh_b)]
+        y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
+        ctx.save_for_backward(lens, U[0], U[1] if U[1] is not None else torch.empty(0, device=gx.device),
+                              hx, hs, gates)
         ctx.plan = plan
-        ctx.shape = (T, N, gstride, steps)
+        ctx.gstride = gx.shape[2]
         ctx.has_bh = (bh_f is not None, bh_b is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        C = _ext.ext()
         lens, U_f, U_b, hx, hs, gates = ctx.saved_tensors
         plan: RnnPlan = ctx.plan
-        T, N, gstride, steps = ctx.shape
-        H, ndir, G = plan.H, plan.ndir, GATES[plan.cell]
-        dev = dy.device
-        d1 = ndir == 2
-        dy = dy.to(torch.bfloat16).contiguous()
-        dgh = torch.empty(ndir, steps, plan.NP, G * H, device=dev, dtype=torch.bfloat16)
-        dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
-        carry = None if plan.persistent else torch.zeros(ndir, plan.NP, H, device=dev, dtype=torch.float32)
-        flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
-        err = torch.zeros(1, device=dev, dtype=torch.int32)
-        has_g = gates.numel() > 0
-        C.rnn_bwd(dy, lens, U_f, U_b if d1 else None, hs[0], hs[1] if d1 else None,
-                  gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
-                  dgh[0], dgh[1] if d1 else None, dgx,
-                  carry[0] if carry is not None else None,
-                  carry[1] if (carry is not None and d1) else None,
-                  flags, err, T, N, plan.NP, H, plan.BG, steps, gstride, ndir,
-                  CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS,
-                  _stamps("bwd", plan, flags.numel(), dev))
-        _pending_errors.append(err)
-        grads_U, grads_b = [], []
-        for d in range(ndir):
-            g2 = dgh[d].view(steps * plan.NP, G * H)
-            h2 = hx[d, :steps].reshape(steps * plan.NP, H)
-            grads_U.append(_mm_f32(g2.t(), h2))
-            grads_b.append(g2.sum(0, dtype=torch.float32) if ctx.has_bh[d] else None)
-        dU_f = grads_U[0].to(U_f.dtype)
-        dU_b = grads_U[1].to(U_f.dtype) if d1 else None
-        return (dgx, None, dU_f, dU_b, grads_b[0], grads_b[1] if d1 else None, None)
+        d1 = plan.ndir == 2
+        dgx, dgh, parts = _run_bwd(dy, lens, [U_f, U_b if d1 else None], hx, hs, gates, plan, ctx.gstride,
+                                   want_bias=any(ctx.has_bh))
+        dbh = parts[1].sum(1) if parts is not None and parts.shape[0] > 1 else None
+        dU = [_dU(dgh, hx, d, plan, None) for d in range(plan.ndir)]
+        gb = [dbh[d] if (dbh is not None and ctx.has_bh[d]) else None for d in range(plan.ndir)]
+        return (dgx, None, dU[0].to(U_f.dtype), dU[1].to(U_f.dtype) if d1 else None,
+                gb[0], gb[1] if d1 else None, None)
+
+
+def _bf16_group(params):
+    """bf16 tensor for the row-concatenation of ``params`` (all 2-D with equal columns, or
+    all 1-D): a zero-copy view of the arena's bf16 shadow when they are packed there."""
+    arena = arena_of(params[0])
+    if arena is not None:
+        v = arena.group_view(params, "p16")
+        if v is not None:
+            if params[0].dim() == 1:
+                return v
+            return v.view(-1, params[0].shape[1])
+    return torch.cat([p.to(torch.bfloat16) for p in params], 0)
+
+
+def _bf16(p):
+    return p.bf16 if arena_of(p) is not None else p.to(torch.bfloat16)
+
+
+def _bias_grads(params, part):
+    """Reduce in-kernel partials [ndir, BG, G*H] over batch groups into the bias grads:
+    one sum kernel writing straight into the packed arena rows when the direction biases
+    are adjacent there; otherwise per-direction (returned for autograd if not arena-managed)."""
+    out = [None, None]
+    if params[0] is None:
+        return out
+    arena = arena_of(params[0])
+    if arena is not None and all(arena.first_write(p) for p in params):
+        grp = arena.group_view(params, "grad")
+        if grp is not None:
+            torch.sum(part, dim=1, out=grp.view(len(params), -1))
+            arena.grad_done(*params)
+            return out
+    for d, p in enumerate(params):
+        out[d] = emit_grad(p, part[d].sum(0))
+    return out
+
+
+class FusedBiLayer(torch.autograd.Function):
+    """One whole (bi)directional recurrent layer with manual backward.
+
+    forward:  gx = alpha * x [W_fw; W_bw]^T + [b_fw; b_bw]     (one GEMM, bf16 out)
+              y  = sum_d recurrence_d(gx_d)                     (persistent kernel)
+    backward: dgx (pre-scaled by alpha), db, db_h               (BPTT kernel, bias sums in-kernel)
+              dx = dgx [W_fw; W_bw]                             (critical path: feeds layer below)
+              dW = dgx^T x, dU_d = dgh_d^T h_d                  (fp32 straight into main_grad)
+    alpha = 1/sqrt(1+eps) folds the reference's frozen sequence-BN (quirk Q3); 1 for 'none'.
+    """
+
+    @staticmethod
+    def forward(ctx, x, lens, plan: RnnPlan, alpha: float, W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b):
+        T, N, D = x.shape
+        dirs_W = [W_f] + ([W_b] if W_b is not None else [])
+        dirs_b = [b_f] + ([b_b] if b_b is not None else [])
+        W16 = _bf16_group(dirs_W)                     # [ndir*G*H, D]
+        b16 = _bf16_group(dirs_b)                     # [ndir*G*H]
+        x16 = x.to(torch.bfloat16).contiguous()
+        x2 = x16.view(T * N, D)
+        gx = torch.addmm(b16, x2, W16.t(), alpha=alpha).view(T, N, -1)
+        lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
+        U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
+        bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
+        y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
+        dev = x.device
+        ctx.save_for_backward(x16, lens, W16, U[0], U[1] if U[1] is not None else torch.empty(0, device=dev),
+                              hx, hs, gates)
+        ctx.params = (W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b)
+        ctx.plan = plan
+        ctx.alpha = alpha
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x16, lens, W16, U_f16, U_b16, hx, hs, gates = ctx.saved_tensors
+        plan: RnnPlan = ctx.plan
+        W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b = ctx.params
+        d1 = plan.ndir == 2
+        T, N, D = x16.shape
+        GH = GATES[plan.cell] * plan.H
+        dgx, dgh, parts = _run_bwd(dy, lens, [U_f16, U_b16 if d1 else None], hx, hs, gates, plan,
+                                   plan.ndir * GH, dgx_scale=ctx.alpha)
+        dgx2 = dgx.view(T * N, plan.ndir * GH)
+        dx = torch.mm(dgx2, W16).view(T, N, D) if ctx.needs_input_grad[0] else None
+        # ---- weight gradients (off the critical path) ----
+        x2 = x16.view(T * N, D)
+        arena = arena_of(W_f)
+        gW = [None, None]
+        grp = arena.group_view([W_f, W_b] if d1 else [W_f], "grad") if arena is not None else None
+        if grp is not None and arena.first_write(W_f) and (not d1 or arena.first_write(W_b)):
+            mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
+            arena.grad_done(W_f, W_b if d1 else None)
+        else:
+            for d, p in enumerate([W_f, W_b] if d1 else [W_f]):
+                g = mm_into(p, dgx2[:, d * GH:(d + 1) * GH].t(), x2)
+                if g is None:
+                    arena.grad_done(p)
+                gW[d] = g
+        gU = [None, None]
+        for d, p in enumerate([U_f, U_b] if d1 else [U_f]):
+            g = _dU(dgh, hx, d, plan, p)
+            if g is None:
+                arena.grad_done(p)
+            gU[d] = g
+        gb = _bias_grads([b_f, b_b] if d1 else [b_f], parts[0])
+        gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
+        return (dx, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
 
 
 _plan_cache = {}
@@ -261,12 +397,19 @@ def input_projection_hip(layer, x: torch.Tensor, lens: torch.Tensor) -> torch.Te
 
 
 def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
-    x = x.to(torch.bfloat16)
     ndir = 2 if layer.bw is not None else 1
     plan = plan_for(x.shape[1], layer.hidden, layer.cell, ndir, x.device)
+    fw, bw = layer.fw, layer.bw
+    if layer.seq_bn in ("frozen", "none"):
+        alpha = sbn_scale() if layer.seq_bn == "frozen" else 1.0
+        return FusedBiLayer.apply(x, lens, plan, alpha, fw.W, bw.W if bw is not None else None,
+                                  fw.U, bw.U if bw is not None else None,
+                                  fw.b, bw.b if bw is not None else None,
+                                  fw.b_h, bw.b_h if bw is not None else None)
+    x = x.to(torch.bfloat16)
     gx = input_projection_hip(layer, x, lens)
-    U_f = layer.fw.U.to(torch.bfloat16)
-    U_b = layer.bw.U.to(torch.bfloat16) if ndir == 2 else None
-    bh_f = layer.fw.b_h if layer.cell == "gru" else None
-    bh_b = layer.bw.b_h if (layer.cell == "gru" and ndir == 2) else None
+    U_f = fw.U.to(torch.bfloat16)
+    U_b = bw.U.to(torch.bfloat16) if ndir == 2 else None
+    bh_f = fw.b_h if layer.cell == "gru" else None
+    bh_b = bw.b_h if (layer.cell == "gru" and ndir == 2) else None
     return BiRecurrence.apply(gx, lens, U_f, U_b, bh_f, bh_b, plan)

@@ -61,16 +61,23 @@ class GradBucketer:
         self._handles = []
         self.enabled = self.world > 1
         if self.enabled:
+            # autograd-accumulated grads fire the tensor hook; fused ops that write
+            # main_grad directly report through the arena
             for i, p in enumerate(arena.params):
                 self._handles.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            if hasattr(arena, "on_grad_ready"):
+                arena.on_grad_ready(self._ready)
         self.prepare()
+
+    def _ready(self, i: int) -> None:
+        b = self.param_bucket[i]
+        self._pending[b] -= 1
+        if self._pending[b] == 0:
+            self._launch(b)
 
     def _make_hook(self, i: int):
         def hook(_p):
-            b = self.param_bucket[i]
-            self._pending[b] -= 1
-            if self._pending[b] == 0:
-                self._launch(b)
+            self._ready(i)
         return hook
 
     def prepare(self) -> None:

@@ -50,13 +50,15 @@ class Trainer:
                  world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
                  nan_policy: str = "abort", collapse_repeated: bool = False):
         self.model = model
-        self.arena = ParamArena(model)
+        # bf16 compute shadows of the weights only for the HIP engine (fused ops read them)
+        self.arena = ParamArena(model, bf16_shadow=(model.engine == "hip"))
         self.opt = FusedAdamEMA(self.arena, lr=lr_schedule.initial_lr, ema_decay=moving_avg_decay)
         self.lr_schedule = lr_schedule
         self.world = world_size
         self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb, compress_bf16=allreduce_bf16)
         if world_size > 1:
             broadcast_params(self.arena)
+            self.arena.mark_dirty()
             if self.opt.ema is not None:
                 self.opt.ema.copy_(self.arena.flat)
         self.global_step = 0
@@ -72,6 +74,7 @@ class Trainer:
     def step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         model = self.model
         model.train()
+        self.arena.ensure_bf16()
         self.arena.zero_grad()
         logits, lens = model(batch["feats"], batch["seq_lens"])
         loss = model.loss(logits, lens, batch["labels"], batch["label_lens"])
@@ -101,3 +104,4 @@ class Trainer:
         tmp = self.arena.flat.clone()
         self.arena.flat.copy_(self.opt.ema)
         self.opt.ema.copy_(tmp)
+        self.arena.mark_dirty()

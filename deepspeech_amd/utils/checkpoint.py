@@ -250,6 +250,7 @@ def restore(trainer, directory_or_file: str) -> Optional[int]:
     tensors = {k: v for k, v in data.items() if isinstance(v, torch.Tensor)}
     load_model_from_tf(trainer.model, tensors, strict=True)
     _load_arena_slots(trainer, tensors)
+    trainer.arena.mark_dirty()
     step = int(data.get("global_step", step_from_path(path)))
     trainer.global_step = step + 1 if data.get("format") else step
     trainer.opt.t = int(data.get("adam_t", step + 1))

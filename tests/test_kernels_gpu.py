@@ -119,6 +119,29 @@ def test_ctc_fused(cuda, dtype):
     assert _rel(x.grad, xr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("Lmax,T", [(60, 150), (150, 241), (300, 700)])
+def test_ctc_long_labels(cuda, Lmax, T):
+    """Lattices of 121..601 states: every register-tile width of the one-wave recursion."""
+    from deepspeech_amd.ops import ctc as CTC
+    torch.manual_seed(1)
+    N, K = 5, 29
+    logits = (torch.randn(T, N, K) * 1.5).bfloat16().to(cuda)
+    lens = torch.tensor([T, T - 7, T - 30, T, T - 1], dtype=torch.int32)
+    Ls = [Lmax, Lmax - 3, Lmax // 2, 1, Lmax - 1]
+    labels = torch.zeros(N, Lmax, dtype=torch.int32)
+    for b, L in enumerate(Ls):
+        labels[b, :L] = torch.randint(0, K - 1, (L,))
+    lab_lens = torch.tensor(Ls, dtype=torch.int32)
+    x = logits.clone().requires_grad_(True)
+    loss = CTC.ctc_loss_hip(x, lens.to(cuda), labels.to(cuda), lab_lens.to(cuda))
+    loss.mean().backward()
+    xr = logits.float().clone().requires_grad_(True)
+    lr = R.ctc_loss_ref(xr, labels.to(cuda), lens.to(cuda), lab_lens.to(cuda))
+    lr.mean().backward()
+    assert torch.allclose(loss, lr, rtol=1e-3, atol=1e-2), (loss, lr)
+    assert _rel(x.grad, xr.grad) < 2e-2
+
+
 def test_ctc_infeasible_zero(cuda):
     from deepspeech_amd.ops import ctc as CTC
     T, N, K = 4, 1, 29
