@@ -50,6 +50,30 @@ int ds2_rnn_bwd(const DS2RnnBwd* d, hipStream_t st);
 int ds2_rnn_fwd_stamps(const DS2RnnFwd* d, hipStream_t st);
 int ds2_rnn_bwd_stamps(const DS2RnnBwd* d, hipStream_t st);
 int ds2_rnn_kpw(int H, int G, int nw, int fwd);
+struct DS2RnnX {
+  int T, N, NP, H, BG, R, steps, gstride, ndir, cell, mt, xcd_map, knobs;
+  const int* lens;
+  const void* gx;
+  const void* U[2];
+  const float* bh[2];
+  void* y[2];
+  void* ex[2];
+  float* hsave[2];
+  float* gates[2];
+  void* dgx;
+  float* dbx_part[2];
+  float* dbh_part[2];
+  float dgx_scale;
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+  unsigned long long* stamps;
+};
+int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st);
+int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st);
+int ds2_rnnx_grid(int H, int ngroups, int xcd_map);
+int ds2_rnnx_kb(int H, int G, int fwd);
+size_t ds2_rnnx_smem(int H, int G, int mt, int fwd);
 int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const int* labels, const int* label_lens,
                   float* loss, void* grad, float* ws, int T, int N, int K, int Lmax, int blank, int zero_inf,
                   hipStream_t st);
@@ -113,6 +137,7 @@ void rnn_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_f
   d.mt = (int)mt; d.persistent = persistent ? 1 : 0;
   TORCH_CHECK(NP == BG * 16 * mt, "NP must equal BG*16*mt");
   TORCH_CHECK(hx_f.numel() >= (steps + 1) * NP * H, "hx too small");
+  d.stamps = ptr_or_null<unsigned long long>(stamps, "stamps");
   d.lens = lens.data_ptr<int>();
   d.gx = gx.data_ptr();
   d.U[0] = U_f.data_ptr();
@@ -181,6 +206,102 @@ void rnn_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tenso
 }
 
 int64_t rnn_kpw(int64_t H, int64_t G, int64_t nw, bool fwd) { return ds2_rnn_kpw((int)H, (int)G, (int)nw, fwd ? 1 : 0); }
+
+// ---- generation-2 recurrence (XCD-local groups, sentinel hand-off): csrc/rnn_xcd.hip
+DS2RnnX rnnx_desc(int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t R, int64_t steps, int64_t gstride,
+                  int64_t ndir, int64_t cell, int64_t mt, at::Tensor census, at::Tensor err, int64_t timeout,
+                  int64_t xcd_map, int64_t knobs) {
+  TORCH_CHECK(H % 32 == 0, "H must be a multiple of 32");
+  TORCH_CHECK(NP == BG * R && R >= 1 && R <= 16 * mt && (mt == 1 || mt == 2), "bad row tiling");
+  const int64_t ngroups = ndir * BG;
+  TORCH_CHECK(census.numel() >= ngroups * (H / 32) && census.scalar_type() == at::kInt, "census too small");
+  need_gpu(census, "census");
+  DS2RnnX d{};
+  d.T = (int)T; d.N = (int)N; d.NP = (int)NP; d.H = (int)H; d.BG = (int)BG; d.R = (int)R; d.steps = (int)steps;
+  d.gstride = (int)gstride; d.ndir = (int)ndir; d.cell = (int)cell; d.mt = (int)mt;
+  d.xcd_map = (int)xcd_map; d.knobs = (int)knobs;
+  d.census = reinterpret_cast<unsigned*>(census.data_ptr<int>());
+  d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  d.timeout = timeout;
+  d.dgx_scale = 1.f;
+  return d;
+}
+
+void rnnx_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_f, OptT bh_b, at::Tensor y_f,
+              OptT y_b, at::Tensor hx_f, OptT hx_b, at::Tensor hs_f, OptT hs_b, OptT gates_f, OptT gates_b,
+              at::Tensor census, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t R,
+              int64_t steps, int64_t gstride, int64_t ndir, int64_t cell, int64_t mt, int64_t timeout,
+              int64_t xcd_map, int64_t knobs, OptT stamps) {
+  need_gpu(gx, "gx");
+  TORCH_CHECK(gx.scalar_type() == at::kBFloat16 && gx.numel() >= T * N * gstride, "gx must be bf16 [T, N, gstride]");
+  TORCH_CHECK(lens.scalar_type() == at::kInt && lens.numel() == N, "lens must be int32 [N]");
+  TORCH_CHECK(hx_f.numel() >= (steps + 1) * NP * H && hs_f.numel() >= (steps + 1) * NP * H, "state buffers too small");
+  DS2RnnX d = rnnx_desc(T, N, NP, H, BG, R, steps, gstride, ndir, cell, mt, census, err, timeout, xcd_map, knobs);
+  d.stamps = ptr_or_null<unsigned long long>(stamps, "stamps");
+  d.lens = lens.data_ptr<int>();
+  d.gx = gx.data_ptr();
+  d.U[0] = U_f.data_ptr();
+  d.U[1] = U_b.has_value() ? U_b->data_ptr() : nullptr;
+  d.bh[0] = ptr_or_null<const float>(bh_f, "bh_f");
+  d.bh[1] = ptr_or_null<const float>(bh_b, "bh_b");
+  d.y[0] = y_f.data_ptr();
+  d.y[1] = ptr_or_null<void>(y_b, "y_b");
+  d.ex[0] = hx_f.data_ptr();
+  d.ex[1] = ptr_or_null<void>(hx_b, "hx_b");
+  d.hsave[0] = hs_f.data_ptr<float>();
+  d.hsave[1] = ptr_or_null<float>(hs_b, "hs_b");
+  d.gates[0] = ptr_or_null<float>(gates_f, "gates_f");
+  d.gates[1] = ptr_or_null<float>(gates_b, "gates_b");
+  TORCH_CHECK(ndir == 1 || (d.U[1] && d.y[1] && d.ex[1] && d.hsave[1]), "backward-direction buffers missing");
+  TORCH_CHECK(cell == 0 || (d.gates[0] && (ndir == 1 || d.gates[1])), "GRU needs gate buffers");
+  check(ds2_rnnx_fwd(&d, cur_stream()), "rnnx_fwd");
+}
+
+void rnnx_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tensor hs_f, OptT hs_b, OptT gates_f,
+              OptT gates_b, at::Tensor dgh_f, OptT dgh_b, at::Tensor dgx, OptT dbx_part, OptT dbh_part,
+              double dgx_scale, at::Tensor census, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H,
+              int64_t BG, int64_t R, int64_t steps, int64_t gstride, int64_t ndir, int64_t cell, int64_t mt,
+              int64_t timeout, int64_t xcd_map, int64_t knobs, OptT stamps) {
+  need_gpu(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dgx.scalar_type() == at::kBFloat16, "dy/dgx must be bf16");
+  TORCH_CHECK(dgx.numel() >= T * N * gstride && dy.numel() >= T * N * H, "dy/dgx too small");
+  const int64_t G = cell == 1 ? 3 : 1;
+  TORCH_CHECK(dgh_f.numel() >= steps * NP * G * H, "dgh too small");
+  DS2RnnX d = rnnx_desc(T, N, NP, H, BG, R, steps, gstride, ndir, cell, mt, census, err, timeout, xcd_map, knobs);
+  d.stamps = ptr_or_null<unsigned long long>(stamps, "stamps");
+  d.lens = lens.data_ptr<int>();
+  d.gx = dy.data_ptr();
+  d.U[0] = U_f.data_ptr();
+  d.U[1] = U_b.has_value() ? U_b->data_ptr() : nullptr;
+  d.hsave[0] = hs_f.data_ptr<float>();
+  d.hsave[1] = ptr_or_null<float>(hs_b, "hs_b");
+  d.gates[0] = ptr_or_null<float>(gates_f, "gates_f");
+  d.gates[1] = ptr_or_null<float>(gates_b, "gates_b");
+  d.ex[0] = dgh_f.data_ptr();
+  d.ex[1] = ptr_or_null<void>(dgh_b, "dgh_b");
+  d.dgx = dgx.data_ptr();
+  float* bx = ptr_or_null<float>(dbx_part, "dbx_part");
+  float* bh = ptr_or_null<float>(dbh_part, "dbh_part");
+  if (bx) TORCH_CHECK(dbx_part->numel() == ndir * BG * G * H && dbx_part->scalar_type() == at::kFloat, "dbx_part must be fp32 [ndir, BG, G*H]");
+  if (bh) TORCH_CHECK(dbh_part->numel() == ndir * BG * G * H && dbh_part->scalar_type() == at::kFloat, "dbh_part must be fp32 [ndir, BG, G*H]");
+  for (int i = 0; i < 2; ++i) {
+    d.dbx_part[i] = (bx && i < ndir) ? bx + (size_t)i * BG * G * H : nullptr;
+    d.dbh_part[i] = (bh && i < ndir) ? bh + (size_t)i * BG * G * H : nullptr;
+  }
+  d.dgx_scale = (float)dgx_scale;
+  TORCH_CHECK(ndir == 1 || (d.U[1] && d.hsave[1] && d.ex[1]), "backward-direction buffers missing");
+  check(ds2_rnnx_bwd(&d, cur_stream()), "rnnx_bwd");
+}
+
+py::dict rnnx_info(int64_t H, int64_t G, int64_t mt, int64_t ngroups, int64_t xcd_map) {
+  py::dict d;
+  d["grid"] = ds2_rnnx_grid((int)H, (int)ngroups, (int)xcd_map);
+  d["kb_fwd"] = ds2_rnnx_kb((int)H, (int)G, 1);
+  d["kb_bwd"] = ds2_rnnx_kb((int)H, (int)G, 0);
+  d["smem_fwd"] = (int64_t)ds2_rnnx_smem((int)H, (int)G, (int)mt, 1);
+  d["smem_bwd"] = (int64_t)ds2_rnnx_smem((int)H, (int)G, (int)mt, 0);
+  return d;
+}
 
 // --------------------------------------------------------------------------- CTC
 int64_t ctc_ws_floats(int64_t T, int64_t N, int64_t Lmax) { return ds2_ctc_ws_floats((int)T, (int)N, (int)Lmax); }
@@ -307,6 +428,19 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stamps") = py::none(), py::arg("dbx_part") = py::none(), py::arg("dbh_part") = py::none(),
         py::arg("dgx_scale") = 1.0);
   m.def("rnn_kpw", &rnn_kpw);
+  m.def("rnnx_fwd", &rnnx_fwd, py::arg("gx"), py::arg("lens"), py::arg("U_f"), py::arg("U_b"), py::arg("bh_f"),
+        py::arg("bh_b"), py::arg("y_f"), py::arg("y_b"), py::arg("hx_f"), py::arg("hx_b"), py::arg("hs_f"),
+        py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("census"), py::arg("err"), py::arg("T"),
+        py::arg("N"), py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("R"), py::arg("steps"), py::arg("gstride"),
+        py::arg("ndir"), py::arg("cell"), py::arg("mt"), py::arg("timeout"), py::arg("xcd_map"), py::arg("knobs"),
+        py::arg("stamps") = py::none());
+  m.def("rnnx_bwd", &rnnx_bwd, py::arg("dy"), py::arg("lens"), py::arg("U_f"), py::arg("U_b"), py::arg("hs_f"),
+        py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("dgh_f"), py::arg("dgh_b"), py::arg("dgx"),
+        py::arg("dbx_part"), py::arg("dbh_part"), py::arg("dgx_scale"), py::arg("census"), py::arg("err"),
+        py::arg("T"), py::arg("N"), py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("R"), py::arg("steps"),
+        py::arg("gstride"), py::arg("ndir"), py::arg("cell"), py::arg("mt"), py::arg("timeout"), py::arg("xcd_map"),
+        py::arg("knobs"), py::arg("stamps") = py::none());
+  m.def("rnnx_info", &rnnx_info);
   m.def("ctc_fused", &ctc_fused);
   m.def("ctc_ws_floats", &ctc_ws_floats);
   m.def("bn_chunks", &bn_chunks);

@@ -20,8 +20,10 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return (bf16_t)(u >> 16);
 }
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float tanhf_(float x) { return 1.0f - 2.0f / (__expf(2.0f * x) + 1.0f); }
+// v_exp_f32 + v_rcp_f32 (1 ulp): the IEEE-correct division would add a 10-instruction
+// div_scale/div_fmas/div_fixup sequence per call on the recurrence's critical path
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f); }
 
 // Buffer resource over [base, base+bytes) — wave-uniform inputs only (T8/T20).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
@@ -44,6 +46,11 @@ __device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
 __device__ __forceinline__ void st_flag(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Workgroup barrier that orders LDS only. __syncthreads() also emits s_waitcnt vmcnt(0),
+// which makes every wave wait for ALL its outstanding global loads and stores at the
+// barrier — fatal for a wave that keeps prefetches in flight across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -1,0 +1,917 @@
+// Persistent bidirectional recurrence, generation 2: XCD-local groups + sentinel hand-off.
+//
+// Reference behaviour: src/custom_ops.py:36-96 (CustomRNNCell2 + stacked_brnn through
+// tf.nn.bidirectional_dynamic_rnn: outputs zero past each length, the backward direction
+// reversed within each utterance, directions summed by the caller). Same buffers and
+// numerics as rnn_persistent.hip (generation 1, kept as the step-mode fallback); what
+// changed is how the per-step state crosses workgroups, measured with
+// tools/exchange_bench.hip on MI355X (all-gather of one step, no math):
+//
+//   gen-1: 4 groups x 50 WGs, flag per producer, sc1 payload      4.4 us/step
+//   gen-2: 8 groups x 25 WGs, sentinel payload, XCD-local, plain   1.1 us/step
+//
+//  * Group = (direction, batch group of R <= 16*MT rows); a workgroup owns UPW = 32 hidden
+//    units of its group (all gates), so a group is P = H/32 workgroups. With <= 8 groups,
+//    group = blockIdx % 8: under the observed round-robin dispatch a group then shares
+//    ONE XCD, its exchange stays in that XCD's L2, and its producers can store plain
+//    (L2-resident) instead of write-through. Placement is never assumed: a start-up census
+//    (every member publishes its HW_REG_XCC_ID) decides per group; a group that straddles
+//    XCDs stores write-through (sc1), which is correct for any placement.
+//  * Sentinel hand-off: the exchange buffer (one slot per step, never reused within a
+//    launch) is pre-filled with 0xFFFF (a bf16 NaN that the producers never store: NaN
+//    results are canonicalised to 0x7FC0). Producers store 16-B granules and move on: no
+//    drain, no flag. Consumers load each granule with sc1 (L1-bypassing) loads and spin on
+//    it until none of its 8 halves is the sentinel, staging it in LDS. 16-B stores were
+//    observed untorn on gfx950; checking all 8 halves keeps the protocol correct even if
+//    a granule landed in pieces (a half is only ever sentinel or final).
+//  * Forward: gh = h_{t-1} . U^T (M = rows, N = 3*32, K = H) with U's slice resident in
+//    VGPRs as MFMA B fragments; one wave per 16-column N-tile runs the whole K from the
+//    LDS A tile, so there is no cross-wave reduction.
+//  * Backward (BPTT): dh = dgh_{t+1} . U[:, slice] (N = 32, K = 3H) with U's columns
+//    resident, K split over the 8 waves, reduced through LDS.
+//  * Every spin is bounded by an s_memrealtime timeout that sets an error word and
+//    aborts the launch, so a grid that is not co-resident cannot hang the GPU.
+#include "common.h"
+
+using namespace ds2;
+
+namespace {
+
+constexpr int CELL_RELU = 0;
+constexpr int CELL_GRU = 1;
+constexpr float RELU_CAP = 20.0f;
+constexpr int UPW = 32;          // hidden units per workgroup
+constexpr int NWV = 8;           // waves per workgroup
+constexpr int NTH = NWV * 64;
+
+struct XFwd {
+  int T, N, NP, H, P, BG, R, steps, gstride, ngroups, xcd_map, knobs;
+  const int* lens;
+  const bf16_t* gx;
+  const bf16_t* U[2];
+  const float* bh[2];
+  bf16_t* y[2];
+  bf16_t* hx[2];          // [steps+1][NP][H]: slot 0 = h0, slots 1.. pre-filled with sentinel
+  float* hsave[2];
+  float* gates[2];
+  unsigned* census;       // [ngroups * P] pre-filled 0xFFFFFFFF
+  unsigned* err;
+  long long timeout;
+  unsigned long long* stamps;   // optional [grid][8] phase cycle sums (diagnostics)
+};
+
+struct XBwd {
+  int T, N, NP, H, P, BG, R, steps, gstride, ngroups, xcd_map, knobs;
+  const int* lens;
+  const bf16_t* dy;
+  const bf16_t* U[2];
+  const float* hsave[2];
+  const float* gates[2];
+  bf16_t* dgh[2];         // [steps][NP][G*H] pre-filled with sentinel
+  bf16_t* dgx;
+  float* dbx_part[2];     // [BG][G*H]
+  float* dbh_part[2];
+  float dgx_scale;
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+  unsigned long long* stamps;
+};
+
+// Phase stamps (diagnostics; a null stamps pointer costs one uniform branch per phase).
+struct Stamps {
+  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long prev = 0;
+  bool on;
+  __device__ explicit Stamps(bool o) : on(o) {}
+  __device__ __forceinline__ void mark(int i) {
+    if (!on) return;
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    if (prev && i >= 0) acc[i] += t - prev;
+    prev = t;
+  }
+  __device__ __forceinline__ void store(unsigned long long* dst, int base) {
+    if (!on) return;
+    for (int k = 0; k < 6; ++k) dst[(size_t)blockIdx.x * 8 + base + k] = acc[k];
+  }
+};
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xf;
+}
+
+// bf16 rounding that never produces the sentinel 0xFFFF (any NaN -> canonical 0x7FC0)
+__device__ __forceinline__ bf16_t f2bf_x(float f) {
+  const bf16_t b = f2bf(f);
+  return ((b & 0x7f80u) == 0x7f80u && (b & 0x7fu)) ? (bf16_t)0x7fc0 : b;
+}
+
+__device__ __forceinline__ bool granule_ready(i32x4 v) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned w = (unsigned)v[i];
+    ok = ok && ((w & 0xffffu) != 0xffffu) && ((w >> 16) != 0xffffu);
+  }
+  return ok;
+}
+
+__device__ __forceinline__ void store_granule(bool plain, __amdgpu_buffer_rsrc_t rs, bf16_t* base, unsigned off,
+                                              i32x4 v) {
+  if (plain) {
+    *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(base) + off) = v;
+  } else {
+    store_sc1_b128(rs, off, v);
+  }
+}
+
+// Group role. xcd_map (host-chosen: <= 8 groups of <= CUs/8 members): group =
+// blockIdx % 8, so under round-robin dispatch a group shares one XCD; otherwise groups
+// are contiguous block ranges. Returns false for surplus blocks (no role).
+__device__ __forceinline__ bool take_role(int xcd_map, int ngroups, int P, int& grp, int& mem) {
+  if (xcd_map) {
+    const int slot = blockIdx.x & 7;
+    if (slot >= ngroups) return false;
+    grp = slot;
+    mem = blockIdx.x >> 3;
+  } else {
+    grp = blockIdx.x / P;
+    mem = blockIdx.x % P;
+  }
+  return mem < P;
+}
+
+// Every member of the group publishes its XCC id; the group is "local" iff all agree.
+// Runs on wave 0; returns 1 (local), 0 (spread) or -1 (timeout).
+__device__ int group_census(unsigned* census, int grp, int mem, int P, long long timeout, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  unsigned* c = census + (size_t)grp * P;
+  if (lane == 0) __hip_atomic_store(c + mem, xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+    bool ready = true;
+    unsigned first = 0xffffffffu;
+    bool same = true;
+    for (int q = lane; q < P; q += 64) {
+      const unsigned v = __hip_atomic_load(c + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ready = ready && (v != 0xffffffffu);
+      if (q == lane) first = v;
+      same = same && (v == first);
+    }
+    if (__all(ready)) {
+      const unsigned x0 = __shfl(first, 0, 64);
+      const bool all_same = __all(same && (lane >= P || first == x0));
+      return all_same ? 1 : 0;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+      if (lane == 0) atomicOr(err, 2u);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Workgroup roles (8 waves):
+//   waves 0..6  gather the step's exchange vector into the LDS A tile (batched sc1 loads,
+//               per-granule sentinel spin);
+//   waves 0..3  cell epilogue (EPT elements each) + the critical 16-B exchange stores;
+//   wave  7     memory wave: prefetches the per-step inputs two steps ahead into an LDS
+//               ring and stores the per-step outputs from an LDS staging area. Its loads
+//               and stores never sit in another wave's vmcnt queue (vmcnt retires in
+//               order per wave), so the gather's waits see only the gather's loads.
+// Three barriers per step: after the gather (#1), after the MFMA phase (#2), and the
+// epilogue runs into the next gather (its LDS use is wave-local).
+// ------------------------------------------------------------------------------------
+constexpr int EW = 4;             // epilogue waves
+constexpr int ETH = EW * 64;
+constexpr int GW = 7;             // gather waves
+constexpr int GTH = GW * 64;
+constexpr int MEMW = 7;           // memory wave
+
+// Batched sentinel gather of NGR 16-B granules (row-major, GPR per row) into LDS rows of
+// pitch LP elements. Returns false on timeout.
+template <int GMAX>   // granules in flight per thread
+__device__ __forceinline__ bool gather_tile(__amdgpu_buffer_rsrc_t rs, size_t base_elem, int row_stride, int GPR,
+                                            int NGR, bf16_t* lds, int LP, int gt, long long timeout) {
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool ok = true;
+  for (int q0 = 0; q0 < NGR; q0 += GTH * GMAX) {
+    i32x4 v[GMAX];
+    unsigned off[GMAX];
+#pragma unroll
+    for (int j = 0; j < GMAX; ++j) {
+      const int q = q0 + gt + j * GTH;
+      const int qq = q < NGR ? q : NGR - 1;
+      const int row = qq / GPR, c8 = qq - row * GPR;
+      off[j] = (unsigned)((base_elem + (size_t)row * row_stride + c8 * 8) * 2);
+      v[j] = load_sc1_b128(rs, off[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < GMAX; ++j) {
+      const int q = q0 + gt + j * GTH;
+      if (q < NGR) {
+        while (!granule_ready(v[j])) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+          v[j] = load_sc1_b128(rs, off[j]);
+        }
+        const int row = q / GPR, c8 = q - row * GPR;
+        *reinterpret_cast<i32x4*>(lds + row * LP + c8 * 8) = v[j];
+      }
+    }
+  }
+  return ok;
+}
+
+// ------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------
+template <int CELL, int MT, int KB>
+__global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
+  constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
+  constexpr int ROWS = 16 * MT;
+  constexpr int EPT = ROWS * UPW / ETH;           // 2 (MT=1) or 4 (MT=2)
+  constexpr int GC = G * UPW;                     // gate columns of the workgroup
+  constexpr int NTL = 2 * G;                      // 16-column N-tiles
+  constexpr int RG = ROWS * G * (UPW / 8);        // gx granules per step (upper bound)
+  constexpr int RGL = (RG + 63) / 64;             // ... per memory-wave lane
+  constexpr int OPL = ROWS * UPW / 64;            // output elements per memory-wave lane
+  constexpr int LP = KB * NWV * 32 + 8;           // A pitch: K zero-padded to KB*8*32
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red_s[NWV][ROWS][GC + 1];      // K-split partials
+  __shared__ __attribute__((aligned(16))) bf16_t st_s[ROWS][UPW];
+  __shared__ float gxr_s[2][ROWS][GC];            // input-projection ring (memory wave -> epilogue)
+  __shared__ float oh_s[2][ROWS][UPW];            // output staging, by step parity
+  __shared__ float oy_s[2][ROWS][UPW];
+  __shared__ float4 og_s[(CELL == CELL_GRU) ? 2 : 1][(CELL == CELL_GRU) ? ROWS : 1][UPW];
+  __shared__ int len_s[ROWS];                     // utterance length per row (0 = padding row)
+  __shared__ float bh_s[G][UPW];                  // recurrent bias slice (GRU)
+  __shared__ int s_mode, s_abort;
+
+  int grp, mem;
+  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, KS = H / 32, N = a.N, NP = a.NP, R = a.R;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW;
+  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  if (tid < G * UPW)
+    bh_s[tid / UPW][tid % UPW] = (CELL == CELL_GRU && a.bh[dir]) ? a.bh[dir][(tid / UPW) * H + u0 + tid % UPW] : 0.f;
+  bf16_t* A = reinterpret_cast<bf16_t*>(smem);     // [ROWS][LP]
+
+  if (wave == 0) {
+    const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+  // zero the A tile once: rows >= R and columns >= H stay zero for the whole launch
+  for (int i = tid; i < ROWS * LP / 8; i += NTH) reinterpret_cast<i32x4*>(A)[i] = i32x4{0, 0, 0, 0};
+
+  // resident U fragments, K split over the 8 waves (k-step ks = wave + kk*8), all 2G
+  // N-tiles per wave: B[k][c] = U[g*H + u0 + 16*half + c][k], zero for k >= H
+  bf16x8 uf[KB][NTL];
+  {
+    const bf16_t* Ud = a.U[dir];
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      const int ks = wave + kk * NWV;
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) {
+        const int g = t >> 1, half = t & 1;
+        bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (ks < KS)
+          v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)(g * H + u0 + 16 * half + (lane & 15)) * H + ks * 32 +
+                                               8 * (lane >> 4));
+        uf[kk][t] = v;
+      }
+    }
+  }
+
+  // epilogue elements (waves 0..3): e = tid + i*ETH -> row = e / 32, unit = e % 32
+  float hreg[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + i * ETH;
+    const int row = e >> 5, c = e & 31;
+    const bool live = tid < ETH && row < R;
+    hreg[i] = live ? a.hsave[dir][(size_t)(r0 + row) * H + u0 + c] : 0.f;        // slot 0 = h0
+  }
+  __syncthreads();   // len_s / bh_s / census
+
+  // memory wave: gx granule q -> (row, gate, 8-unit chunk)
+  i32x4 gpre[RGL];
+  const int NRG = R * G * (UPW / 8);
+  auto mw_load = [&](int s) {          // issue this lane's gx loads for step s
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      const int qq = q < NRG ? q : 0;
+      const int row = qq / (G * 4), rem = qq - row * (G * 4), g = rem >> 2, c8 = rem & 3;
+      const int b = min(r0 + row, N - 1);
+      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+      gpre[j] = *reinterpret_cast<const i32x4*>(a.gx + ((size_t)t * N + b) * a.gstride + dir * G * H + g * H + u0 +
+                                                c8 * 8);
+    }
+  };
+  auto mw_put = [&](int s) {           // ring slot s&1 <- registers (masked past each length)
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      if (q < NRG) {
+        const int row = q / (G * 4), rem = q - row * (G * 4), g = rem >> 2, c8 = rem & 3;
+        const bool act = s < len_s[row];
+        const bf16x8 v = __builtin_bit_cast(bf16x8, gpre[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gxr_s[s & 1][row][g * UPW + c8 * 8 + k] = act ? bf2f((bf16_t)v[k]) : 0.f;
+      }
+    }
+  };
+  auto mw_store = [&](int s) {          // outputs of step s from staging slot s&1
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      if (row < R) {
+        const int b = r0 + row, u = u0 + c;
+        a.hsave[dir][((size_t)(s + 1) * NP + b) * H + u] = oh_s[s & 1][row][c];
+        if (CELL == CELL_GRU)
+          reinterpret_cast<float4*>(a.gates[dir])[((size_t)s * NP + b) * H + u] = og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c];
+        if (b < N) {
+          const int L = len_s[row];
+          const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+          a.y[dir][((size_t)t * N + b) * H + u] = f2bf(oy_s[s & 1][row][c]);
+        }
+      }
+    }
+  };
+  if (s_abort) return;
+  if (wave == MEMW) mw_load(0);
+  const bool plain = s_mode == 1;
+  const unsigned hx_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H * 2);
+  bf16_t* hxd = a.hx[dir];
+  const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
+  Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
+
+  for (int s = 0; s < a.steps; ++s) {
+    st.mark(-1);
+    if (wave < GW) {
+      // (G) gather h_{s-1} (slot s) into the A tile
+      if (!gather_tile<2>(rs_hx, ((size_t)s * NP + r0) * H, H, H / 8, R * (H / 8), A, LP, tid, a.timeout)) {
+        s_abort = 1;
+        atomicOr(a.err, 1u);
+      }
+    } else {
+      // memory wave, while the others wait on the exchange: this step's inputs (loaded
+      // one step ago) into the ring, outputs of step s-2 out of staging, next loads
+      mw_put(s);
+      if (s >= 2) mw_store(s - 2);
+      if (s + 1 < a.steps) mw_load(s + 1);
+    }
+    st.mark(0);
+    lds_barrier();                                                          // #1
+    st.mark(1);
+    if (s_abort) break;
+
+    // (M) partial gh over this wave's k-steps, all N-tiles
+    {
+      f32x4 acc[MT][NTL];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 af[MT][KB];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          af[m][kk] = *reinterpret_cast<const bf16x8*>(A + (m * 16 + (lane & 15)) * LP + (wave + kk * NWV) * 32 +
+                                                       8 * (lane >> 4));
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int t = 0; t < NTL; ++t)
+            acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][t], acc[m][t], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = m * 16 + (lane >> 4) * 4 + j;
+          if (row < R) {
+#pragma unroll
+            for (int t = 0; t < NTL; ++t) red_s[wave][row][t * 16 + (lane & 15)] = acc[m][t][j];
+          }
+        }
+    }
+    st.mark(2);
+    lds_barrier();                                                          // #2
+    st.mark(3);
+
+    // (E) cell epilogue; the exchange copy goes out first
+    if (wave < EW) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * ETH;
+        const int row = e >> 5, c = e & 31;
+        if (row < R) {
+          float pre[G], gxv[G];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) v += red_s[w][row][g * UPW + c];
+            pre[g] = v;
+            gxv[g] = gxr_s[s & 1][row][g * UPW + c];
+          }
+          const bool act = s < len_s[row];
+          float hn;
+          float4 gsv = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (CELL == CELL_GRU) {
+            const float ghn = pre[2] + bh_s[2][c];
+            const float r = sigmoidf_(gxv[0] + pre[0] + bh_s[0][c]);
+            const float z = sigmoidf_(gxv[1] + pre[1] + bh_s[1][c]);
+            const float n = tanhf_(gxv[2] + r * ghn);
+            hn = (1.f - z) * n + z * hreg[i];
+            if (act) gsv = make_float4(r, z, n, ghn);
+          } else {
+            hn = fminf(fmaxf(gxv[0] + pre[0], 0.f), RELU_CAP);
+          }
+          const float hnew = act ? hn : hreg[i];
+          hreg[i] = hnew;
+          st_s[row][c] = f2bf_x(hnew);
+          oh_s[s & 1][row][c] = hnew;
+          oy_s[s & 1][row][c] = act ? hn : 0.f;
+          if (CELL == CELL_GRU) og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c] = gsv;
+        }
+      }
+      st.mark(4);
+      // a wave's lanes cover whole rows of st_s: the granule stores read only LDS that
+      // this wave wrote
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * ETH;
+        const int row = e >> 5, c = e & 31;
+        if ((c & 7) == 0 && row < R) {
+          const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][c]);
+          const unsigned off = (unsigned)((((size_t)(s + 1) * NP + r0 + row) * H + u0 + c) * 2);
+          store_granule(plain, rs_hx, hxd, off, v);
+        }
+      }
+    }
+    st.mark(5);
+  }
+  __syncthreads();
+  if (wave == MEMW && !s_abort) {
+    if (a.steps >= 2) mw_store(a.steps - 2);
+    if (a.steps >= 1) mw_store(a.steps - 1);
+  }
+  if (wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
+}
+
+// ------------------------------------------------------------------------------------
+// backward (BPTT)
+// ------------------------------------------------------------------------------------
+template <int CELL, int MT, int KB>
+__global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
+  constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
+  constexpr int ROWS = 16 * MT;
+  constexpr int EPT = ROWS * UPW / ETH;
+  constexpr int OPL = ROWS * UPW / 64;            // elements per memory-wave lane
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red_s[NWV][ROWS][UPW + 1];
+  __shared__ __attribute__((aligned(16))) bf16_t st_s[ROWS][G * UPW];
+  __shared__ float dyr_s[2][ROWS][UPW];           // prefetch ring (memory wave -> epilogue)
+  __shared__ float hpr_s[2][ROWS][UPW];
+  __shared__ float4 gr_s[2][(CELL == CELL_GRU) ? ROWS : 1][UPW];
+  __shared__ float ox_s[2][ROWS][G][UPW];         // dgx staging by step parity (epilogue -> memory wave)
+  __shared__ int len_s[ROWS];
+  __shared__ int s_mode, s_abort;
+
+  int grp, mem;
+  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, GH = G * H, KS = GH / 32, N = a.N, NP = a.NP, R = a.R;
+  const int LP = KB * NWV * 32 + 8;               // A pitch (K zero-padded to KB*8*32)
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW;
+  bf16_t* A = reinterpret_cast<bf16_t*>(smem);     // [ROWS][LP]
+  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+
+  if (wave == 0) {
+    const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+  for (int i = tid; i < ROWS * LP / 8; i += NTH) reinterpret_cast<i32x4*>(A)[i] = i32x4{0, 0, 0, 0};
+
+  // resident U column fragments, K split over all 8 waves: k-step ks = wave + kk*NWV
+  // B[k][c] = U[k][u0 + 16*nt + c], k over all G*H (zero past it)
+  bf16x8 uf[KB][2];
+  {
+    const bf16_t* Ud = a.U[dir];
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      const int ks = wave + kk * NWV;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (ks < KS) {
+          const int k0 = ks * 32 + 8 * (lane >> 4);
+          const bf16_t* p = Ud + (size_t)k0 * H + u0 + 16 * nt + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (short)p[(size_t)j * H];
+        }
+        uf[kk][nt] = v;
+      }
+    }
+  }
+
+  float carry[EPT];
+  float sbx[EPT][G];
+  float sbh[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    carry[i] = 0.f;
+    sbh[i] = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) sbx[i][g] = 0.f;
+  }
+  __syncthreads();   // len_s
+
+  // memory wave: per-step inputs (dy, gates, h_prev) two steps ahead, dgx stores
+  float pdy[OPL], php[OPL];
+  float4 pg[OPL];
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      const int bp = min(r0 + row, NP - 1), bn = min(r0 + row, N - 1), u = u0 + c;
+      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+      pdy[j] = bf2f(a.dy[((size_t)t * N + bn) * H + u]);
+      if (CELL == CELL_GRU) {
+        pg[j] = reinterpret_cast<const float4*>(a.gates[dir])[((size_t)s * NP + bp) * H + u];
+        php[j] = a.hsave[dir][((size_t)s * NP + bp) * H + u];
+      } else {
+        php[j] = a.hsave[dir][((size_t)(s + 1) * NP + bp) * H + u];     // h_s itself
+      }
+    }
+  };
+  auto mw_put = [&](int s) {
+    const int slot = s & 1;
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      const bool act = s < len_s[row];
+      dyr_s[slot][row][c] = act ? pdy[j] : 0.f;
+      hpr_s[slot][row][c] = act ? php[j] : 0.f;
+      if (CELL == CELL_GRU) gr_s[slot][(CELL == CELL_GRU) ? row : 0][c] = act ? pg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto mw_store = [&](int s) {          // dgx of step s from the staging area
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      const int b = r0 + row, u = u0 + c;
+      if (row < R && b < N) {
+        const int L = len_s[row];
+        const bool act = s < L;
+        const int t = act ? ((dir == 0) ? s : (L - 1 - s)) : s;
+        bf16_t* dst = a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + u;
+#pragma unroll
+        for (int g = 0; g < G; ++g) dst[g * H] = f2bf(ox_s[s & 1][row][g][c] * a.dgx_scale);
+      }
+    }
+  };
+  if (s_abort) return;
+  if (wave == MEMW && a.steps > 0) mw_load(a.steps - 1);
+  const bool plain = s_mode == 1;
+  const unsigned dgh_bytes = (unsigned)((size_t)a.steps * NP * GH * 2);
+  bf16_t* dghd = a.dgh[dir];
+  const __amdgpu_buffer_rsrc_t rs_dgh = make_rsrc(dghd, dgh_bytes);
+  Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
+
+  for (int s = a.steps - 1; s >= 0; --s) {
+    st.mark(-1);
+    const bool has_next = s + 1 < a.steps;
+    // (G) gather dgh_{s+1} into the A tile
+    if (wave < GW) {
+      if (has_next &&
+          !gather_tile<4>(rs_dgh, ((size_t)(s + 1) * NP + r0) * GH, GH, GH / 8, R * (GH / 8), A, LP, tid, a.timeout)) {
+        s_abort = 1;
+        atomicOr(a.err, 1u);
+      }
+    } else {
+      // memory wave, while the others wait on the exchange (see the forward kernel)
+      mw_put(s);
+      if (s + 2 < a.steps) mw_store(s + 2);
+      if (s >= 1) mw_load(s - 1);
+    }
+    st.mark(0);
+    lds_barrier();                                                          // #1
+    st.mark(1);
+    if (s_abort) break;
+
+    // (M) partial dh_rec over this wave's k-steps
+    if (has_next) {
+      f32x4 acc[MT][2];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) { acc[m][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[m][1] = acc[m][0]; }
+      bf16x8 af[MT][KB];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          af[m][kk] = *reinterpret_cast<const bf16x8*>(A + (m * 16 + (lane & 15)) * LP + (wave + kk * NWV) * 32 +
+                                                       8 * (lane >> 4));
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][0], acc[m][0], 0, 0, 0);
+          acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][1], acc[m][1], 0, 0, 0);
+        }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) red_s[wave][m * 16 + (lane >> 4) * 4 + j][nt * 16 + (lane & 15)] = acc[m][nt][j];
+    }
+    st.mark(2);
+    lds_barrier();                                                          // #2
+    st.mark(3);
+
+    // (E) cell backward; the exchange copy (dgh_s) goes out first
+    if (wave < EW) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * ETH;
+        const int row = e >> 5, c = e & 31;
+        if (row < R) {
+          float dhrec = 0.f;
+          if (has_next) {
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) dhrec += red_s[w][row][c];
+          }
+          const bool act = s < len_s[row];
+          const float dh = dyr_s[s & 1][row][c] + carry[i] + dhrec;
+          const float hp = hpr_s[s & 1][row][c];
+          float ghv[G], gxs[G];
+          float cnew = 0.f;
+          if (CELL == CELL_GRU) {
+            const float4 gv = gr_s[s & 1][(CELL == CELL_GRU) ? row : 0][c];
+            const float r = gv.x, z = gv.y, n = gv.z, ghn = gv.w;
+            const float dn = dh * (1.f - z);
+            const float dz = dh * (hp - n);
+            cnew = dh * z;
+            const float dan = dn * (1.f - n * n);
+            const float dr = dan * ghn;
+            const float dghn = dan * r;
+            const float daz = dz * z * (1.f - z);
+            const float dar = dr * r * (1.f - r);
+            ghv[0] = dar; ghv[1] = daz; ghv[2] = dghn;
+            gxs[0] = dar; gxs[1] = daz; gxs[2] = dan;
+          } else {
+            const float da = (hp > 0.f && hp < RELU_CAP) ? dh : 0.f;
+            ghv[0] = da;
+            gxs[0] = da;
+          }
+          if (!act) {
+            cnew = 0.f;
+#pragma unroll
+            for (int g = 0; g < G; ++g) { ghv[g] = 0.f; gxs[g] = 0.f; }
+          }
+          carry[i] = cnew;
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            st_s[row][g * UPW + c] = f2bf_x(ghv[g]);
+            ox_s[s & 1][row][g][c] = gxs[g];
+            sbx[i][g] += gxs[g];
+          }
+          if (CELL == CELL_GRU) sbh[i] += ghv[G - 1];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * ETH;
+        const int row = e >> 5, c = e & 31;
+        if ((c & 7) == 0 && row < R) {
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][g * UPW + c]);
+            const unsigned off = (unsigned)((((size_t)s * NP + r0 + row) * GH + g * H + u0 + c) * 2);
+            store_granule(plain, rs_dgh, dghd, off, v);
+          }
+        }
+      }
+    }
+    st.mark(4);
+  }
+  __syncthreads();
+  if (wave == MEMW && !s_abort) {
+    if (a.steps >= 2) mw_store(1);
+    if (a.steps >= 1) mw_store(0);
+  }
+  if (wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
+
+  // bias gradients: reduce the epilogue waves' rows through LDS, one read-modify-write
+  // per (gate, unit) of the workgroup's own [bg] partial row
+  if (a.dbx_part[dir] != nullptr && !s_abort) {
+    constexpr int BW = (G + 1) * UPW;
+    static_assert(NWV * ROWS * (UPW + 1) >= ROWS * BW, "bias reduction does not fit the LDS scratch");
+    float* bred = &red_s[0][0][0];
+    if (wave < EW) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * ETH;
+        const int row = e >> 5, c = e & 31;
+#pragma unroll
+        for (int g = 0; g < G; ++g) bred[row * BW + g * UPW + c] = sbx[i][g];
+        bred[row * BW + G * UPW + c] = sbh[i];
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < BW; q += NTH) {
+      float sum = 0.f;
+      for (int r = 0; r < ROWS; ++r) sum += bred[r * BW + q];
+      const int g = q / UPW, c = q % UPW;
+      const size_t base = (size_t)bg * GH + u0 + c;
+      if (g < G) {
+        a.dbx_part[dir][base + (size_t)g * H] += sum;
+        if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr && g < G - 1) a.dbh_part[dir][base + (size_t)g * H] += sum;
+      } else if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr) {
+        a.dbh_part[dir][base + (size_t)(G - 1) * H] += sum;
+      }
+    }
+  }
+}
+
+template <int CELL, int MT>
+static int launch_fwd(const XFwd& a, int kb, int grid, size_t smem, hipStream_t st) {
+  switch (kb) {
+#define DS2_CASE(K)                                                                           \
+  case K:                                                                                     \
+    hipLaunchKernelGGL((rnnx_fwd_kernel<CELL, MT, K>), dim3(grid), dim3(NTH), smem, st, a); \
+    break;
+    DS2_CASE(1) DS2_CASE(2) DS2_CASE(3) DS2_CASE(4)
+#undef DS2_CASE
+    default: return -31;
+  }
+  return (int)hipGetLastError();
+}
+
+template <int CELL, int MT>
+static int launch_bwd(const XBwd& a, int kb, int grid, size_t smem, hipStream_t st) {
+  switch (kb) {
+#define DS2_CASE(K)                                                                           \
+  case K:                                                                                     \
+    hipLaunchKernelGGL((rnnx_bwd_kernel<CELL, MT, K>), dim3(grid), dim3(NTH), smem, st, a); \
+    break;
+    DS2_CASE(2) DS2_CASE(4) DS2_CASE(6) DS2_CASE(8) DS2_CASE(10) DS2_CASE(12) DS2_CASE(16)
+#undef DS2_CASE
+    default: return -32;
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename F>
+static int set_smem_attr(F kernel, size_t smem) {
+  return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+}
+
+}  // namespace
+
+extern "C" {
+
+struct DS2RnnX {
+  int T, N, NP, H, BG, R, steps, gstride, ndir, cell, mt, xcd_map, knobs;
+  const int* lens;
+  const void* gx;        // fwd: gx;  bwd: dy
+  const void* U[2];
+  const float* bh[2];
+  void* y[2];            // fwd: y
+  void* ex[2];           // fwd: hx exchange;  bwd: dgh exchange
+  float* hsave[2];
+  float* gates[2];
+  void* dgx;
+  float* dbx_part[2];
+  float* dbh_part[2];
+  float dgx_scale;
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+  unsigned long long* stamps;
+};
+
+// grid size of a launch (blocks with no role exit at once)
+int ds2_rnnx_grid(int H, int ngroups, int xcd_map) {
+  const int P = H / UPW;
+  return (xcd_map && ngroups <= 8) ? 8 * P : ngroups * P;
+}
+
+// k-steps register tile: fwd = whole K per wave, bwd = K split over the 8 waves
+int ds2_rnnx_kb(int H, int G, int fwd) {
+  if (fwd) {
+    const int need = (H / 32 + NWV - 1) / NWV;
+    return need <= 4 ? need : -1;
+  }
+  const int need = (G * H / 32 + NWV - 1) / NWV;
+  for (int k : {2, 4, 6, 8, 10, 12, 16}) if (k >= need) return k;
+  return -1;
+}
+
+// dynamic LDS: the A tile, K zero-padded to the register tile
+size_t ds2_rnnx_smem(int H, int G, int mt, int fwd) {
+  const int kb = ds2_rnnx_kb(H, G, fwd);
+  const int LP = kb * NWV * 32 + 8;
+  return (size_t)16 * mt * LP * 2;
+}
+
+int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
+  if (d->H % UPW != 0 || d->R < 1 || d->R > 16 * d->mt || d->NP != d->BG * d->R) return -30;
+  const int G = d->cell == CELL_GRU ? 3 : 1;
+  const int kb = ds2_rnnx_kb(d->H, G, 1);
+  if (kb < 0) return -31;
+  XFwd a;
+  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = d->H / UPW; a.BG = d->BG; a.R = d->R;
+  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
+  a.xcd_map = d->xcd_map && a.ngroups <= 8; a.knobs = d->knobs;
+  a.lens = d->lens; a.gx = (const bf16_t*)d->gx;
+  for (int i = 0; i < 2; ++i) {
+    a.U[i] = (const bf16_t*)d->U[i]; a.bh[i] = d->bh[i]; a.y[i] = (bf16_t*)d->y[i];
+    a.hx[i] = (bf16_t*)d->ex[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
+  }
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
+  if (d->steps <= 0) return 0;
+  const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
+  const size_t smem = ds2_rnnx_smem(d->H, G, d->mt, 1);
+  int rc;
+#define DS2_FWD(C, M)                                                                        \
+  {                                                                                          \
+    switch (kb) {                                                                            \
+      case 1: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 1>, smem); break;                     \
+      case 2: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 2>, smem); break;                     \
+      case 3: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 3>, smem); break;                     \
+      default: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 4>, smem); break;                    \
+    }                                                                                        \
+    if (rc) return rc;                                                                       \
+    return launch_fwd<C, M>(a, kb, grid, smem, st);                                          \
+  }
+  if (d->mt != 1) return -33;     // 16-row tiles only: the 32-row LDS footprint exceeds 160 KB
+  if (d->cell == CELL_GRU) DS2_FWD(CELL_GRU, 1) else DS2_FWD(CELL_RELU, 1)
+#undef DS2_FWD
+}
+
+int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st) {
+  if (d->H % UPW != 0 || d->R < 1 || d->R > 16 * d->mt || d->NP != d->BG * d->R) return -30;
+  const int G = d->cell == CELL_GRU ? 3 : 1;
+  const int kb = ds2_rnnx_kb(d->H, G, 0);
+  if (kb < 0) return -32;
+  XBwd a;
+  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = d->H / UPW; a.BG = d->BG; a.R = d->R;
+  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
+  a.xcd_map = d->xcd_map && a.ngroups <= 8; a.knobs = d->knobs;
+  a.lens = d->lens; a.dy = (const bf16_t*)d->gx;
+  for (int i = 0; i < 2; ++i) {
+    a.U[i] = (const bf16_t*)d->U[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
+    a.dgh[i] = (bf16_t*)d->ex[i]; a.dbx_part[i] = d->dbx_part[i]; a.dbh_part[i] = d->dbh_part[i];
+  }
+  a.dgx = (bf16_t*)d->dgx; a.dgx_scale = d->dgx_scale;
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
+  if (d->steps <= 0) return 0;
+  const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
+  const size_t smem = ds2_rnnx_smem(d->H, G, d->mt, 0);
+  int rc;
+#define DS2_BWD(C, M)                                                                        \
+  {                                                                                          \
+    switch (kb) {                                                                            \
+      case 2: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 2>, smem); break;                     \
+      case 4: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 4>, smem); break;                     \
+      case 6: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 6>, smem); break;                     \
+      case 8: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 8>, smem); break;                     \
+      case 10: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 10>, smem); break;                   \
+      case 12: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 12>, smem); break;                   \
+      default: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 16>, smem); break;                   \
+    }                                                                                        \
+    if (rc) return rc;                                                                       \
+    return launch_bwd<C, M>(a, kb, grid, smem, st);                                          \
+  }
+  if (d->mt != 1) return -33;
+  if (d->cell == CELL_GRU) DS2_BWD(CELL_GRU, 1) else DS2_BWD(CELL_RELU, 1)
+#undef DS2_BWD
+}
+
+}  // extern "C"

@@ -49,6 +49,68 @@ class RnnPlan:
     S: int
     cell: str
     ndir: int
+    kind: str = "v1"      # "xcd": csrc/rnn_xcd.hip (gen 2); "v1": csrc/rnn_persistent.hip
+    R: int = 0            # xcd: batch rows per group
+    xcd_map: int = 0      # xcd: group = blockIdx % 8 (<= 8 groups of <= CUs/8 workgroups)
+
+
+RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))   # diagnostic timing switches only
+
+
+LDS_BYTES = 160 * 1024
+
+
+def _xcd_kb(H: int, G: int, fwd: bool) -> int:
+    """k-steps per wave of csrc/rnn_xcd.hip (K split over 8 waves)."""
+    need = -(-((H if fwd else G * H) // 32) // 8)
+    opts = (1, 2, 3, 4) if fwd else (2, 4, 6, 8, 10)     # larger bwd tiles spill
+    for k in opts:
+        if k >= need:
+            return k
+    return -1
+
+
+def _xcd_lds(H: int, G: int, mt: int) -> int:
+    """LDS bytes of the larger of the two csrc/rnn_xcd.hip kernels (static + dynamic)."""
+    rows = 16 * mt
+    kf, kb = _xcd_kb(H, G, True), _xcd_kb(H, G, False)
+    if kf < 0 or kb < 0:
+        return 1 << 30
+    gru = G == 3
+    fwd = (rows * (kf * 8 * 32 + 8) * 2 + 8 * rows * (G * 32 + 1) * 4 + rows * 32 * 2 + 2 * rows * G * 32 * 4
+           + 4 * rows * 32 * 4 + (2 * rows * 32 * 16 if gru else 16) + rows * 4 + G * 32 * 4 + 64)
+    bwd = (rows * (kb * 8 * 32 + 8) * 2 + 8 * rows * 33 * 4 + rows * G * 32 * 2 + 4 * rows * 32 * 4
+           + (2 * rows * 32 * 16 if gru else 16) + 2 * rows * G * 32 * 4 + rows * 4 + 64)
+    return max(fwd, bwd)
+
+
+def make_xcd_plan(N: int, H: int, cell: str, ndir: int, cus: int) -> Optional[RnnPlan]:
+    """Generation-2 geometry: groups of R batch rows x all H units (H/32 workgroups of 32
+    units). Prefer the most groups that still fit the chip (smaller per-step gathers), at
+    most 8 so a group can live on one XCD; rows per group R <= 32."""
+    if H % 32 != 0 or H // 32 > 32:       # larger H: the resident U slice would spill
+        return None
+    G = GATES[cell]
+    P = H // 32
+    best = None
+    for R in range(1, 33):
+        BG = -(-N // R)
+        ngroups = ndir * BG
+        if ngroups * P > cus:
+            continue
+        if ngroups > 8 and R < 16:
+            continue                       # many small groups: no XCD locality, keep MFMA rows full
+        mt = 1 if R <= 16 else 2
+        if _xcd_lds(H, G, mt) > LDS_BYTES:
+            continue
+        best = (R, BG, mt)
+        break
+    if best is None:
+        return None
+    R, BG, mt = best
+    xcd_map = int(ndir * BG <= 8 and P <= cus // 8)
+    return RnnPlan(N=N, NP=BG * R, BG=BG, mt=mt, nw=8, persistent=True, H=H, S=H // 16, cell=cell,
+                   ndir=ndir, kind="xcd", R=R, xcd_map=xcd_map)
 
 
 # Largest KPW (k-steps per wave) that compiles WITHOUT register spills, per
@@ -86,6 +148,10 @@ def make_plan(N: int, H: int, cell: str, ndir: int, cus: int, mode: Optional[str
     G = GATES[cell]
     S = H // 16
     mode = mode or os.environ.get("DS2_RNN_MODE", "auto")
+    if mode == "auto" and os.environ.get("DS2_RNN_KERNEL", "xcd") == "xcd":
+        p = make_xcd_plan(N, H, cell, ndir, cus)
+        if p is not None:
+            return p
     force_nw = int(os.environ.get("DS2_RNN_NW", "0"))
     chosen = None
     for mt in (1, 2):
@@ -160,8 +226,23 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan):
     hs[:, 0].zero_()
     gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
              if plan.cell == "gru" else None)
-    flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
     err = torch.zeros(1, device=dev, dtype=torch.int32)
+    if plan.kind == "xcd":
+        hx[:, 1:].view(torch.int16).fill_(-1)             # sentinel 0xFFFF: "not yet produced"
+        census = torch.full((ndir * plan.BG * (H // 32),), -1, device=dev, dtype=torch.int32)
+        C.rnnx_fwd(gx, lens, U[0], U[1] if d1 else None, bh[0], bh[1] if d1 else None,
+                   y2[0], y2[1] if d1 else None, hx[0], hx[1] if d1 else None,
+                   hs[0], hs[1] if d1 else None,
+                   gates[0] if gates is not None else None,
+                   gates[1] if (gates is not None and d1) else None,
+                   census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
+                   CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
+                   _stamps("fwd", plan, int(C.rnnx_info(H, GATES[plan.cell], plan.mt, ndir * plan.BG,
+                                                         plan.xcd_map)["grid"]), dev))
+        _pending_errors.append(err)
+        y = torch.add(y2[0], y2[1]) if d1 else y2[0]
+        return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
+    flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
     C.rnn_fwd(gx, lens, U[0], U[1] if d1 else None,
               bh[0], bh[1] if d1 else None,
               y2[0], y2[1] if d1 else None, hx[0], hx[1] if d1 else None,
@@ -190,12 +271,25 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
     dy = dy.to(torch.bfloat16).contiguous()
     dgh = torch.empty(ndir, steps, plan.NP, G * H, device=dev, dtype=torch.bfloat16)
     dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
-    carry = None if plan.persistent else torch.zeros(ndir, plan.NP, H, device=dev, dtype=torch.float32)
-    flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
     err = torch.zeros(1, device=dev, dtype=torch.int32)
     parts = torch.zeros(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
                         dtype=torch.float32) if want_bias else None
     has_g = gates.numel() > 0
+    if plan.kind == "xcd":
+        dgh.view(torch.int16).fill_(-1)                   # sentinel
+        census = torch.full((ndir * plan.BG * (H // 32),), -1, device=dev, dtype=torch.int32)
+        C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
+                   gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
+                   dgh[0], dgh[1] if d1 else None, dgx,
+                   parts[0] if parts is not None else None,
+                   parts[1] if (parts is not None and plan.cell == "gru") else None,
+                   float(dgx_scale), census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
+                   CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
+                   _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev))
+        _pending_errors.append(err)
+        return dgx, dgh, parts
+    carry = None if plan.persistent else torch.zeros(ndir, plan.NP, H, device=dev, dtype=torch.float32)
+    flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
     C.rnn_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
               gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
               dgh[0], dgh[1] if d1 else None, dgx,

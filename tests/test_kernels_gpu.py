@@ -16,7 +16,7 @@ def _rel(a, b):
 
 
 # --------------------------------------------------------------------------- recurrence
-def _rnn_case(cuda, cell, N, H, T, ndir, mode, seed=0, din=None):
+def _rnn_case(cuda, cell, N, H, T, ndir, mode, seed=0, din=None, kernel="xcd"):
     import os
     from deepspeech_amd.ops import rnn as RNN
     torch.manual_seed(seed)
@@ -29,16 +29,21 @@ def _rnn_case(cuda, cell, N, H, T, ndir, mode, seed=0, din=None):
         gx[int(lens[b]):, b] = 0
     Us = [(torch.randn(G * H, H) / math.sqrt(H)).bfloat16().to(cuda) for _ in range(ndir)]
     bhs = [(torch.randn(G * H) * 0.1).to(cuda) if cell == "gru" else None for _ in range(ndir)]
-    old = os.environ.get("DS2_RNN_MODE")
+    old = os.environ.get("DS2_RNN_MODE"), os.environ.get("DS2_RNN_KERNEL")
     os.environ["DS2_RNN_MODE"] = mode
+    os.environ["DS2_RNN_KERNEL"] = kernel
     try:
         RNN._plan_cache.clear()
         plan = RNN.plan_for(N, H, cell, ndir, cuda)
     finally:
-        if old is None:
-            os.environ.pop("DS2_RNN_MODE")
-        else:
-            os.environ["DS2_RNN_MODE"] = old
+        for k, v in zip(("DS2_RNN_MODE", "DS2_RNN_KERNEL"), old):
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+        RNN._plan_cache.clear()
+    if mode == "auto" and kernel == "xcd" and RNN.make_xcd_plan(N, H, cell, ndir, 256) is not None:
+        assert plan.kind == "xcd", plan
     # HIP
     gx_h = gx.clone().requires_grad_(True)
     U_h = [u.clone().requires_grad_(True) for u in Us]
@@ -80,9 +85,17 @@ def test_birnn_small(cuda, cell, mode):
 
 
 @pytest.mark.parametrize("cell", ["rnn_relu", "gru"])
-def test_birnn_ds2_shape(cuda, cell):
-    # the flagship geometry: batch 32, H=800 (two batch groups, 50 slices per direction)
-    _rnn_case(cuda, cell, N=32, H=800, T=61, ndir=2, mode="auto", seed=3)
+@pytest.mark.parametrize("kernel", ["xcd", "v1"])
+def test_birnn_ds2_shape(cuda, cell, kernel):
+    # the flagship geometry: batch 32, H=800 (xcd: 8 groups of 8 rows x 25 workgroups;
+    # v1: two batch groups, 50 slices per direction)
+    _rnn_case(cuda, cell, N=32, H=800, T=61, ndir=2, mode="auto", seed=3, kernel=kernel)
+
+
+@pytest.mark.parametrize("N,H", [(16, 1280), (48, 512), (3, 96)])
+def test_birnn_xcd_geometries(cuda, N, H):
+    # spread groups (H=1280: 40 workgroups > one XCD), 16-row groups, tiny batch
+    _rnn_case(cuda, "gru", N=N, H=H, T=33, ndir=2, mode="auto", seed=9)
 
 
 def test_unirnn_gru(cuda):

@@ -20,6 +20,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 PHASES = ["wait", "load+mfma", "reduce", "epilogue", "publish", "rest(stores+prefetch)"]
+# csrc/rnn_xcd.hip stamps: wave 0 phases + the memory wave's duty time and its barrier-#2 wait
+XPHASES = ["gather(w0)", "sync1", "mfma(w0)", "sync2", "epilogue", "publish", "memwave duties", "memwave sync1"]
 
 
 def run(cell, N, H, T, ndir, nw, mode, iters, stamps=False):
@@ -54,12 +56,12 @@ def run(cell, N, H, T, ndir, nw, mode, iters, stamps=False):
         log = RNN.STAMP_LOG
         RNN.STAMP_LOG = None
         for kind, p, t in log:
-            w = t[:, :6].double() / T
+            names = XPHASES if p.kind == "xcd" else PHASES
+            w = t[:, :len(names)].double() / T
             active = w.sum(1) > 0
             w = w[active]
             res[kind + "_cycles_per_step"] = {ph: [round(float(w[:, i].mean()), 0), round(float(w[:, i].min()), 0),
-                                                   round(float(w[:, i].max()), 0)] for i, ph in enumerate(PHASES)}
-            res[kind + "_busy_(non-wait)_max"] = round(float((w.sum(1) - w[:, 0]).max()), 0)
+                                                   round(float(w[:, i].max()), 0)] for i, ph in enumerate(names)}
         return res
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     tf, tb = [], []
@@ -90,21 +92,28 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--nw", type=str, default="0,4,8")
     ap.add_argument("--stamps", action="store_true")
-    ap.add_argument("--protos", type=str, default="flag")
+    ap.add_argument("--kernels", type=str, default="xcd,v1", help="recurrence generations to time")
+    ap.add_argument("--knobs", type=str, default="0", help="xcd diagnostic knob sets to time (1 no prefetch, "
+                    "2 no deferred stores, 4 no MFMA; results are wrong when set)")
     a = ap.parse_args()
-    for proto in a.protos.split(","):
-      os.environ["DS2_RNN_PROTO"] = proto
-      for nw in [int(x) for x in a.nw.split(",")]:
+    for proto in a.kernels.split(","):
+      os.environ["DS2_RNN_KERNEL"] = proto
+      for nw in ([int(x) for x in a.nw.split(",")] if proto == "v1" else [int(k) for k in a.knobs.split(",")]):
+        if proto == "xcd":
+            RNN_mod = __import__("deepspeech_amd.ops.rnn", fromlist=["x"])
+            RNN_mod.RNNX_KNOBS = nw
         for mode in ("auto",):
             try:
                 r = run(a.cell, a.N, a.H, a.T, a.ndir, nw, mode, a.iters)
-                print(json.dumps({"proto": proto, "nw": nw, "mode": mode,
+                print(json.dumps({"kernel": proto, "nw": nw, "mode": mode,
                                   **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}}), flush=True)
             except Exception as e:  # noqa: BLE001
-                print(json.dumps({"proto": proto, "nw": nw, "mode": mode, "error": str(e)[:200]}), flush=True)
+                print(json.dumps({"kernel": proto, "nw": nw, "mode": mode, "error": str(e)[:200]}), flush=True)
       if a.stamps:
+        if proto == "xcd":
+            __import__("deepspeech_amd.ops.rnn", fromlist=["x"]).RNNX_KNOBS = 0
         r = run(a.cell, a.N, a.H, a.T, a.ndir, 0, "auto", 1, stamps=True)
-        print(json.dumps({"proto": proto, "stamps [mean,min,max] cycles/step": r}), flush=True)
+        print(json.dumps({"kernel": proto, "stamps [mean,min,max] cycles/step": r}), flush=True)
 
 
 if __name__ == "__main__":
