@@ -10,7 +10,8 @@
 //                         s-1/s-2 (s+1/s+2) neighbours crossing a lane boundary come from a
 //                         cross-lane shuffle, so a frame costs no barrier and no LDS round
 //                         trip; the next frame's lp row is prefetched one frame ahead.
-//                         alpha/beta rows are streamed to ab_ws[2][N][T][SPmax].
+//                         alpha/beta rows are streamed (float4 stores, 64*SPL row stride)
+//                         to ab_ws[2][N][T][64*SPL].
 //   3. ctc_grad_kernel    fully parallel over frames (one wave per (t, b)): occupancy
 //                         gamma_t(s) = alpha+beta-lp-logP, blank states summed with a wave
 //                         reduction, label states with per-wave LDS atomics, then
@@ -98,7 +99,13 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
     skip |= (ok ? 1u : 0u) << j;
   }
   const float* lp = lp_ws + (size_t)b * T * KPAD;
-  float* out = ab_ws + ((size_t)beta * N + b) * (size_t)T * SPmax;
+  constexpr int SPS = 64 * SPL;                    // row stride: whole register tile, 16-B aligned
+  float* out = ab_ws + ((size_t)beta * N + b) * (size_t)T * SPS;
+  auto put_row = [&](int t, const float* v) {
+    float4* o = reinterpret_cast<float4*>(out + (size_t)t * SPS + s0);
+#pragma unroll
+    for (int j = 0; j < SPL / 4; ++j) o[j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+  };
   // lp rows are staged through LDS in chunks of 64 frames (one 128-B row per lane), so
   // the per-frame gathers are LDS reads: a global load in the frame loop would make the
   // wave wait (vmcnt) behind its own streaming alpha/beta stores every frame.
@@ -130,9 +137,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
     if (!beta) v[j] = (s == 0 || s == 1) && s < SP ? l : NEG_INF;
     else v[j] = (s == SP - 1 || s == SP - 2) ? l : NEG_INF;
   }
-#pragma unroll
-  for (int j = 0; j < SPL; ++j)
-    if (s0 + j < SPmax) out[(size_t)t0 * SPmax + s0 + j] = v[j];
+  put_row(t0, v);
 
   for (int step = 1; step < len; ++step) {
     const int t = t0 + dt * step;
@@ -166,10 +171,8 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
       }
     }
 #pragma unroll
-    for (int j = 0; j < SPL; ++j) {
-      v[j] = nv[j];
-      if (s0 + j < SPmax) out[(size_t)t * SPmax + s0 + j] = v[j];
-    }
+    for (int j = 0; j < SPL; ++j) v[j] = nv[j];
+    put_row(t, v);
   }
   if (!beta) {
     // logP = lse(alpha_{len-1}(SP-1), alpha_{len-1}(SP-2))
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const LT* __restrict__ lo
                                                        const int* __restrict__ label_lens,
                                                        const float* __restrict__ ab_ws,
                                                        const float* __restrict__ logp_in, float* __restrict__ loss,
-                                                       LT* __restrict__ grad, int T, int N, int K, int Lmax, int SPmax,
+                                                       LT* __restrict__ grad, int T, int N, int K, int Lmax, int SPS,
                                                        int blank, int zero_inf) {
   __shared__ float occ_s[4][KPAD];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -216,8 +219,8 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const LT* __restrict__ lo
   const float sum = wave_sum((lane < K) ? __expf(x - m) : 0.f);
   const float lpk = (lane < K) ? (x - m - __logf(sum)) : NEG_INF;    // lane k holds lp_t(k)
   const int SP = 2 * L + 1;
-  const float* A = ab_ws + ((size_t)b * T + t) * SPmax;
-  const float* B = ab_ws + ((size_t)(N + b) * T + t) * SPmax;
+  const float* A = ab_ws + ((size_t)b * T + t) * SPS;
+  const float* B = ab_ws + ((size_t)(N + b) * T + t) * SPS;
   float blank_acc = 0.f;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   for (int base = 0; base < SP; base += 64) {       // wave-uniform trip count (shuffles below)
@@ -253,10 +256,17 @@ static void launch_recur(const int* lens, const int* labels, const int* label_le
 
 extern "C" {
 
-// workspace floats: lp [N][T][32] + alpha/beta [2][N][T][SPmax] + logP [N]
+static int ctc_spl(int SPmax) {
+  const int need = (SPmax + 63) / 64;
+  for (int k : {4, 8, 16, 32}) if (k >= need) return k;
+  return -1;
+}
+
+// workspace floats: lp [N][T][32] + alpha/beta [2][N][T][64*SPL] + logP [N]
 long long ds2_ctc_ws_floats(int T, int N, int Lmax) {
-  const long long SPmax = 2LL * Lmax + 1;
-  return (long long)N * T * KPAD + 2LL * N * T * SPmax + N;
+  const int spl = ctc_spl(2 * Lmax + 1);
+  const long long SPS = 64LL * (spl > 0 ? spl : 32);
+  return (long long)N * T * KPAD + 2LL * N * T * SPS + N;
 }
 
 int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const int* labels,
@@ -265,27 +275,27 @@ int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const in
   if (K > 64 || K > KPAD) return -20;
   const int SPmax = 2 * Lmax + 1;
   if (SPmax > 64 * 32) return -21;    // > 1023 labels per utterance
+  const int spl = ctc_spl(SPmax);
+  const int SPS = 64 * spl;
   float* lp_ws = ws;
   float* ab_ws = lp_ws + (size_t)N * T * KPAD;
-  float* logp = ab_ws + 2 * (size_t)N * T * SPmax;
+  float* logp = ab_ws + 2 * (size_t)N * T * SPS;
   const int nw = T * N;
   const dim3 g4((nw + 3) / 4);
   if (logits_bf16)
     hipLaunchKernelGGL(ctc_lsm_kernel<bf16_t>, g4, dim3(256), 0, st, (const bf16_t*)logits, lens, lp_ws, T, N, K);
   else
     hipLaunchKernelGGL(ctc_lsm_kernel<float>, g4, dim3(256), 0, st, (const float*)logits, lens, lp_ws, T, N, K);
-  const int need = (SPmax + 63) / 64;
-  if (need <= 2) launch_recur<2>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else if (need <= 4) launch_recur<4>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else if (need <= 8) launch_recur<8>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else if (need <= 16) launch_recur<16>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  if (spl == 4) launch_recur<4>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else if (spl == 8) launch_recur<8>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else if (spl == 16) launch_recur<16>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
   else launch_recur<32>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
   if (logits_bf16)
     hipLaunchKernelGGL(ctc_grad_kernel<bf16_t>, g4, dim3(256), 0, st, (const bf16_t*)logits, lens, labels, label_lens,
-                       ab_ws, logp, loss, (bf16_t*)grad, T, N, K, Lmax, SPmax, blank, zero_inf);
+                       ab_ws, logp, loss, (bf16_t*)grad, T, N, K, Lmax, SPS, blank, zero_inf);
   else
     hipLaunchKernelGGL(ctc_grad_kernel<float>, g4, dim3(256), 0, st, (const float*)logits, lens, labels, label_lens,
-                       ab_ws, logp, loss, (float*)grad, T, N, K, Lmax, SPmax, blank, zero_inf);
+                       ab_ws, logp, loss, (float*)grad, T, N, K, Lmax, SPS, blank, zero_inf);
   return (int)hipGetLastError();
 }
 

@@ -194,19 +194,23 @@ class DeepSpeech2(nn.Module):
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
 
-    def flops_per_step(self, N: int, T: int) -> float:
-        """Analytic training FLOPs (fwd + 2x bwd) for a [N, T] batch."""
+    def flops_breakdown(self, N: int, T: int) -> Dict[str, float]:
+        """Analytic forward FLOPs per layer for a [N, T] batch (the reference's tfprof
+        flops.log, src/deepSpeech_train.py:368-372)."""
         t1, t2 = conv_out_len(T)
         f1, f2 = freq_out(self.freq_bins)
         C, H, G = self.num_filters, self.num_hidden, GATES[self.cell]
         dirs = 2 if self.bidirectional else 1
-        fwd = 2.0 * N * t1 * f1 * C * 100                     # conv1
-        fwd += 2.0 * N * t2 * f2 * C * C * 50                  # conv2
+        out = {"conv1": 2.0 * N * t1 * f1 * C * 100, "conv2": 2.0 * N * t2 * f2 * C * C * 50}
         for i, layer in enumerate(self.rnn):
             in_dim = layer.fw.W.shape[1]
-            fwd += dirs * 2.0 * N * t2 * G * H * (in_dim + H)
-        fwd += 2.0 * N * t2 * H * self.num_classes
-        return 3.0 * fwd
+            out["rnn_cell_%d" % i] = dirs * 2.0 * N * t2 * G * H * (in_dim + H)
+        out["softmax_linear"] = 2.0 * N * t2 * H * self.num_classes
+        return out
+
+    def flops_per_step(self, N: int, T: int) -> float:
+        """Analytic training FLOPs (fwd + 2x bwd) for a [N, T] batch."""
+        return 3.0 * sum(self.flops_breakdown(N, T).values())
 
     # ------------------------------------------------------------------ forward
     def frontend(self, feats: torch.Tensor) -> torch.Tensor:
@@ -214,21 +218,26 @@ class DeepSpeech2(nn.Module):
         if self.engine == "hip":
             from ..ops import frontend as FE
             return FE.frontend_hip(self, feats)
+        from ..utils import trace as TR
         x = feats.unsqueeze(1)
-        x = self.conv1.forward_ref(x)
-        x = self.conv2.forward_ref(x)
+        with TR.phase(TR.conv(1)):
+            x = self.conv1.forward_ref(x)
+        with TR.phase(TR.conv(2)):
+            x = self.conv2.forward_ref(x)
         N, C, T2, F2 = x.shape
         return x.permute(2, 0, 1, 3).reshape(T2, N, C * F2)
 
     def recurrent(self, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
         inp = x
         out = x
-        for layer in self.rnn:
+        for i, layer in enumerate(self.rnn):
             if self.engine == "hip":
                 from ..ops import rnn as RNN
-                out = RNN.recurrent_layer_hip(layer, inp, lens)
+                out = RNN.recurrent_layer_hip(layer, inp, lens, i)
             else:
-                out = layer.forward_ref(inp, lens)
+                from ..utils import trace as TR
+                with TR.phase(TR.rnn_cell(i)):
+                    out = layer.forward_ref(inp, lens)
             inp = out if self.stack_fix else x
         return out
 
@@ -243,10 +252,9 @@ class DeepSpeech2(nn.Module):
             dirs = [("fw", layer.fw)] + ([("bw", layer.bw)] if layer.bw is not None else [])
             groups.append([(pre + n + ".W", d.W) for n, d in dirs])
             groups.append([(pre + n + ".b", d.b) for n, d in dirs])
-            for n, d in dirs:
-                groups.append([(pre + n + ".U", d.U)])
-                if d.b_h is not None:
-                    groups.append([(pre + n + ".b_h", d.b_h)])
+            groups.append([(pre + n + ".U", d.U) for n, d in dirs])
+            if layer.fw.b_h is not None:
+                groups.append([(pre + n + ".b_h", d.b_h) for n, d in dirs])
         for cname in ("conv2", "conv1"):
             blk = getattr(self, cname)
             for pn in ("bn_beta", "bn_gamma", "bias", "weight"):
@@ -256,7 +264,9 @@ class DeepSpeech2(nn.Module):
     def head(self, h: torch.Tensor) -> torch.Tensor:
         if self.engine == "hip":
             from ..ops.frontend import FusedHead
-            return FusedHead.apply(h, self.fc_weight, self.fc_bias)
+            from ..utils import trace as TR
+            with TR.phase(TR.SOFTMAX_F):
+                return FusedHead.apply(h, self.fc_weight, self.fc_bias)
         T, N, H = h.shape
         w = self.fc_weight.to(h.dtype)
         b = self.fc_bias.to(h.dtype)
@@ -285,7 +295,9 @@ class DeepSpeech2(nn.Module):
         if self.engine == "hip":
             from ..ops import ctc as CTC
             return CTC.ctc_loss_hip(logits, lens, targets, target_lens).mean()
-        return R.ctc_loss_ref(logits, targets, lens, target_lens).mean()
+        from ..utils import trace as TR
+        with TR.phase(TR.CTC_F):
+            return R.ctc_loss_ref(logits, targets, lens, target_lens).mean()
 
 
 def build_model(**kw) -> DeepSpeech2:

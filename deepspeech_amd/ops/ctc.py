@@ -9,6 +9,7 @@ import torch
 
 from .. import BLANK
 from . import _ext
+from ..utils import trace as TR
 
 
 class CTCLossFused(torch.autograd.Function):
@@ -38,7 +39,12 @@ class CTCLossFused(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gloss):
-        (grad,) = ctx.saved_tensors
+        with TR.phase(TR.CTC_B):
+            (grad,) = ctx.saved_tensors
+            return CTCLossFused._scale(grad, gloss)
+
+    @staticmethod
+    def _scale(grad, gloss):
         g = grad * gloss.to(grad.dtype).view(1, -1, 1)
         return g, None, None, None, None, None
 
@@ -46,4 +52,5 @@ class CTCLossFused(torch.autograd.Function):
 def ctc_loss_hip(logits: torch.Tensor, lens: torch.Tensor, labels: torch.Tensor,
                  label_lens: torch.Tensor, blank: int = BLANK, zero_infinity: bool = True) -> torch.Tensor:
     """Per-utterance CTC loss [N] (fp32)."""
-    return CTCLossFused.apply(logits, lens, labels, label_lens, blank, zero_infinity)
+    with TR.phase(TR.CTC_F):
+        return CTCLossFused.apply(logits, lens, labels, label_lens, blank, zero_infinity)

@@ -11,6 +11,7 @@ import torch.nn.functional as F
 
 from . import _ext
 from .optim import arena_of, emit_grad
+from ..utils import trace as TR
 
 BN_EPS = 1e-3
 BN_MOMENTUM = 0.01
@@ -20,7 +21,7 @@ class BNClip(torch.autograd.Function):
     """out = clip(BN_train(y) * gamma + beta, 0, 20); layout 0 = NCHW, 1 = [T, N, C*F]."""
 
     @staticmethod
-    def forward(ctx, y, gamma, beta, run_mean, run_var, training: bool, layout: int, out_dtype):
+    def forward(ctx, y, gamma, beta, run_mean, run_var, training: bool, layout: int, out_dtype, idx: int = 0):
         C_ = _ext.ext()
         y = y.contiguous()
         N, C, T, Fd = y.shape
@@ -46,12 +47,18 @@ class BNClip(torch.autograd.Function):
         ctx.g_param, ctx.b_param = gamma_p, beta_p
         ctx.layout = layout
         ctx.training = training
+        ctx.idx = idx
         return out
 
     @staticmethod
     def backward(ctx, dout):
         if not ctx.training:
             raise RuntimeError("BNClip backward is only defined in training mode")
+        with TR.phase(TR.bn(ctx.idx, True)):
+            return BNClip._backward(ctx, dout)
+
+    @staticmethod
+    def _backward(ctx, dout):
         C_ = _ext.ext()
         y, mean, invstd, gamma, beta = ctx.saved_tensors
         N, C, T, Fd = y.shape
@@ -62,7 +69,7 @@ class BNClip(torch.autograd.Function):
         dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
         dy = torch.empty_like(y)
         C_.bn_bwd(dout, y, mean, invstd, gamma, beta, part, dgamma, dbeta, dy, ctx.layout)
-        return dy, emit_grad(ctx.g_param, dgamma), emit_grad(ctx.b_param, dbeta), None, None, None, None, None
+        return dy, emit_grad(ctx.g_param, dgamma), emit_grad(ctx.b_param, dbeta), None, None, None, None, None, None
 
 
 class ConvFused(torch.autograd.Function):
@@ -73,7 +80,7 @@ class ConvFused(torch.autograd.Function):
     gradient), so no reduction is launched for it in training mode."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, bias_grad_zero: bool):
+    def forward(ctx, x, weight, bias, stride, bias_grad_zero: bool, idx: int = 0):
         w16 = weight.bf16 if arena_of(weight) is not None else weight.to(torch.bfloat16)
         b16 = bias.bf16 if arena_of(bias) is not None else bias.to(torch.bfloat16)
         x16 = x.to(torch.bfloat16)
@@ -82,10 +89,16 @@ class ConvFused(torch.autograd.Function):
         ctx.stride = stride
         ctx.params = (weight, bias)
         ctx.bias_grad_zero = bias_grad_zero
+        ctx.idx = idx
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        with TR.phase(TR.conv(ctx.idx, True)):
+            return ConvFused._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         x16, w16 = ctx.saved_tensors
         weight, bias = ctx.params
         need_x = ctx.needs_input_grad[0]
@@ -102,20 +115,22 @@ class ConvFused(torch.autograd.Function):
                 gb_out = torch.zeros_like(bias)
         else:
             gb_out = emit_grad(bias, gb.float())
-        return (gi if need_x else None), gw_out, gb_out, None, None
+        return (gi if need_x else None), gw_out, gb_out, None, None, None
 
 
-def conv_block_hip(block, x: torch.Tensor, layout: int) -> torch.Tensor:
+def conv_block_hip(block, x: torch.Tensor, layout: int, idx: int) -> torch.Tensor:
     dt = torch.bfloat16
-    y = ConvFused.apply(x, block.weight, block.bias, tuple(block.stride), bool(block.training))
-    return BNClip.apply(y, block.bn_gamma, block.bn_beta, block.running_mean, block.running_var,
-                        block.training, layout, dt)
+    with TR.phase(TR.conv(idx)):
+        y = ConvFused.apply(x, block.weight, block.bias, tuple(block.stride), bool(block.training), idx)
+    with TR.phase(TR.bn(idx)):
+        return BNClip.apply(y, block.bn_gamma, block.bn_beta, block.running_mean, block.running_var,
+                            block.training, layout, dt, idx)
 
 
 def frontend_hip(model, feats: torch.Tensor) -> torch.Tensor:
     x = feats.unsqueeze(1)
-    x = conv_block_hip(model.conv1, x, 0)
-    return conv_block_hip(model.conv2, x, 1)
+    x = conv_block_hip(model.conv1, x, 0, 1)
+    return conv_block_hip(model.conv2, x, 1, 2)
 
 
 class FusedHead(torch.autograd.Function):
@@ -134,6 +149,11 @@ class FusedHead(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        with TR.phase(TR.SOFTMAX_B):
+            return FusedHead._backward(ctx, dout)
+
+    @staticmethod
+    def _backward(ctx, dout):
         h2, w16 = ctx.saved_tensors
         weight, bias = ctx.params
         T, N, K = dout.shape

@@ -27,6 +27,7 @@ import torch
 from . import _ext
 from . import reference as R
 from .optim import arena_of, emit_grad, mm_into
+from ..utils import trace as TR
 
 CELL_CODE = {"rnn_relu": 0, "gru": 1}
 GATES = {"rnn_relu": 1, "gru": 3}
@@ -393,7 +394,7 @@ class FusedBiLayer(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, lens, plan: RnnPlan, alpha: float, W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b):
+    def forward(ctx, x, lens, plan: RnnPlan, alpha: float, idx: int, W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b):
         T, N, D = x.shape
         dirs_W = [W_f] + ([W_b] if W_b is not None else [])
         dirs_b = [b_f] + ([b_b] if b_b is not None else [])
@@ -412,10 +413,16 @@ class FusedBiLayer(torch.autograd.Function):
         ctx.params = (W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b)
         ctx.plan = plan
         ctx.alpha = alpha
+        ctx.idx = idx
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        with TR.phase(TR.rnn_cell(ctx.idx, True)):
+            return FusedBiLayer._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         x16, lens, W16, U_f16, U_b16, hx, hs, gates = ctx.saved_tensors
         plan: RnnPlan = ctx.plan
         W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b = ctx.params
@@ -441,14 +448,27 @@ class FusedBiLayer(torch.autograd.Function):
                     arena.grad_done(p)
                 gW[d] = g
         gU = [None, None]
-        for d, p in enumerate([U_f, U_b] if d1 else [U_f]):
-            g = _dU(dgh, hx, d, plan, p)
-            if g is None:
-                arena.grad_done(p)
-            gU[d] = g
+        ugrp = arena.group_view([U_f, U_b], "grad") if (arena is not None and d1) else None
+        if ugrp is not None and arena.first_write(U_f) and arena.first_write(U_b):
+            # both directions' dU_d = dgh_d^T h_d as ONE batched GEMM into the packed slots
+            steps = dgh.shape[1]
+            g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
+            h3 = hx[:, :steps].reshape(2, steps * plan.NP, plan.H)
+            out = ugrp.view(2, GH, plan.H)
+            try:
+                torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
+            except (RuntimeError, TypeError):
+                out.copy_(torch.bmm(g3, h3))
+            arena.grad_done(U_f, U_b)
+        else:
+            for d, p in enumerate([U_f, U_b] if d1 else [U_f]):
+                g = _dU(dgh, hx, d, plan, p)
+                if g is None:
+                    arena.grad_done(p)
+                gU[d] = g
         gb = _bias_grads([b_f, b_b] if d1 else [b_f], parts[0])
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
-        return (dx, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
+        return (dx, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
 
 
 _plan_cache = {}
@@ -490,13 +510,18 @@ def input_projection_hip(layer, x: torch.Tensor, lens: torch.Tensor) -> torch.Te
     return gx.view(T, N, -1)
 
 
-def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int = 0) -> torch.Tensor:
+    with TR.phase(TR.rnn_cell(idx)):
+        return _recurrent_layer_hip(layer, x, lens, idx)
+
+
+def _recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int) -> torch.Tensor:
     ndir = 2 if layer.bw is not None else 1
     plan = plan_for(x.shape[1], layer.hidden, layer.cell, ndir, x.device)
     fw, bw = layer.fw, layer.bw
     if layer.seq_bn in ("frozen", "none"):
         alpha = sbn_scale() if layer.seq_bn == "frozen" else 1.0
-        return FusedBiLayer.apply(x, lens, plan, alpha, fw.W, bw.W if bw is not None else None,
+        return FusedBiLayer.apply(x, lens, plan, alpha, idx, fw.W, bw.W if bw is not None else None,
                                   fw.U, bw.U if bw is not None else None,
                                   fw.b, bw.b if bw is not None else None,
                                   fw.b_h, bw.b_h if bw is not None else None)

@@ -81,6 +81,31 @@ def build_data(args, ctx, train_dir):
     return src, src.steps_per_epoch()
 
 
+def write_debug_reports(prof, model, args, dev) -> None:
+    """--debug outputs (reference src/deepSpeech_train.py:358-380: chrome trace + tfprof
+    params / flops / timing logs): profiling.json, params.log, flops.log, profile_ops.txt
+    and the per-layer breakdown profile_layers.txt (deepspeech_amd/utils/prof.py)."""
+    from .utils import prof as P
+    d = args.train_dir
+    trace = os.path.join(d, "profiling.json")
+    prof.export_chrome_trace(trace)
+    with open(os.path.join(d, "profile_ops.txt"), "w") as f:
+        f.write(prof.key_averages().table(sort_by="self_cuda_time_total" if dev.type == "cuda"
+                                          else "self_cpu_time_total", row_limit=80))
+    with open(os.path.join(d, "params.log"), "w") as f:
+        tot = 0
+        for n, p in model.named_parameters():
+            f.write("%-40s %-20s %d\n" % (n, tuple(p.shape), p.numel()))
+            tot += p.numel()
+        f.write("total trainable params: %d\n" % tot)
+    with open(os.path.join(d, "flops.log"), "w") as f:
+        for name, fl in model.flops_breakdown(args.batch_size, 1000).items():
+            f.write("%-24s %.3f GFLOP (fwd, per batch of %d x 10 s)\n" % (name, fl / 1e9, args.batch_size))
+    out, _ = P.analyse(P.load_events(trace))
+    with open(os.path.join(d, "profile_layers.txt"), "w") as f:
+        f.write(P.format_table(out) + "\n")
+
+
 def main(argv=None) -> int:
     args = C.parse_train_args(argv)
     ctx = init_distributed(args.device)
@@ -137,6 +162,8 @@ def main(argv=None) -> int:
         data_time = time.time() - t0
         if args.debug and step == 20:
             from torch.profiler import ProfilerActivity, profile
+            from .utils import trace as TR
+            TR.enable(True)
             prof = profile(activities=[ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if dev.type == "cuda" else []),
                            record_shapes=False)
             prof.__enter__()
@@ -151,11 +178,10 @@ def main(argv=None) -> int:
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             prof.__exit__(None, None, None)
+            from .utils import trace as TR
+            TR.enable(False)
             if ctx.is_main:
-                prof.export_chrome_trace(os.path.join(args.train_dir, "profiling.json"))
-                with open(os.path.join(args.train_dir, "profile_ops.txt"), "w") as f:
-                    f.write(prof.key_averages().table(sort_by="self_cuda_time_total" if dev.type == "cuda"
-                                                      else "self_cpu_time_total", row_limit=80))
+                write_debug_reports(prof, model, args, dev)
             prof = None
         do_log = (step > 10 and step % args.log_every == 0) or step + 1 == args.max_steps
         do_sum = ctx.is_main and step % args.summary_every == 0

@@ -25,6 +25,7 @@ import torch
 from .models import DeepSpeech2
 from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
 from .parallel.grad_sync import GradBucketer, broadcast_params
+from .utils import trace as TR
 
 
 @dataclass
@@ -79,13 +80,15 @@ class Trainer:
         logits, lens = model(batch["feats"], batch["seq_lens"])
         loss = model.loss(logits, lens, batch["labels"], batch["label_lens"])
         loss.backward()
-        self.bucketer.finish()
+        with TR.phase(TR.ALLREDUCE):
+            self.bucketer.finish()
         gscale = 1.0 / self.world
         skip = None
         if self.nan_policy == "skip":
             _, skip = self.opt.grad_norm_and_finite(gscale)
             self.last_skip = skip
-        self.opt.step(self.lr, self.global_step, gscale=gscale, skip_flag=skip)
+        with TR.phase(TR.EMA):
+            self.opt.step(self.lr, self.global_step, gscale=gscale, skip_flag=skip)
         self.global_step += 1
         return loss.detach()
 

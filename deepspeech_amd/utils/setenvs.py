@@ -1,0 +1,61 @@
+"""Per-platform process environment (reference: src/setenvs.py, which pins KMP/OMP/MKL
+threads for Intel KNL / Broadwell before the TF session starts).
+
+MI355X equivalents, applied BEFORE torch is imported (the reference applied its settings
+after importing TensorFlow, so its OMP values could not take effect — quirk noted in
+SURVEY §5.6; the CLI shims deepSpeech_train.py / deepSpeech_test.py call this first):
+
+  mi355x  HSA_ENABLE_IPC_MODE_LEGACY=0   dmabuf IPC for RCCL / cross-process tensors
+          HIP_FORCE_DEV_KERNARG=1        kernel arguments in device memory (lower launch
+                                         latency for the many small launches of a step)
+          TORCH_NCCL_HIGH_PRIORITY=1     RCCL on high-priority streams, so bucketed gradient
+                                         all-reduces overlap BPTT instead of queuing behind it
+          OMP_NUM_THREADS                host threads for the loader / featurizer (8)
+  knl/bdw the reference's Intel settings, kept for command-line compatibility.
+
+Existing values in the environment always win (setdefault), so a launcher can override.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+PLATFORMS: Dict[str, Dict[str, str]] = {
+    "mi355x": {
+        "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+        "HIP_FORCE_DEV_KERNARG": "1",
+        "TORCH_NCCL_HIGH_PRIORITY": "1",
+        "OMP_NUM_THREADS": "8",
+    },
+    "bdw": {
+        "KMP_BLOCKTIME": "1", "KMP_SETTINGS": "1", "OMP_NUM_THREADS": "8", "MKL_NUM_THREADS": "8",
+        "OMP_DYNAMIC": "false", "KMP_AFFINITY": "granularity=fine,verbose,compact,1,0",
+    },
+    "knl": {
+        "KMP_BLOCKTIME": "0", "KMP_SETTINGS": "1", "OMP_NUM_THREADS": "8", "MKL_NUM_THREADS": "8",
+        "OMP_DYNAMIC": "false", "KMP_AFFINITY": "granularity=fine,verbose,explicit,proclist=[4-67]",
+    },
+}
+
+
+def platform_from_argv(argv: List[str], default: str = "mi355x") -> str:
+    for i, a in enumerate(argv[:-1]):
+        if a == "--platform":
+            return argv[i + 1]
+        if a.startswith("--platform="):
+            return a.split("=", 1)[1]
+    return default
+
+
+def setenvs(argv: Optional[List[str]] = None, platform: Optional[str] = None) -> Dict[str, str]:
+    """Apply the platform's environment (existing variables are kept). Returns what was set."""
+    import sys
+    plat = platform or platform_from_argv(list(argv if argv is not None else sys.argv))
+    if plat not in PLATFORMS:
+        raise ValueError("unknown platform %r (expected one of %s)" % (plat, sorted(PLATFORMS)))
+    applied = {}
+    for k, v in PLATFORMS[plat].items():
+        if k not in os.environ:
+            os.environ[k] = v
+            applied[k] = v
+    return applied

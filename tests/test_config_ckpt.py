@@ -118,3 +118,63 @@ def test_eval_restores_ema_weights(tmp_path):
     CK.load_model_from_tf(m, {k: v for k, v in data.items() if torch.is_tensor(v)}, use_ema=True)
     ema = t.arena.views(t.opt.ema)
     assert torch.allclose(m.fc_weight, ema["fc_weight"])
+
+
+def test_debug_step_writes_profiles_and_tools_parse_them(tmp_path):
+    """--debug (reference src/deepSpeech_train.py:358-380): chrome trace + params / flops /
+    per-layer reports at step 20; tools/prof.py and tools/parse_log.py read them."""
+    import subprocess
+    import sys
+    from deepspeech_amd import train as T
+    d = tmp_path / "run"
+    rc = T.main(["--train_dir", str(d), "--dummy", "True", "--max_steps", "22", "--batch_size", "2",
+                 "--num_hidden", "32", "--num_rnn_layers", "2", "--debug", "True", "--device", "cpu",
+                 "--checkpoint_every", "100", "--summary_every", "100", "--engine", "ref"])
+    assert rc == 0
+    for f in ("profiling.json", "params.log", "flops.log", "profile_layers.txt", "profile_ops.txt"):
+        assert (d / f).exists(), f
+    layers = (d / "profile_layers.txt").read_text()
+    assert "rnn_forward_cell_0" in layers and "conv1_forward" in layers, layers
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "prof.py"), "-i", str(d / "profiling.json"),
+                        "-o", str(tmp_path / "Output")], capture_output=True, text=True)
+    assert r.returncode == 0 and "rnn_forward_cell_1" in r.stdout, r.stderr
+    assert (tmp_path / "Output" / "layers_exeTime.csv").exists()
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "parse_log.py"), "--train_dir", str(d)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and (d / "prf1.txt").exists() and "rnn_cell_0" in (d / "prf1.txt").read_text()
+
+
+def test_launch_scripts_train_then_test(tmp_path):
+    """scripts/train.sh and scripts/test.sh (reference src/train.sh, src/test.sh) end to end
+    on CPU with synthetic data; the config guard rejects unknown engines."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, dummy="True", engine="ref", layers="1", hidden="32", cell="gru",
+               train_dir=str(tmp_path / "train"),
+               extra_args="--max_steps 3 --batch_size 2 --device cpu --checkpoint_every 1")
+    r = subprocess.run(["bash", os.path.join(root, "scripts", "train.sh")], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert (tmp_path / "train" / "deepSpeech_parameters.json").exists()
+    env2 = dict(os.environ, engine="ref", checkpoint_dir=str(tmp_path / "train"),
+                extra_args="--dummy True --num_examples 2 --batch_size 2 --device cpu --eval_dir %s"
+                           % (tmp_path / "eval"))
+    r = subprocess.run(["bash", os.path.join(root, "scripts", "test.sh")], env=env2, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and "char_err_rate" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    bad = dict(env, engine="cuda")
+    r = subprocess.run(["bash", os.path.join(root, "scripts", "train.sh")], env=bad, capture_output=True, text=True)
+    assert r.returncode != 0 and "unsupported" in r.stdout
+
+
+def test_setenvs_platforms(monkeypatch):
+    from deepspeech_amd.utils import setenvs as S
+    monkeypatch.delenv("HIP_FORCE_DEV_KERNARG", raising=False)
+    got = S.setenvs(["x", "--platform", "mi355x"])
+    assert os.environ["HIP_FORCE_DEV_KERNARG"] == "1" and "HIP_FORCE_DEV_KERNARG" in got
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    S.setenvs([], platform="knl")
+    assert os.environ["OMP_NUM_THREADS"] == "3"          # existing values win
+    with pytest.raises(ValueError):
+        S.setenvs([], platform="pentium")

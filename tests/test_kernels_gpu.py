@@ -179,7 +179,7 @@ def test_bn_clip(cuda, layout, dtype):
     rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
     yh = y.clone().requires_grad_(True)
     gh, bh = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
-    out = BNClip.apply(yh, gh, bh, rm, rv, True, layout, dtype)
+    out = BNClip.apply(yh, gh, bh, rm, rv, True, layout, dtype, 1)
     yr = y.float().clone().requires_grad_(True)
     gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
     ref = R.clipped_relu(F.batch_norm(yr, None, None, gr, br, training=True, eps=BN_EPS))
