@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--bucket_mb", type=float, default=32.0)
     p.add_argument("--allreduce_bf16", action="store_true")
     p.add_argument("--profile_dir", type=str, default="", help="write a torch.profiler trace here")
+    p.add_argument("--fp8", action="store_true",
+                   help="fp8 e4m3 input projections (BASELINE config 5; NOT the headline bf16 number)")
     return p.parse_args()
 
 
@@ -64,7 +66,7 @@ def main():
                         num_rnn_layers=args.num_rnn_layers, cell=args.cell, bidirectional=True,
                         stack_fix=True, seq_bn="frozen").to(dev)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
-    model.set_engine(args.engine, dtype)
+    model.set_engine(args.engine, dtype, fp8=bool(args.fp8 and args.engine == "hip"))
     trainer = Trainer(model, LRSchedule(1e-4, 10 ** 9, 0.9), moving_avg_decay=0.9999,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
                       allreduce_bf16=args.allreduce_bf16)
@@ -124,7 +126,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "dtype": ("fp8(proj)+bf16" if args.fp8 else "bf16") if dtype == torch.bfloat16 else "fp32",
             "data": "synthetic (LibriSpeech-shaped spectrograms, random-init weights)",
             "config": {
                 "model": "DeepSpeech2 2xconv(32) + %dx%s-%d bidirectional + CTC" % (

@@ -1,0 +1,148 @@
+"""Streaming inference (BASELINE.json north-star config 4: unidirectional GRU + CTC
+beam-search decoder, real-time factor on one MI355X).
+
+The reference only evaluates whole utterances (src/deepSpeech_test.py:112-136, greedy
+CTC on a bidirectional model). A unidirectional model (``rnn_type='uni-dir'``, which the
+reference's NHWC path supports: src/deepSpeech.py:173-183) can instead run on audio as it
+arrives:
+
+  * conv front-end: output frame t2 sees input frames [4*t2, 4*t2 + 38) (two strided VALID
+    convs, kernel 20 / 10, stride 2 / 2 in time), so each chunk re-runs the convs on the
+    38-frame-overlapping slice that produces exactly the NEW output frames; BatchNorm is in
+    inference mode (running statistics), so frames are independent;
+  * recurrent stack: every layer carries its final hidden state to the next chunk (the
+    persistent kernels start from an initial state: ops/rnn.py:recurrent_layer_infer);
+  * head + log-softmax per new frame; greedy decoding collapses across chunk boundaries
+    incrementally, prefix beam search (native runtime) runs over all frames at the end.
+
+Batched streams: ``StreamingRecognizer`` takes [B, T_chunk, F] chunks of B concurrent
+streams (equal chunk schedule, per-stream valid lengths), which is how a server batches.
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import BLANK
+from .models.deepspeech2 import DeepSpeech2, conv_out_len
+from .ops import reference as R
+
+RECEPTIVE = 38     # input frames seen by one output frame (see module docstring)
+STRIDE = 4         # input frames per output frame
+
+
+def frames_out(T: int) -> int:
+    return conv_out_len(T)[1] if T >= RECEPTIVE else 0
+
+
+class StreamingRecognizer:
+    def __init__(self, model: DeepSpeech2, decoder: str = "greedy", beam_width: int = 16, batch: int = 1):
+        if model.bidirectional:
+            raise ValueError("streaming needs a unidirectional model (rnn_type='uni-dir')")
+        self.model = model.eval()
+        self.decoder = decoder
+        self.beam_width = beam_width
+        self.B = batch
+        self.dev = model.fc_weight.device
+        self.reset()
+
+    def reset(self) -> None:
+        self.buf = torch.zeros(self.B, 0, self.model.freq_bins, device=self.dev)
+        self.buf_start = 0                  # absolute frame index of buf[:, 0]
+        self.total = 0                      # frames received
+        self.done = 0                       # output (post-conv) frames emitted
+        self.states: List[Optional[torch.Tensor]] = [None] * len(self.model.rnn)
+        self.logprobs: List[torch.Tensor] = []
+        self.last_sym = [-1] * self.B
+        self.greedy: List[List[int]] = [[] for _ in range(self.B)]
+        self.compute_s = 0.0
+
+    @torch.no_grad()
+    def accept(self, chunk: torch.Tensor) -> List[List[int]]:
+        """Feed [B, T_c, F] feature frames; returns the newly decoded (greedy) labels per stream."""
+        t0 = time.perf_counter()
+        m = self.model
+        chunk = chunk.to(self.dev, torch.float32)
+        self.buf = torch.cat([self.buf, chunk], 1)
+        self.total += chunk.shape[1]
+        t2_total = frames_out(self.total)
+        new = t2_total - self.done
+        out: List[List[int]] = [[] for _ in range(self.B)]
+        if new <= 0:
+            return out
+        lo = STRIDE * self.done - self.buf_start
+        hi = STRIDE * (t2_total - 1) + RECEPTIVE - self.buf_start
+        feats = self.buf[:, lo:hi]
+        if m.engine == "hip":
+            feats = feats.to(m.compute_dtype)
+        x = m.frontend(feats)                                  # [new, B, C*F2]
+        assert x.shape[0] == new, (x.shape, new)
+        lens = torch.full((self.B,), new, dtype=torch.int32, device=self.dev)
+        for i, layer in enumerate(m.rnn):
+            x, self.states[i] = self._layer(layer, x, lens, self.states[i])
+            if not m.stack_fix:
+                raise ValueError("streaming requires stack_fix=True")
+        logits = m.head(x).float()
+        lp = torch.log_softmax(logits, -1)                     # [new, B, K]
+        self.logprobs.append(lp)
+        best = lp.argmax(-1).cpu().numpy()                     # [new, B]
+        for b in range(self.B):
+            for t in range(best.shape[0]):
+                s = int(best[t, b])
+                if s != self.last_sym[b] and s != BLANK:
+                    out[b].append(s)
+                self.last_sym[b] = s
+            self.greedy[b].extend(out[b])
+        self.done = t2_total
+        # keep only the input frames future outputs can still see
+        keep_from = STRIDE * self.done
+        if keep_from > self.buf_start:
+            self.buf = self.buf[:, keep_from - self.buf_start:]
+            self.buf_start = keep_from
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+        self.compute_s += time.perf_counter() - t0
+        return out
+
+    def _layer(self, layer, x, lens, h0):
+        m = self.model
+        if m.engine == "hip":
+            from .ops import rnn as RNN
+            y, h = RNN.recurrent_layer_infer(layer, x, lens, None if h0 is None else h0.unsqueeze(0))
+            return y, h[0]
+        gx = layer.input_projection_ref(x, layer.fw, lens)
+        bh = layer.fw.b_h.to(x.dtype) if layer.fw.b_h is not None else None
+        y, h = R.recurrent_scan(layer.cell, gx, layer.fw.U.to(x.dtype), bh, lens, h0)
+        return y, h
+
+    @torch.no_grad()
+    def finish(self) -> List[List[int]]:
+        """Final transcript label ids per stream (beam search over the whole stream if the
+        decoder is 'beam', otherwise the incremental greedy result)."""
+        if self.decoder != "beam" or not self.logprobs:
+            return [list(g) for g in self.greedy]
+        t0 = time.perf_counter()
+        from .runtime import native
+        lp = torch.cat(self.logprobs, 0).cpu().numpy()        # [T2, B, K]
+        lens = np.full((self.B,), lp.shape[0], dtype=np.int32)
+        res = native.load().beam_search_batch(lp, lens, self.beam_width, BLANK, -10.0)
+        self.compute_s += time.perf_counter() - t0
+        return res
+
+
+def rtf(model: DeepSpeech2, seconds: float = 10.0, chunk_s: float = 1.0, batch: int = 1,
+        decoder: str = "greedy", beam_width: int = 16, seed: int = 0):
+    """Real-time factor of streaming synthetic audio: compute time / audio time (per stream;
+    ``batch`` streams are processed together). Returns (rtf, transcripts)."""
+    g = torch.Generator().manual_seed(seed)
+    T = int(round(seconds * 100))
+    feats = torch.randn(batch, T, model.freq_bins, generator=g)
+    rec = StreamingRecognizer(model, decoder=decoder, beam_width=beam_width, batch=batch)
+    step = max(1, int(round(chunk_s * 100)))
+    for s in range(0, T, step):
+        rec.accept(feats[:, s:s + step])
+    res = rec.finish()
+    return rec.compute_s / seconds, res

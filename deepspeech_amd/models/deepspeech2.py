@@ -184,11 +184,19 @@ class DeepSpeech2(nn.Module):
         self.compute_dtype = torch.float32
 
     # ------------------------------------------------------------------ config
-    def set_engine(self, engine: str, compute_dtype: torch.dtype = torch.float32) -> "DeepSpeech2":
+    def set_engine(self, engine: str, compute_dtype: torch.dtype = torch.float32, fp8: bool = False) -> "DeepSpeech2":
+        """engine: 'ref' (pure torch) | 'hip' (gfx950 kernels). fp8=True (HIP engine only):
+        the recurrent layers' input projections run as fp8 e4m3 scaled GEMMs (BASELINE
+        config 5); activations, recurrence and gradients stay bf16."""
         if engine not in ("ref", "hip"):
             raise ValueError(engine)
+        if fp8 and engine != "hip":
+            raise ValueError("fp8 projections need the HIP engine")
         self.engine = engine
         self.compute_dtype = compute_dtype
+        self.fp8 = fp8
+        for layer in self.rnn:
+            layer.fp8 = fp8
         return self
 
     def num_params(self) -> int:

@@ -209,9 +209,10 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return torch.mm(a, b).float()
 
 
-def _run_fwd(gx, lens, U, bh, plan: RnnPlan):
+def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     """Launch the persistent forward recurrence over gx [T, N, ndir*G*H] (bf16).
     U / bh: per-direction lists (bf16 [G*H, H] / fp32 [G*H] or None).
+    h0: optional initial state [ndir, N, H] (streaming state carry; zeros otherwise).
     Returns (y [T, N, H] bf16 = sum of directions, saved-state tuple)."""
     C = _ext.ext()
     T, N, gstride = gx.shape
@@ -225,6 +226,9 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan):
     hx[:, 0].zero_()                         # h0
     hs = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=torch.float32)
     hs[:, 0].zero_()
+    if h0 is not None:
+        hs[:, 0, :N].copy_(h0)
+        hx[:, 0, :N].copy_(h0)
     gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
              if plan.cell == "gru" else None)
     err = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -346,6 +350,25 @@ class BiRecurrence(torch.autograd.Function):
                 gb[0], gb[1] if d1 else None, None)
 
 
+FP8_MAX = 448.0      # OCP e4m3 (gfx950 MFMA fp8 is OCP e4m3fn, not MI300's fnuz)
+
+
+def fp8_linear(x2: torch.Tensor, W16: torch.Tensor, b16: torch.Tensor, alpha: float) -> torch.Tensor:
+    """alpha * x2 @ W16^T + b16 with both operands quantised to fp8 e4m3 (per-tensor
+    amax scaling, scales kept on the device: no host sync) and run as a hipBLASLt scaled
+    GEMM on the CDNA4 fp8 MFMA path; bf16 output. Forward-only precision reduction: the
+    backward GEMMs keep the bf16 copies (fp8 'mixed precision', BASELINE config 5)."""
+    if x2.shape[1] % 16 or W16.shape[0] % 16:
+        # hipBLASLt fp8 GEMMs need K and N multiples of 16: such layers stay bf16
+        return torch.addmm(b16, x2, W16.t(), alpha=alpha)
+    f8 = torch.float8_e4m3fn
+    sx = (x2.abs().amax().float() / FP8_MAX).clamp(min=1e-12)
+    sw = (W16.abs().amax().float() / FP8_MAX).clamp(min=1e-12)
+    x8 = (x2.float() / sx).clamp(-FP8_MAX, FP8_MAX).to(f8)
+    w8 = (W16.float() / sw).clamp(-FP8_MAX, FP8_MAX).to(f8)
+    return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw * alpha, bias=b16, out_dtype=torch.bfloat16)
+
+
 def _bf16_group(params):
     """bf16 tensor for the row-concatenation of ``params`` (all 2-D with equal columns, or
     all 1-D): a zero-copy view of the arena's bf16 shadow when they are packed there."""
@@ -394,7 +417,8 @@ class FusedBiLayer(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, lens, plan: RnnPlan, alpha: float, idx: int, W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b):
+    def forward(ctx, x, lens, plan: RnnPlan, alpha: float, idx: int, fp8: bool, W_f, W_b, U_f, U_b, b_f, b_b,
+                bh_f, bh_b):
         T, N, D = x.shape
         dirs_W = [W_f] + ([W_b] if W_b is not None else [])
         dirs_b = [b_f] + ([b_b] if b_b is not None else [])
@@ -402,7 +426,10 @@ class FusedBiLayer(torch.autograd.Function):
         b16 = _bf16_group(dirs_b)                     # [ndir*G*H]
         x16 = x.to(torch.bfloat16).contiguous()
         x2 = x16.view(T * N, D)
-        gx = torch.addmm(b16, x2, W16.t(), alpha=alpha).view(T, N, -1)
+        if fp8:
+            gx = fp8_linear(x2, W16, b16, alpha).view(T, N, -1)
+        else:
+            gx = torch.addmm(b16, x2, W16.t(), alpha=alpha).view(T, N, -1)
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
@@ -468,7 +495,7 @@ class FusedBiLayer(torch.autograd.Function):
                 gU[d] = g
         gb = _bias_grads([b_f, b_b] if d1 else [b_f], parts[0])
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
-        return (dx, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
+        return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
 
 
 _plan_cache = {}
@@ -510,6 +537,29 @@ def input_projection_hip(layer, x: torch.Tensor, lens: torch.Tensor) -> torch.Te
     return gx.view(T, N, -1)
 
 
+@torch.no_grad()
+def recurrent_layer_infer(layer, x: torch.Tensor, lens: torch.Tensor, h0: Optional[torch.Tensor] = None):
+    """Inference-only layer with state carry: returns (y [T, N, H], h_last [ndir, N, H] fp32).
+    h_last holds each row's state after its last valid step (the kernels freeze the state
+    past an utterance's length), which is what a streaming caller carries to the next chunk."""
+    ndir = 2 if layer.bw is not None else 1
+    T, N, _ = x.shape
+    plan = plan_for(N, layer.hidden, layer.cell, ndir, x.device)
+    dirs = layer.directions()
+    W16 = torch.cat([d.W for d in dirs], 0).to(torch.bfloat16)
+    b16 = torch.cat([d.b for d in dirs], 0).to(torch.bfloat16)
+    alpha = sbn_scale() if layer.seq_bn == "frozen" else 1.0
+    if layer.seq_bn == "batch":
+        gx = input_projection_hip(layer, x.to(torch.bfloat16), lens)
+    else:
+        gx = torch.addmm(b16, x.to(torch.bfloat16).reshape(T * N, -1), W16.t(), alpha=alpha).view(T, N, -1)
+    lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
+    U = [d.U.to(torch.bfloat16).contiguous() for d in dirs] + ([None] if ndir == 1 else [])
+    bh = [d.b_h.float().contiguous() if d.b_h is not None else None for d in dirs] + ([None] if ndir == 1 else [])
+    y, (hx, hs, gates) = _run_fwd(gx.contiguous(), lens, U, bh, plan, h0=h0)
+    return y, hs[:, T, :N].clone()
+
+
 def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int = 0) -> torch.Tensor:
     with TR.phase(TR.rnn_cell(idx)):
         return _recurrent_layer_hip(layer, x, lens, idx)
@@ -521,7 +571,8 @@ def _recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int) -
     fw, bw = layer.fw, layer.bw
     if layer.seq_bn in ("frozen", "none"):
         alpha = sbn_scale() if layer.seq_bn == "frozen" else 1.0
-        return FusedBiLayer.apply(x, lens, plan, alpha, idx, fw.W, bw.W if bw is not None else None,
+        return FusedBiLayer.apply(x, lens, plan, alpha, idx, bool(getattr(layer, "fp8", False)),
+                                  fw.W, bw.W if bw is not None else None,
                                   fw.U, bw.U if bw is not None else None,
                                   fw.b, bw.b if bw is not None else None,
                                   fw.b_h, bw.b_h if bw is not None else None)

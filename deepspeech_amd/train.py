@@ -126,7 +126,7 @@ def main(argv=None) -> int:
     ctx.barrier()
 
     model = DeepSpeech2(**C.model_kwargs_from_args(args)).to(dev)
-    model.set_engine(engine, dtype)
+    model.set_engine(engine, dtype, fp8=(args.dtype == "fp8" and engine == "hip"))
     data, steps_per_epoch = build_data(args, ctx, args.train_dir)
     trainer = Trainer(model, lr_schedule_from_args(args, steps_per_epoch), args.moving_avg_decay,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,

@@ -97,3 +97,42 @@ def test_hip_engine_trains(cuda):
     for _ in range(30):
         last = float(tr.step(batch))
     assert last < 0.8 * first, (first, last)
+
+
+def test_streaming_hip_matches_full_forward(cuda):
+    """Chunked streaming through the HIP engine (state carried between persistent-kernel
+    launches) reproduces the whole-utterance forward of the same engine."""
+    from deepspeech_amd.infer import StreamingRecognizer
+    torch.manual_seed(3)
+    m = DeepSpeech2(num_filters=8, num_hidden=128, num_rnn_layers=2, cell="gru", bidirectional=False).to(cuda)
+    m.set_engine("hip", torch.bfloat16)
+    m.eval()
+    T, B = 640, 3
+    feats = torch.randn(B, T, 161, device=cuda)
+    with torch.no_grad():
+        logits, _ = m(feats, torch.full((B,), T, dtype=torch.int32, device=cuda))
+    full = torch.log_softmax(logits.float(), -1)
+    rec = StreamingRecognizer(m, batch=B)
+    for s in range(0, T, 100):
+        rec.accept(feats[:, s:s + 100])
+    got = torch.cat(rec.logprobs, 0)
+    assert got.shape == full.shape
+    assert (got - full).abs().max() < 0.15, (got - full).abs().max()
+    assert _rel(got.exp(), full.exp()) < 3e-2
+
+
+def test_fp8_projection_close_to_bf16(cuda):
+    """fp8 e4m3 input projections (config 5): loss and gradients stay close to the bf16 engine."""
+    ref, hip = _pair(cuda, "gru", H=128, L=2)
+    hip8 = copy.deepcopy(hip)
+    hip8.set_engine("hip", torch.bfloat16, fp8=True)
+    batch = to_device(FixedShapeBatches(6, max_frames=260, seed=3, pool=1).next(), cuda)
+    l16 = _loss(hip, batch)
+    l16.backward()
+    l8 = _loss(hip8, batch)
+    l8.backward()
+    assert abs(float(l8) - float(l16)) / abs(float(l16)) < 5e-2, (float(l8), float(l16))
+    g16 = dict(hip.named_parameters())
+    for n, p in hip8.named_parameters():
+        if n.startswith("rnn.1") or n.startswith("fc"):
+            assert _rel(p.grad, g16[n].grad) < 0.25, n
