@@ -176,55 +176,52 @@ __device__ int group_census(unsigned* census, int grp, int mem, int P, long long
 
 // ------------------------------------------------------------------------------------
 // Workgroup roles (8 waves):
-//   waves 0..6  gather the step's exchange vector into the LDS A tile (batched sc1 loads,
-//               per-granule sentinel spin);
+//   waves 0..6  MFMA waves, K split 7 ways (k-step ks = wave + 7*kk). A k-step's 32 columns
+//               are ONE producer's 32-unit chunk (forward) or one gate-chunk (backward), so
+//               each lane's MFMA A fragment (row = lane % 16, 8 columns) is exactly one 16-B
+//               exchange granule: the wave polls its fragments straight into registers
+//               (sentinel spin per lane) and issues each k-step's MFMAs as soon as it is
+//               ready. No LDS staging of the exchanged state, no gather barrier.
 //   waves 0..3  cell epilogue (EPT elements each) + the critical 16-B exchange stores;
-//   wave  7     memory wave: prefetches the per-step inputs two steps ahead into an LDS
-//               ring and stores the per-step outputs from an LDS staging area. Its loads
-//               and stores never sit in another wave's vmcnt queue (vmcnt retires in
-//               order per wave), so the gather's waits see only the gather's loads.
-// Three barriers per step: after the gather (#1), after the MFMA phase (#2), and the
-// epilogue runs into the next gather (its LDS use is wave-local).
+//   wave  7     memory wave: per-step inputs two steps ahead into an LDS ring, per-step
+//               outputs out of a double-buffered LDS staging area. Its loads and stores
+//               never sit in another wave's vmcnt queue (vmcnt retires in order per wave).
+// One LDS-only barrier per step (partials ready -> epilogue); partials are double-buffered
+// by step parity because waves 4..6 run into the next step while 0..3 are in the epilogue.
 // ------------------------------------------------------------------------------------
 constexpr int EW = 4;             // epilogue waves
 constexpr int ETH = EW * 64;
-constexpr int GW = 7;             // gather waves
-constexpr int GTH = GW * 64;
+constexpr int MW = 7;             // MFMA waves
 constexpr int MEMW = 7;           // memory wave
 
-// Batched sentinel gather of NGR 16-B granules (row-major, GPR per row) into LDS rows of
-// pitch LP elements. Returns false on timeout.
-template <int GMAX>   // granules in flight per thread
-__device__ __forceinline__ bool gather_tile(__amdgpu_buffer_rsrc_t rs, size_t base_elem, int row_stride, int GPR,
-                                            int NGR, bf16_t* lds, int LP, int gt, long long timeout) {
+// Poll this lane's A-fragment granules (one per k-step) until none carries the sentinel,
+// issuing the k-step's MFMAs as each becomes ready. need = this lane's row is a real row.
+// Returns false on timeout.
+template <int KB, int NT, int CH, typename MfmaFn>
+__device__ __forceinline__ bool poll_mfma(__amdgpu_buffer_rsrc_t rs, const unsigned (&off)[KB], const bool (&kval)[KB],
+                                          bool need, long long timeout, MfmaFn&& mfma) {
+  // at most CH granules in flight per lane (a register budget: the U slice already holds
+  // most of the VGPRs); the load for k-step kk+CH is issued before k-step kk is waited on
+  i32x4 v[KB];
+#pragma unroll
+  for (int kk = 0; kk < (KB < CH ? KB : CH); ++kk) v[kk] = load_sc1_b128(rs, off[kk]);
   const long long t0 = __builtin_amdgcn_s_memrealtime();
-  bool ok = true;
-  for (int q0 = 0; q0 < NGR; q0 += GTH * GMAX) {
-    i32x4 v[GMAX];
-    unsigned off[GMAX];
+  bool ok_all = true;
 #pragma unroll
-    for (int j = 0; j < GMAX; ++j) {
-      const int q = q0 + gt + j * GTH;
-      const int qq = q < NGR ? q : NGR - 1;
-      const int row = qq / GPR, c8 = qq - row * GPR;
-      off[j] = (unsigned)((base_elem + (size_t)row * row_stride + c8 * 8) * 2);
-      v[j] = load_sc1_b128(rs, off[j]);
+  for (int kk = 0; kk < KB; ++kk) {
+    if (kk + CH < KB) v[kk + CH] = load_sc1_b128(rs, off[kk + CH]);
+    if (!kval[kk]) continue;                       // wave-uniform: k-step beyond K
+    while (true) {
+      const bool ok = !need || granule_ready(v[kk]);
+      if (__all(ok)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { ok_all = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+      if (!ok) v[kk] = load_sc1_b128(rs, off[kk]);
     }
-#pragma unroll
-    for (int j = 0; j < GMAX; ++j) {
-      const int q = q0 + gt + j * GTH;
-      if (q < NGR) {
-        while (!granule_ready(v[j])) {
-          if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { ok = false; break; }
-          __builtin_amdgcn_s_sleep(1);
-          v[j] = load_sc1_b128(rs, off[j]);
-        }
-        const int row = q / GPR, c8 = q - row * GPR;
-        *reinterpret_cast<i32x4*>(lds + row * LP + c8 * 8) = v[j];
-      }
-    }
+    const i32x4 z = {0, 0, 0, 0};
+    mfma(kk, __builtin_bit_cast(bf16x8, need ? v[kk] : z));
   }
-  return ok;
+  return ok_all;
 }
 
 // ------------------------------------------------------------------------------------
@@ -232,17 +229,16 @@ __device__ __forceinline__ bool gather_tile(__amdgpu_buffer_rsrc_t rs, size_t ba
 // ------------------------------------------------------------------------------------
 template <int CELL, int MT, int KB>
 __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
+  static_assert(MT == 1, "16-row tiles");
   constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
-  constexpr int ROWS = 16 * MT;
-  constexpr int EPT = ROWS * UPW / ETH;           // 2 (MT=1) or 4 (MT=2)
+  constexpr int ROWS = 16;
+  constexpr int EPT = ROWS * UPW / ETH;           // 2
   constexpr int GC = G * UPW;                     // gate columns of the workgroup
   constexpr int NTL = 2 * G;                      // 16-column N-tiles
   constexpr int RG = ROWS * G * (UPW / 8);        // gx granules per step (upper bound)
   constexpr int RGL = (RG + 63) / 64;             // ... per memory-wave lane
   constexpr int OPL = ROWS * UPW / 64;            // output elements per memory-wave lane
-  constexpr int LP = KB * NWV * 32 + 8;           // A pitch: K zero-padded to KB*8*32
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ float red_s[NWV][ROWS][GC + 1];      // K-split partials
+  __shared__ float red_s[2][MW][ROWS][GC + 1];    // K-split partials, by step parity
   __shared__ __attribute__((aligned(16))) bf16_t st_s[ROWS][UPW];
   __shared__ float gxr_s[2][ROWS][GC];            // input-projection ring (memory wave -> epilogue)
   __shared__ float oh_s[2][ROWS][UPW];            // output staging, by step parity
@@ -261,34 +257,32 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
   if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
   if (tid < G * UPW)
     bh_s[tid / UPW][tid % UPW] = (CELL == CELL_GRU && a.bh[dir]) ? a.bh[dir][(tid / UPW) * H + u0 + tid % UPW] : 0.f;
-  bf16_t* A = reinterpret_cast<bf16_t*>(smem);     // [ROWS][LP]
-
   if (wave == 0) {
     const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
     if (lane == 0) { s_mode = m; s_abort = (m < 0); }
   }
-  // zero the A tile once: rows >= R and columns >= H stay zero for the whole launch
-  for (int i = tid; i < ROWS * LP / 8; i += NTH) reinterpret_cast<i32x4*>(A)[i] = i32x4{0, 0, 0, 0};
 
-  // resident U fragments, K split over the 8 waves (k-step ks = wave + kk*8), all 2G
-  // N-tiles per wave: B[k][c] = U[g*H + u0 + 16*half + c][k], zero for k >= H
+  // resident U fragments of the MFMA waves: B[k][c] = U[g*H + u0 + 16*half + c][k]
   bf16x8 uf[KB][NTL];
+  bool kval[KB];
   {
     const bf16_t* Ud = a.U[dir];
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {
-      const int ks = wave + kk * NWV;
+      const int ks = wave + kk * MW;
+      kval[kk] = wave < MW && ks < KS;
 #pragma unroll
       for (int t = 0; t < NTL; ++t) {
         const int g = t >> 1, half = t & 1;
         bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (ks < KS)
+        if (kval[kk])
           v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)(g * H + u0 + 16 * half + (lane & 15)) * H + ks * 32 +
                                                8 * (lane >> 4));
         uf[kk][t] = v;
       }
     }
   }
+  const bool frag_row = (lane & 15) < R;          // this lane's A row is a real batch row
 
   // epilogue elements (waves 0..3): e = tid + i*ETH -> row = e / 32, unit = e % 32
   float hreg[EPT];
@@ -330,19 +324,28 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
     }
   };
   auto mw_store = [&](int s) {          // outputs of step s from staging slot s&1
+    float vh[OPL], vy[OPL];
+    float4 vg[OPL];
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {       // all LDS reads first, then the stores
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      vh[j] = oh_s[s & 1][row][c];
+      vy[j] = oy_s[s & 1][row][c];
+      if (CELL == CELL_GRU) vg[j] = og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c];
+    }
 #pragma unroll
     for (int j = 0; j < OPL; ++j) {
       const int e = lane + 64 * j;
       const int row = e >> 5, c = e & 31;
       if (row < R) {
         const int b = r0 + row, u = u0 + c;
-        a.hsave[dir][((size_t)(s + 1) * NP + b) * H + u] = oh_s[s & 1][row][c];
-        if (CELL == CELL_GRU)
-          reinterpret_cast<float4*>(a.gates[dir])[((size_t)s * NP + b) * H + u] = og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c];
+        a.hsave[dir][((size_t)(s + 1) * NP + b) * H + u] = vh[j];
+        if (CELL == CELL_GRU) reinterpret_cast<float4*>(a.gates[dir])[((size_t)s * NP + b) * H + u] = vg[j];
         if (b < N) {
           const int L = len_s[row];
           const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
-          a.y[dir][((size_t)t * N + b) * H + u] = f2bf(oy_s[s & 1][row][c]);
+          a.y[dir][((size_t)t * N + b) * H + u] = f2bf(vy[j]);
         }
       }
     }
@@ -354,117 +357,107 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
   bf16_t* hxd = a.hx[dir];
   const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
   Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
+  const int arow = min(r0 + (lane & 15), NP - 1);
 
-  for (int s = 0; s < a.steps; ++s) {
-    st.mark(-1);
-    if (wave < GW) {
-      // (G) gather h_{s-1} (slot s) into the A tile
-      if (!gather_tile<2>(rs_hx, ((size_t)s * NP + r0) * H, H, H / 8, R * (H / 8), A, LP, tid, a.timeout)) {
-        s_abort = 1;
-        atomicOr(a.err, 1u);
-      }
-    } else {
-      // memory wave, while the others wait on the exchange: this step's inputs (loaded
-      // one step ago) into the ring, outputs of step s-2 out of staging, next loads
-      mw_put(s);
-      if (s >= 2) mw_store(s - 2);
-      if (s + 1 < a.steps) mw_load(s + 1);
-    }
-    st.mark(0);
-    lds_barrier();                                                          // #1
-    st.mark(1);
-    if (s_abort) break;
-
-    // (M) partial gh over this wave's k-steps, all N-tiles
-    {
-      f32x4 acc[MT][NTL];
+  // The two roles run separate copies of the step loop (one LDS barrier per iteration in
+  // both), so the memory wave's prefetch registers and the MFMA waves' resident U slice are
+  // never live at the same time: the register budget is their max, not their sum.
+  if (wave < MW) {
+    for (int s = 0; s < a.steps; ++s) {
+      st.mark(-1);
+        // (M) poll this wave's A fragments of h_{s-1} (slot s) and accumulate its k-steps
+        unsigned off[KB];
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+        for (int kk = 0; kk < KB; ++kk)
+          off[kk] = (unsigned)((((size_t)s * NP + arow) * H + min(wave + kk * MW, KS - 1) * 32 + 8 * (lane >> 4)) * 2);
+        f32x4 acc[NTL];
 #pragma unroll
-        for (int t = 0; t < NTL; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      bf16x8 af[MT][KB];
+        for (int t = 0; t < NTL; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool ok = poll_mfma<KB, NTL, KB>(rs_hx, off, kval, frag_row, a.timeout, [&](int kk, bf16x8 af) {
 #pragma unroll
-      for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-          af[m][kk] = *reinterpret_cast<const bf16x8*>(A + (m * 16 + (lane & 15)) * LP + (wave + kk * NWV) * 32 +
-                                                       8 * (lane >> 4));
-#pragma unroll
-      for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int t = 0; t < NTL; ++t)
-            acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][t], acc[m][t], 0, 0, 0);
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
+          for (int t = 0; t < NTL; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, uf[kk][t], acc[t], 0, 0, 0);
+        });
+        if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
+        st.mark(0);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int row = m * 16 + (lane >> 4) * 4 + j;
+          const int row = (lane >> 4) * 4 + j;
           if (row < R) {
 #pragma unroll
-            for (int t = 0; t < NTL; ++t) red_s[wave][row][t * 16 + (lane & 15)] = acc[m][t][j];
+            for (int t = 0; t < NTL; ++t) red_s[s & 1][wave][row][t * 16 + (lane & 15)] = acc[t][j];
           }
         }
-    }
-    st.mark(2);
-    lds_barrier();                                                          // #2
-    st.mark(3);
-
-    // (E) cell epilogue; the exchange copy goes out first
-    if (wave < EW) {
+      st.mark(1);
+      lds_barrier();                                                        // partials ready
+      st.mark(2);
+      if (s_abort) break;
+      // (E) cell epilogue; the exchange copy goes out first
+      if (wave < EW) {
 #pragma unroll
-      for (int i = 0; i < EPT; ++i) {
-        const int e = tid + i * ETH;
-        const int row = e >> 5, c = e & 31;
-        if (row < R) {
-          float pre[G], gxv[G];
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * ETH;
+          const int row = e >> 5, c = e & 31;
+          if (row < R) {
+            float pre[G], gxv[G];
 #pragma unroll
-          for (int g = 0; g < G; ++g) {
-            float v = 0.f;
+            for (int g = 0; g < G; ++g) {
+              float v = 0.f;
 #pragma unroll
-            for (int w = 0; w < NWV; ++w) v += red_s[w][row][g * UPW + c];
-            pre[g] = v;
-            gxv[g] = gxr_s[s & 1][row][g * UPW + c];
+              for (int w = 0; w < MW; ++w) v += red_s[s & 1][w][row][g * UPW + c];
+              pre[g] = v;
+              gxv[g] = gxr_s[s & 1][row][g * UPW + c];
+            }
+            const bool act = s < len_s[row];
+            float hn;
+            float4 gsv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (CELL == CELL_GRU) {
+              const float ghn = pre[2] + bh_s[2][c];
+              const float r = sigmoidf_(gxv[0] + pre[0] + bh_s[0][c]);
+              const float z = sigmoidf_(gxv[1] + pre[1] + bh_s[1][c]);
+              const float n = tanhf_(gxv[2] + r * ghn);
+              hn = (1.f - z) * n + z * hreg[i];
+              if (act) gsv = make_float4(r, z, n, ghn);
+            } else {
+              hn = fminf(fmaxf(gxv[0] + pre[0], 0.f), RELU_CAP);
+            }
+            const float hnew = act ? hn : hreg[i];
+            hreg[i] = hnew;
+            st_s[row][c] = f2bf_x(hnew);
+            oh_s[s & 1][row][c] = hnew;
+            oy_s[s & 1][row][c] = act ? hn : 0.f;
+            if (CELL == CELL_GRU) og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c] = gsv;
           }
-          const bool act = s < len_s[row];
-          float hn;
-          float4 gsv = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (CELL == CELL_GRU) {
-            const float ghn = pre[2] + bh_s[2][c];
-            const float r = sigmoidf_(gxv[0] + pre[0] + bh_s[0][c]);
-            const float z = sigmoidf_(gxv[1] + pre[1] + bh_s[1][c]);
-            const float n = tanhf_(gxv[2] + r * ghn);
-            hn = (1.f - z) * n + z * hreg[i];
-            if (act) gsv = make_float4(r, z, n, ghn);
-          } else {
-            hn = fminf(fmaxf(gxv[0] + pre[0], 0.f), RELU_CAP);
+        }
+        // a wave's lanes cover whole rows of st_s: the granule stores read only LDS that
+        // this wave wrote
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * ETH;
+          const int row = e >> 5, c = e & 31;
+          if ((c & 7) == 0 && row < R) {
+            const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][c]);
+            const unsigned off = (unsigned)((((size_t)(s + 1) * NP + r0 + row) * H + u0 + c) * 2);
+            store_granule(plain, rs_hx, hxd, off, v);
           }
-          const float hnew = act ? hn : hreg[i];
-          hreg[i] = hnew;
-          st_s[row][c] = f2bf_x(hnew);
-          oh_s[s & 1][row][c] = hnew;
-          oy_s[s & 1][row][c] = act ? hn : 0.f;
-          if (CELL == CELL_GRU) og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c] = gsv;
         }
       }
       st.mark(4);
-      // a wave's lanes cover whole rows of st_s: the granule stores read only LDS that
-      // this wave wrote
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int i = 0; i < EPT; ++i) {
-        const int e = tid + i * ETH;
-        const int row = e >> 5, c = e & 31;
-        if ((c & 7) == 0 && row < R) {
-          const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][c]);
-          const unsigned off = (unsigned)((((size_t)(s + 1) * NP + r0 + row) * H + u0 + c) * 2);
-          store_granule(plain, rs_hx, hxd, off, v);
-        }
-      }
     }
-    st.mark(5);
+  } else {
+    for (int s = 0; s < a.steps; ++s) {
+      // memory wave: this step's inputs (loaded one step ago) into the ring, outputs of
+      // step s-2 out of staging, next loads
+      st.mark(-1);
+      mw_put(s);
+      if (s >= 2) mw_store(s - 2);
+      if (s + 1 < a.steps) mw_load(s + 1);
+      st.mark(0);
+      lds_barrier();
+      st.mark(1);
+      if (s_abort) break;
+    }
   }
   __syncthreads();
   if (wave == MEMW && !s_abort) {
@@ -475,8 +468,50 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
   if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
 }
 
+constexpr int GW = 7;             // gather waves of the backward kernel
+constexpr int GTH = GW * 64;
+
+// Batched sentinel gather of NGR 16-B granules (row-major, GPR per row) into LDS rows of
+// pitch LP elements (backward kernel: its 3H-wide exchange row is swept coalesced, a full
+// 128-B line per 8 lanes, which beats per-fragment polling there). Returns false on timeout.
+template <int GMAX>   // granules in flight per thread
+__device__ __forceinline__ bool gather_tile(__amdgpu_buffer_rsrc_t rs, size_t base_elem, int row_stride, int GPR,
+                                            int NGR, bf16_t* lds, int LP, int gt, long long timeout) {
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool ok = true;
+  for (int q0 = 0; q0 < NGR; q0 += GTH * GMAX) {
+    i32x4 v[GMAX];
+    unsigned off[GMAX];
+#pragma unroll
+    for (int j = 0; j < GMAX; ++j) {
+      const int q = q0 + gt + j * GTH;
+      const int qq = q < NGR ? q : NGR - 1;
+      const int row = qq / GPR, c8 = qq - row * GPR;
+      off[j] = (unsigned)((base_elem + (size_t)row * row_stride + c8 * 8) * 2);
+      v[j] = load_sc1_b128(rs, off[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < GMAX; ++j) {
+      const int q = q0 + gt + j * GTH;
+      if (q < NGR) {
+        while (!granule_ready(v[j])) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+          v[j] = load_sc1_b128(rs, off[j]);
+        }
+        const int row = q / GPR, c8 = q - row * GPR;
+        *reinterpret_cast<i32x4*>(lds + row * LP + c8 * 8) = v[j];
+      }
+    }
+  }
+  return ok;
+}
+
 // ------------------------------------------------------------------------------------
-// backward (BPTT)
+// backward (BPTT). Structure of generation 2 (measured faster for the 3H-wide exchange
+// than the forward's per-fragment polling): waves 0..6 sweep dgh_{s+1} into an LDS A tile,
+// barrier, all 8 waves run the K-split MFMA, barrier, epilogue. Wave 7 does the memory
+// duties while the others gather. The A tile is dynamic LDS (K zero-padded to 8*KB*32).
 // ------------------------------------------------------------------------------------
 template <int CELL, int MT, int KB>
 __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
@@ -765,7 +800,7 @@ static int launch_fwd(const XFwd& a, int kb, int grid, size_t smem, hipStream_t 
   case K:                                                                                     \
     hipLaunchKernelGGL((rnnx_fwd_kernel<CELL, MT, K>), dim3(grid), dim3(NTH), smem, st, a); \
     break;
-    DS2_CASE(1) DS2_CASE(2) DS2_CASE(3) DS2_CASE(4)
+    DS2_CASE(1) DS2_CASE(2) DS2_CASE(3) DS2_CASE(4) DS2_CASE(5)
 #undef DS2_CASE
     default: return -31;
   }
@@ -779,7 +814,7 @@ static int launch_bwd(const XBwd& a, int kb, int grid, size_t smem, hipStream_t 
   case K:                                                                                     \
     hipLaunchKernelGGL((rnnx_bwd_kernel<CELL, MT, K>), dim3(grid), dim3(NTH), smem, st, a); \
     break;
-    DS2_CASE(2) DS2_CASE(4) DS2_CASE(6) DS2_CASE(8) DS2_CASE(10) DS2_CASE(12) DS2_CASE(16)
+    DS2_CASE(2) DS2_CASE(4) DS2_CASE(6) DS2_CASE(8) DS2_CASE(10)
 #undef DS2_CASE
     default: return -32;
   }
@@ -825,19 +860,20 @@ int ds2_rnnx_grid(int H, int ngroups, int xcd_map) {
 // k-steps register tile: fwd = whole K per wave, bwd = K split over the 8 waves
 int ds2_rnnx_kb(int H, int G, int fwd) {
   if (fwd) {
-    const int need = (H / 32 + NWV - 1) / NWV;
-    return need <= 4 ? need : -1;
+    const int need = (H / 32 + MW - 1) / MW;
+    return need <= 5 ? need : -1;
   }
-  const int need = (G * H / 32 + NWV - 1) / NWV;
-  for (int k : {2, 4, 6, 8, 10, 12, 16}) if (k >= need) return k;
+  const int need = (G * H / 32 + NWV - 1) / NWV;          // backward: K split over all 8 waves
+  for (int k : {2, 4, 6, 8, 10}) if (k >= need) return k;
   return -1;
 }
 
-// dynamic LDS: the A tile, K zero-padded to the register tile
+// dynamic LDS: forward none (the exchanged state goes straight into MFMA registers);
+// backward the A tile, K zero-padded to the register tile
 size_t ds2_rnnx_smem(int H, int G, int mt, int fwd) {
-  const int kb = ds2_rnnx_kb(H, G, fwd);
-  const int LP = kb * NWV * 32 + 8;
-  return (size_t)16 * mt * LP * 2;
+  if (fwd) return 0;
+  const int kb = ds2_rnnx_kb(H, G, 0);
+  return (size_t)16 * mt * (kb * NWV * 32 + 8) * 2;
 }
 
 int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
@@ -865,7 +901,8 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
       case 1: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 1>, smem); break;                     \
       case 2: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 2>, smem); break;                     \
       case 3: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 3>, smem); break;                     \
-      default: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 4>, smem); break;                    \
+      case 4: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 4>, smem); break;                     \
+      default: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 5>, smem); break;                    \
     }                                                                                        \
     if (rc) return rc;                                                                       \
     return launch_fwd<C, M>(a, kb, grid, smem, st);                                          \
@@ -902,9 +939,7 @@ int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st) {
       case 4: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 4>, smem); break;                     \
       case 6: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 6>, smem); break;                     \
       case 8: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 8>, smem); break;                     \
-      case 10: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 10>, smem); break;                   \
-      case 12: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 12>, smem); break;                   \
-      default: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 16>, smem); break;                   \
+      default: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 10>, smem); break;                   \
     }                                                                                        \
     if (rc) return rc;                                                                       \
     return launch_bwd<C, M>(a, kb, grid, smem, st);                                          \

@@ -21,7 +21,7 @@ import torch  # noqa: E402
 
 PHASES = ["wait", "load+mfma", "reduce", "epilogue", "publish", "rest(stores+prefetch)"]
 # csrc/rnn_xcd.hip stamps: wave 0 phases + the memory wave's duty time and its barrier-#2 wait
-XPHASES = ["gather(w0)", "sync1", "mfma(w0)", "sync2", "epilogue", "publish", "memwave duties", "memwave sync1"]
+XPHASES = ["gather(w0)", "sync1", "mfma(w0)", "sync2", "epilogue", "(mode)", "memwave duties", "memwave sync1"]
 
 
 def run(cell, N, H, T, ndir, nw, mode, iters, stamps=False):
@@ -62,6 +62,10 @@ def run(cell, N, H, T, ndir, nw, mode, iters, stamps=False):
             w = w[active]
             res[kind + "_cycles_per_step"] = {ph: [round(float(w[:, i].mean()), 0), round(float(w[:, i].min()), 0),
                                                    round(float(w[:, i].max()), 0)] for i, ph in enumerate(names)}
+            if p.kind == "xcd":
+                # slot 5 of wave 0 holds the census verdict + 10 (11: XCD-local plain stores, 10: sc1)
+                modes = t[:, 5][active].tolist()
+                res[kind + "_groups_xcd_local"] = "%d of %d workgroups" % (sum(1 for m in modes if m == 11), len(modes))
         return res
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     tf, tb = [], []

@@ -128,11 +128,14 @@ int main() {
       {8, 25, 512, 1, 1, 512, 1, "  same, sentinel"},
       {8, 25, 512, 1, 0, 512, 1, "  same, sentinel, sc1 stores"},
       {8, 25, 512, 1, 1, 256, 1, "  same, sentinel, plain, 256 threads"},
+      {8, 25, 1536, 1, 1, 512, 1, "bwd-sized: 8 groups x 25 WG, 8 rows x 96 cols, XCD-local, sentinel, plain"},
+      {8, 25, 1536, 1, 0, 512, 1, "  same, sc1 stores"},
+      {8, 25, 1536, 1, 1, 448, 1, "  plain, 448 gather threads"},
   };
   const int steps = 1000;
   unsigned *slab, *flags, *xcc, *err;
   long long* t;
-  const size_t slab_bytes = (size_t)(steps + 2) * 8 * 25 * 1024;   // per-step slots for sentinel mode
+  const size_t slab_bytes = (size_t)(steps + 2) * 8 * 25 * 1536;   // per-step slots for sentinel mode
   hipMalloc(&slab, slab_bytes);
   hipMalloc(&flags, 8 * 64 * 4);
   hipMalloc(&xcc, 1024 * 4);
@@ -157,6 +160,7 @@ int main() {
       hipMemset(flags, 0, 8 * 64 * 4);
       hipMemset(err, 0, 4);
       if (c.nt == 512) hipLaunchKernelGGL(xbench<512>, dim3(g2), dim3(512), 0, 0, a);
+      else if (c.nt == 448) hipLaunchKernelGGL(xbench<448>, dim3(g2), dim3(448), 0, 0, a);
       else hipLaunchKernelGGL(xbench<256>, dim3(g2), dim3(256), 0, 0, a);
       if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
       std::vector<long long> tt(2 * g2);
