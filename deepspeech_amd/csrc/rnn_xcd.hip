@@ -476,7 +476,7 @@ constexpr int GTH = GW * 64;
 // 128-B line per 8 lanes, which beats per-fragment polling there). Returns false on timeout.
 template <int GMAX>   // granules in flight per thread
 __device__ __forceinline__ bool gather_tile(__amdgpu_buffer_rsrc_t rs, size_t base_elem, int row_stride, int GPR,
-                                            int NGR, bf16_t* lds, int LP, int gt, long long timeout) {
+                                            int NGR, bf16_t* lds, int LP, int gt, long long timeout, int nap = 1) {
   const long long t0 = __builtin_amdgcn_s_memrealtime();
   bool ok = true;
   for (int q0 = 0; q0 < NGR; q0 += GTH * GMAX) {
@@ -496,7 +496,7 @@ __device__ __forceinline__ bool gather_tile(__amdgpu_buffer_rsrc_t rs, size_t ba
       if (q < NGR) {
         while (!granule_ready(v[j])) {
           if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { ok = false; break; }
-          __builtin_amdgcn_s_sleep(1);
+          for (int z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(1);   // poll back-off (L2 traffic)
           v[j] = load_sc1_b128(rs, off[j]);
         }
         const int row = q / GPR, c8 = q - row * GPR;
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
   constexpr int EPT = ROWS * UPW / ETH;
   constexpr int OPL = ROWS * UPW / 64;            // elements per memory-wave lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ float red_s[NWV][ROWS][UPW + 1];
+  __shared__ float red_s[MW][ROWS][UPW + 1];
   __shared__ __attribute__((aligned(16))) bf16_t st_s[ROWS][G * UPW];
   __shared__ float dyr_s[2][ROWS][UPW];           // prefetch ring (memory wave -> epilogue)
   __shared__ float hpr_s[2][ROWS][UPW];
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
   if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, GH = G * H, KS = GH / 32, N = a.N, NP = a.NP, R = a.R;
-  const int LP = KB * NWV * 32 + 8;               // A pitch (K zero-padded to KB*8*32)
+  const int LP = KB * MW * 32 + 8;                // A pitch (K zero-padded to KB*7*32)
   const int bg = grp % a.BG, dir = grp / a.BG;
   const int r0 = bg * R, u0 = mem * UPW;
   bf16_t* A = reinterpret_cast<bf16_t*>(smem);     // [ROWS][LP]
@@ -545,18 +545,18 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
   }
   for (int i = tid; i < ROWS * LP / 8; i += NTH) reinterpret_cast<i32x4*>(A)[i] = i32x4{0, 0, 0, 0};
 
-  // resident U column fragments, K split over all 8 waves: k-step ks = wave + kk*NWV
+  // resident U column fragments of the MFMA waves (0..6): k-step ks = wave + kk*7
   // B[k][c] = U[k][u0 + 16*nt + c], k over all G*H (zero past it)
   bf16x8 uf[KB][2];
   {
     const bf16_t* Ud = a.U[dir];
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {
-      const int ks = wave + kk * NWV;
+      const int ks = wave + kk * MW;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (ks < KS) {
+        if (wave < MW && ks < KS) {
           const int k0 = ks * 32 + 8 * (lane >> 4);
           const bf16_t* p = Ud + (size_t)k0 * H + u0 + 16 * nt + (lane & 15);
 #pragma unroll
@@ -634,124 +634,140 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
   const __amdgpu_buffer_rsrc_t rs_dgh = make_rsrc(dghd, dgh_bytes);
   Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
 
-  for (int s = a.steps - 1; s >= 0; --s) {
-    st.mark(-1);
-    const bool has_next = s + 1 < a.steps;
-    // (G) gather dgh_{s+1} into the A tile
-    if (wave < GW) {
-      if (has_next &&
-          !gather_tile<4>(rs_dgh, ((size_t)(s + 1) * NP + r0) * GH, GH, GH / 8, R * (GH / 8), A, LP, tid, a.timeout)) {
-        s_abort = 1;
-        atomicOr(a.err, 1u);
+  // Role-split step loops (see the forward kernel): the memory wave's prefetch registers
+  // and the workers' U slice + in-flight gather granules are never live together.
+  if (wave < MW) {
+    for (int s = a.steps - 1; s >= 0; --s) {
+      st.mark(-1);
+      const bool has_next = s + 1 < a.steps;
+      {
+        // 4 granules in flight per thread measured fastest (6: +12 %); knobs (diagnostics):
+        // bit 0 -> 6 in flight, bits 4..7 -> poll back-off naps
+        const int nap = ((a.knobs >> 4) & 15) + 1;
+        const bool ok = !has_next ||
+            (!(a.knobs & 1) ? gather_tile<4>(rs_dgh, ((size_t)(s + 1) * NP + r0) * GH, GH, GH / 8, R * (GH / 8), A, LP,
+                                            tid, a.timeout, nap)
+                           : gather_tile<6>(rs_dgh, ((size_t)(s + 1) * NP + r0) * GH, GH, GH / 8, R * (GH / 8), A, LP,
+                                            tid, a.timeout, nap));
+        if (!ok) {
+          s_abort = 1;
+          atomicOr(a.err, 1u);
+        }
       }
-    } else {
-      // memory wave, while the others wait on the exchange (see the forward kernel)
+      st.mark(0);
+      lds_barrier();                                                        // #1
+      st.mark(1);
+      if (s_abort) break;
+      // (M) partial dh_rec over this wave's k-steps
+      if (has_next) {
+        f32x4 acc[MT][2];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) { acc[m][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[m][1] = acc[m][0]; }
+        bf16x8 af[MT][KB];
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            af[m][kk] = *reinterpret_cast<const bf16x8*>(A + (m * 16 + (lane & 15)) * LP + (wave + kk * MW) * 32 +
+                                                         8 * (lane >> 4));
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][0], acc[m][0], 0, 0, 0);
+            acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][1], acc[m][1], 0, 0, 0);
+          }
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) red_s[wave][m * 16 + (lane >> 4) * 4 + j][nt * 16 + (lane & 15)] = acc[m][nt][j];
+      }
+      st.mark(2);
+      lds_barrier();                                                        // #2
+      st.mark(3);
+      // (E) cell backward; the exchange copy (dgh_s) goes out first
+      if (wave < EW) {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * ETH;
+          const int row = e >> 5, c = e & 31;
+          if (row < R) {
+            float dhrec = 0.f;
+            if (has_next) {
+#pragma unroll
+              for (int w = 0; w < MW; ++w) dhrec += red_s[w][row][c];
+            }
+            const bool act = s < len_s[row];
+            const float dh = dyr_s[s & 1][row][c] + carry[i] + dhrec;
+            const float hp = hpr_s[s & 1][row][c];
+            float ghv[G], gxs[G];
+            float cnew = 0.f;
+            if (CELL == CELL_GRU) {
+              const float4 gv = gr_s[s & 1][(CELL == CELL_GRU) ? row : 0][c];
+              const float r = gv.x, z = gv.y, n = gv.z, ghn = gv.w;
+              const float dn = dh * (1.f - z);
+              const float dz = dh * (hp - n);
+              cnew = dh * z;
+              const float dan = dn * (1.f - n * n);
+              const float dr = dan * ghn;
+              const float dghn = dan * r;
+              const float daz = dz * z * (1.f - z);
+              const float dar = dr * r * (1.f - r);
+              ghv[0] = dar; ghv[1] = daz; ghv[2] = dghn;
+              gxs[0] = dar; gxs[1] = daz; gxs[2] = dan;
+            } else {
+              const float da = (hp > 0.f && hp < RELU_CAP) ? dh : 0.f;
+              ghv[0] = da;
+              gxs[0] = da;
+            }
+            if (!act) {
+              cnew = 0.f;
+#pragma unroll
+              for (int g = 0; g < G; ++g) { ghv[g] = 0.f; gxs[g] = 0.f; }
+            }
+            carry[i] = cnew;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+              st_s[row][g * UPW + c] = f2bf_x(ghv[g]);
+              ox_s[s & 1][row][g][c] = gxs[g];
+              sbx[i][g] += gxs[g];
+            }
+            if (CELL == CELL_GRU) sbh[i] += ghv[G - 1];
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * ETH;
+          const int row = e >> 5, c = e & 31;
+          if ((c & 7) == 0 && row < R) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+              const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][g * UPW + c]);
+              const unsigned off = (unsigned)((((size_t)s * NP + r0 + row) * GH + g * H + u0 + c) * 2);
+              store_granule(plain, rs_dgh, dghd, off, v);
+            }
+          }
+        }
+      }
+      st.mark(4);
+    }
+  } else {
+    for (int s = a.steps - 1; s >= 0; --s) {
+      // memory wave, while the others wait on the exchange
+      st.mark(-1);
       mw_put(s);
       if (s + 2 < a.steps) mw_store(s + 2);
       if (s >= 1) mw_load(s - 1);
+      st.mark(0);
+      lds_barrier();                                                        // #1
+      st.mark(1);
+      if (s_abort) break;
+      lds_barrier();                                                        // #2
     }
-    st.mark(0);
-    lds_barrier();                                                          // #1
-    st.mark(1);
-    if (s_abort) break;
-
-    // (M) partial dh_rec over this wave's k-steps
-    if (has_next) {
-      f32x4 acc[MT][2];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) { acc[m][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[m][1] = acc[m][0]; }
-      bf16x8 af[MT][KB];
-#pragma unroll
-      for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-          af[m][kk] = *reinterpret_cast<const bf16x8*>(A + (m * 16 + (lane & 15)) * LP + (wave + kk * NWV) * 32 +
-                                                       8 * (lane >> 4));
-#pragma unroll
-      for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][0], acc[m][0], 0, 0, 0);
-          acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][1], acc[m][1], 0, 0, 0);
-        }
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) red_s[wave][m * 16 + (lane >> 4) * 4 + j][nt * 16 + (lane & 15)] = acc[m][nt][j];
-    }
-    st.mark(2);
-    lds_barrier();                                                          // #2
-    st.mark(3);
-
-    // (E) cell backward; the exchange copy (dgh_s) goes out first
-    if (wave < EW) {
-#pragma unroll
-      for (int i = 0; i < EPT; ++i) {
-        const int e = tid + i * ETH;
-        const int row = e >> 5, c = e & 31;
-        if (row < R) {
-          float dhrec = 0.f;
-          if (has_next) {
-#pragma unroll
-            for (int w = 0; w < NWV; ++w) dhrec += red_s[w][row][c];
-          }
-          const bool act = s < len_s[row];
-          const float dh = dyr_s[s & 1][row][c] + carry[i] + dhrec;
-          const float hp = hpr_s[s & 1][row][c];
-          float ghv[G], gxs[G];
-          float cnew = 0.f;
-          if (CELL == CELL_GRU) {
-            const float4 gv = gr_s[s & 1][(CELL == CELL_GRU) ? row : 0][c];
-            const float r = gv.x, z = gv.y, n = gv.z, ghn = gv.w;
-            const float dn = dh * (1.f - z);
-            const float dz = dh * (hp - n);
-            cnew = dh * z;
-            const float dan = dn * (1.f - n * n);
-            const float dr = dan * ghn;
-            const float dghn = dan * r;
-            const float daz = dz * z * (1.f - z);
-            const float dar = dr * r * (1.f - r);
-            ghv[0] = dar; ghv[1] = daz; ghv[2] = dghn;
-            gxs[0] = dar; gxs[1] = daz; gxs[2] = dan;
-          } else {
-            const float da = (hp > 0.f && hp < RELU_CAP) ? dh : 0.f;
-            ghv[0] = da;
-            gxs[0] = da;
-          }
-          if (!act) {
-            cnew = 0.f;
-#pragma unroll
-            for (int g = 0; g < G; ++g) { ghv[g] = 0.f; gxs[g] = 0.f; }
-          }
-          carry[i] = cnew;
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            st_s[row][g * UPW + c] = f2bf_x(ghv[g]);
-            ox_s[s & 1][row][g][c] = gxs[g];
-            sbx[i][g] += gxs[g];
-          }
-          if (CELL == CELL_GRU) sbh[i] += ghv[G - 1];
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int i = 0; i < EPT; ++i) {
-        const int e = tid + i * ETH;
-        const int row = e >> 5, c = e & 31;
-        if ((c & 7) == 0 && row < R) {
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][g * UPW + c]);
-            const unsigned off = (unsigned)((((size_t)s * NP + r0 + row) * GH + g * H + u0 + c) * 2);
-            store_granule(plain, rs_dgh, dghd, off, v);
-          }
-        }
-      }
-    }
-    st.mark(4);
   }
   __syncthreads();
   if (wave == MEMW && !s_abort) {
@@ -765,7 +781,7 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
   // per (gate, unit) of the workgroup's own [bg] partial row
   if (a.dbx_part[dir] != nullptr && !s_abort) {
     constexpr int BW = (G + 1) * UPW;
-    static_assert(NWV * ROWS * (UPW + 1) >= ROWS * BW, "bias reduction does not fit the LDS scratch");
+    static_assert(MW * ROWS * (UPW + 1) >= ROWS * BW, "bias reduction does not fit the LDS scratch");
     float* bred = &red_s[0][0][0];
     if (wave < EW) {
 #pragma unroll
@@ -814,7 +830,7 @@ static int launch_bwd(const XBwd& a, int kb, int grid, size_t smem, hipStream_t 
   case K:                                                                                     \
     hipLaunchKernelGGL((rnnx_bwd_kernel<CELL, MT, K>), dim3(grid), dim3(NTH), smem, st, a); \
     break;
-    DS2_CASE(2) DS2_CASE(4) DS2_CASE(6) DS2_CASE(8) DS2_CASE(10)
+    DS2_CASE(2) DS2_CASE(4) DS2_CASE(6) DS2_CASE(8) DS2_CASE(11)
 #undef DS2_CASE
     default: return -32;
   }
@@ -863,8 +879,8 @@ int ds2_rnnx_kb(int H, int G, int fwd) {
     const int need = (H / 32 + MW - 1) / MW;
     return need <= 5 ? need : -1;
   }
-  const int need = (G * H / 32 + NWV - 1) / NWV;          // backward: K split over all 8 waves
-  for (int k : {2, 4, 6, 8, 10}) if (k >= need) return k;
+  const int need = (G * H / 32 + MW - 1) / MW;            // backward: K split over the 7 workers
+  for (int k : {2, 4, 6, 8, 11}) if (k >= need) return k;
   return -1;
 }
 
@@ -873,7 +889,7 @@ int ds2_rnnx_kb(int H, int G, int fwd) {
 size_t ds2_rnnx_smem(int H, int G, int mt, int fwd) {
   if (fwd) return 0;
   const int kb = ds2_rnnx_kb(H, G, 0);
-  return (size_t)16 * mt * (kb * NWV * 32 + 8) * 2;
+  return (size_t)16 * mt * (kb * MW * 32 + 8) * 2;
 }
 
 int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
@@ -939,7 +955,7 @@ int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st) {
       case 4: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 4>, smem); break;                     \
       case 6: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 6>, smem); break;                     \
       case 8: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 8>, smem); break;                     \
-      default: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 10>, smem); break;                   \
+      default: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 11>, smem); break;                   \
     }                                                                                        \
     if (rc) return rc;                                                                       \
     return launch_bwd<C, M>(a, kb, grid, smem, st);                                          \

@@ -62,10 +62,10 @@ LDS_BYTES = 160 * 1024
 
 
 def _xcd_kb(H: int, G: int, fwd: bool) -> int:
-    """k-steps per MFMA wave of csrc/rnn_xcd.hip (forward: K split over the 7 MFMA waves,
-    the 8th is the memory wave; backward: over all 8). -1 if the tile would not fit."""
-    need = -(-((H if fwd else G * H) // 32) // (7 if fwd else 8))
-    opts = (1, 2, 3, 4, 5) if fwd else (2, 4, 6, 8, 10)
+    """k-steps per MFMA wave of csrc/rnn_xcd.hip (K split over the 7 worker waves; the
+    8th is the memory wave). -1 if the tile would not fit."""
+    need = -(-((H if fwd else G * H) // 32) // 7)
+    opts = (1, 2, 3, 4, 5) if fwd else (2, 4, 6, 8, 11)
     for k in opts:
         if k >= need:
             return k
@@ -80,7 +80,7 @@ def _xcd_lds(H: int, G: int, mt: int) -> int:
     fwd = (2 * 7 * rows * (G * 32 + 1) * 4 + rows * 32 * 2 + 2 * rows * G * 32 * 4 + 2 * 2 * rows * 32 * 4
            + (2 * rows * 32 * 16 if gru else 16) + rows * 4 + G * 32 * 4 + 64)
     kb = _xcd_kb(H, G, False)
-    bwd = (rows * (kb * 8 * 32 + 8) * 2 + 8 * rows * 33 * 4 + rows * G * 32 * 2 + 2 * 2 * rows * 32 * 4
+    bwd = (rows * (kb * 7 * 32 + 8) * 2 + 7 * rows * 33 * 4 + rows * G * 32 * 2 + 2 * 2 * rows * 32 * 4
            + (2 * rows * 32 * 16 if gru else 16) + 2 * rows * G * 32 * 4 + rows * 4 + 64)
     return max(fwd, bwd)
 
