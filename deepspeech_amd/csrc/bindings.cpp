@@ -91,6 +91,29 @@ int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void*
 int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
+size_t ds2_conv2_fwd_smem(int F1);
+size_t ds2_conv2_dgrad_smem(int F2);
+size_t ds2_conv2_wgrad_smem(int F1);
+long long ds2_conv2_wgrad_part_floats(int grid);
+long long ds2_conv1_wgrad_part_floats(int grid);
+int ds2_conv1_fwd_grid(int N, int T1);
+int ds2_conv2_fwd(const void* x, const void* w, const float* bias, void* y, float* part, int grid, int N, int T1,
+                  int F1, int T2, int F2, hipStream_t st);
+int ds2_conv2_dgrad(const void* dy, const void* w, void* dx, int grid, int N, int T1, int F1, int T2, int F2,
+                    hipStream_t st);
+int ds2_conv2_wgrad(const void* dy, const void* x, float* part, int grid, float* dw, int N, int T1, int F1, int T2,
+                    int F2, hipStream_t st);
+int ds2_conv1_fwd(const void* x, const void* w, const float* bias, void* y, float* part, int N, int T, int F0,
+                  int T1, int F1, hipStream_t st);
+int ds2_conv1_wgrad(const void* dy, const void* x, float* part, int grid, float* dw, int N, int T, int F0, int T1,
+                    int F1, hipStream_t st);
+int ds2_bn_cl_finalize(const float* part, int nb, double M, float eps, float* mean, float* invstd, float* run_mean,
+                       float* run_var, float momentum, hipStream_t st);
+int ds2_bn_cl_apply(const void* y, const float* mean, const float* invstd, const float* gamma, const float* beta,
+                    void* out, int N, int T, int F, int tmaj, hipStream_t st);
+int ds2_bn_cl_bwd(const void* dz, const void* y, const float* mean, const float* invstd, const float* gamma,
+                  const float* beta, float* part, int nb, float* dgamma, float* dbeta, void* dy, int N, int T, int F,
+                  int tmaj, hipStream_t st);
 }
 
 namespace {
@@ -396,6 +419,109 @@ void cast_bf16(at::Tensor x, at::Tensor y) {
   check(ds2_cast_bf16(x.data_ptr<float>(), y.data_ptr(), x.numel(), cur_stream()), "cast_bf16");
 }
 
+// --------------------------------------------------------------------------- conv front-end
+void need_bf16(const at::Tensor& t, const char* name) {
+  need_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+}
+void need_f32(const at::Tensor& t, const char* name, int64_t numel) {
+  need_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.numel() >= numel, name, " too small (", t.numel(), " < ", numel, ")");
+}
+
+// x [N,T,F0] bf16, w [32,1,20,5] bf16 -> y [N,T1,F1,32] bf16, part [grid, 64] f32
+void conv1_fwd(at::Tensor x, at::Tensor w, OptT bias, at::Tensor y, at::Tensor part) {
+  need_bf16(x, "x"); need_bf16(w, "w"); need_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 3 && y.dim() == 4 && y.size(3) == 32 && w.numel() == 32 * 100, "conv1_fwd shapes");
+  const int N = (int)x.size(0), T = (int)x.size(1), F0 = (int)x.size(2), T1 = (int)y.size(1), F1 = (int)y.size(2);
+  TORCH_CHECK(y.size(0) == N, "conv1_fwd batch");
+  need_f32(part, "part", (int64_t)ds2_conv1_fwd_grid(N, T1) * 64);
+  check(ds2_conv1_fwd(x.data_ptr(), w.data_ptr(), ptr_or_null<float>(bias, "bias"), y.data_ptr(),
+                      part.data_ptr<float>(), N, T, F0, T1, F1, cur_stream()), "conv1_fwd");
+}
+int64_t conv1_fwd_grid(int64_t N, int64_t T1) { return ds2_conv1_fwd_grid((int)N, (int)T1); }
+
+// x [N,T1,F1,32], w [32,32,10,5] -> y [N,T2,F2,32], part [grid, 64]
+void conv2_fwd(at::Tensor x, at::Tensor w, OptT bias, at::Tensor y, at::Tensor part, int64_t grid) {
+  need_bf16(x, "x"); need_bf16(w, "w"); need_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(3) == 32 && y.size(3) == 32 && w.numel() == 32 * 32 * 50,
+              "conv2_fwd shapes");
+  TORCH_CHECK(grid > 0, "grid");
+  need_f32(part, "part", grid * 64);
+  check(ds2_conv2_fwd(x.data_ptr(), w.data_ptr(), ptr_or_null<float>(bias, "bias"), y.data_ptr(),
+                      part.data_ptr<float>(), (int)grid, (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                      (int)y.size(1), (int)y.size(2), cur_stream()), "conv2_fwd");
+}
+
+// dy [N,T2,F2,32], w [32,32,10,5] -> dx [N,T1,F1,32]
+void conv2_dgrad(at::Tensor dy, at::Tensor w, at::Tensor dx, int64_t grid) {
+  need_bf16(dy, "dy"); need_bf16(w, "w"); need_bf16(dx, "dx");
+  TORCH_CHECK(dy.dim() == 4 && dx.dim() == 4 && dy.size(3) == 32 && dx.size(3) == 32 && w.numel() == 32 * 32 * 50,
+              "conv2_dgrad shapes");
+  TORCH_CHECK(grid > 0, "grid");
+  check(ds2_conv2_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), (int)grid, (int)dx.size(0), (int)dx.size(1),
+                        (int)dx.size(2), (int)dy.size(1), (int)dy.size(2), cur_stream()), "conv2_dgrad");
+}
+
+// dy [N,T2,F2,32], x [N,T1,F1,32] -> dw (fp32, 32*32*10*5), part scratch
+void conv2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor part, at::Tensor dw, int64_t grid) {
+  need_bf16(dy, "dy"); need_bf16(x, "x");
+  TORCH_CHECK(grid > 0, "grid");
+  need_f32(part, "part", ds2_conv2_wgrad_part_floats((int)grid));
+  need_f32(dw, "dw", 32 * 32 * 50);
+  check(ds2_conv2_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), (int)grid, dw.data_ptr<float>(),
+                        (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)dy.size(1), (int)dy.size(2),
+                        cur_stream()), "conv2_wgrad");
+}
+
+// dy [N,T1,F1,32], x [N,T,F0] -> dw (fp32, 32*20*5)
+void conv1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor part, at::Tensor dw, int64_t grid) {
+  need_bf16(dy, "dy"); need_bf16(x, "x");
+  TORCH_CHECK(grid > 0, "grid");
+  need_f32(part, "part", ds2_conv1_wgrad_part_floats((int)grid));
+  need_f32(dw, "dw", 32 * 100);
+  check(ds2_conv1_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), (int)grid, dw.data_ptr<float>(),
+                        (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)dy.size(1), (int)dy.size(2),
+                        cur_stream()), "conv1_wgrad");
+}
+int64_t conv2_wgrad_part_floats(int64_t grid) { return ds2_conv2_wgrad_part_floats((int)grid); }
+int64_t conv1_wgrad_part_floats(int64_t grid) { return ds2_conv1_wgrad_part_floats((int)grid); }
+
+void bn_cl_finalize(at::Tensor part, int64_t nb, double M, double eps, at::Tensor mean, at::Tensor invstd,
+                    OptT run_mean, OptT run_var, double momentum) {
+  need_f32(part, "part", nb * 64);
+  need_f32(mean, "mean", 32); need_f32(invstd, "invstd", 32);
+  check(ds2_bn_cl_finalize(part.data_ptr<float>(), (int)nb, M, (float)eps, mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), ptr_or_null<float>(run_mean, "run_mean"),
+                           ptr_or_null<float>(run_var, "run_var"), (float)momentum, cur_stream()), "bn_cl_finalize");
+}
+
+// y [N,T,F,32] -> out [N,T,F,32] (tmaj=0) or [T,N,32*F] (tmaj=1)
+void bn_cl_apply(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor beta, at::Tensor out,
+                 bool tmaj) {
+  need_bf16(y, "y"); need_bf16(out, "out");
+  TORCH_CHECK(y.dim() == 4 && y.size(3) == 32 && out.numel() == y.numel(), "bn_cl_apply shapes");
+  need_f32(mean, "mean", 32); need_f32(invstd, "invstd", 32); need_f32(gamma, "gamma", 32); need_f32(beta, "beta", 32);
+  check(ds2_bn_cl_apply(y.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(), gamma.data_ptr<float>(),
+                        beta.data_ptr<float>(), out.data_ptr(), (int)y.size(0), (int)y.size(1), (int)y.size(2),
+                        tmaj ? 1 : 0, cur_stream()), "bn_cl_apply");
+}
+
+void bn_cl_bwd(at::Tensor dz, at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor beta,
+               at::Tensor part, int64_t nb, at::Tensor dgamma, at::Tensor dbeta, at::Tensor dy, bool tmaj) {
+  need_bf16(dz, "dz"); need_bf16(y, "y"); need_bf16(dy, "dy");
+  TORCH_CHECK(y.dim() == 4 && y.size(3) == 32 && dz.numel() == y.numel() && dy.numel() == y.numel(),
+              "bn_cl_bwd shapes");
+  need_f32(part, "part", nb * 64);
+  need_f32(mean, "mean", 32); need_f32(invstd, "invstd", 32); need_f32(gamma, "gamma", 32); need_f32(beta, "beta", 32);
+  need_f32(dgamma, "dgamma", 32); need_f32(dbeta, "dbeta", 32);
+  check(ds2_bn_cl_bwd(dz.data_ptr(), y.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                      gamma.data_ptr<float>(), beta.data_ptr<float>(), part.data_ptr<float>(), (int)nb,
+                      dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dy.data_ptr(), (int)y.size(0),
+                      (int)y.size(1), (int)y.size(2), tmaj ? 1 : 0, cur_stream()), "bn_cl_bwd");
+}
+
 // --------------------------------------------------------------------------- device info
 py::dict device_info(int64_t dev) {
   hipDeviceProp_t prop;
@@ -452,4 +578,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("cast_bf16", &cast_bf16);
   m.def("device_info", &device_info);
+  m.def("conv1_fwd", &conv1_fwd);
+  m.def("conv1_fwd_grid", &conv1_fwd_grid);
+  m.def("conv2_fwd", &conv2_fwd);
+  m.def("conv2_dgrad", &conv2_dgrad);
+  m.def("conv2_wgrad", &conv2_wgrad);
+  m.def("conv1_wgrad", &conv1_wgrad);
+  m.def("conv2_wgrad_part_floats", &conv2_wgrad_part_floats);
+  m.def("conv1_wgrad_part_floats", &conv1_wgrad_part_floats);
+  m.def("bn_cl_finalize", &bn_cl_finalize);
+  m.def("bn_cl_apply", &bn_cl_apply);
+  m.def("bn_cl_bwd", &bn_cl_bwd);
 }

@@ -127,7 +127,155 @@ def conv_block_hip(block, x: torch.Tensor, layout: int, idx: int) -> torch.Tenso
                             block.training, layout, dt, idx)
 
 
+def _bf16_of(p: torch.Tensor) -> torch.Tensor:
+    return p.bf16 if arena_of(p) is not None else p.detach().to(torch.bfloat16).contiguous()
+
+
+def _grad_buffer(p: torch.Tensor):
+    """(fp32 buffer a kernel may overwrite with p's full gradient, written_in_place)."""
+    a = arena_of(p)
+    if a is not None and a.first_write(p):
+        return p.main_grad, True
+    return torch.empty(p.shape, device=p.device, dtype=torch.float32), False
+
+
+def _deliver(p: torch.Tensor, buf: torch.Tensor, in_place: bool):
+    if in_place:
+        arena_of(p).grad_done(p)
+        return None
+    return emit_grad(p, buf)
+
+
+def _zero_grad_of(p: torch.Tensor):
+    """Gradient of a conv bias that feeds a train-mode BatchNorm: identically zero."""
+    a = arena_of(p)
+    if a is not None:
+        a.grad_done(p)              # main_grad was zeroed by zero_grad(); adding zero is a no-op
+        return None
+    return torch.zeros_like(p)
+
+
+class FrontendCL(torch.autograd.Function):
+    """Whole conv front-end on the channels-last MFMA kernels of csrc/conv_frontend.hip.
+
+    feats [N, T, F0] -> time-major RNN input [T2, N, 32*F2] (bf16). Forward: conv1 (+bias,
+    BN statistics in the epilogue) -> BN finalize -> BN+clip apply -> conv2 (+bias, stats)
+    -> finalize -> BN+clip apply with the time-major transpose in the store. Backward:
+    BN2 backward (reads the time-major gradient through an LDS transpose) -> conv2 wgrad
+    (fp32 straight into the arena) and dgrad -> BN1 backward -> conv1 wgrad. Reference:
+    src/deepSpeech_NCHW.py:110-168, src/custom_ops.py:99-160."""
+
+    @staticmethod
+    def forward(ctx, feats, w1, b1, g1, be1, w2, b2, g2, be2, model):
+        C_ = _ext.ext()
+        dev = feats.device
+        x = feats.to(torch.bfloat16).contiguous()
+        N, T, F0 = x.shape
+        T1, F1 = (T - 20) // 2 + 1, (F0 - 5) // 2 + 1
+        T2, F2 = (T1 - 10) // 2 + 1, F1 - 4
+        c1, c2 = model.conv1, model.conv2
+        training = bool(c1.training)
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        ncu = _ext.num_cus(dev.index or 0)
+
+        def stats(part, nb, M, blk):
+            if training:
+                mean = torch.empty(32, **f32)
+                inv = torch.empty(32, **f32)
+                C_.bn_cl_finalize(part, nb, float(M), BN_EPS, mean, inv, blk.running_mean, blk.running_var,
+                                  BN_MOMENTUM)
+                return mean, inv
+            return (blk.running_mean.float().contiguous(),
+                    torch.rsqrt(blk.running_var.float() + BN_EPS).contiguous())
+
+        g1f, be1f = g1.detach().float().contiguous(), be1.detach().float().contiguous()
+        g2f, be2f = g2.detach().float().contiguous(), be2.detach().float().contiguous()
+        with TR.phase(TR.conv(1)):
+            y1 = torch.empty(N, T1, F1, 32, **bf)
+            nb1 = int(C_.conv1_fwd_grid(N, T1))
+            part1 = torch.empty(nb1 * 64, **f32)
+            C_.conv1_fwd(x, _bf16_of(w1), b1.detach().float().contiguous(), y1, part1)
+        with TR.phase(TR.bn(1)):
+            mean1, inv1 = stats(part1, nb1, N * T1 * F1, c1)
+            z1 = torch.empty_like(y1)
+            C_.bn_cl_apply(y1, mean1, inv1, g1f, be1f, z1, False)
+        w2_16 = _bf16_of(w2)
+        with TR.phase(TR.conv(2)):
+            y2 = torch.empty(N, T2, F2, 32, **bf)
+            grid = max(1, min(N * T2, ncu))
+            part2 = torch.empty(grid * 64, **f32)
+            C_.conv2_fwd(z1, w2_16, b2.detach().float().contiguous(), y2, part2, grid)
+        with TR.phase(TR.bn(2)):
+            mean2, inv2 = stats(part2, grid, N * T2 * F2, c2)
+            out = torch.empty(T2, N, 32 * F2, **bf)
+            C_.bn_cl_apply(y2, mean2, inv2, g2f, be2f, out, True)
+        ctx.save_for_backward(x, y1, z1, y2, mean1, inv1, mean2, inv2, g1f, be1f, g2f, be2f, w2_16)
+        ctx.params = (w1, b1, g1, be1, w2, b2, g2, be2)
+        ctx.training = training
+        ctx.ncu = ncu
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        if not ctx.training:
+            raise RuntimeError("FrontendCL backward is only defined in training mode")
+        C_ = _ext.ext()
+        x, y1, z1, y2, mean1, inv1, mean2, inv2, g1f, be1f, g2f, be2f, w2_16 = ctx.saved_tensors
+        w1, b1, g1, be1, w2, b2, g2, be2 = ctx.params
+        dev = x.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        dout = dout.to(torch.bfloat16).contiguous()
+        N, T2, F2, _ = y2.shape
+        T1 = y1.shape[1]
+        grid = max(1, min(N * T2, ctx.ncu))
+        nb2 = max(1, min(N * T2, 1024))
+        nb1 = max(1, min(N * T1, 1024))
+        part = torch.empty(max(nb1, nb2) * 64, **f32)
+        with TR.phase(TR.bn(2, True)):
+            dg2 = torch.empty(32, **f32)
+            db2 = torch.empty(32, **f32)
+            dy2 = torch.empty_like(y2)
+            C_.bn_cl_bwd(dout, y2, mean2, inv2, g2f, be2f, part, nb2, dg2, db2, dy2, True)
+        with TR.phase(TR.conv(2, True)):
+            wpart = torch.empty(int(C_.conv2_wgrad_part_floats(grid)), **f32)
+            dw2, ip2 = _grad_buffer(w2)
+            C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
+            gw2 = _deliver(w2, dw2, ip2)
+            dz1 = torch.empty_like(y1)
+            C_.conv2_dgrad(dy2, w2_16, dz1, max(1, min(N * ((T1 + 1) // 2), ctx.ncu)))
+        gg2, gb2, gbias2 = emit_grad(g2, dg2), emit_grad(be2, db2), _zero_grad_of(b2)
+        with TR.phase(TR.bn(1, True)):
+            dg1 = torch.empty(32, **f32)
+            db1 = torch.empty(32, **f32)
+            dy1 = torch.empty_like(y1)
+            C_.bn_cl_bwd(dz1, y1, mean1, inv1, g1f, be1f, part, nb1, dg1, db1, dy1, False)
+        with TR.phase(TR.conv(1, True)):
+            g1grid = max(1, min(N * ((T1 + 3) // 4), ctx.ncu))
+            wpart1 = torch.empty(int(C_.conv1_wgrad_part_floats(g1grid)), **f32)
+            dw1, ip1 = _grad_buffer(w1)
+            C_.conv1_wgrad(dy1, x, wpart1, dw1, g1grid)
+            gw1 = _deliver(w1, dw1, ip1)
+        gg1, gb1, gbias1 = emit_grad(g1, dg1), emit_grad(be1, db1), _zero_grad_of(b1)
+        return None, gw1, gbias1, gg1, gb1, gw2, gbias2, gg2, gb2, None
+
+
+def cl_supported(model, feats: torch.Tensor) -> bool:
+    """The channels-last MFMA front-end covers the reference geometry (32 filters and
+    F1 = (F0-5)/2+1 <= 80 frequency positions, i.e. up to 163 bins); other widths take the
+    library-conv path below."""
+    if model.num_filters != 32 or feats.dim() != 3:
+        return False
+    F1 = (feats.shape[2] - 5) // 2 + 1
+    return 9 <= F1 <= 80 and feats.shape[1] >= 38
+
+
 def frontend_hip(model, feats: torch.Tensor) -> torch.Tensor:
+    import os
+    if cl_supported(model, feats) and os.environ.get("DS2_CONV", "hip") == "hip":
+        c1, c2 = model.conv1, model.conv2
+        return FrontendCL.apply(feats, c1.weight, c1.bias, c1.bn_gamma, c1.bn_beta,
+                                c2.weight, c2.bias, c2.bn_gamma, c2.bn_beta, model)
     x = feats.unsqueeze(1)
     x = conv_block_hip(model.conv1, x, 0, 1)
     return conv_block_hip(model.conv2, x, 1, 2)
