@@ -110,22 +110,53 @@ struct Conv2Fwd {
   int N, T1, F1, T2, F2;
 };
 constexpr int C2_KT = 10, C2_KF = 5;
-constexpr int C2_KPW = C2_KT * C2_KF * 2 / 4;   // 25 k-steps (of 100) per wave
+constexpr int C2_WAVES = 8;                     // 2 waves per SIMD: one's LDS reads hide under the other's MFMAs
+constexpr int C2_KPW = 13;                      // k-steps per wave (100 = 4 x 13 + 4 x 12 for fwd)
+constexpr int PR = 80;                          // LDS bytes per position row: 64 data + 16 pad
+// With 80-B rows the 16 lanes of every ds_read_b128 lane group (consecutive positions, one
+// 16-B chunk) hit 16 distinct 16-B bank slots: conflict-free with affine addresses, so each
+// A-fragment read is one lane-base VGPR + a wave-uniform offset.
+constexpr int C2_STG = 7;                       // 16-B staging loads per thread (512 threads)
 
-__global__ __launch_bounds__(256) void conv2_fwd_kernel(Conv2Fwd a) {
+// copy `nch` 16-B chunks of a contiguous run of 64-B position rows into 80-B LDS rows
+struct Stager {
+  i32x4 v[C2_STG];
+  __device__ __forceinline__ void load(const unsigned char* src, int nch) {
+#pragma unroll
+    for (int k = 0; k < C2_STG; ++k) {
+      const int p = min((int)threadIdx.x + 512 * k, nch - 1);     // clamp, never predicate a load
+      v[k] = *(const i32x4*)(src + (size_t)p * 16);
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char* dst, int nch) const {
+#pragma unroll
+    for (int k = 0; k < C2_STG; ++k) {
+      const int p = (int)threadIdx.x + 512 * k;
+      if (p < nch) *(i32x4*)(dst + (p >> 2) * PR + (p & 3) * 16) = v[k];
+    }
+  }
+};
+
+// wave w's k-step range within a K of `total` steps split over `nw` waves (first waves +1)
+__device__ __forceinline__ void kspan(int w, int nw, int total, int& s0, int& n) {
+  const int q = total / nw, r = total % nw;
+  n = q + (w < r ? 1 : 0);
+  s0 = w * q + min(w, r);
+}
+
+__global__ __launch_bounds__(512) void conv2_fwd_kernel(Conv2Fwd a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
   const int hi = lane >> 5, col = lane & 31;
-  const int inBytes = C2_KT * a.F1 * 64;
-  unsigned char* const buf0 = smem;
-  unsigned char* const buf1 = smem + inBytes;
-  f32x4* red = (f32x4*)(smem + 2 * inBytes);                 // [4 waves][12][64] f32x4
-  float* statsh = (float*)(smem + 2 * inBytes + 4 * 12 * 64 * 16);
+  unsigned char* const buf = smem;                                   // [10*F1][80 B]
+  f32x4* red = (f32x4*)(smem + C2_KT * a.F1 * PR);                   // [8 waves][12][64] f32x4
+  int s0, nks;
+  kspan(w, C2_WAVES, C2_KT * C2_KF * 2, s0, nks);
 
   bf16x8 bfr[C2_KPW];
 #pragma unroll
   for (int i = 0; i < C2_KPW; ++i) {
-    const int s = w * C2_KPW + i;
+    const int s = s0 + min(i, nks - 1);
     const int kt = s / 10, kf = (s % 10) >> 1, hh = s & 1;
     bf16x8 v;
 #pragma unroll
@@ -135,67 +166,66 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(Conv2Fwd a) {
     }
     bfr[i] = v;
   }
-  unsigned f2c[MT];
+  unsigned lb[MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) f2c[m] = (unsigned)min(32 * m + col, a.F2 - 1);
+  for (int m = 0; m < MT; ++m) lb[m] = (unsigned)(min(32 * m + col, a.F2 - 1) * PR + hi * 16);
   const float bco = a.bias ? a.bias[col] : 0.f;
 
   const int ntiles = a.N * a.T2;
-  const int nchunks = C2_KT * a.F1 * 4;
-  auto issue = [&](int t, unsigned char* dst) {
+  const int nch = C2_KT * a.F1 * 4;
+  auto src_of = [&](int t) {
     const int n = t / a.T2, t2 = t - n * a.T2;
-    const unsigned char* src = (const unsigned char*)(a.x + ((size_t)n * a.T1 + 2 * t2) * a.F1 * CC);
-    for (int p0 = w * 64; p0 < nchunks; p0 += 256) {
-      const int p = p0 + lane;
-      if (p < nchunks) {
-        const unsigned R = (unsigned)p >> 2, c = (unsigned)p & 3u;
-        glds16(src + (size_t)(R * 4u + (c ^ ((R >> 2) & 3u))) * 16u, dst + (size_t)p0 * 16);
-      }
-    }
+    return (const unsigned char*)(a.x + ((size_t)n * a.T1 + 2 * t2) * a.F1 * CC);
   };
-
+  Stager stg;
   float ssum = 0.f, ssq = 0.f;
-  int it = 0;
-  if ((int)blockIdx.x < ntiles) issue(blockIdx.x, buf0);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
-    const unsigned char* cur = (it & 1) ? buf1 : buf0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x, (it & 1) ? buf0 : buf1);
-
+  if ((int)blockIdx.x < ntiles) {
+    stg.load(src_of(blockIdx.x), nch);
+    stg.store(buf, nch);
+    if ((int)(blockIdx.x + gridDim.x) < ntiles) stg.load(src_of(blockIdx.x + gridDim.x), nch);
+  }
+  lds_barrier();
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     f32x16 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x16){};
+    bf16x8 af[2][MT];
+    auto ldA = [&](int i, bf16x8 (&dst)[MT]) {
+      const int s = s0 + i;
+      const unsigned off = (unsigned)(((s / 10) * a.F1 + ((s % 10) >> 1)) * PR + (s & 1) * 32);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) dst[m] = *(const bf16x8*)(buf + lb[m] + off);
+    };
+    ldA(0, af[0]);
 #pragma unroll
     for (int i = 0; i < C2_KPW; ++i) {
-      const int s = w * C2_KPW + i;
-      const int kt = s / 10, kf = (s % 10) >> 1;
-      const unsigned c = (unsigned)(((s & 1) << 1) | hi);
-      const unsigned rb = (unsigned)(kt * a.F1 + kf);
+      if (i < nks) {                               // wave-uniform (only the last step varies)
+        if (i + 1 < nks) ldA(i + 1, af[(i + 1) & 1]);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const bf16x8 av = *(const bf16x8*)(cur + swz(rb + f2c[m], c));
-        acc[m] = mfma32(av, bfr[i], acc[m]);
+        for (int m = 0; m < MT; ++m) acc[m] = mfma32(af[i & 1][m], bfr[i], acc[m]);
       }
     }
+    lds_barrier();                                   // every wave is done reading buf
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4)
         red[(w * 12 + m * 4 + r4) * 64 + lane] =
             (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
+    const int next = tile + gridDim.x;
+    if (next < ntiles) stg.store(buf, nch);
     lds_barrier();
+    if (next + (int)gridDim.x < ntiles) stg.load(src_of(next + gridDim.x), nch);
     const int n = tile / a.T2, t2 = tile - n * a.T2;
     bf16_t* yrow = a.y + ((size_t)n * a.T2 + t2) * a.F2 * CC;
+    for (int item = tid; item < 12 * 64; item += 512) {   // (e = m*4 + r4, lane) items; channel = tid & 31
+      const int e = item >> 6, l2 = item & 63, m = e >> 2, r4 = e & 3;
+      f32x4 v = red[e * 64 + l2];
 #pragma unroll
-    for (int e3 = 0; e3 < 3; ++e3) {
-      const int e = w * 3 + e3, m = e >> 2, r4 = e & 3;
-      f32x4 v = red[e * 64 + lane];
-#pragma unroll
-      for (int wv = 1; wv < 4; ++wv) v += red[(wv * 12 + e) * 64 + lane];
+      for (int wv = 1; wv < C2_WAVES; ++wv) v += red[(wv * 12 + e) * 64 + l2];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int f2 = 32 * m + j + 8 * r4 + 4 * hi;
+        const int f2 = 32 * m + j + 8 * r4 + 4 * (l2 >> 5);
         if (f2 < a.F2) {
           const bf16_t b = f2bf(v[j] + bco);
           yrow[f2 * CC + col] = b;
@@ -205,9 +235,10 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(Conv2Fwd a) {
         }
       }
     }
-    // the next iteration's first barrier orders these reads before red is rewritten
+    // red is rewritten only after the next tile's MFMA loop and its barrier
   }
-  write_stats(ssum, ssq, statsh, 4, a.part);
+  lds_barrier();
+  write_stats(ssum, ssq, (float*)red, C2_WAVES, a.part);
 }
 
 // =====================================================================================
@@ -219,21 +250,22 @@ struct Conv2Dgrad {
   bf16_t* dx;         // [N][T1][F1][32]
   int N, T1, F1, T2, F2;
 };
+constexpr int C2D_STG = 3;                       // 16-B staging loads per thread (5 rows x F2 <= 76)
 
-__global__ __launch_bounds__(256) void conv2_dgrad_kernel(Conv2Dgrad a) {
+__global__ __launch_bounds__(512) void conv2_dgrad_kernel(Conv2Dgrad a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
   const int hi = lane >> 5, col = lane & 31;
-  const int par = w >> 1, wp = w & 1;
-  const int inBytes = 5 * a.F2 * 64;
-  unsigned char* const buf0 = smem;
-  unsigned char* const buf1 = smem + inBytes;
-  f32x4* red = (f32x4*)(smem + 2 * inBytes);
+  const int par = w >> 2, wq = w & 3;            // waves 0-3: even output row, 4-7: odd
+  unsigned char* const buf = smem;                                   // [5*F2][80 B]
+  f32x4* red = (f32x4*)(smem + 5 * a.F2 * PR);                       // [8 waves][12][64]
+  int s0, nks;
+  kspan(wq, 4, C2_KT * C2_KF, s0, nks);          // 50 k-steps per parity
 
   bf16x8 bfr[C2_KPW];
 #pragma unroll
   for (int i = 0; i < C2_KPW; ++i) {
-    const int s = wp * C2_KPW + i;                 // 0..49 within this parity
+    const int s = s0 + min(i, nks - 1);
     const int ai = s / 10, kf = (s % 10) >> 1, hh = s & 1;
     const int kt = 2 * ai + par;
     bf16x8 v;
@@ -246,72 +278,81 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(Conv2Dgrad a) {
   }
   const int U = (a.T1 + 1) >> 1;
   const int ntiles = a.N * U;
-  auto issue = [&](int t, unsigned char* dst) {
+  const int nch = 5 * a.F2 * 4;
+  const size_t rowEl = (size_t)a.F2 * CC;
+  // rows u-4 .. u of dy (row slot j = row - (u-4)); rows outside [0, T2) are never read
+  i32x4 stg[C2D_STG];
+  auto load = [&](int t) {
     const int n = t / U, u = t - n * U;
-    const int r0 = max(0, u - 4), r1 = min(u, a.T2 - 1);
-    if (r0 > r1) return;
-    const int P0 = (r0 - (u - 4)) * a.F2 * 4, P1 = (r1 - (u - 4) + 1) * a.F2 * 4;
-    const long long base = ((long long)n * a.T2 + (u - 4)) * a.F2 * CC;   // may point before row 0
-    for (int p0 = P0 + w * 64; p0 < P1; p0 += 256) {
-      const int p = p0 + lane;
-      if (p < P1) {
-        const unsigned R = (unsigned)p >> 2, c = (unsigned)p & 3u;
-        const long long el = base + (long long)(R * 4u + (c ^ ((R >> 2) & 3u))) * 8;
-        glds16(a.dy + el, dst + (size_t)p0 * 16);
-      }
+    const bf16_t* base = a.dy + (size_t)n * a.T2 * rowEl;
+#pragma unroll
+    for (int k = 0; k < C2D_STG; ++k) {
+      const int p = min(tid + 512 * k, nch - 1);
+      const int row = min(max(u - 4 + (p >> 2) / a.F2, 0), a.T2 - 1);
+      const int pos = (p >> 2) % a.F2;
+      stg[k] = *(const i32x4*)(base + row * rowEl + pos * CC + (p & 3) * 8);
     }
   };
-
-  int it = 0;
-  if ((int)blockIdx.x < ntiles) issue(blockIdx.x, buf0);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x, ++it) {
-    const unsigned char* cur = (it & 1) ? buf1 : buf0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) issue(tile + gridDim.x, (it & 1) ? buf0 : buf1);
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < C2D_STG; ++k) {
+      const int p = tid + 512 * k;
+      if (p < nch) *(i32x4*)(buf + (p >> 2) * PR + (p & 3) * 16) = stg[k];
+    }
+  };
+  if ((int)blockIdx.x < ntiles) {
+    load(blockIdx.x);
+    store();
+    if ((int)(blockIdx.x + gridDim.x) < ntiles) load(blockIdx.x + gridDim.x);
+  }
+  lds_barrier();
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int n = tile / U, u = tile - n * U;
-
     f32x16 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x16){};
 #pragma unroll
     for (int i = 0; i < C2_KPW; ++i) {
-      const int s = wp * C2_KPW + i;
+      const int s = s0 + i;
       const int ai = s / 10, kf = (s % 10) >> 1;
-      const unsigned c = (unsigned)(((s & 1) << 1) | hi);
       const int t2 = u - ai;
-      if (t2 >= 0 && t2 < a.T2) {                  // wave-uniform
+      if (i < nks && t2 >= 0 && t2 < a.T2) {     // wave-uniform
         const int slotb = (4 - ai) * a.F2;
+        bf16x8 av[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const int f2 = 32 * m + col - kf;
-          const bool ok = f2 >= 0 && f2 < a.F2;
           const unsigned R = (unsigned)(slotb + min(max(f2, 0), a.F2 - 1));
-          bf16x8 av = *(const bf16x8*)(cur + swz(R, c));
-          if (!ok) av = (bf16x8){};
-          acc[m] = mfma32(av, bfr[i], acc[m]);
+          av[m] = *(const bf16x8*)(buf + R * PR + (s & 1) * 32 + hi * 16);
+          if (!(f2 >= 0 && f2 < a.F2)) av[m] = (bf16x8){};
         }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = mfma32(av[m], bfr[i], acc[m]);
       }
     }
+    lds_barrier();
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4)
         red[(w * 12 + m * 4 + r4) * 64 + lane] =
             (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
+    const int next = tile + gridDim.x;
+    if (next < ntiles) store();
     lds_barrier();
-    const int opar = w >> 1, half = w & 1;
-    const int t1 = 2 * u + opar;
-    if (t1 < a.T1) {
-      bf16_t* xrow = a.dx + ((size_t)n * a.T1 + t1) * a.F1 * CC;
+    if (next + (int)gridDim.x < ntiles) load(next + gridDim.x);
+    for (int item = tid; item < 2 * 12 * 64; item += 512) {
+      const int opar = item / 768, e = (item >> 6) % 12, l2 = item & 63, m = e >> 2, r4 = e & 3;
+      const int t1 = 2 * u + opar;
+      f32x4 v = red[((4 * opar) * 12 + e) * 64 + l2];
 #pragma unroll
-      for (int e6 = 0; e6 < 6; ++e6) {
-        const int e = half * 6 + e6, m = e >> 2, r4 = e & 3;
-        const f32x4 v = red[((2 * opar) * 12 + e) * 64 + lane] + red[((2 * opar + 1) * 12 + e) * 64 + lane];
+      for (int wv = 1; wv < 4; ++wv) v += red[((4 * opar + wv) * 12 + e) * 64 + l2];
+      if (t1 < a.T1) {
+        bf16_t* xrow = a.dx + ((size_t)n * a.T1 + t1) * a.F1 * CC;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int f1 = 32 * m + j + 8 * r4 + 4 * hi;
-          if (f1 < a.F1) xrow[f1 * CC + col] = f2bf(v[j]);
+          const int f1 = 32 * m + j + 8 * r4 + 4 * (l2 >> 5);
+          if (f1 < a.F1) xrow[f1 * CC + (l2 & 31)] = f2bf(v[j]);
         }
       }
     }
@@ -405,17 +446,40 @@ __global__ __launch_bounds__(512) void conv2_wgrad_kernel(Conv2Wgrad a) {
   }
 }
 
-// sum of per-workgroup partials -> dw2 [32][32][10][5] (fp32, arena)
-__global__ __launch_bounds__(256) void conv2_wgrad_reduce_kernel(const float* __restrict__ part, int nb,
-                                                                  float* __restrict__ dw) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= C2W_PAIRS * 1024) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(size_t)b * C2W_PAIRS * 1024 + e];
-  const int P = e >> 10, rem = e & 1023, r4 = rem >> 8, lane = (rem >> 2) & 63, j = rem & 3;
-  const int co = j + 8 * r4 + 4 * (lane >> 5), ci = lane & 31;
-  const int kt = P / 5, kf = P % 5;
-  dw[((co * CC + ci) * C2_KT + kt) * C2_KF + kf] = s;
+// sum of per-workgroup partials (fragment order) -> dw in OIHW, KIND 0: conv2 [32][32][10][5],
+// KIND 1: conv1 [32][1][20][5]. A block owns 256 consecutive elements (64 f32x4 columns)
+// and 4 interleaved groups of partials, so every thread keeps several 16-B loads in flight.
+template <int KIND>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int nb, int E,
+                                                           float* __restrict__ dw) {
+  __shared__ f32x4 sh[4][64];
+  const int tid = threadIdx.x, g = tid >> 6, l = tid & 63;
+  const int e4 = blockIdx.x * 64 + l, E4 = E >> 2;
+  const f32x4* p4 = (const f32x4*)part;
+  f32x4 s0 = {}, s1 = {};
+  int b = g;
+  for (; b + 4 < nb; b += 8) {
+    s0 += p4[(size_t)b * E4 + e4];
+    s1 += p4[(size_t)(b + 4) * E4 + e4];
+  }
+  if (b < nb) s0 += p4[(size_t)b * E4 + e4];
+  sh[g][l] = s0 + s1;
+  __syncthreads();
+  if (g != 0) return;
+  const f32x4 v = sh[0][l] + sh[1][l] + sh[2][l] + sh[3][l];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = e4 * 4 + j;
+    const int P = e >> 10, rem = e & 1023, r4 = rem >> 8, ln = (rem >> 2) & 63;
+    const int row = (rem & 3) + 8 * r4 + 4 * (ln >> 5), c = ln & 31;
+    if (KIND == 0) {
+      const int kt = P / 5, kf = P % 5;
+      dw[((row * CC + c) * C2_KT + kt) * C2_KF + kf] = v[j];
+    } else {
+      const int kt = 4 * P + (c >> 3), kf = c & 7;
+      if (kf < 5) dw[(row * 20 + kt) * 5 + kf] = v[j];
+    }
+  }
 }
 
 // =====================================================================================
@@ -434,6 +498,26 @@ constexpr int C1_XS = 200;     // staged row stride (elements): covers 2*95 + 7
 constexpr int C1_ROWS = 4;     // output rows per workgroup (one per wave)
 constexpr int C1_IN = 2 * (C1_ROWS - 1) + C1_KT;   // 26 input rows
 
+// stage input rows t0 .. t0+C1_IN-1 of one utterance ([T][F0] bf16, rows 2-B aligned only) into
+// LDS rows of C1_XS elements, zero outside the utterance / beyond F0. Loads are unconditional
+// (clamped addresses) so all of them are in flight together; the select happens afterwards.
+__device__ __forceinline__ void stage_rows(bf16_t* xs, const bf16_t* xu, int t0, int T, int F0) {
+  constexpr int NE = C1_IN * C1_XS, K = (NE + 255) / 256;
+  bf16_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int idx = min((int)threadIdx.x + 256 * k, NE - 1);
+    const int r = idx / C1_XS, c = idx - r * C1_XS;
+    v[k] = xu[(size_t)min(t0 + r, T - 1) * F0 + min(c, F0 - 1)];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int idx = (int)threadIdx.x + 256 * k;
+    const int r = idx / C1_XS, c = idx - r * C1_XS;
+    if (idx < NE) xs[idx] = (t0 + r < T && c < F0) ? v[k] : (bf16_t)0;
+  }
+}
+
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Fwd a) {
   __shared__ __attribute__((aligned(16))) bf16_t xs[C1_IN * C1_XS];
   __shared__ float statsh[4 * 32 * 2];
@@ -441,11 +525,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Fwd a) {
   const int hi = lane >> 5, col = lane & 31;
   const int tb = (a.T1 + C1_ROWS - 1) / C1_ROWS;
   const int n = blockIdx.x / tb, t1_0 = (blockIdx.x - n * tb) * C1_ROWS;
-  for (int idx = tid; idx < C1_IN * C1_XS; idx += 256) {
-    const int r = idx / C1_XS, c = idx - r * C1_XS;
-    const int t = 2 * t1_0 + r;
-    xs[idx] = (t < a.T && c < a.F0) ? a.x[((size_t)n * a.T + t) * a.F0 + c] : (bf16_t)0;
-  }
+  stage_rows(xs, a.x + (size_t)n * a.T * a.F0, 2 * t1_0, a.T, a.F0);
   bf16x8 bfr[10];
 #pragma unroll
   for (int s = 0; s < 10; ++s) {
@@ -505,7 +585,8 @@ constexpr int C1W_XP = 88;                       // de-interleaved row stride (p
 constexpr int C1W_DY = C1_ROWS * 80 * 64;        // dy image bytes (4 rows x 80 positions)
 constexpr int C1W_XD = C1_IN * 8 * C1W_XP * 2;   // x image bytes
 constexpr int C1W_RED = 4 * 5 * 4 * 64 * 16;     // wave partials
-constexpr int C1W_SMEM = (C1W_DY + C1W_XD) > C1W_RED ? (C1W_DY + C1W_XD) : C1W_RED;
+constexpr int C1W_RAW = C1_IN * C1_XS * 2;             // raw input rows
+constexpr int C1W_SMEM = (C1W_DY + C1W_XD + C1W_RAW) > C1W_RED ? (C1W_DY + C1W_XD + C1W_RAW) : C1W_RED;
 
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(Conv1Wgrad a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -513,6 +594,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(Conv1Wgrad a) {
   const int hi = lane >> 5, col = lane & 31;
   unsigned char* dys = smem;
   bf16_t* xd = (bf16_t*)(smem + C1W_DY);
+  bf16_t* raw = (bf16_t*)(smem + C1W_DY + C1W_XD);
   const int tb = (a.T1 + C1_ROWS - 1) / C1_ROWS;
   const int ntiles = a.N * tb;
   const int g = lane >> 4, h = g >> 1, cb = (g & 1) * 16, q = (lane & 15) >> 2, pp = lane & 3;
@@ -534,17 +616,14 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(Conv1Wgrad a) {
         v = *(const i32x4*)(a.dy + (((size_t)n * a.T1 + t1) * a.F1 + pos) * CC + c4 * 8);
       *(i32x4*)(dys + ch * 16) = v;
     }
-    // x rows 2*t1_0 + r, de-interleaved: xd[r][kf'][p] = x[t][2p + kf'] (zero outside)
+    // x rows 2*t1_0 + r: raw rows into LDS, then de-interleaved xd[r][kf'][p] = x[t][2p + kf']
+    stage_rows(raw, a.x + (size_t)n * a.T * a.F0, 2 * t1_0, a.T, a.F0);
+    __syncthreads();
     for (int ch = tid; ch < C1_IN * 8 * 10; ch += 256) {
       const int r = ch / 80, rem = ch - r * 80, kf = rem / 10, p0 = (rem - kf * 10) * 8;
-      const int t = 2 * t1_0 + r;
       bf16x8 v;
-      const bf16_t* src = a.x + ((size_t)n * a.T + min(t, a.T - 1)) * a.F0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = 2 * (p0 + j) + kf;
-        v[j] = (t < a.T && c < a.F0) ? (short)src[c] : (short)0;
-      }
+      for (int j = 0; j < 8; ++j) v[j] = (short)raw[r * C1_XS + min(2 * (p0 + j) + kf, C1_XS - 1)];
       *(bf16x8*)(xd + (r * 8 + kf) * C1W_XP + p0) = v;
     }
     __syncthreads();
@@ -579,19 +658,6 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(Conv1Wgrad a) {
     for (int wv = 1; wv < 4; ++wv) v += red[wv * 5 * 4 * 64 + e];
     out[e] = v;
   }
-}
-
-__global__ __launch_bounds__(256) void conv1_wgrad_reduce_kernel(const float* __restrict__ part, int nb,
-                                                                  float* __restrict__ dw) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= 5 * 1024) return;
-  const int nt = e >> 10, rem = e & 1023, r4 = rem >> 8, lane = (rem >> 2) & 63, j = rem & 3;
-  const int c = lane & 31, kt = 4 * nt + (c >> 3), kf = c & 7;
-  if (kf >= C1_KF) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(size_t)b * 5 * 1024 + e];
-  const int co = j + 8 * r4 + 4 * (lane >> 5);
-  dw[(co * C1_KT + kt) * C1_KF + kf] = s;
 }
 
 // =====================================================================================
@@ -855,7 +921,7 @@ int set_smem(K kernel, size_t bytes) {
 }
 
 int shape_ok(int T1, int F1, int T2, int F2) {
-  if (F1 < 5 || F1 > 84 || F2 != F1 - 4 || F2 > 80) return -40;
+  if (F1 < 5 || F1 > 80 || F2 != F1 - 4) return -40;   // LDS (10*F1*80 + 96 KiB) and staging capacity
   if (T1 < 10 || T2 != (T1 - 10) / 2 + 1) return -41;
   return 0;
 }
@@ -864,8 +930,8 @@ int shape_ok(int T1, int F1, int T2, int F2) {
 
 extern "C" {
 
-size_t ds2_conv2_fwd_smem(int F1) { return (size_t)2 * C2_KT * F1 * 64 + 4 * 12 * 64 * 16 + 4 * 32 * 2 * 4; }
-size_t ds2_conv2_dgrad_smem(int F2) { return (size_t)2 * 5 * F2 * 64 + 4 * 12 * 64 * 16; }
+size_t ds2_conv2_fwd_smem(int F1) { return (size_t)C2_KT * F1 * PR + C2_WAVES * 12 * 64 * 16; }
+size_t ds2_conv2_dgrad_smem(int F2) { return (size_t)5 * F2 * PR + C2_WAVES * 12 * 64 * 16; }
 size_t ds2_conv2_wgrad_smem(int F1) { return (size_t)2 * (80 * 64 + (9 * F1 + 84) * 64); }
 long long ds2_conv2_wgrad_part_floats(int grid) { return (long long)grid * C2W_PAIRS * 1024; }
 long long ds2_conv1_wgrad_part_floats(int grid) { return (long long)grid * 5 * 1024; }
@@ -877,7 +943,7 @@ int ds2_conv2_fwd(const void* x, const void* w, const float* bias, void* y, floa
   const size_t smem = ds2_conv2_fwd_smem(F1);
   DS2_HIP_CHECK((hipError_t)set_smem(conv2_fwd_kernel, smem));
   Conv2Fwd a{(const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y, part, N, T1, F1, T2, F2};
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(grid), dim3(256), smem, st, a);
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(grid), dim3(512), smem, st, a);
   return (int)hipGetLastError();
 }
 
@@ -887,7 +953,7 @@ int ds2_conv2_dgrad(const void* dy, const void* w, void* dx, int grid, int N, in
   const size_t smem = ds2_conv2_dgrad_smem(F2);
   DS2_HIP_CHECK((hipError_t)set_smem(conv2_dgrad_kernel, smem));
   Conv2Dgrad a{(const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, N, T1, F1, T2, F2};
-  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(grid), dim3(256), smem, st, a);
+  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(grid), dim3(512), smem, st, a);
   return (int)hipGetLastError();
 }
 
@@ -898,7 +964,8 @@ int ds2_conv2_wgrad(const void* dy, const void* x, float* part, int grid, float*
   DS2_HIP_CHECK((hipError_t)set_smem(conv2_wgrad_kernel, smem));
   Conv2Wgrad a{(const bf16_t*)dy, (const bf16_t*)x, part, N, T1, F1, T2, F2};
   hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(grid), dim3(512), smem, st, a);
-  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(C2W_PAIRS * 1024 / 256), dim3(256), 0, st, part, grid, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel<0>, dim3(C2W_PAIRS * 1024 / 256), dim3(256), 0, st, part, grid,
+                     C2W_PAIRS * 1024, dw);
   return (int)hipGetLastError();
 }
 
@@ -916,7 +983,7 @@ int ds2_conv1_wgrad(const void* dy, const void* x, float* part, int grid, float*
   DS2_HIP_CHECK((hipError_t)set_smem(conv1_wgrad_kernel, C1W_SMEM));
   Conv1Wgrad a{(const bf16_t*)dy, (const bf16_t*)x, part, N, T, F0, T1, F1};
   hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(grid), dim3(256), C1W_SMEM, st, a);
-  hipLaunchKernelGGL(conv1_wgrad_reduce_kernel, dim3(5 * 1024 / 256), dim3(256), 0, st, part, grid, dw);
+  hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(5 * 1024 / 256), dim3(256), 0, st, part, grid, 5 * 1024, dw);
   return (int)hipGetLastError();
 }
 

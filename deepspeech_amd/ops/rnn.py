@@ -461,6 +461,28 @@ class FusedBiLayer(torch.autograd.Function):
         dgx2 = dgx.view(T * N, plan.ndir * GH)
         dx = torch.mm(dgx2, W16).view(T, N, D) if ctx.needs_input_grad[0] else None
         # ---- weight gradients (off the critical path) ----
+        # only arena-managed weights (gradients written to main_grad, nothing returned to
+        # autograd) may be produced on another stream; the Trainer joins it before Adam
+        side = wgrad_stream(x16.device) if arena_of(ctx.params[0]) is not None else None
+        if side is None:
+            return FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx)
+        # The layer below only needs dx: its BPTT (200 of the 256 CUs, latency-bound) runs
+        # while these GEMMs fill the idle CUs. Gradients land in the arena on the side
+        # stream, and the bucket hooks fire inside it, so an all-reduce waits for them.
+        side.wait_stream(torch.cuda.current_stream(x16.device))
+        with torch.cuda.stream(side):
+            for t in (x16, dgx, dgh, hx, parts):
+                if t is not None:
+                    t.record_stream(side)
+            return FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx)
+
+    @staticmethod
+    def _weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx):
+        plan: RnnPlan = ctx.plan
+        W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b = ctx.params
+        d1 = plan.ndir == 2
+        T, N, D = x16.shape
+        GH = GATES[plan.cell] * plan.H
         x2 = x16.view(T * N, D)
         arena = arena_of(W_f)
         gW = [None, None]
@@ -496,6 +518,28 @@ class FusedBiLayer(torch.autograd.Function):
         gb = _bias_grads([b_f, b_b] if d1 else [b_f], parts[0])
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
+
+
+_side_streams = {}
+
+
+def wgrad_stream(device: torch.device) -> Optional["torch.cuda.Stream"]:
+    """Side stream for the recurrent layers' weight-gradient GEMMs (DS2_WGRAD_STREAM=0
+    keeps them on the current stream). Callers join it with :func:`join_wgrad_streams`
+    before the optimizer reads the gradients."""
+    if device.type != "cuda" or os.environ.get("DS2_WGRAD_STREAM", "1") != "1":
+        return None
+    s = _side_streams.get(device.index)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _side_streams[device.index] = s
+    return s
+
+
+def join_wgrad_streams() -> None:
+    """Make the current stream wait for every pending side-stream weight gradient."""
+    for idx, s in _side_streams.items():
+        torch.cuda.current_stream(idx).wait_stream(s)
 
 
 _plan_cache = {}

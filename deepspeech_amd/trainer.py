@@ -24,6 +24,7 @@ import torch
 
 from .models import DeepSpeech2
 from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
+from .ops.rnn import join_wgrad_streams
 from .parallel.grad_sync import GradBucketer, broadcast_params
 from .utils import trace as TR
 
@@ -80,6 +81,7 @@ class Trainer:
         logits, lens = model(batch["feats"], batch["seq_lens"])
         loss = model.loss(logits, lens, batch["labels"], batch["label_lens"])
         loss.backward()
+        join_wgrad_streams()
         with TR.phase(TR.ALLREDUCE):
             self.bucketer.finish()
         gscale = 1.0 / self.world
