@@ -91,6 +91,8 @@ int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void*
 int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
+int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
+                   int* labels, int* counts, float* score, hipStream_t st);
 size_t ds2_conv2_fwd_smem(int F1);
 size_t ds2_conv2_dgrad_smem(int F2);
 size_t ds2_conv2_wgrad_smem(int F1);
@@ -522,6 +524,22 @@ void bn_cl_bwd(at::Tensor dz, at::Tensor y, at::Tensor mean, at::Tensor invstd, 
                       (int)y.size(1), (int)y.size(2), tmaj ? 1 : 0, cur_stream()), "bn_cl_bwd");
 }
 
+// --------------------------------------------------------------------------- greedy CTC decode
+// logits [T, N, K] (fp32/bf16, time-major) -> labels [N, T] int32 (first counts[n] valid),
+// counts [N] int32, optional score [N] fp32 (greedy path log-probability)
+void ctc_greedy(at::Tensor logits, at::Tensor lens, at::Tensor labels, at::Tensor counts, int64_t blank,
+                OptT score) {
+  need_gpu(logits, "logits"); need_gpu(lens, "lens"); need_gpu(labels, "labels"); need_gpu(counts, "counts");
+  TORCH_CHECK(logits.dim() == 3, "logits must be [T, N, K]");
+  const int T = (int)logits.size(0), N = (int)logits.size(1), K = (int)logits.size(2);
+  TORCH_CHECK(lens.scalar_type() == at::kInt && lens.numel() == N, "lens must be int32 [N]");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.numel() >= (int64_t)N * T, "labels must be int32 [N, T]");
+  TORCH_CHECK(counts.scalar_type() == at::kInt && counts.numel() == N, "counts must be int32 [N]");
+  check(ds2_ctc_greedy(logits.data_ptr(), is_bf16(logits), lens.data_ptr<int>(), T, N, K, (int)blank,
+                       labels.data_ptr<int>(), counts.data_ptr<int>(), ptr_or_null<float>(score, "score"),
+                       cur_stream()), "ctc_greedy");
+}
+
 // --------------------------------------------------------------------------- device info
 py::dict device_info(int64_t dev) {
   hipDeviceProp_t prop;
@@ -578,6 +596,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("cast_bf16", &cast_bf16);
   m.def("device_info", &device_info);
+  m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),
+        py::arg("blank"), py::arg("score") = py::none());
   m.def("conv1_fwd", &conv1_fwd);
   m.def("conv1_fwd_grid", &conv1_fwd_grid);
   m.def("conv2_fwd", &conv2_fwd);

@@ -13,7 +13,8 @@ arrives:
   * recurrent stack: every layer carries its final hidden state to the next chunk (the
     persistent kernels start from an initial state: ops/rnn.py:recurrent_layer_infer);
   * head + log-softmax per new frame; greedy decoding collapses across chunk boundaries
-    incrementally, prefix beam search (native runtime) runs over all frames at the end.
+    incrementally, and the prefix beam search (native runtime, one host thread per stream
+    group) also advances chunk by chunk, so a transcript is ready when the audio ends.
 
 Batched streams: ``StreamingRecognizer`` takes [B, T_chunk, F] chunks of B concurrent
 streams (equal chunk schedule, per-stream valid lengths), which is how a server batches.
@@ -56,6 +57,10 @@ class StreamingRecognizer:
         self.done = 0                       # output (post-conv) frames emitted
         self.states: List[Optional[torch.Tensor]] = [None] * len(self.model.rnn)
         self.logprobs: List[torch.Tensor] = []
+        self.beams = None
+        if self.decoder == "beam":
+            from .runtime import native
+            self.beams = native.load().BatchBeamSearch(self.B, self.beam_width, BLANK, -10.0)
         self.last_sym = [-1] * self.B
         self.greedy: List[List[int]] = [[] for _ in range(self.B)]
         self.compute_s = 0.0
@@ -89,6 +94,10 @@ class StreamingRecognizer:
         lp = torch.log_softmax(logits, -1)                     # [new, B, K]
         self.logprobs.append(lp)
         best = lp.argmax(-1).cpu().numpy()                     # [new, B]
+        if self.beams is not None:
+            # prefix beam search advances chunk by chunk (beams carried in the native
+            # runtime, streams decoded on parallel host threads)
+            self.beams.feed(lp.cpu().numpy(), np.full((self.B,), new, dtype=np.int32))
         for b in range(self.B):
             for t in range(best.shape[0]):
                 s = int(best[t, b])
@@ -122,15 +131,9 @@ class StreamingRecognizer:
     def finish(self) -> List[List[int]]:
         """Final transcript label ids per stream (beam search over the whole stream if the
         decoder is 'beam', otherwise the incremental greedy result)."""
-        if self.decoder != "beam" or not self.logprobs:
+        if self.beams is None:
             return [list(g) for g in self.greedy]
-        t0 = time.perf_counter()
-        from .runtime import native
-        lp = torch.cat(self.logprobs, 0).cpu().numpy()        # [T2, B, K]
-        lens = np.full((self.B,), lp.shape[0], dtype=np.int32)
-        res = native.load().beam_search_batch(lp, lens, self.beam_width, BLANK, -10.0)
-        self.compute_s += time.perf_counter() - t0
-        return res
+        return self.beams.best()
 
 
 def rtf(model: DeepSpeech2, seconds: float = 10.0, chunk_s: float = 1.0, batch: int = 1,

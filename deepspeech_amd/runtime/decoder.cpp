@@ -9,6 +9,10 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <stdexcept>
+#include <thread>
 #include <cmath>
 #include <limits>
 #include <map>
@@ -68,28 +72,19 @@ int levenshtein_str(const std::string& a, const std::string& b) { return edit_di
 int levenshtein_ids(const std::vector<int>& a, const std::vector<int>& b) { return edit_distance(a, b); }
 
 // ---------------------------------------------------------------- prefix beam search
-struct Beam {
-  std::vector<int> prefix;
-  float pb;    // log prob ending in blank
-  float pnb;   // log prob ending in non-blank
-  float total() const { return log_add(pb, pnb); }
-};
-
-struct VecHash {
-  size_t operator()(const std::vector<int>& v) const {
-    size_t h = 1469598103934665603ull;
-    for (int x : v) h = (h ^ (size_t)(x + 1)) * 1099511628211ull;
-    return h;
-  }
-};
-
+// Prefixes live in a trie (node = parent + last label), so extending a prefix, testing its
+// last label and merging two hypotheses that reach the same prefix are O(1) integer
+// operations instead of copying and hashing label vectors. Per frame, the candidate set
+// is the classes within `prune` (log) of the frame's best class.
 class PrefixBeamSearch {
  public:
   PrefixBeamSearch(int beam, int blank, float prune) : beam_(beam), blank_(blank), prune_(prune) { reset(); }
 
   void reset() {
-    beams_.clear();
-    beams_.push_back(Beam{{}, 0.f, -INFINITY});
+    nodes_.assign(1, Node{-1, -1});
+    children_.clear();
+    slot_.assign(1, -1);
+    beams_.assign(1, Hyp{0, 0.f, -INFINITY});
   }
 
   // log_probs: [T, K] log-softmax rows of ONE utterance (a streaming chunk or the whole thing)
@@ -98,72 +93,134 @@ class PrefixBeamSearch {
     const int T = (int)lp.shape(0), K = (int)lp.shape(1);
     const float* data = log_probs.data();
     py::gil_scoped_release rel;
-    feed_raw(data, T, K);
+    feed_raw(data, T, K, K);
   }
 
-  void feed_raw(const float* lp, int T, int K) {
+  // rows t at lp + t * stride (stride >= K: rows of a [T, B, K] tensor for one stream)
+  void feed_raw(const float* lp, int T, int K, size_t stride) {
     std::vector<int> cand;
+    std::vector<Hyp> next;
+    std::vector<int> touched;
     for (int t = 0; t < T; ++t) {
-      const float* row = lp + (size_t)t * K;
+      const float* row = lp + (size_t)t * stride;
       cand.clear();
       float mx = -INFINITY;
       for (int k = 0; k < K; ++k) mx = std::max(mx, row[k]);
       for (int k = 0; k < K; ++k)
         if (row[k] >= mx + prune_) cand.push_back(k);
-      std::unordered_map<std::vector<int>, Beam, VecHash> next;
-      next.reserve(beams_.size() * (cand.size() + 1) * 2);
-      auto get = [&](const std::vector<int>& p) -> Beam& {
-        auto it = next.find(p);
-        if (it == next.end()) it = next.emplace(p, Beam{p, -INFINITY, -INFINITY}).first;
-        return it->second;
+      next.clear();
+      touched.clear();
+      auto get = [&](int node) -> Hyp& {
+        if ((size_t)node >= slot_.size()) slot_.resize(nodes_.size(), -1);
+        int& s = slot_[node];
+        if (s < 0) {
+          s = (int)next.size();
+          next.push_back(Hyp{node, -INFINITY, -INFINITY});
+          touched.push_back(node);
+        }
+        return next[s];
       };
-      for (const Beam& b : beams_) {
-        const float tot = b.total();
+      for (size_t bi = 0; bi < beams_.size(); ++bi) {
+        const Hyp b = beams_[bi];
+        const float tot = log_add(b.pb, b.pnb);
+        const int last = nodes_[b.node].label;
         for (int k : cand) {
           const float p = row[k];
           if (k == blank_) {
-            Beam& nb = get(b.prefix);
+            Hyp& nb = get(b.node);
             nb.pb = log_add(nb.pb, tot + p);
             continue;
           }
-          const int last = b.prefix.empty() ? -1 : b.prefix.back();
-          std::vector<int> ext = b.prefix;
-          ext.push_back(k);
-          Beam& ne = get(ext);
+          const int ext = child(b.node, k);
           if (k == last) {
+            Hyp& ne = get(ext);
             ne.pnb = log_add(ne.pnb, b.pb + p);        // repeated char needs a blank between
-            Beam& same = get(b.prefix);
+            Hyp& same = get(b.node);
             same.pnb = log_add(same.pnb, b.pnb + p);   // collapse into the same prefix
           } else {
+            Hyp& ne = get(ext);
             ne.pnb = log_add(ne.pnb, tot + p);
           }
         }
       }
-      beams_.clear();
-      beams_.reserve(next.size());
-      for (auto& kv : next) beams_.push_back(std::move(kv.second));
-      std::sort(beams_.begin(), beams_.end(), [](const Beam& a, const Beam& b) { return a.total() > b.total(); });
-      if ((int)beams_.size() > beam_) beams_.resize(beam_);
+      for (int node : touched) slot_[node] = -1;
+      const size_t keep = std::min<size_t>((size_t)beam_, next.size());
+      std::partial_sort(next.begin(), next.begin() + keep, next.end(),
+                        [](const Hyp& a, const Hyp& b) { return log_add(a.pb, a.pnb) > log_add(b.pb, b.pnb); });
+      next.resize(keep);
+      beams_.swap(next);
     }
   }
 
   std::vector<std::pair<std::vector<int>, float>> results() const {
     std::vector<std::pair<std::vector<int>, float>> r;
-    for (const Beam& b : beams_) r.emplace_back(b.prefix, b.total());
+    for (const Hyp& b : beams_) r.emplace_back(prefix(b.node), log_add(b.pb, b.pnb));
     return r;
   }
 
-  std::vector<int> best() const { return beams_.empty() ? std::vector<int>{} : beams_[0].prefix; }
+  std::vector<int> best() const { return beams_.empty() ? std::vector<int>{} : prefix(beams_[0].node); }
 
  private:
+  struct Node {
+    int parent, label;
+  };
+  struct Hyp {
+    int node;
+    float pb;    // log prob ending in blank
+    float pnb;   // log prob ending in non-blank
+  };
+
+  int child(int parent, int label) {
+    const uint64_t key = ((uint64_t)(uint32_t)parent << 16) | (uint32_t)label;
+    auto it = children_.find(key);
+    if (it != children_.end()) return it->second;
+    const int id = (int)nodes_.size();
+    nodes_.push_back(Node{parent, label});
+    children_.emplace(key, id);
+    return id;
+  }
+
+  std::vector<int> prefix(int node) const {
+    std::vector<int> out;
+    for (int n = node; n > 0; n = nodes_[n].parent) out.push_back(nodes_[n].label);
+    std::reverse(out.begin(), out.end());
+    return out;
+  }
+
   int beam_, blank_;
   float prune_;
-  std::vector<Beam> beams_;
+  std::vector<Node> nodes_;
+  std::unordered_map<uint64_t, int> children_;
+  std::vector<int> slot_;     // node -> index into this frame's hypothesis list, -1 if none
+  std::vector<Hyp> beams_;
 };
+
+// run fn(i) for i in [0, n) on up to `threads` worker threads (GIL released by the caller)
+template <typename Fn>
+void parallel_for(int n, int threads, Fn&& fn) {
+  int nt = std::max(1, std::min(n, threads));
+  if (nt == 1) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::atomic<int> next{0};
+  std::vector<std::thread> pool;
+  pool.reserve(nt);
+  for (int w = 0; w < nt; ++w)
+    pool.emplace_back([&]() {
+      for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) fn(i);
+    });
+  for (auto& th : pool) th.join();
+}
+
+int default_threads() {
+  const unsigned hc = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(hc == 0 ? 1u : hc, 16u));
+}
 
 std::vector<std::vector<int>> beam_search_batch(py::array_t<float, py::array::c_style | py::array::forcecast> lp,
                                                 py::array_t<int, py::array::c_style | py::array::forcecast> lens,
-                                                int beam, int blank, float prune) {
+                                                int beam, int blank, float prune, int threads) {
   auto a = lp.unchecked<3>();   // [T, N, K] time-major log-probs
   auto l = lens.unchecked<1>();
   const int T = (int)a.shape(0), N = (int)a.shape(1), K = (int)a.shape(2);
@@ -172,17 +229,48 @@ std::vector<std::vector<int>> beam_search_batch(py::array_t<float, py::array::c_
   const float* base = lp.data();
   std::vector<std::vector<int>> out(N);
   py::gil_scoped_release rel;
-  std::vector<float> slab;
-  for (int n = 0; n < N; ++n) {
-    slab.resize((size_t)L[n] * K);
-    for (int t = 0; t < L[n]; ++t)
-      for (int k = 0; k < K; ++k) slab[(size_t)t * K + k] = base[((size_t)t * N + n) * K + k];
+  parallel_for(N, threads > 0 ? threads : default_threads(), [&](int n) {
     PrefixBeamSearch bs(beam, blank, prune);
-    bs.feed_raw(slab.data(), L[n], K);
+    bs.feed_raw(base + (size_t)n * K, L[n], K, (size_t)N * K);
     out[n] = bs.best();
-  }
+  });
   return out;
 }
+
+// B independent streams decoded incrementally chunk by chunk (streaming inference): the
+// beams persist across feed() calls, streams are spread over worker threads.
+class BatchBeamSearch {
+ public:
+  BatchBeamSearch(int streams, int beam, int blank, float prune, int threads)
+      : threads_(threads > 0 ? threads : default_threads()) {
+    for (int i = 0; i < streams; ++i) s_.emplace_back(beam, blank, prune);
+  }
+  void reset() {
+    for (auto& b : s_) b.reset();
+  }
+  // log_probs [T, B, K]; lens [B] valid frames of this chunk per stream
+  void feed(py::array_t<float, py::array::c_style | py::array::forcecast> lp,
+            py::array_t<int, py::array::c_style | py::array::forcecast> lens) {
+    auto a = lp.unchecked<3>();
+    auto l = lens.unchecked<1>();
+    const int T = (int)a.shape(0), B = (int)a.shape(1), K = (int)a.shape(2);
+    if (B != (int)s_.size()) throw std::runtime_error("BatchBeamSearch.feed: stream count mismatch");
+    std::vector<int> L(B);
+    for (int b = 0; b < B; ++b) L[b] = std::min<int>(T, l(b));
+    const float* base = lp.data();
+    py::gil_scoped_release rel;
+    parallel_for(B, threads_, [&](int b) { s_[b].feed_raw(base + (size_t)b * K, L[b], K, (size_t)B * K); });
+  }
+  std::vector<std::vector<int>> best() const {
+    std::vector<std::vector<int>> r;
+    for (const auto& b : s_) r.push_back(b.best());
+    return r;
+  }
+
+ private:
+  int threads_;
+  std::vector<PrefixBeamSearch> s_;
+};
 
 }  // namespace ds2rt
 
@@ -195,7 +283,13 @@ PYBIND11_MODULE(_native, m) {
   m.def("levenshtein", &ds2rt::levenshtein_str);
   m.def("levenshtein_ids", &ds2rt::levenshtein_ids);
   m.def("beam_search_batch", &ds2rt::beam_search_batch, py::arg("log_probs"), py::arg("lens"), py::arg("beam"),
-        py::arg("blank"), py::arg("prune") = -10.0f);
+        py::arg("blank"), py::arg("prune") = -10.0f, py::arg("threads") = 0);
+  py::class_<ds2rt::BatchBeamSearch>(m, "BatchBeamSearch")
+      .def(py::init<int, int, int, float, int>(), py::arg("streams"), py::arg("beam"), py::arg("blank"),
+           py::arg("prune") = -10.0f, py::arg("threads") = 0)
+      .def("reset", &ds2rt::BatchBeamSearch::reset)
+      .def("feed", &ds2rt::BatchBeamSearch::feed)
+      .def("best", &ds2rt::BatchBeamSearch::best);
   py::class_<ds2rt::PrefixBeamSearch>(m, "PrefixBeamSearch")
       .def(py::init<int, int, float>(), py::arg("beam"), py::arg("blank"), py::arg("prune") = -10.0f)
       .def("reset", &ds2rt::PrefixBeamSearch::reset)

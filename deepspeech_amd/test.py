@@ -57,17 +57,18 @@ def levenshtein(a, b) -> int:
 
 
 def decode(logits: torch.Tensor, lens: torch.Tensor, decoder: str, beam_width: int) -> List[List[int]]:
-    lp = torch.log_softmax(logits.float(), dim=-1)
+    from .ops import decode as D
     if decoder == "greedy":
+        if logits.is_cuda:
+            return D.greedy_decode(logits, lens)          # csrc/decode.hip
+        lp = torch.log_softmax(logits.float(), dim=-1)
         try:
             from .runtime import native
             best = lp.argmax(-1).to(torch.int32).cpu().numpy()
             return native.load().greedy_collapse(best, lens.cpu().numpy().astype(np.int32), BLANK)
         except RuntimeError:
             return R.greedy_decode(lp, lens)
-    from .runtime import native
-    return native.load().beam_search_batch(lp.cpu().numpy(), lens.cpu().numpy().astype(np.int32),
-                                           beam_width, BLANK, -10.0)
+    return D.beam_decode(logits, lens, beam_width, BLANK, -10.0)
 
 
 def eval_once(model, args, data, num_iter: int, display: bool) -> float:

@@ -151,6 +151,26 @@ def test_prefix_beam_search_exact_for_wide_beam():
         assert bs2.best() == list(ref)
 
 
+def test_beam_search_batch_threads_and_streaming_match_single():
+    rng = np.random.default_rng(11)
+    T, B, K = 40, 6, 29
+    lp = np.log(rng.dirichlet(np.ones(K) * 0.3, size=(T, B))).astype(np.float32)   # [T, B, K]
+    lens = np.array([40, 33, 17, 40, 1, 25], np.int32)
+    single = []
+    for b in range(B):
+        bs = N.PrefixBeamSearch(8, 28, -8.0)
+        bs.feed(np.ascontiguousarray(lp[: lens[b], b]))
+        single.append(bs.best())
+    for threads in (1, 4):
+        assert N.beam_search_batch(lp, lens, 8, 28, -8.0, threads) == single
+    # incremental (streaming) batch decoder: chunks of 15 frames, per-chunk valid lengths
+    bb = N.BatchBeamSearch(B, 8, 28, -8.0, 3)
+    for s in range(0, T, 15):
+        chunk = np.ascontiguousarray(lp[s:s + 15])
+        bb.feed(chunk, np.clip(lens - s, 0, chunk.shape[0]).astype(np.int32))
+    assert bb.best() == single
+
+
 def test_featurizer_mfcc_shape_and_dct():
     from scipy.fft import dct
     from deepspeech_amd.data import featurizer as FZ

@@ -235,3 +235,25 @@ def test_grad_norm(cuda):
     arena.grad[3] = float("nan")
     n, bad = opt.grad_norm_and_finite(1.0)
     assert int(bad) == 1
+
+
+# --------------------------------------------------------------------------- greedy decode
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("T", [7, 300, 700])
+def test_ctc_greedy_kernel(cuda, dtype, T):
+    from deepspeech_amd.ops import decode as D
+    torch.manual_seed(T)
+    N, K = 9, 29
+    logits = torch.randn(T, N, K, device=cuda) * 2
+    # long runs of blanks / repeats so merging is exercised across 256-frame blocks
+    logits[T // 3: T // 3 + 40, :, 28] += 10
+    logits[T // 2: T // 2 + 300, :, 5] += 10
+    logits = logits.to(dtype)
+    lens = torch.randint(1, T + 1, (N,), dtype=torch.int32)
+    lens[0] = T
+    got, score = D.greedy_decode(logits, lens.to(cuda), with_scores=True)
+    lp = torch.log_softmax(logits.float(), -1).cpu()
+    want = R.greedy_decode(lp, lens)
+    assert got == want
+    ref_score = torch.stack([lp[: int(lens[n]), n].max(-1).values.sum() for n in range(N)])
+    assert torch.allclose(score, ref_score, atol=1e-2, rtol=1e-4)
