@@ -68,8 +68,11 @@ struct DS2RnnX {
   unsigned* err;
   long long timeout;
   unsigned long long* stamps;
+  void* ring[2];
 };
 int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st);
+int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
+long long ds2_rnnx_ring_floats(int H, int BG, int R);
 int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st);
 int ds2_rnnx_grid(int H, int ngroups, int xcd_map);
 int ds2_rnnx_kb(int H, int G, int fwd);
@@ -286,7 +289,7 @@ void rnnx_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tens
               OptT gates_b, at::Tensor dgh_f, OptT dgh_b, at::Tensor dgx, OptT dbx_part, OptT dbh_part,
               double dgx_scale, at::Tensor census, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H,
               int64_t BG, int64_t R, int64_t steps, int64_t gstride, int64_t ndir, int64_t cell, int64_t mt,
-              int64_t timeout, int64_t xcd_map, int64_t knobs, OptT stamps) {
+              int64_t timeout, int64_t xcd_map, int64_t knobs, OptT stamps, OptT ring_f, OptT ring_b) {
   need_gpu(dy, "dy");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dgx.scalar_type() == at::kBFloat16, "dy/dgx must be bf16");
   TORCH_CHECK(dgx.numel() >= T * N * gstride && dy.numel() >= T * N * H, "dy/dgx too small");
@@ -315,6 +318,18 @@ void rnnx_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tens
   }
   d.dgx_scale = (float)dgx_scale;
   TORCH_CHECK(ndir == 1 || (d.U[1] && d.hsave[1] && d.ex[1]), "backward-direction buffers missing");
+  if (ring_f.has_value() && ring_f->defined()) {
+    // reduce-scatter BPTT (generation 3): dgh is a plain output, the exchange is the ring
+    const int64_t rf = ds2_rnnx_ring_floats((int)H, (int)BG, (int)R);
+    TORCH_CHECK(ring_f->scalar_type() == at::kFloat && ring_f->numel() >= rf, "ring_f must be fp32 [", rf, "]");
+    d.ring[0] = ring_f->data_ptr();
+    if (ndir == 2) {
+      TORCH_CHECK(ring_b.has_value() && ring_b->scalar_type() == at::kFloat && ring_b->numel() >= rf, "ring_b missing");
+      d.ring[1] = ring_b->data_ptr();
+    }
+    check(ds2_rnnx_bwd_rs(&d, cur_stream()), "rnnx_bwd_rs");
+    return;
+  }
   check(ds2_rnnx_bwd(&d, cur_stream()), "rnnx_bwd");
 }
 
@@ -583,8 +598,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dbx_part"), py::arg("dbh_part"), py::arg("dgx_scale"), py::arg("census"), py::arg("err"),
         py::arg("T"), py::arg("N"), py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("R"), py::arg("steps"),
         py::arg("gstride"), py::arg("ndir"), py::arg("cell"), py::arg("mt"), py::arg("timeout"), py::arg("xcd_map"),
-        py::arg("knobs"), py::arg("stamps") = py::none());
+        py::arg("knobs"), py::arg("stamps") = py::none(), py::arg("ring_f") = py::none(),
+        py::arg("ring_b") = py::none());
   m.def("rnnx_info", &rnnx_info);
+  m.def("rnnx_ring_floats", [](int64_t H, int64_t BG, int64_t R) { return ds2_rnnx_ring_floats((int)H, (int)BG, (int)R); });
   m.def("ctc_fused", &ctc_fused);
   m.def("ctc_ws_floats", &ctc_ws_floats);
   m.def("bn_chunks", &bn_chunks);

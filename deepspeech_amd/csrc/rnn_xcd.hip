@@ -809,6 +809,393 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// backward (BPTT), generation 3: reduce-scatter exchange.
+//
+// The gather kernel above moves dgh_{s+1} (R rows x 3H gate columns, bf16) to EVERY
+// workgroup of the group each step, because a workgroup's dh slice needs all 3H columns
+// of dgh times its U columns. Here each workgroup instead multiplies ITS OWN gate columns
+// by the U rows they index, producing a partial dh for ALL H units,
+//     P_j(s) = dgh_s[:, cols_j] . U[cols_j, :]          (R x H, fp32)
+// and a consumer sums the 25 producers' partials of its own 32 units:
+//     dh_rec(s-1)[:, units_k] = sum_j P_j(s)[:, units_k].
+// Per step a consumer then reads P x R x 32 fp32 (25.6 KB at H = 800, R = 8) instead of
+// R x 3H bf16 (38.4 KB), and the exchange lives in a 3-slot ring (a few MB per group, L2
+// resident) instead of a T-step buffer:
+//  * ring[dir][slot][bg][producer][row][H] fp32, pre-filled with the sentinel 0xFFFFFFFF
+//    (never produced: NaN results are canonicalised); P(s) goes to slot s % 3;
+//  * a consumer resets every granule it read to the sentinel at the START of its next
+//    step and drains those stores (vmcnt(0)) before that step's first barrier, i.e. before
+//    it publishes its own next partial. A producer rewrites slot s % 3 only at step s - 3,
+//    after it has received every consumer's partial of step s - 1, which each consumer
+//    published after its resets of slot s % 3 had completed: the protocol is safe for any
+//    timing, and the ring is sentinel-clean again when the launch ends;
+//  * dgh (bf16) is now a plain output for the dU GEMM, stored by the memory wave off the
+//    critical path; no T-step sentinel fill is needed.
+// Worker waves 0..6: gather+sum (producer j = wave + 7i), then the MFMA
+//   D[unit][row] = sum_k U[col_k][unit] . dgh[row][col_k]  (A = U resident, 16-unit tiles
+//   w + 7i; B = the dgh tile from LDS), one 16-B fp32 granule per lane published straight
+//   from the accumulator. Waves 0..3 run the cell epilogue; wave 7 is the memory wave.
+// ------------------------------------------------------------------------------------
+struct XBwdRS {
+  int T, N, NP, H, P, BG, R, steps, gstride, ngroups, xcd_map, knobs;
+  const int* lens;
+  const bf16_t* dy;
+  const bf16_t* U[2];
+  const float* hsave[2];
+  const float* gates[2];
+  bf16_t* dgh[2];         // [steps][NP][G*H] output (dU GEMM operand)
+  bf16_t* dgx;
+  float* ring[2];         // [3][BG][P][R][H] fp32, sentinel-filled
+  float* dbx_part[2];
+  float* dbh_part[2];
+  float dgx_scale;
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+  unsigned long long* stamps;
+};
+
+constexpr unsigned SENT32 = 0xffffffffu;
+
+__device__ __forceinline__ bool granule_ready32(i32x4 v) {
+  return ((unsigned)v[0] != SENT32) && ((unsigned)v[1] != SENT32) && ((unsigned)v[2] != SENT32) &&
+         ((unsigned)v[3] != SENT32);
+}
+__device__ __forceinline__ float canon32(float f) { return (f != f) ? __uint_as_float(0x7fc00000u) : f; }
+
+template <int CELL, int MTU>
+__global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
+  constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
+  constexpr int ROWS = 16;
+  constexpr int EPT = ROWS * UPW / ETH;
+  constexpr int OPL = ROWS * UPW / 64;            // elements per memory-wave lane
+  constexpr int GPT = 4;                          // producers per gather thread (7 x 4 >= P)
+  constexpr int DGP = G * UPW + 8;                // dgh tile pitch (bf16)
+  __shared__ float red_s[MW][ROWS][UPW + 1];
+  __shared__ __attribute__((aligned(16))) bf16_t dg_s[ROWS][DGP];
+  __shared__ float dyr_s[2][ROWS][UPW];           // prefetch ring (memory wave -> epilogue)
+  __shared__ float hpr_s[2][ROWS][UPW];
+  __shared__ float4 gr_s[2][(CELL == CELL_GRU) ? ROWS : 1][UPW];
+  __shared__ float ox_s[2][ROWS][G][UPW];         // dgx staging by step parity
+  __shared__ bf16_t oh_s[2][ROWS][G][UPW];        // dgh staging by step parity (already rounded)
+  __shared__ int len_s[ROWS];
+  __shared__ int s_mode, s_abort;
+
+  int grp, mem;
+  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, GH = G * H, N = a.N, NP = a.NP, R = a.R, P = a.P, MTS = H / 16;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW;
+  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  for (int i = tid; i < ROWS * DGP; i += NTH) (&dg_s[0][0])[i] = 0;
+  if (wave == 0) {
+    const int m = group_census(a.census, grp, mem, P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+
+  // resident A fragments of the worker waves: A[m][k] = U[g*H + u0 + k][16*mt + m],
+  // m-tile mt = wave + 7*i, k-step g (this workgroup's 32 columns of gate g)
+  bf16x8 ua[MTU][G];
+  {
+    const bf16_t* Ud = a.U[dir];
+#pragma unroll
+    for (int i = 0; i < MTU; ++i) {
+      const int mt = wave + MW * i;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (wave < MW && mt < MTS) {
+          const bf16_t* p = Ud + (size_t)(g * H + u0 + 8 * (lane >> 4)) * H + 16 * mt + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (short)p[(size_t)j * H];
+        }
+        ua[i][g] = v;
+      }
+    }
+  }
+
+  float carry[EPT];
+  float sbx[EPT][G];
+  float sbh[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    carry[i] = 0.f;
+    sbh[i] = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) sbx[i][g] = 0.f;
+  }
+  __syncthreads();   // len_s, dg_s zero rows, census
+
+  // memory wave: per-step inputs (dy, gates, h_prev) one step ahead, dgx / dgh stores
+  float pdy[OPL], php[OPL];
+  float4 pg[OPL];
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      const int bp = min(r0 + row, NP - 1), bn = min(r0 + row, N - 1), u = u0 + c;
+      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+      pdy[j] = bf2f(a.dy[((size_t)t * N + bn) * H + u]);
+      if (CELL == CELL_GRU) {
+        pg[j] = reinterpret_cast<const float4*>(a.gates[dir])[((size_t)s * NP + bp) * H + u];
+        php[j] = a.hsave[dir][((size_t)s * NP + bp) * H + u];
+      } else {
+        php[j] = a.hsave[dir][((size_t)(s + 1) * NP + bp) * H + u];     // h_s itself
+      }
+    }
+  };
+  auto mw_put = [&](int s) {
+    const int slot = s & 1;
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      const bool act = s < len_s[row];
+      dyr_s[slot][row][c] = act ? pdy[j] : 0.f;
+      hpr_s[slot][row][c] = act ? php[j] : 0.f;
+      if (CELL == CELL_GRU) gr_s[slot][(CELL == CELL_GRU) ? row : 0][c] = act ? pg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto mw_store = [&](int s) {          // dgx and dgh of step s from the staging area
+#pragma unroll
+    for (int j = 0; j < OPL; ++j) {
+      const int e = lane + 64 * j;
+      const int row = e >> 5, c = e & 31;
+      const int b = r0 + row, u = u0 + c;
+      if (row < R) {
+        bf16_t* dh = a.dgh[dir] + ((size_t)s * NP + b) * GH + u;
+#pragma unroll
+        for (int g = 0; g < G; ++g) dh[g * H] = oh_s[s & 1][row][g][c];
+        if (b < N) {
+          const int L = len_s[row];
+          const bool act = s < L;
+          const int t = act ? ((dir == 0) ? s : (L - 1 - s)) : s;
+          bf16_t* dst = a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + u;
+#pragma unroll
+          for (int g = 0; g < G; ++g) dst[g * H] = f2bf(ox_s[s & 1][row][g][c] * a.dgx_scale);
+        }
+      }
+    }
+  };
+  if (s_abort) return;
+  if (wave == MEMW && a.steps > 0) mw_load(a.steps - 1);
+  const bool plain = s_mode == 1;
+  float* ringd = a.ring[dir];
+  const size_t slot_floats = (size_t)a.BG * P * R * H;
+  const unsigned ring_bytes = (unsigned)(3 * slot_floats * 4);
+  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(ringd, ring_bytes);
+  Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
+
+  // gather geometry (workers): combo = lane + 64*cb -> (row, 4-unit granule q8) for rows < 16;
+  // this wave sums producers j = wave + 7*i
+  const int pg7 = wave;
+  auto grow_of = [&](int cb) { return (lane + 64 * cb) >> 3; };
+  const int gq8 = lane & 7;
+  const int ncb = (R * 8 + 63) / 64;          // combos per thread: 1 (R <= 8) or 2
+  auto ring_off = [&](int slot, int j, int row, int unit) -> unsigned {
+    return (unsigned)((((size_t)slot * a.BG + bg) * P + j) * R * H + (size_t)row * H + unit) * 4u;
+  };
+  const i32x4 sent = {(int)SENT32, (int)SENT32, (int)SENT32, (int)SENT32};
+  auto reset_slot = [&](int slot) {       // sentinel back into every granule this thread read
+    for (int cb = 0; cb < ncb; ++cb) {
+      const int grow = grow_of(cb);
+      if (grow >= R) continue;
+#pragma unroll
+      for (int i = 0; i < GPT; ++i) {
+        const int j = pg7 + MW * i;
+        if (j < P) {
+          const unsigned off = ring_off(slot, j, grow, u0 + 4 * gq8);
+          if (plain) *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ringd) + off) = sent;
+          else store_sc1_b128(rs_ring, off, sent);
+        }
+      }
+    }
+  };
+
+  if (wave < MW) {
+    for (int s = a.steps - 1; s >= 0; --s) {
+      st.mark(-1);
+      const bool has_next = s + 1 < a.steps;
+      // (R) reset the granules read last step (slot (s+2) % 3) to the sentinel
+      if (s + 2 < a.steps) reset_slot((s + 2) % 3);
+      // (G) sum this thread's producers' partials of dh_rec for (row, 4 units)
+      for (int cb = 0; cb < ncb; ++cb) {
+        const int grow = grow_of(cb);
+        if (grow >= R) continue;
+        f32x4 acc4 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (has_next) {
+          const int cs = (s + 1) % 3;
+          unsigned off[GPT];
+          i32x4 v[GPT];
+#pragma unroll
+          for (int i = 0; i < GPT; ++i) {
+            const int j = min(pg7 + MW * i, P - 1);
+            off[i] = ring_off(cs, j, grow, u0 + 4 * gq8);
+            v[i] = load_sc1_b128(rs_ring, off[i]);
+          }
+          const long long t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+          for (int i = 0; i < GPT; ++i) {
+            if (pg7 + MW * i < P) {
+              while (!granule_ready32(v[i])) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
+                __builtin_amdgcn_s_sleep(1);
+                v[i] = load_sc1_b128(rs_ring, off[i]);
+              }
+              acc4 += __builtin_bit_cast(f32x4, v[i]);
+            }
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) red_s[wave][grow][4 * gq8 + jj] = acc4[jj];
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // resets (and loads) complete
+      st.mark(0);
+      lds_barrier();                                                        // #1
+      st.mark(1);
+      if (s_abort) break;
+      // (E) cell backward (waves 0..3): dgh tile for the MFMA, dgx / dgh staging
+      if (wave < EW) {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * ETH;
+          const int row = e >> 5, c = e & 31;
+          if (row < R) {
+            float dhrec = 0.f;
+            if (has_next) {
+#pragma unroll
+              for (int w = 0; w < MW; ++w) dhrec += red_s[w][row][c];
+            }
+            const bool act = s < len_s[row];
+            const float dh = dyr_s[s & 1][row][c] + carry[i] + dhrec;
+            const float hp = hpr_s[s & 1][row][c];
+            float ghv[G], gxs[G];
+            float cnew = 0.f;
+            if (CELL == CELL_GRU) {
+              const float4 gv = gr_s[s & 1][(CELL == CELL_GRU) ? row : 0][c];
+              const float r = gv.x, z = gv.y, n = gv.z, ghn = gv.w;
+              const float dn = dh * (1.f - z);
+              const float dz = dh * (hp - n);
+              cnew = dh * z;
+              const float dan = dn * (1.f - n * n);
+              const float dr = dan * ghn;
+              const float dghn = dan * r;
+              const float daz = dz * z * (1.f - z);
+              const float dar = dr * r * (1.f - r);
+              ghv[0] = dar; ghv[1] = daz; ghv[2] = dghn;
+              gxs[0] = dar; gxs[1] = daz; gxs[2] = dan;
+            } else {
+              const float da = (hp > 0.f && hp < RELU_CAP) ? dh : 0.f;
+              ghv[0] = da;
+              gxs[0] = da;
+            }
+            if (!act) {
+              cnew = 0.f;
+#pragma unroll
+              for (int g = 0; g < G; ++g) { ghv[g] = 0.f; gxs[g] = 0.f; }
+            }
+            carry[i] = cnew;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+              const bf16_t hb = f2bf(ghv[g]);
+              dg_s[row][g * UPW + c] = hb;
+              oh_s[s & 1][row][g][c] = hb;
+              ox_s[s & 1][row][g][c] = gxs[g];
+              sbx[i][g] += gxs[g];
+            }
+            if (CELL == CELL_GRU) sbh[i] += ghv[G - 1];
+          }
+        }
+      }
+      st.mark(2);
+      lds_barrier();                                                        // #2
+      st.mark(3);
+      // (M) publish P(s) = dgh_s[:, own cols] . U[own cols, :] into ring slot s % 3
+      if (s > 0) {
+        const int ws = s % 3;
+        const bool prow = (lane & 15) < R;
+        bf16x8 bfr[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          bfr[g] = *reinterpret_cast<const bf16x8*>(&dg_s[lane & 15][g * UPW + 8 * (lane >> 4)]);
+#pragma unroll
+        for (int i = 0; i < MTU; ++i) {
+          const int mt = wave + MW * i;
+          if (mt < MTS) {
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int g = 0; g < G; ++g) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], acc, 0, 0, 0);
+            if (prow) {
+              const i32x4 v = {(int)__float_as_uint(canon32(acc[0])), (int)__float_as_uint(canon32(acc[1])),
+                               (int)__float_as_uint(canon32(acc[2])), (int)__float_as_uint(canon32(acc[3]))};
+              const unsigned off = ring_off(ws, mem, lane & 15, 16 * mt + 4 * (lane >> 4));
+              if (plain) *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ringd) + off) = v;
+              else store_sc1_b128(rs_ring, off, v);
+            }
+          }
+        }
+      }
+      st.mark(4);
+    }
+    // leave the ring sentinel-clean: reset what step 0 read (slot 1 % 3)
+    if (!s_abort && a.steps >= 2) reset_slot(1);
+  } else {
+    for (int s = a.steps - 1; s >= 0; --s) {
+      // memory wave, while the others wait on the exchange
+      st.mark(-1);
+      mw_put(s);
+      if (s + 2 < a.steps) mw_store(s + 2);
+      if (s >= 1) mw_load(s - 1);
+      st.mark(0);
+      lds_barrier();                                                        // #1
+      st.mark(1);
+      if (s_abort) break;
+      lds_barrier();                                                        // #2
+    }
+  }
+  __syncthreads();
+  if (wave == MEMW && !s_abort) {
+    if (a.steps >= 2) mw_store(1);
+    if (a.steps >= 1) mw_store(0);
+  }
+  if (wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
+
+  // bias gradients: reduce the epilogue waves' rows through LDS, one read-modify-write
+  // per (gate, unit) of the workgroup's own [bg] partial row
+  if (a.dbx_part[dir] != nullptr && !s_abort) {
+    constexpr int BW = (G + 1) * UPW;
+    static_assert(MW * ROWS * (UPW + 1) >= ROWS * BW, "bias reduction does not fit the LDS scratch");
+    float* bred = &red_s[0][0][0];
+    if (wave < EW) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * ETH;
+        const int row = e >> 5, c = e & 31;
+#pragma unroll
+        for (int g = 0; g < G; ++g) bred[row * BW + g * UPW + c] = sbx[i][g];
+        bred[row * BW + G * UPW + c] = sbh[i];
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < BW; q += NTH) {
+      float sum = 0.f;
+      for (int r = 0; r < ROWS; ++r) sum += bred[r * BW + q];
+      const int g = q / UPW, c = q % UPW;
+      const size_t base = (size_t)bg * GH + u0 + c;
+      if (g < G) {
+        a.dbx_part[dir][base + (size_t)g * H] += sum;
+        if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr && g < G - 1) a.dbh_part[dir][base + (size_t)g * H] += sum;
+      } else if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr) {
+        a.dbh_part[dir][base + (size_t)(G - 1) * H] += sum;
+      }
+    }
+  }
+}
+
 template <int CELL, int MT>
 static int launch_fwd(const XFwd& a, int kb, int grid, size_t smem, hipStream_t st) {
   switch (kb) {
@@ -865,6 +1252,7 @@ struct DS2RnnX {
   unsigned* err;
   long long timeout;
   unsigned long long* stamps;
+  void* ring[2];         // bwd reduce-scatter exchange ring (fp32, sentinel-filled)
 };
 
 // grid size of a launch (blocks with no role exit at once)
@@ -963,6 +1351,43 @@ int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st) {
   if (d->mt != 1) return -33;
   if (d->cell == CELL_GRU) DS2_BWD(CELL_GRU, 1) else DS2_BWD(CELL_RELU, 1)
 #undef DS2_BWD
+}
+
+// floats of the reduce-scatter ring of ONE direction: [3 slots][BG][P][R][H]
+long long ds2_rnnx_ring_floats(int H, int BG, int R) { return 3LL * BG * (H / UPW) * R * H; }
+
+int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st) {
+  if (d->H % UPW != 0 || d->R < 1 || d->R > 16 || d->NP != d->BG * d->R || d->mt != 1) return -30;
+  if (d->ring[0] == nullptr || (d->ndir == 2 && d->ring[1] == nullptr)) return -34;
+  const int P = d->H / UPW;
+  if (P > 4 * MW) return -35;                       // GPT = 4 producers per gather thread
+  const int mtu_need = (d->H / 16 + MW - 1) / MW;
+  XBwdRS a;
+  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = P; a.BG = d->BG; a.R = d->R;
+  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
+  a.xcd_map = d->xcd_map && a.ngroups <= 8; a.knobs = d->knobs;
+  a.lens = d->lens; a.dy = (const bf16_t*)d->gx;
+  for (int i = 0; i < 2; ++i) {
+    a.U[i] = (const bf16_t*)d->U[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
+    a.dgh[i] = (bf16_t*)d->ex[i]; a.ring[i] = (float*)d->ring[i];
+    a.dbx_part[i] = d->dbx_part[i]; a.dbh_part[i] = d->dbh_part[i];
+  }
+  a.dgx = (bf16_t*)d->dgx; a.dgx_scale = d->dgx_scale;
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
+  if (d->steps <= 0) return 0;
+  const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
+#define DS2_RS(C, M) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M>), dim3(grid), dim3(NTH), 0, st, a)
+#define DS2_RS_CELL(C)                          \
+  if (mtu_need <= 2) DS2_RS(C, 2);              \
+  else if (mtu_need <= 4) DS2_RS(C, 4);         \
+  else if (mtu_need <= 6) DS2_RS(C, 6);         \
+  else if (mtu_need <= 8) DS2_RS(C, 8);         \
+  else if (mtu_need <= 10) DS2_RS(C, 10);       \
+  else return -36;
+  if (d->cell == CELL_GRU) { DS2_RS_CELL(CELL_GRU) } else { DS2_RS_CELL(CELL_RELU) }
+#undef DS2_RS_CELL
+#undef DS2_RS
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

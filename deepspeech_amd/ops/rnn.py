@@ -56,6 +56,9 @@ class RnnPlan:
 
 
 RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))   # diagnostic timing switches only
+# BPTT exchange of the xcd kernels: "rs" = reduce-scatter of fp32 partial dh (generation 3),
+# "gather" = all-gather of dgh (generation 2)
+BWD_EXCHANGE = os.environ.get("DS2_RNN_BWD", "rs")
 
 
 LDS_BYTES = 160 * 1024
@@ -94,7 +97,7 @@ def make_xcd_plan(N: int, H: int, cell: str, ndir: int, cus: int) -> Optional[Rn
     G = GATES[cell]
     P = H // 32
     best = None
-    for R in range(1, 33):
+    for R in range(max(1, int(os.environ.get("DS2_RNNX_MINR", "1"))), 33):
         BG = -(-N // R)
         ngroups = ndir * BG
         if ngroups * P > cus:
@@ -281,8 +284,24 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
                         dtype=torch.float32) if want_bias else None
     has_g = gates.numel() > 0
     if plan.kind == "xcd":
-        dgh.view(torch.int16).fill_(-1)                   # sentinel
         census = torch.full((ndir * plan.BG * (H // 32),), -1, device=dev, dtype=torch.int32)
+        if BWD_EXCHANGE == "rs" and H // 32 <= 28:
+            # generation-3 BPTT: reduce-scatter of fp32 partials through a 3-slot ring
+            # (sentinel 0xFFFFFFFF); dgh is a plain output, no T-step sentinel fill
+            rf = int(C.rnnx_ring_floats(H, plan.BG, plan.R))
+            ring = torch.full((ndir, rf), -1, device=dev, dtype=torch.int32).view(torch.float32)
+            C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
+                       gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
+                       dgh[0], dgh[1] if d1 else None, dgx,
+                       parts[0] if parts is not None else None,
+                       parts[1] if (parts is not None and plan.cell == "gru") else None,
+                       float(dgx_scale), census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
+                       CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
+                       _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev),
+                       ring[0], ring[1] if d1 else None)
+            _pending_errors.append(err)
+            return dgx, dgh, parts
+        dgh.view(torch.int16).fill_(-1)                   # sentinel
         C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
                    gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
                    dgh[0], dgh[1] if d1 else None, dgx,
@@ -546,7 +565,8 @@ _plan_cache = {}
 
 
 def plan_for(N: int, H: int, cell: str, ndir: int, device: torch.device) -> RnnPlan:
-    key = (N, H, cell, ndir, device.index, os.environ.get("DS2_RNN_MODE"), os.environ.get("DS2_RNN_NW"))
+    key = (N, H, cell, ndir, device.index, os.environ.get("DS2_RNN_MODE"), os.environ.get("DS2_RNN_NW"),
+           os.environ.get("DS2_RNNX_MINR"))
     p = _plan_cache.get(key)
     if p is None:
         p = make_plan(N, H, cell, ndir, _ext.num_cus(device.index or 0))
