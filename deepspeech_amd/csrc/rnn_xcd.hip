@@ -877,8 +877,8 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   __shared__ float dyr_s[2][ROWS][UPW];           // prefetch ring (memory wave -> epilogue)
   __shared__ float hpr_s[2][ROWS][UPW];
   __shared__ float4 gr_s[2][(CELL == CELL_GRU) ? ROWS : 1][UPW];
-  __shared__ float ox_s[2][ROWS][G][UPW];         // dgx staging by step parity
-  __shared__ bf16_t oh_s[2][ROWS][G][UPW];        // dgh staging by step parity (already rounded)
+  __shared__ __attribute__((aligned(16))) float ox_s[2][ROWS][G][UPW];     // dgx staging by step parity
+  __shared__ __attribute__((aligned(16))) bf16_t oh_s[2][ROWS][G][UPW];    // dgh staging (already rounded)
   __shared__ int len_s[ROWS];
   __shared__ int s_mode, s_abort;
 
@@ -928,54 +928,75 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   }
   __syncthreads();   // len_s, dg_s zero rows, census
 
-  // memory wave: per-step inputs (dy, gates, h_prev) one step ahead, dgx / dgh stores
-  float pdy[OPL], php[OPL];
-  float4 pg[OPL];
+  // memory wave: per-step inputs (dy, gates, h_prev) one step ahead, dgx / dgh stores,
+  // all in 8- / 16-B pieces: load task = (row, 4 units), store task = (row, gate, 8 units)
+  constexpr int LT = ROWS * 8 / 64, ST = (ROWS * G * 4 + 63) / 64;
+  uint2 pdy[LT];
+  float4 php[LT];
+  float4 pg[LT][4];
   auto mw_load = [&](int s) {
 #pragma unroll
-    for (int j = 0; j < OPL; ++j) {
-      const int e = lane + 64 * j;
-      const int row = e >> 5, c = e & 31;
-      const int bp = min(r0 + row, NP - 1), bn = min(r0 + row, N - 1), u = u0 + c;
-      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
-      pdy[j] = bf2f(a.dy[((size_t)t * N + bn) * H + u]);
-      if (CELL == CELL_GRU) {
-        pg[j] = reinterpret_cast<const float4*>(a.gates[dir])[((size_t)s * NP + bp) * H + u];
-        php[j] = a.hsave[dir][((size_t)s * NP + bp) * H + u];
-      } else {
-        php[j] = a.hsave[dir][((size_t)(s + 1) * NP + bp) * H + u];     // h_s itself
+    for (int k = 0; k < LT; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q >> 3, c4 = (q & 7) * 4;
+      if (row < R) {
+        const int bp = min(r0 + row, NP - 1), bn = min(r0 + row, N - 1), u = u0 + c4;
+        const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+        pdy[k] = *reinterpret_cast<const uint2*>(a.dy + ((size_t)t * N + bn) * H + u);
+        if (CELL == CELL_GRU) {
+          const float4* gp = reinterpret_cast<const float4*>(a.gates[dir]) + ((size_t)s * NP + bp) * H + u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pg[k][i] = gp[i];
+          php[k] = *reinterpret_cast<const float4*>(a.hsave[dir] + ((size_t)s * NP + bp) * H + u);
+        } else {
+          php[k] = *reinterpret_cast<const float4*>(a.hsave[dir] + ((size_t)(s + 1) * NP + bp) * H + u);  // h_s
+        }
       }
     }
   };
   auto mw_put = [&](int s) {
     const int slot = s & 1;
 #pragma unroll
-    for (int j = 0; j < OPL; ++j) {
-      const int e = lane + 64 * j;
-      const int row = e >> 5, c = e & 31;
-      const bool act = s < len_s[row];
-      dyr_s[slot][row][c] = act ? pdy[j] : 0.f;
-      hpr_s[slot][row][c] = act ? php[j] : 0.f;
-      if (CELL == CELL_GRU) gr_s[slot][(CELL == CELL_GRU) ? row : 0][c] = act ? pg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < LT; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q >> 3, c4 = (q & 7) * 4;
+      if (row < R) {
+        const bool act = s < len_s[row];
+        const float dv[4] = {bf2f((bf16_t)(pdy[k].x & 0xffffu)), bf2f((bf16_t)(pdy[k].x >> 16)),
+                             bf2f((bf16_t)(pdy[k].y & 0xffffu)), bf2f((bf16_t)(pdy[k].y >> 16))};
+        const float hv[4] = {php[k].x, php[k].y, php[k].z, php[k].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dyr_s[slot][row][c4 + i] = act ? dv[i] : 0.f;
+          hpr_s[slot][row][c4 + i] = act ? hv[i] : 0.f;
+          if (CELL == CELL_GRU)
+            gr_s[slot][(CELL == CELL_GRU) ? row : 0][c4 + i] = act ? pg[k][i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
     }
   };
   auto mw_store = [&](int s) {          // dgx and dgh of step s from the staging area
 #pragma unroll
-    for (int j = 0; j < OPL; ++j) {
-      const int e = lane + 64 * j;
-      const int row = e >> 5, c = e & 31;
-      const int b = r0 + row, u = u0 + c;
+    for (int k = 0; k < ST; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q / (G * 4), rem = q - row * (G * 4), g = rem >> 2, c8 = (rem & 3) * 8;
       if (row < R) {
-        bf16_t* dh = a.dgh[dir] + ((size_t)s * NP + b) * GH + u;
-#pragma unroll
-        for (int g = 0; g < G; ++g) dh[g * H] = oh_s[s & 1][row][g][c];
+        const int b = r0 + row, u = u0 + c8;
+        *reinterpret_cast<i32x4*>(a.dgh[dir] + ((size_t)s * NP + b) * GH + g * H + u) =
+            *reinterpret_cast<const i32x4*>(&oh_s[s & 1][row][g][c8]);
         if (b < N) {
           const int L = len_s[row];
           const bool act = s < L;
           const int t = act ? ((dir == 0) ? s : (L - 1 - s)) : s;
-          bf16_t* dst = a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + u;
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(&ox_s[s & 1][row][g][c8]);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(&ox_s[s & 1][row][g][c8 + 4]);
+          bf16x8 o;
 #pragma unroll
-          for (int g = 0; g < G; ++g) dst[g * H] = f2bf(ox_s[s & 1][row][g][c] * a.dgx_scale);
+          for (int i = 0; i < 4; ++i) {
+            o[i] = (short)f2bf(x0[i] * a.dgx_scale);
+            o[4 + i] = (short)f2bf(x1[i] * a.dgx_scale);
+          }
+          *reinterpret_cast<bf16x8*>(a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + g * H + u) = o;
         }
       }
     }
