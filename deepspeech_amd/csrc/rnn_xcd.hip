@@ -1142,20 +1142,33 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 #pragma unroll
         for (int g = 0; g < G; ++g)
           bfr[g] = *reinterpret_cast<const bf16x8*>(&dg_s[lane & 15][g * UPW + 8 * (lane >> 4)]);
+        auto put = [&](int mt, f32x4 acc) {
+          if (prow) {
+            const i32x4 v = {(int)__float_as_uint(canon32(acc[0])), (int)__float_as_uint(canon32(acc[1])),
+                             (int)__float_as_uint(canon32(acc[2])), (int)__float_as_uint(canon32(acc[3]))};
+            const unsigned off = ring_off(ws, mem, lane & 15, 16 * mt + 4 * (lane >> 4));
+            if (plain) *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ringd) + off) = v;
+            else store_sc1_b128(rs_ring, off, v);
+          }
+        };
+        // two independent accumulator chains at a time hide the MFMA dependency latency
 #pragma unroll
-        for (int i = 0; i < MTU; ++i) {
-          const int mt = wave + MW * i;
-          if (mt < MTS) {
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < MTU; i += 2) {
+          const int mt0 = wave + MW * i, mt1 = wave + MW * (i + 1);
+          if (mt1 < MTS) {
+            f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
-            for (int g = 0; g < G; ++g) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], acc, 0, 0, 0);
-            if (prow) {
-              const i32x4 v = {(int)__float_as_uint(canon32(acc[0])), (int)__float_as_uint(canon32(acc[1])),
-                               (int)__float_as_uint(canon32(acc[2])), (int)__float_as_uint(canon32(acc[3]))};
-              const unsigned off = ring_off(ws, mem, lane & 15, 16 * mt + 4 * (lane >> 4));
-              if (plain) *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ringd) + off) = v;
-              else store_sc1_b128(rs_ring, off, v);
+            for (int g = 0; g < G; ++g) {
+              a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], a0, 0, 0, 0);
+              a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i + 1][g], bfr[g], a1, 0, 0, 0);
             }
+            put(mt0, a0);
+            put(mt1, a1);
+          } else if (mt0 < MTS) {
+            f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int g = 0; g < G; ++g) a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], a0, 0, 0, 0);
+            put(mt0, a0);
           }
         }
       }
