@@ -10,6 +10,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 extern "C" {
 struct DS2RnnFwd {
@@ -94,6 +95,8 @@ int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void*
 int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
+int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
+                   hipStream_t st);
 int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
                    int* labels, int* counts, float* score, hipStream_t st);
 size_t ds2_conv2_fwd_smem(int F1);
@@ -555,6 +558,22 @@ void ctc_greedy(at::Tensor logits, at::Tensor lens, at::Tensor labels, at::Tenso
                        cur_stream()), "ctc_greedy");
 }
 
+// --------------------------------------------------------------------------- multi-fill
+// fill each (contiguous tensor, 32-bit pattern) region in ONE launch (<= 8 regions)
+void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
+  TORCH_CHECK(ts.size() == patterns.size() && ts.size() <= 8, "multi_fill: <= 8 (tensor, pattern) pairs");
+  void* ptrs[8];
+  unsigned long long bytes[8];
+  unsigned pats[8];
+  for (size_t i = 0; i < ts.size(); ++i) {
+    need_gpu(ts[i], "multi_fill region");
+    ptrs[i] = ts[i].data_ptr();
+    bytes[i] = (unsigned long long)ts[i].numel() * ts[i].element_size();
+    pats[i] = (unsigned)(uint32_t)patterns[i];
+  }
+  check(ds2_multi_fill((int)ts.size(), ptrs, bytes, pats, cur_stream()), "multi_fill");
+}
+
 // --------------------------------------------------------------------------- device info
 py::dict device_info(int64_t dev) {
   hipDeviceProp_t prop;
@@ -613,6 +632,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("cast_bf16", &cast_bf16);
   m.def("device_info", &device_info);
+  m.def("multi_fill", &multi_fill);
   m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),
         py::arg("blank"), py::arg("score") = py::none());
   m.def("conv1_fwd", &conv1_fwd);

@@ -1,8 +1,13 @@
 """Conv front-end on the HIP engine.
 
-conv1/conv2 run as bf16 convolutions; their BatchNorm + clipped-ReLU epilogues are the
-fused kernels of csrc/bn_act.hip. The conv2 epilogue writes the RNN input directly in
-time-major [T2, N, C*F2] order (reference transpose+reshape, src/deepSpeech_NCHW.py:166-168).
+Default (32 filters, the reference geometry): FrontendCL — the channels-last implicit-GEMM
+MFMA kernels of csrc/conv_frontend.hip for conv fwd / dgrad / wgrad with BatchNorm
+statistics fused into the conv epilogues and channels-last BN + clipped-ReLU kernels; the
+conv2 BN apply writes the RNN input directly in time-major [T2, N, C*F2] order (reference
+transpose+reshape, src/deepSpeech_NCHW.py:166-168).
+
+Other filter counts: library bf16 convolutions (ConvFused) with the NCHW BN + clip kernels
+of csrc/bn_act.hip (BNClip).
 """
 from __future__ import annotations
 
@@ -108,11 +113,7 @@ class ConvFused(torch.autograd.Function):
             [need_x, True, not ctx.bias_grad_zero])
         gw_out = emit_grad(weight, gw.float())
         if ctx.bias_grad_zero:
-            if arena_of(bias) is not None:
-                arena_of(bias).grad_done(bias)    # main_grad already zeroed by zero_grad()
-                gb_out = None
-            else:
-                gb_out = torch.zeros_like(bias)
+            gb_out = _zero_grad_of(bias)
         else:
             gb_out = emit_grad(bias, gb.float())
         return (gi if need_x else None), gw_out, gb_out, None, None, None
@@ -150,7 +151,9 @@ def _zero_grad_of(p: torch.Tensor):
     """Gradient of a conv bias that feeds a train-mode BatchNorm: identically zero."""
     a = arena_of(p)
     if a is not None:
-        a.grad_done(p)              # main_grad was zeroed by zero_grad(); adding zero is a no-op
+        if a.first_write(p):
+            p.main_grad.zero_()     # the arena may be zeroed lazily: write the zeros
+        a.grad_done(p)
         return None
     return torch.zeros_like(p)
 

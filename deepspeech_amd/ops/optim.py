@@ -107,13 +107,23 @@ class ParamArena:
         return None if b is None else b[start:pos]
 
     # ---- gradients ----------------------------------------------------------------
-    def zero_grad(self) -> None:
-        self.grad.zero_()
+    def zero_grad(self, lazy: bool = False) -> None:
+        """Start a new gradient step. ``lazy``: skip the memset of the whole arena — valid
+        when every gradient is delivered by the fused ops (first write overwrites, later
+        writes accumulate); call :meth:`zero_unwritten` before anything reads the arena."""
+        if not lazy:
+            self.grad.zero_()
         self._written.clear()
         # re-attach in case an op replaced a .grad (e.g. set_to_none elsewhere)
         for p, (o, n) in zip(self.params, self.offsets):
             if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
                 p.grad = self.grad[o:o + n].view_as(p)
+
+    def zero_unwritten(self) -> None:
+        """Zero the gradient of every parameter no op has written this step (lazy zeroing)."""
+        for p, (o, n) in zip(self.params, self.offsets):
+            if id(p) not in self._written:
+                self.grad[o:o + n].zero_()
 
     def first_write(self, p) -> bool:
         """True if ``p``'s gradient has not been written yet this step (fused ops then

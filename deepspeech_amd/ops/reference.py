@@ -33,11 +33,12 @@ def clipped_relu(x: torch.Tensor, cap: float = RELU_CLIP) -> torch.Tensor:
 
 
 def get_rnn_seqlen(seq_lens: torch.Tensor) -> torch.Tensor:
-    """T2 = ceil((ceil((T-19)/2) - 9)/2) computed in float64 like the reference."""
-    s = seq_lens.to(torch.float64)
-    s = torch.ceil((s - 19.0) / 2.0)
-    s = torch.ceil((s - 9.0) / 2.0)
-    return s.to(torch.int32)
+    """T2 = ceil((ceil((T-19)/2) - 9)/2) of the reference (src/deepSpeech.py:38-48).
+
+    For integer T this is floor((floor((T-18)/2) - 8)/2) = floor((T-34)/4): two integer
+    kernels instead of a float64 round trip (exact for every integer, negative included)."""
+    s = seq_lens.to(torch.int32) if seq_lens.dtype != torch.int32 else seq_lens
+    return torch.div(s - 34, 4, rounding_mode="floor").to(torch.int32)
 
 
 def reverse_index(lens: torch.Tensor, T: int) -> torch.Tensor:

@@ -226,18 +226,20 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     bf16 = torch.bfloat16
     y2 = torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
     hx = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=bf16)
-    hx[:, 0].zero_()                         # h0
     hs = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=torch.float32)
-    hs[:, 0].zero_()
-    if h0 is not None:
-        hs[:, 0, :N].copy_(h0)
-        hx[:, 0, :N].copy_(h0)
     gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
              if plan.cell == "gru" else None)
-    err = torch.zeros(1, device=dev, dtype=torch.int32)
     if plan.kind == "xcd":
-        hx[:, 1:].view(torch.int16).fill_(-1)             # sentinel 0xFFFF: "not yet produced"
-        census = torch.full((ndir * plan.BG * (H // 32),), -1, device=dev, dtype=torch.int32)
+        # one launch: h0 slots zero, exchange slots 1..T sentinel 0xFFFF ("not yet
+        # produced"), census words -1, error word 0
+        aux = torch.empty(4 + ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
+        err, census = aux[:1], aux[4:]
+        regions = ([hx[d, 0] for d in range(ndir)] + [hx[d, 1:] for d in range(ndir)] +
+                   [hs[d, 0] for d in range(ndir)] + [aux[:4], census])
+        C.multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [0, -1])
+        if h0 is not None:
+            hs[:, 0, :N].copy_(h0)
+            hx[:, 0, :N].copy_(h0)
         C.rnnx_fwd(gx, lens, U[0], U[1] if d1 else None, bh[0], bh[1] if d1 else None,
                    y2[0], y2[1] if d1 else None, hx[0], hx[1] if d1 else None,
                    hs[0], hs[1] if d1 else None,
@@ -250,6 +252,12 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
         _pending_errors.append(err)
         y = torch.add(y2[0], y2[1]) if d1 else y2[0]
         return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
+    hx[:, 0].zero_()                         # h0
+    hs[:, 0].zero_()
+    if h0 is not None:
+        hs[:, 0, :N].copy_(h0)
+        hx[:, 0, :N].copy_(h0)
+    err = torch.zeros(1, device=dev, dtype=torch.int32)
     flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
     C.rnn_fwd(gx, lens, U[0], U[1] if d1 else None,
               bh[0], bh[1] if d1 else None,
@@ -279,17 +287,22 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
     dy = dy.to(torch.bfloat16).contiguous()
     dgh = torch.empty(ndir, steps, plan.NP, G * H, device=dev, dtype=torch.bfloat16)
     dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
-    err = torch.zeros(1, device=dev, dtype=torch.int32)
-    parts = torch.zeros(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
-                        dtype=torch.float32) if want_bias else None
     has_g = gates.numel() > 0
     if plan.kind == "xcd":
-        census = torch.full((ndir * plan.BG * (H // 32),), -1, device=dev, dtype=torch.int32)
+        aux = torch.empty(4 + ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
+        err, census = aux[:1], aux[4:]
+        parts = torch.empty(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
+                            dtype=torch.float32) if want_bias else None
+        regions, pats = [aux[:4], census], [0, -1]
+        if parts is not None:
+            regions.append(parts)
+            pats.append(0)
         if BWD_EXCHANGE == "rs" and H // 32 <= 28:
             # generation-3 BPTT: reduce-scatter of fp32 partials through a 3-slot ring
             # (sentinel 0xFFFFFFFF); dgh is a plain output, no T-step sentinel fill
             rf = int(C.rnnx_ring_floats(H, plan.BG, plan.R))
-            ring = torch.full((ndir, rf), -1, device=dev, dtype=torch.int32).view(torch.float32)
+            ring = torch.empty(ndir, rf, device=dev, dtype=torch.float32)
+            C.multi_fill(regions + [ring], pats + [-1])     # one launch for every init
             C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
                        gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
                        dgh[0], dgh[1] if d1 else None, dgx,
@@ -301,7 +314,7 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
                        ring[0], ring[1] if d1 else None)
             _pending_errors.append(err)
             return dgx, dgh, parts
-        dgh.view(torch.int16).fill_(-1)                   # sentinel
+        C.multi_fill(regions + [dgh], pats + [-1])         # dgh: sentinel 0xFFFF pairs
         C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
                    gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
                    dgh[0], dgh[1] if d1 else None, dgx,
@@ -312,6 +325,9 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
                    _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev))
         _pending_errors.append(err)
         return dgx, dgh, parts
+    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    parts = torch.zeros(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
+                        dtype=torch.float32) if want_bias else None
     carry = None if plan.persistent else torch.zeros(ndir, plan.NP, H, device=dev, dtype=torch.float32)
     flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
     C.rnn_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,

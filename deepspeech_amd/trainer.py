@@ -5,8 +5,9 @@ backward, Adam with staircase-decayed LR, weight EMA (0.9999, num_updates=global
 loss EMA (0.9), NaN assert.
 
 MI355X step:
-  arena.zero_grad()                       one memset over the flat gradient arena
-  logits = model(feats)                   conv (bf16) + fused BN/clip -> persistent RNN
+  arena.zero_grad(lazy)                   HIP engine: no memset (every fused op's first
+                                          gradient write overwrites); ref engine: one memset
+  logits = model(feats)                   MFMA conv + fused BN/clip -> persistent RNN
                                           layers -> FC GEMM
   loss = fused CTC(logits)                loss and dlogits in one kernel
   loss.backward()                         RCCL bucket all-reduces launch from grad hooks
@@ -77,11 +78,16 @@ class Trainer:
         model = self.model
         model.train()
         self.arena.ensure_bf16()
-        self.arena.zero_grad()
+        # the HIP engine delivers every gradient through the arena (first write overwrites),
+        # so the per-step memset of the whole gradient buffer is skipped
+        lazy = model.engine == "hip"
+        self.arena.zero_grad(lazy=lazy)
         logits, lens = model(batch["feats"], batch["seq_lens"])
         loss = model.loss(logits, lens, batch["labels"], batch["label_lens"])
         loss.backward()
         join_wgrad_streams()
+        if lazy:
+            self.arena.zero_unwritten()
         with TR.phase(TR.ALLREDUCE):
             self.bucketer.finish()
         gscale = 1.0 / self.world
