@@ -195,6 +195,9 @@ class DeepSpeech2(nn.Module):
         self.engine = engine
         self.compute_dtype = compute_dtype
         self.fp8 = fp8
+        if engine == "hip":
+            from ..ops.gemm_tuning import enable_tuned_gemms
+            enable_tuned_gemms()          # measured hipBLASLt/rocBLAS picks for the projections
         for layer in self.rnn:
             layer.fp8 = fp8
         return self
