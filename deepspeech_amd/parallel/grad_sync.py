@@ -91,6 +91,12 @@ class GradBucketer:
         self._launched[b] = True
         s, e, _ = self.buckets[b]
         g = self.arena.grad[s:e]
+        if g.is_cuda:
+            # a bucket may mix gradients produced on the current stream and on the
+            # recurrent layers' weight-gradient side stream: the collective (which waits on
+            # the current stream only) must see both
+            from ..ops.rnn import join_wgrad_streams
+            join_wgrad_streams()
         if self.compress:
             sh = self._shadow[b]
             if sh is None or sh.numel() != g.numel():
