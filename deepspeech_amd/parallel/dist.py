@@ -62,16 +62,20 @@ def init_distributed(device_pref: str = "auto", timeout_s: int = 600) -> DistCon
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = (device_pref in ("auto", "cuda")) and torch.cuda.is_available()
     if use_cuda:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # DS2_DEVICE_INDEX pins every rank to one device (multi-rank rehearsal on a 1-GPU box)
+        dev_idx = int(os.environ.get("DS2_DEVICE_INDEX", local))
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     ctx = DistContext(rank=rank, local_rank=local, world_size=world, device=device)
     if world > 1:
-        backend = "nccl" if use_cuda else "gloo"
+        # RCCL ("nccl") on GPUs; DS2_DIST_BACKEND=gloo runs the same collectives through host
+        # memory (ranks sharing one GPU, where RCCL refuses duplicate devices)
+        backend = os.environ.get("DS2_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_cuda:
+        if use_cuda and backend == "nccl":
             kw["device_id"] = device
         if not dist.is_initialized():
             dist.init_process_group(**kw)

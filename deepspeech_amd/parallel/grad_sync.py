@@ -24,11 +24,14 @@ import torch.distributed as dist
 
 class GradBucketer:
     def __init__(self, arena, bucket_mb: float = 32.0, compress_bf16: bool = False,
-                 process_group=None):
+                 process_group=None, world_size: Optional[int] = None):
         self.arena = arena
         self.pg = process_group
         self.compress = compress_bf16
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # world_size given by the caller wins (a world_size=1 trainer inside an initialised
+        # process group keeps its gradients local)
+        self.world = (world_size if world_size is not None else
+                      (dist.get_world_size(process_group) if dist.is_initialized() else 1))
         limit = int(bucket_mb * 1024 * 1024 / 4)
         # snap buckets to parameter boundaries, in arena (= gradient production) order
         self.buckets: List[Tuple[int, int, List[int]]] = []
@@ -76,7 +79,15 @@ class GradBucketer:
             self._launch(b)
 
     def _make_hook(self, i: int):
-        def hook(_p):
+        # autograd runs a parameter's post-accumulate hook even when the producing op
+        # returned no gradient for it (the fused ops deliver theirs through the arena and
+        # return None): count each parameter once per step, whichever path reports first
+        def hook(p):
+            written = getattr(self.arena, "_written", None)
+            if written is not None:
+                if id(p) in written:
+                    return
+                written.add(id(p))
             self._ready(i)
         return hook
 

@@ -58,7 +58,8 @@ class Trainer:
         self.opt = FusedAdamEMA(self.arena, lr=lr_schedule.initial_lr, ema_decay=moving_avg_decay)
         self.lr_schedule = lr_schedule
         self.world = world_size
-        self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb, compress_bf16=allreduce_bf16)
+        self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb, compress_bf16=allreduce_bf16,
+                                     world_size=world_size)
         if world_size > 1:
             broadcast_params(self.arena)
             self.arena.mark_dirty()

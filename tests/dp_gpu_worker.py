@@ -1,0 +1,74 @@
+"""Worker of tests/test_dp_gpu.py (run under torch.distributed.run, 2 ranks on cuda:0 over
+gloo): checks that the all-reduced gradient of the HIP engine — with the recurrent weight
+gradients produced on the side stream and small buckets that mix streams — equals the sum
+of the ranks' local gradients."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device  # noqa: E402
+from deepspeech_amd.models import DeepSpeech2  # noqa: E402
+from deepspeech_amd.ops.rnn import join_wgrad_streams  # noqa: E402
+from deepspeech_amd.parallel.dist import init_distributed, shutdown  # noqa: E402
+from deepspeech_amd.trainer import LRSchedule, Trainer  # noqa: E402
+
+
+def model(dev):
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=32, num_hidden=64, num_rnn_layers=2, cell="gru").to(dev)
+    return m.set_engine("hip", torch.bfloat16)
+
+
+def grads(tr, batch, dp):
+    tr.model.train()
+    tr.arena.zero_grad(lazy=True)
+    logits, lens = tr.model(batch["feats"], batch["seq_lens"])
+    tr.model.loss(logits, lens, batch["labels"], batch["label_lens"]).backward()
+    join_wgrad_streams()
+    tr.arena.zero_unwritten()
+    if dp:
+        tr.bucketer.finish()
+    torch.cuda.synchronize()
+    return tr.arena.grad.clone()
+
+
+def diagnose(out, names_offsets):
+    g = [torch.load("%s.%d" % (out, k), weights_only=True) for k in range(2)]
+    want = g[0]["local"] + g[1]["local"]
+    for name, (o, n) in names_offsets:
+        w = want[o:o + n]
+        for k in range(2):
+            d = g[k]["dp"][o:o + n]
+            err = ((d - w).norm() / (w.norm() + 1e-30)).item()
+            if err > 1e-5:
+                print("rank%d %-22s err %.3e  |dp| %.3e |want| %.3e |local%d| %.3e" % (
+                    k, name, err, d.norm(), w.norm(), k, g[k]["local"][o:o + n].norm()))
+
+
+def main():
+    out = sys.argv[1]
+    ctx = init_distributed("cuda")
+    dev = ctx.device
+    batch = to_device(FixedShapeBatches(4, max_frames=300, seed=100 + ctx.rank, pool=1).next(), dev)
+    local = Trainer(model(dev), LRSchedule(1e-3, 10 ** 6, 0.9), world_size=1)
+    g_local = grads(local, batch, dp=False)
+    bmb = float(os.environ.get("DS2_DP_BUCKET_MB", "0.05"))
+    dp = Trainer(model(dev), LRSchedule(1e-3, 10 ** 6, 0.9), world_size=ctx.world_size, bucket_mb=bmb)
+    assert len(dp.bucketer.buckets) >= (3 if bmb < 1 else 1)
+    if ctx.rank == 0 and os.environ.get("DS2_DP_DIAG"):
+        for bi, (s0, e0, idx) in enumerate(dp.bucketer.buckets):
+            print("bucket", bi, s0, e0, [dp.arena.names[i] for i in idx])
+    g_dp = grads(dp, batch, dp=True)
+    torch.save({"local": g_local.cpu(), "dp": g_dp.cpu()}, "%s.%d" % (out, ctx.rank))
+    torch.distributed.barrier()
+    if ctx.rank == 0 and os.environ.get("DS2_DP_DIAG"):
+        diagnose(out, list(zip(dp.arena.names, dp.arena.offsets)))
+    shutdown(ctx)
+
+
+if __name__ == "__main__":
+    main()
+

@@ -1,0 +1,35 @@
+"""Data-parallel gradient path of the HIP engine on a GPU: 2 ranks sharing cuda:0 over gloo
+(torch.distributed.run), side-stream weight gradients + multi-bucket all-reduce."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_dp2_gradients_equal_sum_of_local(cuda, tmp_path):
+    out = str(tmp_path / "g")
+    env = dict(os.environ, PYTHONPATH=ROOT, DS2_DIST_BACKEND="gloo", DS2_DEVICE_INDEX="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dp_gpu_worker.py"), out]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    g = [torch.load("%s.%d" % (out, k), weights_only=True) for k in range(2)]
+    want = g[0]["local"] + g[1]["local"]
+    for k in range(2):
+        err = ((g[k]["dp"] - want).norm() / want.norm()).item()
+        assert err < 1e-5, (k, err)
