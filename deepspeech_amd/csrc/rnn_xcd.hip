@@ -822,14 +822,17 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
 // Per step a consumer then reads P x R x 32 fp32 (25.6 KB at H = 800, R = 8) instead of
 // R x 3H bf16 (38.4 KB), and the exchange lives in a 3-slot ring (a few MB per group, L2
 // resident) instead of a T-step buffer:
-//  * ring[dir][slot][bg][producer][row][H] fp32, pre-filled with the sentinel 0xFFFFFFFF
-//    (never produced: NaN results are canonicalised); P(s) goes to slot s % 3;
-//  * a consumer resets every granule it read to the sentinel at the START of its next
-//    step and drains those stores (vmcnt(0)) before that step's first barrier, i.e. before
-//    it publishes its own next partial. A producer rewrites slot s % 3 only at step s - 3,
-//    after it has received every consumer's partial of step s - 1, which each consumer
-//    published after its resets of slot s % 3 had completed: the protocol is safe for any
-//    timing, and the ring is sentinel-clean again when the launch ends;
+//  * ring[dir][slot][bg][producer][row][H] fp32, P(s) goes to slot s % 3. Readiness is a
+//    use TAG in every word's mantissa LSB: slot s % 3 is written at processing index
+//    k = steps-1-s, i.e. at k, k+3, k+6, ..., with tag (k/3) & 1, which alternates between
+//    consecutive uses of a slot. The host fills the ring with 0xFFFFFFFF (tag 1) before each
+//    launch and every slot's first use has tag 0. A consumer spins until all four words of
+//    a 16-B granule carry the tag it expects, so a stale value (previous use) or a granule
+//    landing in pieces is never taken. Nothing is reset: a producer rewrites slot s % 3 only
+//    after it has gathered every producer's P(s+1), each published after that producer's
+//    gather of P(s+2) and P(s+3) had returned, so no one still reads the old contents.
+//    (Generation 3a reset every granule read to a sentinel: 25.6 KB of extra stores per
+//    workgroup-step plus a vmcnt(0) drain before the first barrier.)
 //  * dgh (bf16) is now a plain output for the dU GEMM, stored by the memory wave off the
 //    critical path; no T-step sentinel fill is needed.
 // Worker waves 0..6: gather+sum (producer j = wave + 7i), then the MFMA
@@ -846,7 +849,7 @@ struct XBwdRS {
   const float* gates[2];
   bf16_t* dgh[2];         // [steps][NP][G*H] output (dU GEMM operand)
   bf16_t* dgx;
-  float* ring[2];         // [3][BG][P][R][H] fp32, sentinel-filled
+  float* ring[2];         // [3][BG][P][R][H] fp32, filled with 0xFFFFFFFF (tag 1) per launch
   float* dbx_part[2];
   float* dbh_part[2];
   float dgx_scale;
@@ -856,11 +859,11 @@ struct XBwdRS {
   unsigned long long* stamps;
 };
 
-constexpr unsigned SENT32 = 0xffffffffu;
-
-__device__ __forceinline__ bool granule_ready32(i32x4 v) {
-  return ((unsigned)v[0] != SENT32) && ((unsigned)v[1] != SENT32) && ((unsigned)v[2] != SENT32) &&
-         ((unsigned)v[3] != SENT32);
+// A ring word carries its use tag in the mantissa LSB (see rnnrs_bwd_kernel): the granule is
+// ready when all four words carry the expected tag.
+__device__ __forceinline__ bool granule_tagged(i32x4 v, unsigned tag) {
+  return (((unsigned)v[0] & 1u) == tag) && (((unsigned)v[1] & 1u) == tag) && (((unsigned)v[2] & 1u) == tag) &&
+         (((unsigned)v[3] & 1u) == tag);
 }
 __device__ __forceinline__ float canon32(float f) { return (f != f) ? __uint_as_float(0x7fc00000u) : f; }
 
@@ -1019,29 +1022,15 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   auto ring_off = [&](int slot, int j, int row, int unit) -> unsigned {
     return (unsigned)((((size_t)slot * a.BG + bg) * P + j) * R * H + (size_t)row * H + unit) * 4u;
   };
-  const i32x4 sent = {(int)SENT32, (int)SENT32, (int)SENT32, (int)SENT32};
-  auto reset_slot = [&](int slot) {       // sentinel back into every granule this thread read
-    for (int cb = 0; cb < ncb; ++cb) {
-      const int grow = grow_of(cb);
-      if (grow >= R) continue;
-#pragma unroll
-      for (int i = 0; i < GPT; ++i) {
-        const int j = pg7 + MW * i;
-        if (j < P) {
-          const unsigned off = ring_off(slot, j, grow, u0 + 4 * gq8);
-          if (plain) *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ringd) + off) = sent;
-          else store_sc1_b128(rs_ring, off, sent);
-        }
-      }
-    }
-  };
+  // use tag of P(s): slot s % 3 is written at processing index k = steps-1-s, so its uses
+  // are k, k+3, k+6, ... and (k / 3) & 1 alternates between consecutive uses; the ring is
+  // filled with 0xFFFFFFFF (tag 1) and every slot's first use has tag 0
+  auto tag_of = [&](int s) -> unsigned { return (unsigned)(((a.steps - 1 - s) / 3) & 1); };
 
   if (wave < MW) {
     for (int s = a.steps - 1; s >= 0; --s) {
       st.mark(-1);
       const bool has_next = s + 1 < a.steps;
-      // (R) reset the granules read last step (slot (s+2) % 3) to the sentinel
-      if (s + 2 < a.steps) reset_slot((s + 2) % 3);
       // (G) sum this thread's producers' partials of dh_rec for (row, 4 units)
       for (int cb = 0; cb < ncb; ++cb) {
         const int grow = grow_of(cb);
@@ -1049,6 +1038,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
         f32x4 acc4 = f32x4{0.f, 0.f, 0.f, 0.f};
         if (has_next) {
           const int cs = (s + 1) % 3;
+          const unsigned want = has_next ? tag_of(s + 1) : 0u;
           unsigned off[GPT];
           i32x4 v[GPT];
 #pragma unroll
@@ -1061,7 +1051,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 #pragma unroll
           for (int i = 0; i < GPT; ++i) {
             if (pg7 + MW * i < P) {
-              while (!granule_ready32(v[i])) {
+              while (!granule_tagged(v[i], want)) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
                 __builtin_amdgcn_s_sleep(1);
                 v[i] = load_sc1_b128(rs_ring, off[i]);
@@ -1073,7 +1063,6 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) red_s[wave][grow][4 * gq8 + jj] = acc4[jj];
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // resets (and loads) complete
       st.mark(0);
       lds_barrier();                                                        // #1
       st.mark(1);
@@ -1137,6 +1126,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
       // (M) publish P(s) = dgh_s[:, own cols] . U[own cols, :] into ring slot s % 3
       if (s > 0) {
         const int ws = s % 3;
+        const unsigned tg = tag_of(s);
         const bool prow = (lane & 15) < R;
         bf16x8 bfr[G];
 #pragma unroll
@@ -1144,8 +1134,11 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
           bfr[g] = *reinterpret_cast<const bf16x8*>(&dg_s[lane & 15][g * UPW + 8 * (lane >> 4)]);
         auto put = [&](int mt, f32x4 acc) {
           if (prow) {
-            const i32x4 v = {(int)__float_as_uint(canon32(acc[0])), (int)__float_as_uint(canon32(acc[1])),
-                             (int)__float_as_uint(canon32(acc[2])), (int)__float_as_uint(canon32(acc[3]))};
+            // the tag replaces the mantissa LSB (a 2^-23 relative perturbation of a partial)
+            const i32x4 v = {(int)((__float_as_uint(canon32(acc[0])) & ~1u) | tg),
+                             (int)((__float_as_uint(canon32(acc[1])) & ~1u) | tg),
+                             (int)((__float_as_uint(canon32(acc[2])) & ~1u) | tg),
+                             (int)((__float_as_uint(canon32(acc[3])) & ~1u) | tg)};
             const unsigned off = ring_off(ws, mem, lane & 15, 16 * mt + 4 * (lane >> 4));
             if (plain) *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ringd) + off) = v;
             else store_sc1_b128(rs_ring, off, v);
@@ -1174,8 +1167,6 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
       }
       st.mark(4);
     }
-    // leave the ring sentinel-clean: reset what step 0 read (slot 1 % 3)
-    if (!s_abort && a.steps >= 2) reset_slot(1);
   } else {
     for (int s = a.steps - 1; s >= 0; --s) {
       // memory wave, while the others wait on the exchange

@@ -299,7 +299,7 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
             pats.append(0)
         if BWD_EXCHANGE == "rs" and H // 32 <= 28:
             # generation-3 BPTT: reduce-scatter of fp32 partials through a 3-slot ring
-            # (sentinel 0xFFFFFFFF); dgh is a plain output, no T-step sentinel fill
+            # (readiness = per-use tag in each word's LSB, ring filled with 0xFFFFFFFF); dgh is a plain output
             rf = int(C.rnnx_ring_floats(H, plan.BG, plan.R))
             ring = torch.empty(ndir, rf, device=dev, dtype=torch.float32)
             C.multi_fill(regions + [ring], pats + [-1])     # one launch for every init
