@@ -40,6 +40,14 @@ __device__ __forceinline__ void store_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigne
                                          r, off, 0, AUX_SC1);
 }
 
+// plain (L2 write-back) store through the same resource: the base stays in the resource's
+// SGPRs (a pointer store made the compiler re-load the base from the kernel arguments, an
+// s_load + lgkmcnt(0) wait per store inside the latency-critical publish loops)
+__device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, unsigned off, i32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         r, off, 0, 0);
+}
+
 __device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
   return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

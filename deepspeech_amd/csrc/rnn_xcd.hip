@@ -121,8 +121,9 @@ __device__ __forceinline__ bool granule_ready(i32x4 v) {
 
 __device__ __forceinline__ void store_granule(bool plain, __amdgpu_buffer_rsrc_t rs, bf16_t* base, unsigned off,
                                               i32x4 v) {
+  (void)base;
   if (plain) {
-    *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(base) + off) = v;
+    store_b128(rs, off, v);
   } else {
     store_sc1_b128(rs, off, v);
   }
@@ -775,7 +776,7 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
     if (a.steps >= 1) mw_store(0);
   }
   if (wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
-  if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
+  if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[2]; }
 
   // bias gradients: reduce the epilogue waves' rows through LDS, one read-modify-write
   // per (gate, unit) of the workgroup's own [bg] partial row
@@ -1013,14 +1014,23 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(ringd, ring_bytes);
   Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
 
-  // gather geometry (workers): combo = lane + 64*cb -> (row, 4-unit granule q8) for rows < 16;
-  // this wave sums producers j = wave + 7*i
+  // ring layout [slot][bg][producer][m-tile of 16 units][row][16] fp32: a producer's MFMA
+  // tile (R rows x 16 units) is R*64 contiguous bytes (whole cache lines per store
+  // instruction), and a consumer's 32 units from one producer (m-tiles 2*mem, 2*mem+1) are
+  // 2*R*64 contiguous bytes, read by one wave as one coalesced sweep.
+  // gather geometry (workers): combo c = lane + 64*cb -> (half = c / 4R, row, 4-unit
+  // granule); this wave sums producers j = wave + 7*i
   const int pg7 = wave;
-  auto grow_of = [&](int cb) { return (lane + 64 * cb) >> 3; };
-  const int gq8 = lane & 7;
   const int ncb = (R * 8 + 63) / 64;          // combos per thread: 1 (R <= 8) or 2
-  auto ring_off = [&](int slot, int j, int row, int unit) -> unsigned {
-    return (unsigned)((((size_t)slot * a.BG + bg) * P + j) * R * H + (size_t)row * H + unit) * 4u;
+  auto combo = [&](int cb, int& row, int& ucol) -> bool {
+    const int c = lane + 64 * cb;
+    const int half = c / (4 * R), rem = c - half * 4 * R;
+    row = rem >> 2;
+    ucol = 16 * half + 4 * (rem & 3);         // unit within this workgroup's 32
+    return half < 2;
+  };
+  auto ring_off = [&](int slot, int j, int mt, int row, int u16) -> unsigned {
+    return (unsigned)(((((((size_t)slot * a.BG + bg) * P + j) * MTS + mt) * R + row) * 16) + u16) * 4u;
   };
   // use tag of P(s): slot s % 3 is written at processing index k = steps-1-s, so its uses
   // are k, k+3, k+6, ... and (k / 3) & 1 alternates between consecutive uses; the ring is
@@ -1033,8 +1043,8 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
       const bool has_next = s + 1 < a.steps;
       // (G) sum this thread's producers' partials of dh_rec for (row, 4 units)
       for (int cb = 0; cb < ncb; ++cb) {
-        const int grow = grow_of(cb);
-        if (grow >= R) continue;
+        int grow, gcol;
+        if (!combo(cb, grow, gcol)) continue;
         f32x4 acc4 = f32x4{0.f, 0.f, 0.f, 0.f};
         if (has_next) {
           const int cs = (s + 1) % 3;
@@ -1044,14 +1054,14 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 #pragma unroll
           for (int i = 0; i < GPT; ++i) {
             const int j = min(pg7 + MW * i, P - 1);
-            off[i] = ring_off(cs, j, grow, u0 + 4 * gq8);
+            off[i] = ring_off(cs, j, 2 * mem + (gcol >> 4), grow, gcol & 15);
             v[i] = load_sc1_b128(rs_ring, off[i]);
           }
           const long long t0 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
           for (int i = 0; i < GPT; ++i) {
             if (pg7 + MW * i < P) {
-              while (!granule_tagged(v[i], want)) {
+              while (!(a.knobs & 4) && !granule_tagged(v[i], want)) {   // knob 4: no wait (timing only)
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
                 __builtin_amdgcn_s_sleep(1);
                 v[i] = load_sc1_b128(rs_ring, off[i]);
@@ -1061,7 +1071,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
           }
         }
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) red_s[wave][grow][4 * gq8 + jj] = acc4[jj];
+        for (int jj = 0; jj < 4; ++jj) red_s[wave][grow][gcol + jj] = acc4[jj];
       }
       st.mark(0);
       lds_barrier();                                                        // #1
@@ -1139,8 +1149,8 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
                              (int)((__float_as_uint(canon32(acc[1])) & ~1u) | tg),
                              (int)((__float_as_uint(canon32(acc[2])) & ~1u) | tg),
                              (int)((__float_as_uint(canon32(acc[3])) & ~1u) | tg)};
-            const unsigned off = ring_off(ws, mem, lane & 15, 16 * mt + 4 * (lane >> 4));
-            if (plain) *reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ringd) + off) = v;
+            const unsigned off = ring_off(ws, mem, mt, lane & 15, 4 * (lane >> 4));
+            if (plain) store_b128(rs_ring, off, v);
             else store_sc1_b128(rs_ring, off, v);
           }
         };
@@ -1150,10 +1160,12 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
           const int mt0 = wave + MW * i, mt1 = wave + MW * (i + 1);
           if (mt1 < MTS) {
             f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+            if (!(a.knobs & 8)) {                        // knob 8: no MFMA (timing only)
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-              a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], a0, 0, 0, 0);
-              a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i + 1][g], bfr[g], a1, 0, 0, 0);
+              for (int g = 0; g < G; ++g) {
+                a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i + 1][g], bfr[g], a1, 0, 0, 0);
+              }
             }
             put(mt0, a0);
             put(mt1, a1);
@@ -1172,6 +1184,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
       // memory wave, while the others wait on the exchange
       st.mark(-1);
       mw_put(s);
+      st.mark(2);                 // memory wave: acc[2] = put (incl. its load wait), acc[0] = store + load issue
       if (s + 2 < a.steps) mw_store(s + 2);
       if (s >= 1) mw_load(s - 1);
       st.mark(0);

@@ -115,7 +115,7 @@ def main():
                 print(json.dumps({"kernel": proto, "nw": nw, "mode": mode, "error": str(e)[:200]}), flush=True)
       if a.stamps:
         if proto == "xcd":
-            __import__("deepspeech_amd.ops.rnn", fromlist=["x"]).RNNX_KNOBS = 0
+            __import__("deepspeech_amd.ops.rnn", fromlist=["x"]).RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))
         r = run(a.cell, a.N, a.H, a.T, a.ndir, 0, "auto", 1, stamps=True)
         print(json.dumps({"kernel": proto, "stamps [mean,min,max] cycles/step": r}), flush=True)
 
