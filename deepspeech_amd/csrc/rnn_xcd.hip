@@ -823,7 +823,7 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
 // Per step a consumer then reads P x R x 32 fp32 (25.6 KB at H = 800, R = 8) instead of
 // R x 3H bf16 (38.4 KB), and the exchange lives in a 3-slot ring (a few MB per group, L2
 // resident) instead of a T-step buffer:
-//  * ring[dir][slot][bg][producer][row][H] fp32, P(s) goes to slot s % 3. Readiness is a
+//  * ring[dir][slot][bg][producer][H/16 m-tiles][row][16] fp32, P(s) goes to slot s % 3. Readiness is a
 //    use TAG in every word's mantissa LSB: slot s % 3 is written at processing index
 //    k = steps-1-s, i.e. at k, k+3, k+6, ..., with tag (k/3) & 1, which alternates between
 //    consecutive uses of a slot. The host fills the ring with 0xFFFFFFFF (tag 1) before each
@@ -850,7 +850,7 @@ struct XBwdRS {
   const float* gates[2];
   bf16_t* dgh[2];         // [steps][NP][G*H] output (dU GEMM operand)
   bf16_t* dgx;
-  float* ring[2];         // [3][BG][P][R][H] fp32, filled with 0xFFFFFFFF (tag 1) per launch
+  float* ring[2];         // [3][BG][P][H/16][R][16] fp32, filled with 0xFFFFFFFF (tag 1) per launch
   float* dbx_part[2];
   float* dbh_part[2];
   float dgx_scale;
