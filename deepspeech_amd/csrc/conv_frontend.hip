@@ -763,7 +763,8 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_reduce_kernel(const bf16_t* __r
                                                                const float* __restrict__ invstd,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, float* part,
-                                                               int N, int T, int F, int tmaj) {
+                                                               int N, int T, int F, int tmaj,
+                                                               bf16_t* __restrict__ dz_cl) {
   __shared__ bf16_t tr[32 * 97];
   const int tid = threadIdx.x, c0 = (tid & 3) * 8;
   float mu[8], is[8], g[8], bt[8], s[8], q[8];
@@ -792,6 +793,8 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_reduce_kernel(const bf16_t* __r
       if (tmaj) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) d[j] = (short)tr[(c0 + j) * stride + f];
+        // the transposed (channels-last) copy, so the apply pass reads it coalesced
+        if (dz_cl != nullptr) *(bf16x8*)(dz_cl + (size_t)row * F * CC + ch * 8) = d;
       } else {
         d = *(const bf16x8*)(dz + (size_t)row * F * CC + ch * 8);
       }
@@ -859,8 +862,9 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_finalize_kernel(const float* __
   }
 }
 
-// dy = gamma*invstd*(dz*m - dbeta/M - xhat*dgamma/M), channels-last out
-__global__ __launch_bounds__(256) void bn_cl_bwd_apply_kernel(const bf16_t* __restrict__ dz,
+// dy = gamma*invstd*(dz*m - dbeta/M - xhat*dgamma/M), channels-last out. dz may alias dy
+// (each thread reads and writes the same 16 B), so neither is __restrict__.
+__global__ __launch_bounds__(256) void bn_cl_bwd_apply_kernel(const bf16_t* dz,
                                                               const bf16_t* __restrict__ y,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd,
@@ -868,7 +872,7 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_apply_kernel(const bf16_t* __re
                                                               const float* __restrict__ beta,
                                                               const float* __restrict__ dbeta,
                                                               const float* __restrict__ dgamma,
-                                                              bf16_t* __restrict__ dy, int N, int T, int F, int tmaj) {
+                                                              bf16_t* dy, int N, int T, int F, int tmaj) {
   __shared__ bf16_t tr[32 * 97];
   const int tid = threadIdx.x, c0 = (tid & 3) * 8;
   const float M = (float)N * T * F;
@@ -1015,12 +1019,16 @@ int ds2_bn_cl_bwd(const void* dz, const void* y, const float* mean, const float*
                   const float* beta, float* part, int nb, float* dgamma, float* dbeta, void* dy, int N, int T, int F,
                   int tmaj, hipStream_t st) {
   if (F > 96) return -45;
+  // time-major dz: the reduce pass (which transposes it through LDS anyway) leaves a
+  // channels-last copy in dy, and the apply pass then works in place on dy, coalesced
+  // (the apply's own per-row LDS transpose ran at ~1/9 of the bandwidth roofline)
   hipLaunchKernelGGL(bn_cl_bwd_reduce_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)dz, (const bf16_t*)y, mean,
-                     invstd, gamma, beta, part, N, T, F, tmaj);
+                     invstd, gamma, beta, part, N, T, F, tmaj, tmaj ? (bf16_t*)dy : (bf16_t*)nullptr);
   hipLaunchKernelGGL(bn_cl_bwd_finalize_kernel, dim3(CC), dim3(256), 0, st, part, nb, dbeta, dgamma);
   const int rows = N * T;
-  hipLaunchKernelGGL(bn_cl_bwd_apply_kernel, dim3(rows < 4096 ? rows : 4096), dim3(256), 0, st, (const bf16_t*)dz,
-                     (const bf16_t*)y, mean, invstd, gamma, beta, dbeta, dgamma, (bf16_t*)dy, N, T, F, tmaj);
+  hipLaunchKernelGGL(bn_cl_bwd_apply_kernel, dim3(rows < 4096 ? rows : 4096), dim3(256), 0, st,
+                     tmaj ? (const bf16_t*)dy : (const bf16_t*)dz, (const bf16_t*)y, mean, invstd, gamma, beta,
+                     dbeta, dgamma, (bf16_t*)dy, N, T, F, 0);
   return (int)hipGetLastError();
 }
 
