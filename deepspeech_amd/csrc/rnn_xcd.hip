@@ -240,7 +240,6 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
   constexpr int RGL = (RG + 63) / 64;             // ... per memory-wave lane
   constexpr int OPL = ROWS * UPW / 64;            // output elements per memory-wave lane
   __shared__ float red_s[2][MW][ROWS][GC + 1];    // K-split partials, by step parity
-  __shared__ __attribute__((aligned(16))) bf16_t st_s[ROWS][UPW];
   __shared__ float gxr_s[2][ROWS][GC];            // input-projection ring (memory wave -> epilogue)
   __shared__ float oh_s[2][ROWS][UPW];            // output staging, by step parity
   __shared__ float oy_s[2][ROWS][UPW];
@@ -394,10 +393,12 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
       if (s_abort) break;
       // (E) cell epilogue; the exchange copy goes out first
       if (wave < EW) {
+        unsigned hq[EPT];                  // this lane's new h (bf16 bits) per epilogue element
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
           const int e = tid + i * ETH;
           const int row = e >> 5, c = e & 31;
+          hq[i] = 0u;
           if (row < R) {
             float pre[G], gxv[G];
 #pragma unroll
@@ -423,22 +424,25 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
             }
             const float hnew = act ? hn : hreg[i];
             hreg[i] = hnew;
-            st_s[row][c] = f2bf_x(hnew);
+            hq[i] = (unsigned)(unsigned short)f2bf_x(hnew);
             oh_s[s & 1][row][c] = hnew;
             oy_s[s & 1][row][c] = act ? hn : 0.f;
             if (CELL == CELL_GRU) og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c] = gsv;
           }
         }
-        // a wave's lanes cover whole rows of st_s: the granule stores read only LDS that
-        // this wave wrote
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        // assemble each 16-B granule (8 consecutive units = 8 consecutive lanes of one row)
+        // in its first lane with DPP row shifts instead of an LDS round trip + fence
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
+          if ((i * ETH) / UPW >= R) break;                 // wave-uniform: no row of this pass
           const int e = tid + i * ETH;
           const int row = e >> 5, c = e & 31;
+          const unsigned pr = hq[i] | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)hq[i], 0x101, 0xf, 0xf, false) << 16);
+          const int q1 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x102, 0xf, 0xf, false);
+          const int q2 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x104, 0xf, 0xf, false);
+          const int q3 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x106, 0xf, 0xf, false);
           if ((c & 7) == 0 && row < R) {
-            const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][c]);
+            const i32x4 v = {(int)pr, q1, q2, q3};
             const unsigned off = (unsigned)((((size_t)(s + 1) * NP + r0 + row) * H + u0 + c) * 2);
             store_granule(plain, rs_hx, hxd, off, v);
           }
