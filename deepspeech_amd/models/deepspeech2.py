@@ -305,7 +305,7 @@ class DeepSpeech2(nn.Module):
         """Mean CTC loss over the batch (src/deepSpeech_NCHW.py:204-228)."""
         if self.engine == "hip":
             from ..ops import ctc as CTC
-            return CTC.ctc_loss_hip(logits, lens, targets, target_lens).mean()
+            return CTC.ctc_mean_loss_hip(logits, lens, targets, target_lens)
         from ..utils import trace as TR
         with TR.phase(TR.CTC_F):
             return R.ctc_loss_ref(logits, targets, lens, target_lens).mean()

@@ -49,6 +49,31 @@ class CTCLossFused(torch.autograd.Function):
         return g, None, None, None, None, None
 
 
+class CTCMeanFused(CTCLossFused):
+    """Mean CTC loss over the batch. The gradient for the mean is the saved per-utterance
+    gradient times gloss / N, one scalar-broadcast multiply (instead of the mean's expand +
+    divide and a per-utterance broadcast multiply)."""
+
+    @staticmethod
+    def forward(ctx, logits, lens, labels, label_lens, blank: int, zero_infinity: bool):
+        loss = CTCLossFused.forward(ctx, logits, lens, labels, label_lens, blank, zero_infinity)
+        ctx.n = loss.numel()
+        return loss.mean()
+
+    @staticmethod
+    def backward(ctx, gloss):
+        with TR.phase(TR.CTC_B):
+            (grad,) = ctx.saved_tensors
+            return grad * (gloss / ctx.n), None, None, None, None, None
+
+
+def ctc_mean_loss_hip(logits: torch.Tensor, lens: torch.Tensor, labels: torch.Tensor,
+                      label_lens: torch.Tensor, blank: int = BLANK, zero_infinity: bool = True) -> torch.Tensor:
+    """Mean CTC loss over the batch (fp32 scalar)."""
+    with TR.phase(TR.CTC_F):
+        return CTCMeanFused.apply(logits, lens, labels, label_lens, blank, zero_infinity)
+
+
 def ctc_loss_hip(logits: torch.Tensor, lens: torch.Tensor, labels: torch.Tensor,
                  label_lens: torch.Tensor, blank: int = BLANK, zero_infinity: bool = True) -> torch.Tensor:
     """Per-utterance CTC loss [N] (fp32)."""

@@ -151,9 +151,10 @@ def _zero_grad_of(p: torch.Tensor):
     """Gradient of a conv bias that feeds a train-mode BatchNorm: identically zero."""
     a = arena_of(p)
     if a is not None:
-        if a.first_write(p):
+        if a.first_write(p) and not a.known_zero(p):
             p.main_grad.zero_()     # the arena may be zeroed lazily: write the zeros
         a.grad_done(p)
+        a.set_known_zero(p)         # until another op writes it, later steps need no kernel
         return None
     return torch.zeros_like(p)
 
@@ -236,8 +237,7 @@ class FrontendCL(torch.autograd.Function):
         nb1 = max(1, min(N * T1, 1024))
         part = torch.empty(max(nb1, nb2) * 64, **f32)
         with TR.phase(TR.bn(2, True)):
-            dg2 = torch.empty(32, **f32)
-            db2 = torch.empty(32, **f32)
+            (dg2, ipg2), (db2, ipb2) = _grad_buffer(g2), _grad_buffer(be2)
             dy2 = torch.empty_like(y2)
             C_.bn_cl_bwd(dout, y2, mean2, inv2, g2f, be2f, part, nb2, dg2, db2, dy2, True)
         with TR.phase(TR.conv(2, True)):
@@ -247,10 +247,9 @@ class FrontendCL(torch.autograd.Function):
             gw2 = _deliver(w2, dw2, ip2)
             dz1 = torch.empty_like(y1)
             C_.conv2_dgrad(dy2, w2_16, dz1, max(1, min(N * ((T1 + 1) // 2), ctx.ncu)))
-        gg2, gb2, gbias2 = emit_grad(g2, dg2), emit_grad(be2, db2), _zero_grad_of(b2)
+        gg2, gb2, gbias2 = _deliver(g2, dg2, ipg2), _deliver(be2, db2, ipb2), _zero_grad_of(b2)
         with TR.phase(TR.bn(1, True)):
-            dg1 = torch.empty(32, **f32)
-            db1 = torch.empty(32, **f32)
+            (dg1, ipg1), (db1, ipb1) = _grad_buffer(g1), _grad_buffer(be1)
             dy1 = torch.empty_like(y1)
             C_.bn_cl_bwd(dz1, y1, mean1, inv1, g1f, be1f, part, nb1, dg1, db1, dy1, False)
         with TR.phase(TR.conv(1, True)):
@@ -259,7 +258,7 @@ class FrontendCL(torch.autograd.Function):
             dw1, ip1 = _grad_buffer(w1)
             C_.conv1_wgrad(dy1, x, wpart1, dw1, g1grid)
             gw1 = _deliver(w1, dw1, ip1)
-        gg1, gb1, gbias1 = emit_grad(g1, dg1), emit_grad(be1, db1), _zero_grad_of(b1)
+        gg1, gb1, gbias1 = _deliver(g1, dg1, ipg1), _deliver(be1, db1, ipb1), _zero_grad_of(b1)
         return None, gw1, gbias1, gg1, gb1, gw2, gbias2, gg2, gb2, None
 
 

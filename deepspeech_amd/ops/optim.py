@@ -68,6 +68,7 @@ class ParamArena:
         self._index = {}
         self._ready_cbs = []
         self._written = set()
+        self._known_zero = set()
         for i, (p, (o, n)) in enumerate(zip(self.params, self.offsets)):
             self.flat[o:o + n].copy_(p.data.reshape(-1).float())
             p.data = self.flat[o:o + n].view_as(p)
@@ -125,6 +126,14 @@ class ParamArena:
             if id(p) not in self._written:
                 self.grad[o:o + n].zero_()
 
+    def known_zero(self, p) -> bool:
+        """True if ``p``'s gradient slice holds zeros that no op has overwritten since
+        :meth:`set_known_zero` (a structurally-zero gradient needs no per-step memset)."""
+        return id(p) in self._known_zero
+
+    def set_known_zero(self, p) -> None:
+        self._known_zero.add(id(p))
+
     def first_write(self, p) -> bool:
         """True if ``p``'s gradient has not been written yet this step (fused ops then
         overwrite instead of accumulate)."""
@@ -136,6 +145,7 @@ class ParamArena:
             if p is None:
                 continue
             self._written.add(id(p))
+            self._known_zero.discard(id(p))
             i = self._index[id(p)]
             for cb in self._ready_cbs:
                 cb(i)
