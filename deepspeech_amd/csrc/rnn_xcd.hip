@@ -872,13 +872,13 @@ __device__ __forceinline__ bool granule_tagged(i32x4 v, unsigned tag) {
 }
 __device__ __forceinline__ float canon32(float f) { return (f != f) ? __uint_as_float(0x7fc00000u) : f; }
 
-template <int CELL, int MTU>
+template <int CELL, int MTU, int GPT>
 __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
   constexpr int ROWS = 16;
   constexpr int EPT = ROWS * UPW / ETH;
   constexpr int OPL = ROWS * UPW / 64;            // elements per memory-wave lane
-  constexpr int GPT = 4;                          // producers per gather thread (7 x 4 >= P)
+  // GPT: producers per gather thread (7 x GPT >= P)
   constexpr int DGP = G * UPW + 8;                // dgh tile pitch (bf16)
   __shared__ float red_s[MW][ROWS][UPW + 1];
   __shared__ __attribute__((aligned(16))) bf16_t dg_s[ROWS][DGP];
@@ -1245,7 +1245,7 @@ static int launch_fwd(const XFwd& a, int kb, int grid, size_t smem, hipStream_t 
   case K:                                                                                     \
     hipLaunchKernelGGL((rnnx_fwd_kernel<CELL, MT, K>), dim3(grid), dim3(NTH), smem, st, a); \
     break;
-    DS2_CASE(1) DS2_CASE(2) DS2_CASE(3) DS2_CASE(4) DS2_CASE(5)
+    DS2_CASE(1) DS2_CASE(2) DS2_CASE(3) DS2_CASE(4) DS2_CASE(5) DS2_CASE(6)
 #undef DS2_CASE
     default: return -31;
   }
@@ -1307,7 +1307,7 @@ int ds2_rnnx_grid(int H, int ngroups, int xcd_map) {
 int ds2_rnnx_kb(int H, int G, int fwd) {
   if (fwd) {
     const int need = (H / 32 + MW - 1) / MW;
-    return need <= 5 ? need : -1;
+    return need <= 6 ? need : -1;
   }
   const int need = (G * H / 32 + MW - 1) / MW;            // backward: K split over the 7 workers
   for (int k : {2, 4, 6, 8, 11}) if (k >= need) return k;
@@ -1348,7 +1348,8 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
       case 2: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 2>, smem); break;                     \
       case 3: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 3>, smem); break;                     \
       case 4: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 4>, smem); break;                     \
-      default: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 5>, smem); break;                    \
+      case 5: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 5>, smem); break;                     \
+      default: rc = set_smem_attr(rnnx_fwd_kernel<C, M, 6>, smem); break;                    \
     }                                                                                        \
     if (rc) return rc;                                                                       \
     return launch_fwd<C, M>(a, kb, grid, smem, st);                                          \
@@ -1402,7 +1403,7 @@ int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st) {
   if (d->H % UPW != 0 || d->R < 1 || d->R > 16 || d->NP != d->BG * d->R || d->mt != 1) return -30;
   if (d->ring[0] == nullptr || (d->ndir == 2 && d->ring[1] == nullptr)) return -34;
   const int P = d->H / UPW;
-  if (P > 4 * MW) return -35;                       // GPT = 4 producers per gather thread
+  if (P > 6 * MW) return -35;                       // at most GPT = 6 producers per gather thread
   const int mtu_need = (d->H / 16 + MW - 1) / MW;
   XBwdRS a;
   a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = P; a.BG = d->BG; a.R = d->R;
@@ -1418,13 +1419,14 @@ int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st) {
   a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->steps <= 0) return 0;
   const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
-#define DS2_RS(C, M) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M>), dim3(grid), dim3(NTH), 0, st, a)
-#define DS2_RS_CELL(C)                          \
-  if (mtu_need <= 2) DS2_RS(C, 2);              \
-  else if (mtu_need <= 4) DS2_RS(C, 4);         \
-  else if (mtu_need <= 6) DS2_RS(C, 6);         \
-  else if (mtu_need <= 8) DS2_RS(C, 8);         \
-  else if (mtu_need <= 10) DS2_RS(C, 10);       \
+#define DS2_RS(C, M, GP) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP>), dim3(grid), dim3(NTH), 0, st, a)
+#define DS2_RS_CELL(C)                                  \
+  if (mtu_need <= 2) DS2_RS(C, 2, 4);                   \
+  else if (mtu_need <= 4) DS2_RS(C, 4, 4);              \
+  else if (mtu_need <= 6) DS2_RS(C, 6, 4);              \
+  else if (mtu_need <= 8) DS2_RS(C, 8, 4);              \
+  else if (mtu_need <= 10 && P <= 4 * MW) DS2_RS(C, 10, 4); \
+  else if (mtu_need <= 12) DS2_RS(C, 12, 6);            \
   else return -36;
   if (d->cell == CELL_GRU) { DS2_RS_CELL(CELL_GRU) } else { DS2_RS_CELL(CELL_RELU) }
 #undef DS2_RS_CELL

@@ -68,17 +68,28 @@ def _xcd_kb(H: int, G: int, fwd: bool) -> int:
     """k-steps per MFMA wave of csrc/rnn_xcd.hip (K split over the 7 worker waves; the
     8th is the memory wave). -1 if the tile would not fit."""
     need = -(-((H if fwd else G * H) // 32) // 7)
-    opts = (1, 2, 3, 4, 5) if fwd else (2, 4, 6, 8, 11)
+    opts = (1, 2, 3, 4, 5, 6) if fwd else (2, 4, 6, 8, 11)
     for k in opts:
         if k >= need:
             return k
     return -1
 
 
+def _rs_ok(H: int) -> bool:
+    """The reduce-scatter BPTT (generation 3) serves P = H/32 <= 42 workgroups per group."""
+    return BWD_EXCHANGE == "rs" and H // 32 <= 42
+
+
 def _xcd_lds(H: int, G: int, mt: int) -> int:
     """Static LDS bytes of the larger of the two csrc/rnn_xcd.hip kernels (16-row tiles only)."""
-    if mt != 1 or _xcd_kb(H, G, True) < 0 or _xcd_kb(H, G, False) < 0:
+    if mt != 1 or _xcd_kb(H, G, True) < 0:
         return 1 << 30
+    if _xcd_kb(H, G, False) < 0:
+        # no gather-BPTT tile: only the forward + reduce-scatter BPTT (static ~61 KB) run
+        if not _rs_ok(H):
+            return 1 << 30
+        return 2 * 7 * 16 * (G * 32 + 1) * 4 + 16 * 32 * 2 + 2 * 16 * G * 32 * 4 + 2 * 2 * 16 * 32 * 4 \
+            + (2 * 16 * 32 * 16 if G == 3 else 16) + 16 * 4 + G * 32 * 4 + 64
     rows, gru = 16, G == 3
     fwd = (2 * 7 * rows * (G * 32 + 1) * 4 + rows * 32 * 2 + 2 * rows * G * 32 * 4 + 2 * 2 * rows * 32 * 4
            + (2 * rows * 32 * 16 if gru else 16) + rows * 4 + G * 32 * 4 + 64)
@@ -92,7 +103,7 @@ def make_xcd_plan(N: int, H: int, cell: str, ndir: int, cus: int) -> Optional[Rn
     """Generation-2 geometry: groups of R batch rows x all H units (H/32 workgroups of 32
     units). Prefer the most groups that still fit the chip (smaller per-step gathers), at
     most 8 so a group can live on one XCD; rows per group R <= 32."""
-    if H % 32 != 0 or H // 32 > 32:       # larger H: the resident U slice would spill
+    if H % 32 != 0 or H // 32 > (42 if _rs_ok(H) else 32):   # larger H: the resident U slice would spill
         return None
     G = GATES[cell]
     P = H // 32
@@ -297,7 +308,7 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
         if parts is not None:
             regions.append(parts)
             pats.append(0)
-        if BWD_EXCHANGE == "rs" and H // 32 <= 28:
+        if _rs_ok(H):
             # generation-3 BPTT: reduce-scatter of fp32 partials through a 3-slot ring
             # (readiness = per-use tag in each word's LSB, ring filled with 0xFFFFFFFF); dgh is a plain output
             rf = int(C.rnnx_ring_floats(H, plan.BG, plan.R))

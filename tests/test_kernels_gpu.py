@@ -99,7 +99,7 @@ def test_birnn_xcd_geometries(cuda, N, H):
 
 
 @pytest.mark.parametrize("exchange", ["rs", "gather"])
-@pytest.mark.parametrize("cell,N,H", [("gru", 32, 800), ("rnn_relu", 32, 800), ("gru", 40, 256), ("gru", 7, 96)])
+@pytest.mark.parametrize("cell,N,H", [("gru", 32, 800), ("rnn_relu", 32, 800), ("gru", 40, 256), ("gru", 7, 96), ("gru", 32, 1280)])
 def test_bptt_exchanges(cuda, exchange, cell, N, H):
     # generation-3 reduce-scatter BPTT and generation-2 all-gather BPTT against the reference
     from deepspeech_amd.ops import rnn as RNN
