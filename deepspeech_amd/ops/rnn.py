@@ -76,7 +76,11 @@ def _xcd_kb(H: int, G: int, fwd: bool) -> int:
 
 
 def _rs_ok(H: int) -> bool:
-    """The reduce-scatter BPTT (generation 3) serves P = H/32 <= 42 workgroups per group."""
+    """The reduce-scatter BPTT (generation 3) serves P = H/32 <= 42 workgroups per group.
+    Groups wider than one XCD (P > 32) exchange write-through across XCDs; measured on
+    MI355X that still beats the generation-1 kernels for the 3-gate GRU (H=1280: fwd 1.52 vs
+    1.93, BPTT 2.05 vs 3.68 ms per layer) but not for the one-gate clipped ReLU (H=1760 with
+    8-producer gathers: 1.84 / 2.35 vs 1.26 / 1.41), which make_xcd_plan leaves on gen 1."""
     return BWD_EXCHANGE == "rs" and H // 32 <= 42
 
 
@@ -103,12 +107,16 @@ def make_xcd_plan(N: int, H: int, cell: str, ndir: int, cus: int) -> Optional[Rn
     """Generation-2 geometry: groups of R batch rows x all H units (H/32 workgroups of 32
     units). Prefer the most groups that still fit the chip (smaller per-step gathers), at
     most 8 so a group can live on one XCD; rows per group R <= 32."""
-    if H % 32 != 0 or H // 32 > (42 if _rs_ok(H) else 32):   # larger H: the resident U slice would spill
-        return None
     G = GATES[cell]
+    wide = 42 if (_rs_ok(H) and G == 3) else 32         # see _rs_ok
+    if H % 32 != 0 or H // 32 > wide:   # larger H: the resident U slice would spill
+        return None
     P = H // 32
     best = None
-    for R in range(max(1, int(os.environ.get("DS2_RNNX_MINR", "1"))), 33):
+    # groups wider than an XCD (P > CUs/8) exchange across XCDs (write-through): fewer,
+    # taller groups measured faster there (H=1280: R=16 27.9 vs R=11 30.3 ms/step)
+    minr = int(os.environ.get("DS2_RNNX_MINR", "0")) or (min(16, N) if P > cus // 8 else 1)
+    for R in range(max(1, minr), 33):
         BG = -(-N // R)
         ngroups = ndir * BG
         if ngroups * P > cus:

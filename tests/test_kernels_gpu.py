@@ -65,10 +65,13 @@ def _rnn_case(cuda, cell, N, H, T, ndir, mode, seed=0, din=None, kernel="xcd"):
                      U_r[1] if ndir == 2 else None, b_r[0], b_r[1] if ndir == 2 else None,
                      lens.to(cuda), mm_dtype=torch.bfloat16)
     yr.backward(dy.float())
+    # wide clipped-ReLU layers: bf16 state exchange flips near-zero ReLU masks against the
+    # reference; both kernel generations sit at ~3 % there (measured: v1 3.2 %, xcd 3.1 %)
+    gtol = 5e-2 if (cell == "rnn_relu" and H > 1024) else 3e-2
     assert _rel(y, yr) < 2e-2, ("y", _rel(y, yr))
-    assert _rel(gx_h.grad, gx_r.grad) < 3e-2, ("dgx", _rel(gx_h.grad, gx_r.grad))
+    assert _rel(gx_h.grad, gx_r.grad) < gtol, ("dgx", _rel(gx_h.grad, gx_r.grad))
     for d in range(ndir):
-        assert _rel(U_h[d].grad, U_r[d].grad) < 3e-2, ("dU", d, _rel(U_h[d].grad, U_r[d].grad))
+        assert _rel(U_h[d].grad, U_r[d].grad) < gtol, ("dU", d, _rel(U_h[d].grad, U_r[d].grad))
         if cell == "gru":
             assert _rel(b_h[d].grad, b_r[d].grad) < 3e-2, ("dbh", d)
     # padding positions must be exactly zero
@@ -99,7 +102,7 @@ def test_birnn_xcd_geometries(cuda, N, H):
 
 
 @pytest.mark.parametrize("exchange", ["rs", "gather"])
-@pytest.mark.parametrize("cell,N,H", [("gru", 32, 800), ("rnn_relu", 32, 800), ("gru", 40, 256), ("gru", 7, 96), ("gru", 32, 1280)])
+@pytest.mark.parametrize("cell,N,H", [("gru", 32, 800), ("rnn_relu", 32, 800), ("gru", 40, 256), ("gru", 7, 96), ("gru", 32, 1280), ("rnn_relu", 32, 1760)])
 def test_bptt_exchanges(cuda, exchange, cell, N, H):
     # generation-3 reduce-scatter BPTT and generation-2 all-gather BPTT against the reference
     from deepspeech_amd.ops import rnn as RNN
