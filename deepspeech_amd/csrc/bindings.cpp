@@ -95,6 +95,9 @@ int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void*
 int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
+int ds2_fp8_quant_blocks(long long na, long long nb_el);
+int ds2_fp8_quant2(const void* a, long long na, const void* b, long long nb_el, float alpha, void* a8, void* b8,
+                   float* part, float* scales, hipStream_t st);
 int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                    hipStream_t st);
 int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
@@ -574,6 +577,32 @@ void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
   check(ds2_multi_fill((int)ts.size(), ptrs, bytes, pats, cur_stream()), "multi_fill");
 }
 
+// --------------------------------------------------------------------------- fp8 quantisation
+int64_t fp8_quant_blocks(int64_t na, int64_t nb) { return ds2_fp8_quant_blocks(na, nb); }
+
+// per-tensor e4m3fn quantisation of two bf16 operands; scales[0] = amax_a/448,
+// scales[1] = amax_b/448 * alpha (device-side, for the scaled GEMM)
+void fp8_quant2(at::Tensor a, at::Tensor b, double alpha, at::Tensor a8, at::Tensor b8, at::Tensor part,
+                at::Tensor scales) {
+  need_gpu(a, "a");
+  need_gpu(b, "b");
+  need_gpu(a8, "a8");
+  need_gpu(b8, "b8");
+  need_gpu(part, "part");
+  need_gpu(scales, "scales");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "bf16 operands expected");
+  TORCH_CHECK(a8.scalar_type() == at::kFloat8_e4m3fn && b8.scalar_type() == at::kFloat8_e4m3fn, "e4m3fn outputs");
+  TORCH_CHECK(a8.numel() == a.numel() && b8.numel() == b.numel(), "size mismatch");
+  TORCH_CHECK(scales.scalar_type() == at::kFloat && scales.numel() >= 2, "scales: 2 floats");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0,
+              "16-B aligned operands expected");
+  const int nb = ds2_fp8_quant_blocks(a.numel(), b.numel());
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= 2 * nb, "part: 2*blocks floats");
+  check(ds2_fp8_quant2(a.data_ptr(), a.numel(), b.data_ptr(), b.numel(), (float)alpha, a8.data_ptr(), b8.data_ptr(),
+                       part.data_ptr<float>(), scales.data_ptr<float>(), cur_stream()),
+        "fp8_quant2");
+}
+
 // --------------------------------------------------------------------------- device info
 py::dict device_info(int64_t dev) {
   hipDeviceProp_t prop;
@@ -632,6 +661,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm", &grad_norm);
   m.def("cast_bf16", &cast_bf16);
   m.def("device_info", &device_info);
+  m.def("fp8_quant_blocks", &fp8_quant_blocks);
+  m.def("fp8_quant2", &fp8_quant2);
   m.def("multi_fill", &multi_fill);
   m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),
         py::arg("blank"), py::arg("score") = py::none());

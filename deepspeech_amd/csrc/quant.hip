@@ -1,0 +1,126 @@
+// Per-tensor fp8 (OCP e4m3fn) quantisation of the two operands of a projection GEMM
+// (BASELINE config 5, `--fp8`): amax -> scale = amax / 448 -> saturating cast, for the input
+// activations AND the weights in two launches, scales left on the device for
+// hipBLASLt's scaled GEMM (no host sync).
+//
+// The torch-level version (abs, amax, divide, clamp, float round trip, cast, for each
+// operand) was ~10 launches and ~0.9 ms per config-5 step (profiles/r1_s3_config5_fp8.md),
+// more than the fp8 GEMMs saved.
+//   1. amax2_kernel   blocks [0, nb) sweep operand a, [nb, 2nb) operand b (16-B loads),
+//                     one partial max per block (no zero-initialised accumulator needed);
+//   2. quant2_kernel  every block first reduces the partials of its operand (<= 1024
+//                     floats, L2-resident), then casts its slice; block 0 publishes
+//                     scales = {amax_a / 448, amax_b / 448 * alpha}.
+#include <hip/hip_fp8.h>
+
+#include "common.h"
+
+using namespace ds2;
+
+namespace {
+
+constexpr float FP8_MAX = 448.0f;
+constexpr int QT = 256;             // threads per block
+
+__device__ __forceinline__ float block_max(float v, float* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  float r = sh[0];
+#pragma unroll
+  for (int i = 1; i < QT / 64; ++i) r = fmaxf(r, sh[i]);
+  return r;
+}
+
+__global__ __launch_bounds__(QT) void amax2_kernel(const bf16_t* __restrict__ a, long long na,
+                                                   const bf16_t* __restrict__ b, long long nb_el, int nb,
+                                                   float* __restrict__ part) {
+  __shared__ float sh[QT / 64];
+  const bool second = blockIdx.x >= (unsigned)nb;
+  const bf16_t* x = second ? b : a;
+  const long long n = second ? nb_el : na;
+  const int blk = second ? blockIdx.x - nb : blockIdx.x;
+  float m = 0.f;
+  const long long n8 = n / 8;
+  for (long long i = (long long)blk * QT + threadIdx.x; i < n8; i += (long long)nb * QT) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f((bf16_t)v[j])));
+  }
+  for (long long i = n8 * 8 + (long long)blk * QT + threadIdx.x; i < n; i += (long long)nb * QT)
+    m = fmaxf(m, fabsf(bf2f(x[i])));
+  m = block_max(m, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = m;
+}
+
+__device__ __forceinline__ unsigned char to_e4m3(float f) {
+  const __hip_fp8_e4m3 q(fminf(fmaxf(f, -FP8_MAX), FP8_MAX));
+  return *reinterpret_cast<const unsigned char*>(&q);
+}
+
+__global__ __launch_bounds__(QT) void quant2_kernel(const bf16_t* __restrict__ a, long long na,
+                                                    const bf16_t* __restrict__ b, long long nb_el, int nb,
+                                                    const float* __restrict__ part, float alpha,
+                                                    unsigned char* __restrict__ a8, unsigned char* __restrict__ b8,
+                                                    float* __restrict__ scales) {
+  __shared__ float sh[QT / 64];
+  const bool second = blockIdx.x >= (unsigned)nb;
+  // amax of this block's operand from the partials (and of the other for block 0's scales)
+  float ma = 0.f, mb = 0.f;
+  for (int i = threadIdx.x; i < nb; i += QT) {
+    ma = fmaxf(ma, part[i]);
+    mb = fmaxf(mb, part[nb + i]);
+  }
+  ma = block_max(ma, sh);
+  mb = block_max(mb, sh);
+  const float sa = fmaxf(ma / FP8_MAX, 1e-12f), sb = fmaxf(mb / FP8_MAX, 1e-12f);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    scales[0] = sa;
+    scales[1] = sb * alpha;
+  }
+  const bf16_t* x = second ? b : a;
+  unsigned char* y = second ? b8 : a8;
+  const long long n = second ? nb_el : na;
+  const float inv = 1.f / (second ? sb : sa);
+  const int blk = second ? blockIdx.x - nb : blockIdx.x;
+  const long long n8 = n / 8;
+  for (long long i = (long long)blk * QT + threadIdx.x; i < n8; i += (long long)nb * QT) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
+    unsigned lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lo |= (unsigned)to_e4m3(bf2f((bf16_t)v[j]) * inv) << (8 * j);
+      hi |= (unsigned)to_e4m3(bf2f((bf16_t)v[4 + j]) * inv) << (8 * j);
+    }
+    *reinterpret_cast<uint2*>(y + i * 8) = make_uint2(lo, hi);
+  }
+  for (long long i = n8 * 8 + (long long)blk * QT + threadIdx.x; i < n; i += (long long)nb * QT)
+    y[i] = to_e4m3(bf2f(x[i]) * inv);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ds2_fp8_quant_blocks(long long na, long long nb_el) {
+  const long long m = na > nb_el ? na : nb_el;
+  long long nb = (m / 8 + QT - 1) / QT;
+  if (nb > 1024) nb = 1024;
+  return (int)(nb < 1 ? 1 : nb);
+}
+
+// a, b: bf16 (16-B aligned); a8, b8: fp8 e4m3fn outputs; part: 2*nb floats; scales: 2 floats
+int ds2_fp8_quant2(const void* a, long long na, const void* b, long long nb_el, float alpha, void* a8, void* b8,
+                   float* part, float* scales, hipStream_t st) {
+  const int nb = ds2_fp8_quant_blocks(na, nb_el);
+  hipLaunchKernelGGL(amax2_kernel, dim3(2 * nb), dim3(QT), 0, st, (const bf16_t*)a, na, (const bf16_t*)b, nb_el, nb,
+                     part);
+  hipLaunchKernelGGL(quant2_kernel, dim3(2 * nb), dim3(QT), 0, st, (const bf16_t*)a, na, (const bf16_t*)b, nb_el, nb,
+                     (const float*)part, alpha, (unsigned char*)a8, (unsigned char*)b8, scales);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -416,6 +416,18 @@ def fp8_linear(x2: torch.Tensor, W16: torch.Tensor, b16: torch.Tensor, alpha: fl
         # hipBLASLt fp8 GEMMs need K and N multiples of 16: such layers stay bf16
         return torch.addmm(b16, x2, W16.t(), alpha=alpha)
     f8 = torch.float8_e4m3fn
+    if x2.is_cuda:
+        # csrc/quant.hip: amax + scale + saturating cast of both operands in two launches
+        C = _ext.ext()
+        x2 = x2.contiguous()
+        W16 = W16.contiguous()
+        x8 = torch.empty(x2.shape, device=x2.device, dtype=f8)
+        w8 = torch.empty(W16.shape, device=x2.device, dtype=f8)
+        nb = int(C.fp8_quant_blocks(x2.numel(), W16.numel()))
+        ws = torch.empty(2 * nb + 2, device=x2.device, dtype=torch.float32)
+        C.fp8_quant2(x2, W16, float(alpha), x8, w8, ws[:2 * nb], ws[2 * nb:])
+        return torch._scaled_mm(x8, w8.t(), scale_a=ws[2 * nb], scale_b=ws[2 * nb + 1], bias=b16,
+                                out_dtype=torch.bfloat16)
     sx = (x2.abs().amax().float() / FP8_MAX).clamp(min=1e-12)
     sw = (W16.abs().amax().float() / FP8_MAX).clamp(min=1e-12)
     x8 = (x2.float() / sx).clamp(-FP8_MAX, FP8_MAX).to(f8)

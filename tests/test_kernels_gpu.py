@@ -273,3 +273,30 @@ def test_ctc_greedy_kernel(cuda, dtype, T):
     assert got == want
     ref_score = torch.stack([lp[: int(lens[n]), n].max(-1).values.sum() for n in range(N)])
     assert torch.allclose(score, ref_score, atol=1e-2, rtol=1e-4)
+
+
+# --------------------------------------------------------------------------- fp8 quantisation
+def test_fp8_quant2_matches_torch(cuda):
+    """csrc/quant.hip per-tensor e4m3fn quantisation == the torch formulation (amax/448
+    scale, saturating cast); x * (1/s) vs x / s may round a handful of values one fp8 step
+    apart."""
+    from deepspeech_amd.ops import _ext
+    C = _ext.ext()
+    torch.manual_seed(0)
+    a = (torch.randn(1000, 136) * 3).bfloat16().to(cuda)
+    b = (torch.randn(512, 136) * 0.02).bfloat16().to(cuda)
+    b[3, 7] = 5.0                                   # an outlier sets b's scale
+    f8 = torch.float8_e4m3fn
+    a8 = torch.empty(a.shape, device=cuda, dtype=f8)
+    b8 = torch.empty(b.shape, device=cuda, dtype=f8)
+    nb = int(C.fp8_quant_blocks(a.numel(), b.numel()))
+    ws = torch.empty(2 * nb + 2, device=cuda, dtype=torch.float32)
+    C.fp8_quant2(a, b, 0.5, a8, b8, ws[:2 * nb], ws[2 * nb:])
+    for x, x8, s_got, mul in ((a, a8, ws[2 * nb], 1.0), (b, b8, ws[2 * nb + 1], 0.5)):
+        s = (x.float().abs().amax() / 448.0).clamp(min=1e-12)
+        assert abs(float(s_got) - float(s) * mul) <= 1e-6 * float(s) * mul
+        ref = (x.float() / s).clamp(-448, 448).to(f8).float()
+        got = x8.float()
+        bad = (got != ref)
+        assert bad.float().mean().item() < 1e-3
+        assert ((got - ref).abs()[bad] <= ref.abs()[bad] * 0.125 + 1e-6).all()
