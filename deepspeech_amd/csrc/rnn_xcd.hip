@@ -1154,7 +1154,8 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
                              (int)((__float_as_uint(canon32(acc[2])) & ~1u) | tg),
                              (int)((__float_as_uint(canon32(acc[3])) & ~1u) | tg)};
             const unsigned off = ring_off(ws, mem, mt, lane & 15, 4 * (lane >> 4));
-            if (plain) store_b128(rs_ring, off, v);
+            if (a.knobs & 32) {                          // knob 32 (timing only, with 4): no publish stores
+            } else if (plain) store_b128(rs_ring, off, v);
             else store_sc1_b128(rs_ring, off, v);
           }
         };
