@@ -82,6 +82,10 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip")))
     hip_srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
     common = ["-O3", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-I" + CSRC]
+    if os.environ.get("DS2_DEBUG", "0") == "1":
+        # device-side DS2_DCHECKs (csrc/common.h) print failing conditions; objects are keyed
+        # by their flags, so debug and release objects coexist in build/
+        common += ["-DDS2_DEBUG=1", "-g"]
     hip_flags = [HIPCC, "--offload-arch=" + ARCH, "-fno-gpu-rdc", "-munsafe-fp-atomics"] + common
     torch_defs = ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1",
                   "-D_GLIBCXX_USE_CXX11_ABI=%d" % abi]

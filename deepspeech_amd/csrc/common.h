@@ -40,6 +40,22 @@ __device__ __forceinline__ void store_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigne
                                          r, off, 0, AUX_SC1);
 }
 
+// Device-side checks of the debug build (DS2_DEBUG=1 python build.py): print the failing
+// condition with its block/thread and carry on. Deliberately no trap: on the shared MI355X
+// pool a faulting kernel can reset every GPU of the node, so a debug build reports instead.
+#ifdef DS2_DEBUG
+#define DS2_DCHECK(cond)                                                                      \
+  do {                                                                                        \
+    if (!(cond))                                                                              \
+      printf("DS2_DCHECK failed %s:%d block %d thread %d: %s\n", __FILE__, __LINE__,          \
+             (int)blockIdx.x, (int)threadIdx.x, #cond);                                       \
+  } while (0)
+#else
+#define DS2_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 // plain (L2 write-back) store through the same resource: the base stays in the resource's
 // SGPRs (a pointer store made the compiler re-load the base from the kernel arguments, an
 // s_load + lgkmcnt(0) wait per store inside the latency-critical publish loops)

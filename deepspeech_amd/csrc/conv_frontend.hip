@@ -146,6 +146,7 @@ __device__ __forceinline__ void kspan(int w, int nw, int total, int& s0, int& n)
 
 __global__ __launch_bounds__(512) void conv2_fwd_kernel(Conv2Fwd a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  DS2_DCHECK(a.T2 == (a.T1 - C2_KT) / 2 + 1 && a.F2 == a.F1 - 4 && a.F1 <= 80);
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
   const int hi = lane >> 5, col = lane & 31;
   unsigned char* const buf = smem;                                   // [10*F1][80 B]

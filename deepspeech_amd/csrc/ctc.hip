@@ -91,6 +91,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
   for (int j = 0; j < SPL; ++j) {
     const int s = s0 + j;
     cls[j] = (s < SP) ? state_class(labels, b, Lmax, s, blank) : blank;
+    DS2_DCHECK(cls[j] >= 0 && cls[j] < KPAD);      // label ids index the 32-wide lp rows
     bool ok = false;
     if (s < SP && cls[j] != blank) {
       if (!beta) ok = s >= 2 && cls[j] != state_class(labels, b, Lmax, s - 2, blank);

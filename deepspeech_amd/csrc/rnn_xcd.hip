@@ -250,6 +250,7 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
 
   int grp, mem;
   if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  DS2_DCHECK(grp < a.ngroups && mem < a.P && a.NP >= a.BG * a.R && a.R <= 16);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, KS = H / 32, N = a.N, NP = a.NP, R = a.R;
   const int bg = grp % a.BG, dir = grp / a.BG;
@@ -536,6 +537,7 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
 
   int grp, mem;
   if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  DS2_DCHECK(grp < a.ngroups && mem < a.P && a.NP >= a.BG * a.R && a.R <= 16);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, GH = G * H, KS = GH / 32, N = a.N, NP = a.NP, R = a.R;
   const int LP = KB * MW * 32 + 8;                // A pitch (K zero-padded to KB*7*32)
@@ -892,6 +894,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 
   int grp, mem;
   if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  DS2_DCHECK(grp < a.ngroups && mem < a.P && a.NP >= a.BG * a.R && a.R <= 16);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, GH = G * H, N = a.N, NP = a.NP, R = a.R, P = a.P, MTS = H / 16;
   const int bg = grp % a.BG, dir = grp / a.BG;

@@ -4,9 +4,13 @@
 // python-Levenshtein CER of src/deepSpeech_test.py:130. Adds a CTC prefix beam search
 // (BASELINE config 4: streaming uni-GRU + beam-search decoder) that can carry its beam
 // across streaming chunks.
+// The cores take raw pointers; the pybind11 wrappers are compiled out with DS2_NO_PYBIND
+// (tests/native/sanitize_driver.cpp builds the cores under ASan/UBSan and TSan).
+#ifndef DS2_NO_PYBIND
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 
 #include <algorithm>
 #include <atomic>
@@ -20,7 +24,9 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef DS2_NO_PYBIND
 namespace py = pybind11;
+#endif
 
 namespace ds2rt {
 
@@ -32,24 +38,30 @@ static inline float log_add(float a, float b) {
 }
 
 // ---------------------------------------------------------------- greedy
-std::vector<std::vector<int>> greedy_collapse(py::array_t<int, py::array::c_style | py::array::forcecast> best,
-                                              py::array_t<int, py::array::c_style | py::array::forcecast> lens,
-                                              int blank) {
-  auto b = best.unchecked<2>();   // [T, N]
-  auto l = lens.unchecked<1>();
-  const int T = (int)b.shape(0), N = (int)b.shape(1);
+// best [T, N] argmax classes (time-major), lens [N]
+std::vector<std::vector<int>> greedy_collapse_raw(const int* best, int T, int N, const int* lens, int blank) {
   std::vector<std::vector<int>> out(N);
   for (int n = 0; n < N; ++n) {
     int prev = -1;
-    const int L = std::min<int>(T, l(n));
+    const int L = std::max(0, std::min<int>(T, lens[n]));
     for (int t = 0; t < L; ++t) {
-      const int c = b(t, n);
+      const int c = best[(size_t)t * N + n];
       if (c != prev && c != blank) out[n].push_back(c);
       prev = c;
     }
   }
   return out;
 }
+
+#ifndef DS2_NO_PYBIND
+std::vector<std::vector<int>> greedy_collapse(py::array_t<int, py::array::c_style | py::array::forcecast> best,
+                                              py::array_t<int, py::array::c_style | py::array::forcecast> lens,
+                                              int blank) {
+  if (best.ndim() != 2 || lens.ndim() != 1 || lens.shape(0) != best.shape(1))
+    throw std::runtime_error("greedy_collapse: best [T, N], lens [N] expected");
+  return greedy_collapse_raw(best.data(), (int)best.shape(0), (int)best.shape(1), lens.data(), blank);
+}
+#endif
 
 // ---------------------------------------------------------------- edit distance
 template <typename Seq>
@@ -87,14 +99,16 @@ class PrefixBeamSearch {
     beams_.assign(1, Hyp{0, 0.f, -INFINITY});
   }
 
+#ifndef DS2_NO_PYBIND
   // log_probs: [T, K] log-softmax rows of ONE utterance (a streaming chunk or the whole thing)
   void feed(py::array_t<float, py::array::c_style | py::array::forcecast> log_probs) {
-    auto lp = log_probs.unchecked<2>();
-    const int T = (int)lp.shape(0), K = (int)lp.shape(1);
+    if (log_probs.ndim() != 2) throw std::runtime_error("PrefixBeamSearch.feed: [T, K] expected");
+    const int T = (int)log_probs.shape(0), K = (int)log_probs.shape(1);
     const float* data = log_probs.data();
     py::gil_scoped_release rel;
     feed_raw(data, T, K, K);
   }
+#endif
 
   // rows t at lp + t * stride (stride >= K: rows of a [T, B, K] tensor for one stream)
   void feed_raw(const float* lp, int T, int K, size_t stride) {
@@ -218,17 +232,12 @@ int default_threads() {
   return (int)std::max(1u, std::min(hc == 0 ? 1u : hc, 16u));
 }
 
-std::vector<std::vector<int>> beam_search_batch(py::array_t<float, py::array::c_style | py::array::forcecast> lp,
-                                                py::array_t<int, py::array::c_style | py::array::forcecast> lens,
-                                                int beam, int blank, float prune, int threads) {
-  auto a = lp.unchecked<3>();   // [T, N, K] time-major log-probs
-  auto l = lens.unchecked<1>();
-  const int T = (int)a.shape(0), N = (int)a.shape(1), K = (int)a.shape(2);
+// lp [T, N, K] time-major log-probs, lens [N]; utterances spread over worker threads
+std::vector<std::vector<int>> beam_search_batch_raw(const float* base, int T, int N, int K, const int* lens, int beam,
+                                                    int blank, float prune, int threads) {
   std::vector<int> L(N);
-  for (int n = 0; n < N; ++n) L[n] = std::min<int>(T, l(n));
-  const float* base = lp.data();
+  for (int n = 0; n < N; ++n) L[n] = std::max(0, std::min<int>(T, lens[n]));
   std::vector<std::vector<int>> out(N);
-  py::gil_scoped_release rel;
   parallel_for(N, threads > 0 ? threads : default_threads(), [&](int n) {
     PrefixBeamSearch bs(beam, blank, prune);
     bs.feed_raw(base + (size_t)n * K, L[n], K, (size_t)N * K);
@@ -236,6 +245,20 @@ std::vector<std::vector<int>> beam_search_batch(py::array_t<float, py::array::c_
   });
   return out;
 }
+
+#ifndef DS2_NO_PYBIND
+std::vector<std::vector<int>> beam_search_batch(py::array_t<float, py::array::c_style | py::array::forcecast> lp,
+                                                py::array_t<int, py::array::c_style | py::array::forcecast> lens,
+                                                int beam, int blank, float prune, int threads) {
+  if (lp.ndim() != 3 || lens.ndim() != 1 || lens.shape(0) != lp.shape(1))
+    throw std::runtime_error("beam_search_batch: log_probs [T, N, K], lens [N] expected");
+  const int T = (int)lp.shape(0), N = (int)lp.shape(1), K = (int)lp.shape(2);
+  const float* base = lp.data();
+  const int* l = lens.data();
+  py::gil_scoped_release rel;
+  return beam_search_batch_raw(base, T, N, K, l, beam, blank, prune, threads);
+}
+#endif
 
 // B independent streams decoded incrementally chunk by chunk (streaming inference): the
 // beams persist across feed() calls, streams are spread over worker threads.
@@ -249,18 +272,24 @@ class BatchBeamSearch {
     for (auto& b : s_) b.reset();
   }
   // log_probs [T, B, K]; lens [B] valid frames of this chunk per stream
-  void feed(py::array_t<float, py::array::c_style | py::array::forcecast> lp,
-            py::array_t<int, py::array::c_style | py::array::forcecast> lens) {
-    auto a = lp.unchecked<3>();
-    auto l = lens.unchecked<1>();
-    const int T = (int)a.shape(0), B = (int)a.shape(1), K = (int)a.shape(2);
+  void feed_raw(const float* base, int T, int B, int K, const int* lens) {
     if (B != (int)s_.size()) throw std::runtime_error("BatchBeamSearch.feed: stream count mismatch");
     std::vector<int> L(B);
-    for (int b = 0; b < B; ++b) L[b] = std::min<int>(T, l(b));
-    const float* base = lp.data();
-    py::gil_scoped_release rel;
+    for (int b = 0; b < B; ++b) L[b] = std::max(0, std::min<int>(T, lens[b]));
     parallel_for(B, threads_, [&](int b) { s_[b].feed_raw(base + (size_t)b * K, L[b], K, (size_t)B * K); });
   }
+#ifndef DS2_NO_PYBIND
+  void feed(py::array_t<float, py::array::c_style | py::array::forcecast> lp,
+            py::array_t<int, py::array::c_style | py::array::forcecast> lens) {
+    if (lp.ndim() != 3 || lens.ndim() != 1 || lens.shape(0) != lp.shape(1))
+      throw std::runtime_error("BatchBeamSearch.feed: log_probs [T, B, K], lens [B] expected");
+    const int T = (int)lp.shape(0), B = (int)lp.shape(1), K = (int)lp.shape(2);
+    const float* base = lp.data();
+    const int* l = lens.data();
+    py::gil_scoped_release rel;
+    feed_raw(base, T, B, K, l);
+  }
+#endif
   std::vector<std::vector<int>> best() const {
     std::vector<std::vector<int>> r;
     for (const auto& b : s_) r.push_back(b.best());
@@ -274,6 +303,7 @@ class BatchBeamSearch {
 
 }  // namespace ds2rt
 
+#ifndef DS2_NO_PYBIND
 void register_loader(py::module_& m);
 void register_tfrecord(py::module_& m);
 
@@ -299,3 +329,4 @@ PYBIND11_MODULE(_native, m) {
   register_loader(m);
   register_tfrecord(m);
 }
+#endif  // DS2_NO_PYBIND

@@ -18,9 +18,11 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#ifndef DS2_NO_PYBIND
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 
 #include <algorithm>
 #include <atomic>
@@ -36,7 +38,9 @@
 #include <thread>
 #include <vector>
 
+#ifndef DS2_NO_PYBIND
 namespace py = pybind11;
+#endif
 
 namespace ds2rt {
 
@@ -47,17 +51,14 @@ namespace ds2rt {
 // sorted=true: SortaGrad order (ascending length); else buckets shuffled with `seed`.
 // Distributed: batches are grouped in runs of `world` consecutive batches taken from the
 // same bucket, so every rank of a step sees the same length class (no stragglers).
-std::vector<std::vector<int64_t>> plan_batches(py::array_t<int, py::array::c_style | py::array::forcecast> lengths,
-                                               py::array_t<int, py::array::c_style | py::array::forcecast> min_frames,
-                                               int batch_size, int bucket, int max_frames, bool sorted, uint64_t seed,
-                                               int world, bool drop_last) {
-  auto L = lengths.unchecked<1>();
-  auto MF = min_frames.unchecked<1>();
-  const int64_t n = L.shape(0);
+std::vector<std::vector<int64_t>> plan_batches_raw(const int* L, const int* MF, int64_t n, int batch_size, int bucket,
+                                                   int max_frames, bool sorted, uint64_t seed, int world,
+                                                   bool drop_last) {
+  if (batch_size < 1 || bucket < 1 || world < 1) throw std::runtime_error("plan_batches: sizes must be >= 1");
   std::map<int, std::vector<int64_t>> buckets;
   for (int64_t i = 0; i < n; ++i) {
-    const int len = L(i);
-    if (len > max_frames || len < MF(i)) continue;
+    const int len = L[i];
+    if (len > max_frames || len < MF[i]) continue;
     buckets[len / bucket].push_back(i);
   }
   std::mt19937_64 rng(seed);
@@ -65,7 +66,7 @@ std::vector<std::vector<int64_t>> plan_batches(py::array_t<int, py::array::c_sty
   for (auto& kv : buckets) {
     auto& ids = kv.second;
     if (sorted) {
-      std::stable_sort(ids.begin(), ids.end(), [&](int64_t a, int64_t b) { return L(a) < L(b); });
+      std::stable_sort(ids.begin(), ids.end(), [&](int64_t a, int64_t b) { return L[a] < L[b]; });
     } else {
       std::shuffle(ids.begin(), ids.end(), rng);
     }
@@ -89,18 +90,37 @@ std::vector<std::vector<int64_t>> plan_batches(py::array_t<int, py::array::c_sty
   return out;
 }
 
+#ifndef DS2_NO_PYBIND
+std::vector<std::vector<int64_t>> plan_batches(py::array_t<int, py::array::c_style | py::array::forcecast> lengths,
+                                               py::array_t<int, py::array::c_style | py::array::forcecast> min_frames,
+                                               int batch_size, int bucket, int max_frames, bool sorted, uint64_t seed,
+                                               int world, bool drop_last) {
+  if (lengths.ndim() != 1 || min_frames.ndim() != 1 || lengths.shape(0) != min_frames.shape(0))
+    throw std::runtime_error("plan_batches: lengths and min_frames must be 1-D of equal size");
+  return plan_batches_raw(lengths.data(), min_frames.data(), lengths.shape(0), batch_size, bucket, max_frames, sorted,
+                          seed, world, drop_last);
+}
+#endif
+
 // ---------------------------------------------------------------- mmap store
 class FeatureStore {
  public:
   FeatureStore(const std::string& path, int freq) : freq_(freq) {
+    if (freq < 1) throw std::runtime_error("feature store: freq must be >= 1");
     fd_ = ::open(path.c_str(), O_RDONLY);
     if (fd_ < 0) throw std::runtime_error("cannot open feature store " + path);
     struct stat st;
-    if (fstat(fd_, &st) != 0) throw std::runtime_error("stat failed on " + path);
+    if (fstat(fd_, &st) != 0) {
+      ::close(fd_);                  // the destructor does not run when the constructor throws
+      throw std::runtime_error("stat failed on " + path);
+    }
     bytes_ = (size_t)st.st_size;
     if (bytes_ > 0) {
       base_ = ::mmap(nullptr, bytes_, PROT_READ, MAP_SHARED, fd_, 0);
-      if (base_ == MAP_FAILED) throw std::runtime_error("mmap failed on " + path);
+      if (base_ == MAP_FAILED) {
+        ::close(fd_);
+        throw std::runtime_error("mmap failed on " + path);
+      }
       ::madvise(base_, bytes_, MADV_WILLNEED);
     }
   }
@@ -129,22 +149,35 @@ struct Assembled {
 
 class BatchLoader {
  public:
-  BatchLoader(const std::string& feat_path, int freq, py::array_t<int64_t> offsets, py::array_t<int32_t> lengths,
-              py::array_t<int32_t> labels, py::array_t<int64_t> label_offsets, py::array_t<int32_t> label_lens,
+  BatchLoader(const std::string& feat_path, int freq, std::vector<int64_t> offsets, std::vector<int32_t> lengths,
+              std::vector<int32_t> labels, std::vector<int64_t> label_offsets, std::vector<int32_t> label_lens,
               int num_threads, int pad_to)
-      : store_(feat_path, freq), pad_to_(std::max(1, pad_to)) {
-    auto cp64 = [](py::array_t<int64_t>& a) { return std::vector<int64_t>(a.data(), a.data() + a.size()); };
-    auto cp32 = [](py::array_t<int32_t>& a) { return std::vector<int32_t>(a.data(), a.data() + a.size()); };
-    off_ = cp64(offsets);
-    len_ = cp32(lengths);
-    lab_ = cp32(labels);
-    loff_ = cp64(label_offsets);
-    llen_ = cp32(label_lens);
-    for (size_t i = 0; i < off_.size(); ++i)
-      if (off_[i] + len_[i] > store_.frames()) throw std::runtime_error("utterance outside the feature store");
+      : store_(feat_path, freq), pad_to_(std::max(1, pad_to)), off_(std::move(offsets)),
+        loff_(std::move(label_offsets)), len_(std::move(lengths)), lab_(std::move(labels)),
+        llen_(std::move(label_lens)) {
+    const size_t n = off_.size();
+    if (len_.size() != n || loff_.size() != n || llen_.size() != n)
+      throw std::runtime_error("BatchLoader: offsets/lengths/label_offsets/label_lens sizes differ");
+    for (size_t i = 0; i < n; ++i) {
+      if (off_[i] < 0 || len_[i] < 0 || off_[i] + len_[i] > store_.frames())
+        throw std::runtime_error("utterance outside the feature store");
+      if (loff_[i] < 0 || llen_[i] < 0 || loff_[i] + llen_[i] > (int64_t)lab_.size())
+        throw std::runtime_error("label slice outside the label array");
+    }
     const int nt = std::max(1, num_threads);
     for (int i = 0; i < nt; ++i) workers_.emplace_back([this] { work(); });
   }
+#ifndef DS2_NO_PYBIND
+  BatchLoader(const std::string& feat_path, int freq, py::array_t<int64_t> offsets, py::array_t<int32_t> lengths,
+              py::array_t<int32_t> labels, py::array_t<int64_t> label_offsets, py::array_t<int32_t> label_lens,
+              int num_threads, int pad_to)
+      : BatchLoader(feat_path, freq, cp(offsets), cp(lengths), cp(labels), cp(label_offsets), cp(label_lens),
+                    num_threads, pad_to) {}
+  template <typename T>
+  static std::vector<T> cp(py::array_t<T>& a) {
+    return std::vector<T>(a.data(), a.data() + a.size());
+  }
+#endif
   ~BatchLoader() { shutdown(); }
 
   void shutdown() {
@@ -173,18 +206,27 @@ class BatchLoader {
     return next_submit_ - next_take_;
   }
 
+  // blocks until the next batch in submission order is assembled
+  std::unique_ptr<Assembled> next_raw() {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (next_take_ >= next_submit_) throw std::runtime_error("BatchLoader.next(): nothing submitted");
+    cv_done_.wait(lk, [&] { return stop_ || done_.count(next_take_); });
+    if (stop_) throw std::runtime_error("loader stopped");
+    std::unique_ptr<Assembled> a = std::move(done_[next_take_]);
+    done_.erase(next_take_);
+    ++next_take_;
+    if (!error_.empty()) throw std::runtime_error(error_);
+    return a;
+  }
+
+  int freq() const { return store_.freq(); }
+
+#ifndef DS2_NO_PYBIND
   py::tuple next() {
     std::unique_ptr<Assembled> a;
     {
       py::gil_scoped_release rel;
-      std::unique_lock<std::mutex> lk(mu_);
-      if (next_take_ >= next_submit_) throw std::runtime_error("BatchLoader.next(): nothing submitted");
-      cv_done_.wait(lk, [&] { return stop_ || done_.count(next_take_); });
-      if (stop_) throw std::runtime_error("loader stopped");
-      a = std::move(done_[next_take_]);
-      done_.erase(next_take_);
-      ++next_take_;
-      if (!error_.empty()) throw std::runtime_error(error_);
+      a = next_raw();
     }
     Assembled* raw = a.release();
     py::capsule owner(raw, [](void* p) { delete reinterpret_cast<Assembled*>(p); });
@@ -195,6 +237,7 @@ class BatchLoader {
     py::array_t<int32_t> ll({raw->N}, raw->llen.data(), owner);
     return py::make_tuple(feats, seq, lab, ll);
   }
+#endif
 
  private:
   void work() {
@@ -249,7 +292,7 @@ class BatchLoader {
   FeatureStore store_;
   int pad_to_;
   std::vector<int64_t> off_, loff_;
-  std::vector<int32_t> len_, lab_, llen_;
+  std::vector<int32_t> len_, lab_, llen_;   // (declaration order = constructor init order)
   std::vector<std::thread> workers_;
   std::mutex mu_;
   std::condition_variable cv_jobs_, cv_done_;
@@ -262,6 +305,7 @@ class BatchLoader {
 
 }  // namespace ds2rt
 
+#ifndef DS2_NO_PYBIND
 void register_loader(py::module_& m) {
   m.def("plan_batches", &ds2rt::plan_batches, py::arg("lengths"), py::arg("min_frames"), py::arg("batch_size"),
         py::arg("bucket") = 100, py::arg("max_frames") = 1800, py::arg("sorted") = true, py::arg("seed") = 0,
@@ -276,3 +320,4 @@ void register_loader(py::module_& m) {
       .def("pending", &ds2rt::BatchLoader::pending)
       .def("shutdown", &ds2rt::BatchLoader::shutdown);
 }
+#endif  // DS2_NO_PYBIND

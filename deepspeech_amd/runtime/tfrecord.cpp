@@ -6,9 +6,13 @@
 // records so preprocessed reference data can be consumed (and produced) here.
 //
 // TFRecord: uint64 len | uint32 masked_crc32c(len) | data | uint32 masked_crc32c(data)
+// Cores are pybind-free (raw bytes / std containers); the wrappers are compiled out with
+// DS2_NO_PYBIND for the sanitizer driver (tests/native/sanitize_driver.cpp).
+#ifndef DS2_NO_PYBIND
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 
 #include <cstdint>
 #include <cstdio>
@@ -17,26 +21,27 @@
 #include <string>
 #include <vector>
 
+#ifndef DS2_NO_PYBIND
 namespace py = pybind11;
+#endif
 
 namespace ds2rt {
 
 // ---------------------------------------------------------------- crc32c (Castagnoli)
-static uint32_t crc_table[256];
-static bool crc_init = false;
-static void init_crc() {
-  if (crc_init) return;
-  for (uint32_t i = 0; i < 256; ++i) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? (0x82F63B78u ^ (c >> 1)) : (c >> 1);
-    crc_table[i] = c;
+struct CrcTable {
+  uint32_t t[256];
+  CrcTable() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? (0x82F63B78u ^ (c >> 1)) : (c >> 1);
+      t[i] = c;
+    }
   }
-  crc_init = true;
-}
+};
 uint32_t crc32c(const uint8_t* d, size_t n) {
-  init_crc();
+  static const CrcTable tab;      // thread-safe one-time init (was an unsynchronised flag)
   uint32_t c = 0xFFFFFFFFu;
-  for (size_t i = 0; i < n; ++i) c = crc_table[(c ^ d[i]) & 0xFF] ^ (c >> 8);
+  for (size_t i = 0; i < n; ++i) c = tab.t[(c ^ d[i]) & 0xFF] ^ (c >> 8);
   return c ^ 0xFFFFFFFFu;
 }
 uint32_t masked_crc(const uint8_t* d, size_t n) {
@@ -44,10 +49,10 @@ uint32_t masked_crc(const uint8_t* d, size_t n) {
   return ((c >> 15) | (c << 17)) + 0xa282ead8u;
 }
 
-std::vector<py::bytes> read_records(const std::string& path, bool check_crc) {
+std::vector<std::string> read_records_raw(const std::string& path, bool check_crc) {
   FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) throw std::runtime_error("cannot open " + path);
-  std::vector<py::bytes> out;
+  std::vector<std::string> out;
   std::vector<uint8_t> buf;
   while (true) {
     uint8_t hdr[12];
@@ -59,6 +64,7 @@ std::vector<py::bytes> read_records(const std::string& path, bool check_crc) {
     uint32_t lcrc;
     std::memcpy(&lcrc, hdr + 8, 4);
     if (check_crc && masked_crc(hdr, 8) != lcrc) { std::fclose(f); throw std::runtime_error("length crc mismatch"); }
+    if (len > (1ull << 34)) { std::fclose(f); throw std::runtime_error("implausible record length"); }
     buf.resize(len + 4);
     if (std::fread(buf.data(), 1, len + 4, f) != len + 4) { std::fclose(f); throw std::runtime_error("truncated record"); }
     uint32_t dcrc;
@@ -92,6 +98,9 @@ struct Reader {
   const uint8_t* p;
   const uint8_t* e;
   bool done() const { return p >= e; }
+  void need(size_t n) const {
+    if ((size_t)(e - p) < n) throw std::runtime_error("truncated field");
+  }
   uint64_t varint() {
     uint64_t v = 0;
     int s = 0;
@@ -105,16 +114,16 @@ struct Reader {
   }
   Reader sub() {
     const uint64_t n = varint();
-    if (p + n > e) throw std::runtime_error("bad length");
+    if (n > (uint64_t)(e - p)) throw std::runtime_error("bad length");
     Reader r{p, p + n};
     p += n;
     return r;
   }
   void skip(int wt) {
     if (wt == 0) varint();
-    else if (wt == 1) p += 8;
+    else if (wt == 1) { need(8); p += 8; }
     else if (wt == 2) sub();
-    else if (wt == 5) p += 4;
+    else if (wt == 5) { need(4); p += 4; }
     else throw std::runtime_error("unsupported wire type");
   }
 };
@@ -140,12 +149,12 @@ static Feature parse_feature(Reader r) {
         if (wt2 == 2) {   // packed
           Reader pk = lst.sub();
           if (field == 2) {
-            while (!pk.done()) { float v; std::memcpy(&v, pk.p, 4); pk.p += 4; ft.f.push_back(v); }
+            while (!pk.done()) { pk.need(4); float v; std::memcpy(&v, pk.p, 4); pk.p += 4; ft.f.push_back(v); }
           } else {
             while (!pk.done()) ft.i.push_back((int64_t)pk.varint());
           }
         } else if (wt2 == 5 && field == 2) {
-          float v; std::memcpy(&v, lst.p, 4); lst.p += 4; ft.f.push_back(v);
+          lst.need(4); float v; std::memcpy(&v, lst.p, 4); lst.p += 4; ft.f.push_back(v);
         } else if (wt2 == 0 && field == 3) {
           ft.i.push_back((int64_t)lst.varint());
         } else {
@@ -173,10 +182,16 @@ static std::pair<std::string, Reader> parse_entry(Reader r) {
   return {key, val};
 }
 
-// parse a SequenceExample: returns (seq_len, labels int32 [L], feats float32 [T, F])
-py::tuple parse_sequence_example(py::bytes data, const std::string& feats_key) {
-  std::string s = data;
-  Reader r{reinterpret_cast<const uint8_t*>(s.data()), reinterpret_cast<const uint8_t*>(s.data()) + s.size()};
+struct SeqExample {
+  int64_t seq_len = 0;
+  std::vector<int32_t> labels;
+  std::vector<float> feats;   // [T, F] row-major
+  int T = 0, F = 0;
+};
+
+// parse a SequenceExample: (seq_len, labels int32 [L], feats float32 [T, F])
+SeqExample parse_sequence_example_raw(const uint8_t* data, size_t size, const std::string& feats_key) {
+  Reader r{data, data + size};
   int64_t seq_len = -1;
   std::vector<int64_t> labels;
   std::vector<std::vector<float>> frames;
@@ -218,18 +233,17 @@ py::tuple parse_sequence_example(py::bytes data, const std::string& feats_key) {
       r.skip(wt);
     }
   }
-  const int T = (int)frames.size();
-  const int F = T ? (int)frames[0].size() : 0;
-  py::array_t<float> feats({T, F});
-  auto fm = feats.mutable_unchecked<2>();
-  for (int t = 0; t < T; ++t) {
-    if ((int)frames[t].size() != F) throw std::runtime_error("ragged frames");
-    for (int j = 0; j < F; ++j) fm(t, j) = frames[t][j];
+  SeqExample ex;
+  ex.T = (int)frames.size();
+  ex.F = ex.T ? (int)frames[0].size() : 0;
+  ex.feats.resize((size_t)ex.T * ex.F);
+  for (int t = 0; t < ex.T; ++t) {
+    if ((int)frames[t].size() != ex.F) throw std::runtime_error("ragged frames");
+    std::memcpy(ex.feats.data() + (size_t)t * ex.F, frames[t].data(), sizeof(float) * ex.F);
   }
-  py::array_t<int32_t> lab({(int)labels.size()});
-  auto lm = lab.mutable_unchecked<1>();
-  for (size_t i = 0; i < labels.size(); ++i) lm(i) = (int32_t)labels[i];
-  return py::make_tuple(seq_len < 0 ? T : seq_len, lab, feats);
+  ex.labels.assign(labels.begin(), labels.end());
+  ex.seq_len = seq_len < 0 ? ex.T : seq_len;
+  return ex;
 }
 
 // ---------------------------------------------------------------- writer
@@ -262,24 +276,48 @@ static std::string map_entry(const std::string& key, const std::string& val) {
   return e;
 }
 
-py::bytes make_sequence_example(int64_t seq_len, py::array_t<float, py::array::c_style | py::array::forcecast> feats,
-                                py::array_t<int64_t, py::array::c_style | py::array::forcecast> labels,
-                                const std::string& feats_key) {
-  auto fa = feats.unchecked<2>();
-  const int T = (int)fa.shape(0), F = (int)fa.shape(1);
-  std::vector<int64_t> lab(labels.data(), labels.data() + labels.size());
+std::string make_sequence_example_raw(int64_t seq_len, const float* feats, int T, int F, const int64_t* labels,
+                                      size_t L, const std::string& feats_key) {
+  std::vector<int64_t> lab(labels, labels + L);
   std::string ctx, fl, lst, out;
   put_bytes(ctx, 1, map_entry("seq_len", int64_feature({seq_len})));
   put_bytes(ctx, 1, map_entry("labels", int64_feature(lab)));
-  for (int t = 0; t < T; ++t) put_bytes(lst, 1, float_feature(feats.data() + (size_t)t * F, F));
+  for (int t = 0; t < T; ++t) put_bytes(lst, 1, float_feature(feats + (size_t)t * F, F));
   put_bytes(fl, 1, map_entry(feats_key, lst));
   put_bytes(out, 1, ctx);
   put_bytes(out, 2, fl);
-  return py::bytes(out);
+  return out;
 }
+
+#ifndef DS2_NO_PYBIND
+std::vector<py::bytes> read_records(const std::string& path, bool check_crc) {
+  std::vector<py::bytes> out;
+  for (auto& r : read_records_raw(path, check_crc)) out.emplace_back(r);
+  return out;
+}
+
+py::tuple parse_sequence_example(py::bytes data, const std::string& feats_key) {
+  std::string s = data;
+  SeqExample ex = parse_sequence_example_raw(reinterpret_cast<const uint8_t*>(s.data()), s.size(), feats_key);
+  py::array_t<float> feats({ex.T, ex.F});
+  if (!ex.feats.empty()) std::memcpy(feats.mutable_data(), ex.feats.data(), sizeof(float) * ex.feats.size());
+  py::array_t<int32_t> lab({(int)ex.labels.size()});
+  if (!ex.labels.empty()) std::memcpy(lab.mutable_data(), ex.labels.data(), sizeof(int32_t) * ex.labels.size());
+  return py::make_tuple(ex.seq_len, lab, feats);
+}
+
+py::bytes make_sequence_example(int64_t seq_len, py::array_t<float, py::array::c_style | py::array::forcecast> feats,
+                                py::array_t<int64_t, py::array::c_style | py::array::forcecast> labels,
+                                const std::string& feats_key) {
+  if (feats.ndim() != 2) throw std::runtime_error("make_sequence_example: feats [T, F] expected");
+  return py::bytes(make_sequence_example_raw(seq_len, feats.data(), (int)feats.shape(0), (int)feats.shape(1),
+                                             labels.data(), (size_t)labels.size(), feats_key));
+}
+#endif
 
 }  // namespace ds2rt
 
+#ifndef DS2_NO_PYBIND
 void register_tfrecord(py::module_& m) {
   m.def("crc32c", [](py::bytes b) {
     std::string s = b;
@@ -291,3 +329,4 @@ void register_tfrecord(py::module_& m) {
   m.def("make_sequence_example", &ds2rt::make_sequence_example, py::arg("seq_len"), py::arg("feats"),
         py::arg("labels"), py::arg("feats_key") = "feats");
 }
+#endif  // DS2_NO_PYBIND

@@ -136,3 +136,25 @@ def test_fp8_projection_close_to_bf16(cuda):
     for n, p in hip8.named_parameters():
         if n.startswith("rnn.1") or n.startswith("fc"):
             assert _rel(p.grad, g16[n].grad) < 0.25, n
+
+
+def test_step_is_bitwise_reproducible(cuda):
+    """Two trainers from the same initial state on the same batch produce bitwise-identical
+    losses, gradients and updated weights (every fused kernel reduces in a fixed order; the
+    side-stream weight-gradient GEMMs write disjoint arena slices). SURVEY.md 5.2's
+    'deterministic mode' is therefore the default on the HIP engine."""
+    from deepspeech_amd.trainer import Trainer, LRSchedule
+    torch.manual_seed(0)
+    base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
+    batch = to_device(FixedShapeBatches(8, max_frames=300, seed=3, pool=1).next(), cuda)
+    runs = []
+    for _ in range(2):
+        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
+        losses = [float(tr.step(batch)) for _ in range(3)]
+        torch.cuda.synchronize()
+        runs.append((losses, tr.arena.grad.clone(), tr.arena.flat.clone()))
+    (l0, g0, w0), (l1, g1, w1) = runs
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(g0, g1), (g0 - g1).abs().max()
+    assert torch.equal(w0, w1)
