@@ -554,8 +554,16 @@ class FusedBiLayer(torch.autograd.Function):
         gW = [None, None]
         grp = arena.group_view([W_f, W_b] if d1 else [W_f], "grad") if arena is not None else None
         if grp is not None and arena.first_write(W_f) and (not d1 or arena.first_write(W_b)):
-            mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
-            arena.grad_done(W_f, W_b if d1 else None)
+            def dw(grp=grp, dgx2=dgx2, x2=x2):
+                mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
+                arena.grad_done(W_f, W_b if d1 else None)
+            on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
+            if _defer_input_wgrad and on_side and ctx.idx > 0:
+                _deferred.append(dw)              # run after the last recurrent layer's BPTT
+            else:
+                dw()
+            if ctx.idx == 0:
+                flush_deferred_wgrads()
         else:
             for d, p in enumerate([W_f, W_b] if d1 else [W_f]):
                 g = mm_into(p, dgx2[:, d * GH:(d + 1) * GH].t(), x2)
@@ -602,8 +610,41 @@ def wgrad_stream(device: torch.device) -> Optional["torch.cuda.Stream"]:
     return s
 
 
+# Input-weight gradients (dW = dgx^T x) of layers > 0 may be deferred until the last
+# recurrent layer's BPTT has been issued: the side stream then carries only the recurrent
+# dU GEMMs while the BPTT chain runs, which competes less with it (measured 1 GPU: 10.40-10.47
+# vs 10.60-10.64 ms/step on the same boxes; deferring dU too was slower). With data
+# parallelism it would hold those gradient buckets back to the end of backward, so the
+# Trainer enables it for world_size == 1 only (DS2_DEFER_DW=0/1 overrides).
+_defer_input_wgrad = False
+_deferred = []
+
+
+def set_input_wgrad_deferral(on: bool) -> None:
+    global _defer_input_wgrad
+    env = os.environ.get("DS2_DEFER_DW")
+    _defer_input_wgrad = (env == "1") if env in ("0", "1") else bool(on)
+
+
+def discard_deferred_wgrads() -> None:
+    """Drop deferred GEMMs of an aborted backward (called at the start of a step)."""
+    _deferred.clear()
+
+
+def flush_deferred_wgrads() -> None:
+    """Issue every deferred input-weight gradient GEMM (on the current stream)."""
+    while _deferred:
+        _deferred.pop(0)()
+
+
 def join_wgrad_streams() -> None:
     """Make the current stream wait for every pending side-stream weight gradient."""
+    if _deferred:                         # e.g. a backward that never reached layer 0
+        for idx, s in _side_streams.items():
+            s.wait_stream(torch.cuda.current_stream(idx))
+            with torch.cuda.stream(s):
+                flush_deferred_wgrads()
+        flush_deferred_wgrads()
     for idx, s in _side_streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
 

@@ -25,7 +25,7 @@ import torch
 
 from .models import DeepSpeech2
 from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
-from .ops.rnn import join_wgrad_streams
+from .ops.rnn import discard_deferred_wgrads, join_wgrad_streams
 from .parallel.grad_sync import GradBucketer, broadcast_params
 from .utils import trace as TR
 
@@ -65,6 +65,8 @@ class Trainer:
             self.arena.mark_dirty()
             if self.opt.ema is not None:
                 self.opt.ema.copy_(self.arena.flat)
+        from .ops.rnn import set_input_wgrad_deferral
+        set_input_wgrad_deferral(world_size == 1)
         self.global_step = 0
         self.nan_policy = nan_policy
         self.collapse_repeated = collapse_repeated
@@ -82,6 +84,7 @@ class Trainer:
         # the HIP engine delivers every gradient through the arena (first write overwrites),
         # so the per-step memset of the whole gradient buffer is skipped
         lazy = model.engine == "hip"
+        discard_deferred_wgrads()
         self.arena.zero_grad(lazy=lazy)
         logits, lens = model(batch["feats"], batch["seq_lens"])
         loss = model.loss(logits, lens, batch["labels"], batch["label_lens"])
