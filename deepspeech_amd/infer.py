@@ -21,6 +21,7 @@ streams (equal chunk schedule, per-stream valid lengths), which is how a server 
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import List, Optional
 
@@ -40,7 +41,8 @@ def frames_out(T: int) -> int:
 
 
 class StreamingRecognizer:
-    def __init__(self, model: DeepSpeech2, decoder: str = "greedy", beam_width: int = 16, batch: int = 1):
+    def __init__(self, model: DeepSpeech2, decoder: str = "greedy", beam_width: int = 16, batch: int = 1,
+                 graphs: Optional[bool] = None):
         if model.bidirectional:
             raise ValueError("streaming needs a unidirectional model (rnn_type='uni-dir')")
         self.model = model.eval()
@@ -48,6 +50,15 @@ class StreamingRecognizer:
         self.beam_width = beam_width
         self.B = batch
         self.dev = model.fc_weight.device
+        # HIP graphs: a chunk's ~40 launches (conv front-end, 5 x (projection GEMM, sentinel
+        # fill, persistent recurrence), head, log-softmax, argmax) are captured once per chunk
+        # shape and replayed, so the per-chunk cost is GPU time, not host launch overhead.
+        # The recurrent state lives in static buffers the graph reads and rewrites.
+        if graphs is None:
+            graphs = os.environ.get("DS2_INFER_GRAPHS", "1") != "0"
+        self.use_graphs = bool(graphs) and self.dev.type == "cuda" and model.engine == "hip"
+        self._graphs = {}
+        self._h = None
         self.reset()
 
     def reset(self) -> None:
@@ -56,6 +67,9 @@ class StreamingRecognizer:
         self.total = 0                      # frames received
         self.done = 0                       # output (post-conv) frames emitted
         self.states: List[Optional[torch.Tensor]] = [None] * len(self.model.rnn)
+        if self._h is not None:
+            for h in self._h:
+                h.zero_()
         self.logprobs: List[torch.Tensor] = []
         self.beams = None
         if self.decoder == "beam":
@@ -83,17 +97,22 @@ class StreamingRecognizer:
         feats = self.buf[:, lo:hi]
         if m.engine == "hip":
             feats = feats.to(m.compute_dtype)
-        x = m.frontend(feats)                                  # [new, B, C*F2]
-        assert x.shape[0] == new, (x.shape, new)
-        lens = torch.full((self.B,), new, dtype=torch.int32, device=self.dev)
-        for i, layer in enumerate(m.rnn):
-            x, self.states[i] = self._layer(layer, x, lens, self.states[i])
-            if not m.stack_fix:
-                raise ValueError("streaming requires stack_fix=True")
-        logits = m.head(x).float()
-        lp = torch.log_softmax(logits, -1)                     # [new, B, K]
+        if not m.stack_fix:
+            raise ValueError("streaming requires stack_fix=True")
+        if self.use_graphs:
+            lp, best_t = self._graph_chunk(feats.contiguous())
+        else:
+            x = m.frontend(feats)                              # [new, B, C*F2]
+            assert x.shape[0] == new, (x.shape, new)
+            lens = torch.full((self.B,), new, dtype=torch.int32, device=self.dev)
+            for i, layer in enumerate(m.rnn):
+                x, self.states[i] = self._layer(layer, x, lens, self.states[i])
+            logits = m.head(x).float()
+            lp = torch.log_softmax(logits, -1)                 # [new, B, K]
+            best_t = lp.argmax(-1)
+        assert lp.shape[0] == new, (lp.shape, new)
         self.logprobs.append(lp)
-        best = lp.argmax(-1).cpu().numpy()                     # [new, B]
+        best = best_t.cpu().numpy()                            # [new, B]
         if self.beams is not None:
             # prefix beam search advances chunk by chunk (beams carried in the native
             # runtime, streams decoded on parallel host threads)
@@ -115,6 +134,42 @@ class StreamingRecognizer:
             torch.cuda.synchronize(self.dev)
         self.compute_s += time.perf_counter() - t0
         return out
+
+    # ---- HIP-graph path -------------------------------------------------------------
+    def _chunk_body(self, feats):
+        """The whole GPU part of a chunk on static state buffers (capturable: no host sync)."""
+        m = self.model
+        x = m.frontend(feats)
+        lens = torch.full((self.B,), x.shape[0], dtype=torch.int32, device=self.dev)
+        for i, layer in enumerate(m.rnn):
+            x, h = self._layer(layer, x, lens, self._h[i])
+            self._h[i].copy_(h)                                # state carried in place
+        lp = torch.log_softmax(m.head(x).float(), -1)
+        return lp, lp.argmax(-1)
+
+    def _graph_chunk(self, feats):
+        if self._h is None:
+            self._h = [torch.zeros(self.B, layer.hidden, device=self.dev, dtype=torch.float32)
+                       for layer in self.model.rnn]
+        key = tuple(feats.shape)
+        g = self._graphs.get(key)
+        if g is None:
+            # first chunk of this shape: run it eagerly (real result, warms plans/handles),
+            # then capture the same work into a graph for every later chunk of this shape
+            lp, best = self._chunk_body(feats)
+            static_in = feats.clone()
+            saved = [h.clone() for h in self._h]              # capture records, never runs
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self._chunk_body(static_in)
+            for h, s in zip(self._h, saved):
+                h.copy_(s)
+            self._graphs[key] = (graph, static_in, out)
+            return lp.clone(), best.clone()
+        graph, static_in, out = g
+        static_in.copy_(feats)
+        graph.replay()
+        return out[0].clone(), out[1].clone()
 
     def _layer(self, layer, x, lens, h0):
         m = self.model

@@ -698,16 +698,28 @@ def recurrent_layer_infer(layer, x: torch.Tensor, lens: torch.Tensor, h0: Option
     T, N, _ = x.shape
     plan = plan_for(N, layer.hidden, layer.cell, ndir, x.device)
     dirs = layer.directions()
-    W16 = torch.cat([d.W for d in dirs], 0).to(torch.bfloat16)
-    b16 = torch.cat([d.b for d in dirs], 0).to(torch.bfloat16)
+    # bf16 operand copies are cached per layer and rebuilt only when a parameter changed
+    # (its version counter moves with every in-place update): a streaming chunk no longer
+    # re-casts W and U on every call
+    params = [p for d in dirs for p in (d.W, d.b, d.U, d.b_h) if p is not None]
+    key = (x.device, tuple(p._version for p in params), tuple(p.data_ptr() for p in params))
+    cache = getattr(layer, "_infer_cache", None)
+    if cache is None or cache[0] != key:
+        with torch.no_grad():
+            cache = (key,
+                     torch.cat([d.W for d in dirs], 0).to(torch.bfloat16),
+                     torch.cat([d.b for d in dirs], 0).to(torch.bfloat16),
+                     [d.U.to(torch.bfloat16).contiguous() for d in dirs] + ([None] if ndir == 1 else []),
+                     [d.b_h.float().contiguous() if d.b_h is not None else None for d in dirs]
+                     + ([None] if ndir == 1 else []))
+        layer._infer_cache = cache
+    _, W16, b16, U, bh = cache
     alpha = sbn_scale() if layer.seq_bn == "frozen" else 1.0
     if layer.seq_bn == "batch":
         gx = input_projection_hip(layer, x.to(torch.bfloat16), lens)
     else:
         gx = torch.addmm(b16, x.to(torch.bfloat16).reshape(T * N, -1), W16.t(), alpha=alpha).view(T, N, -1)
     lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
-    U = [d.U.to(torch.bfloat16).contiguous() for d in dirs] + ([None] if ndir == 1 else [])
-    bh = [d.b_h.float().contiguous() if d.b_h is not None else None for d in dirs] + ([None] if ndir == 1 else [])
     y, (hx, hs, gates) = _run_fwd(gx.contiguous(), lens, U, bh, plan, h0=h0)
     return y, hs[:, T, :N].clone()
 
