@@ -558,7 +558,7 @@ class FusedBiLayer(torch.autograd.Function):
                 mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
                 arena.grad_done(W_f, W_b if d1 else None)
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
-            if _defer_input_wgrad and on_side and ctx.idx > 0:
+            if _defer_input_wgrad and on_side and ctx.idx >= _DEFER_MIN_LAYER:
                 _deferred.append(dw)              # run after the last recurrent layer's BPTT
             else:
                 dw()
@@ -617,6 +617,7 @@ def wgrad_stream(device: torch.device) -> Optional["torch.cuda.Stream"]:
 # parallelism it would hold those gradient buckets back to the end of backward, so the
 # Trainer enables it for world_size == 1 only (DS2_DEFER_DW=0/1 overrides).
 _defer_input_wgrad = False
+_DEFER_MIN_LAYER = int(os.environ.get("DS2_DEFER_MIN_LAYER", "1"))
 _deferred = []
 
 
