@@ -1077,7 +1077,46 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
       st.mark(-1);
       const bool has_next = s + 1 < a.steps;
       // (G) sum this thread's producers' partials of dh_rec
-      if constexpr (PBF) {
+      if constexpr (PBF == 2) {
+        // 8 < R <= 16: lane -> (row, granule g), one producer per load instruction
+        const int grow = lane >> 2, gg = lane & 3;
+        float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (has_next && grow < R) {
+          const int cs = (s + 1) % 3;
+          const unsigned want = tag_of(s + 1);
+          unsigned off[GPT];
+          i32x4 v[GPT];
+#pragma unroll
+          for (int i = 0; i < GPT; ++i) {
+            const int j = min(pg7 + MW * i, P - 1);
+            off[i] = ring_off16(cs, j, mem, grow, gg);
+            v[i] = load_sc1_b128(rs_ring, off[i]);
+          }
+          const long long t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+          for (int i = 0; i < GPT; ++i) {
+            if (pg7 + MW * i < P) {
+              while (!(a.knobs & 4) && !granule_tagged16(v[i], want)) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
+                __builtin_amdgcn_s_sleep(1);
+                v[i] = load_sc1_b128(rs_ring, off[i]);
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                acc8[2 * q] += __uint_as_float((unsigned)v[i][q] << 16);
+                acc8[2 * q + 1] += __uint_as_float((unsigned)v[i][q] & 0xffff0000u);
+              }
+            }
+          }
+        }
+        if (grow < R) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            red_s[wave][grow][4 * gg + q] = acc8[q];
+            red_s[wave][grow][16 + 4 * gg + q] = acc8[4 + q];
+          }
+        }
+      } else if constexpr (PBF == 1) {
         // lane -> (producer half h, row, granule g); two producers per load instruction,
         // h = 1 partial sums go to red_s rows R..2R-1 (R <= 8), added in the epilogue
         const int h = lane >> 5, grow = (lane >> 2) & 7, gg = lane & 3;
@@ -1165,7 +1204,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
             if (has_next) {
 #pragma unroll
               for (int w = 0; w < MW; ++w) dhrec += red_s[w][row][c];
-              if constexpr (PBF) {
+              if constexpr (PBF == 1) {
 #pragma unroll
                 for (int w = 0; w < MW; ++w) dhrec += red_s[w][row + 8][c];
               }
@@ -1524,10 +1563,12 @@ int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st) {
   a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->steps <= 0) return 0;
   const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
-  const bool pbf = d->R <= 8 && (d->H / 16) % 2 == 0 && !(d->knobs & 64);   // knob 64: fp32 partials
+  // bf16 partials (knob 64: fp32): PBF 1 for R <= 8 (two producers per load), 2 for R <= 16
+  const int pbf = ((d->H / 16) % 2 != 0 || (d->knobs & 64)) ? 0 : (d->R <= 8 ? 1 : 2);
 #define DS2_RS(C, M, GP)                                                                    \
   do {                                                                                      \
-    if (pbf) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP, 1>), dim3(grid), dim3(NTH), 0, st, a); \
+    if (pbf == 1) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP, 1>), dim3(grid), dim3(NTH), 0, st, a); \
+    else if (pbf == 2) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP, 2>), dim3(grid), dim3(NTH), 0, st, a); \
     else hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP, 0>), dim3(grid), dim3(NTH), 0, st, a);     \
   } while (0)
 #define DS2_RS_CELL(C)                                  \
