@@ -97,8 +97,10 @@ def main():
     ap.add_argument("--nw", type=str, default="0,4,8")
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--kernels", type=str, default="xcd,v1", help="recurrence generations to time")
-    ap.add_argument("--knobs", type=str, default="0", help="xcd diagnostic knob sets to time (1 no prefetch, "
-                    "2 no deferred stores, 4 no MFMA; results are wrong when set)")
+    ap.add_argument("--knobs", type=str, default="0", help="xcd diagnostic knob sets to time (results are "
+                    "wrong when set). Forward: 1 no prefetch, 2 no deferred stores, 4 no MFMA. Reduce-scatter "
+                    "BPTT: 4 no exchange wait, 8 no publish MFMA, 32 no publish stores (with 4), 64 fp32 "
+                    "partials instead of tagged bf16 (results correct)")
     a = ap.parse_args()
     for proto in a.kernels.split(","):
       os.environ["DS2_RNN_KERNEL"] = proto
