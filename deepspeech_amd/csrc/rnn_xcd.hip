@@ -872,14 +872,20 @@ struct XBwdRS {
   unsigned long long* stamps;
 };
 
-// bf16 partial with its use tag in the mantissa LSB: of the two bf16 neighbours of x's
-// truncation, the nearest one whose LSB equals the tag (error < 1 bf16 ulp; NaN -> 0x7FC0|tag)
-__device__ __forceinline__ unsigned bf16_tagged(float x, unsigned tag) {
-  const unsigned u = __float_as_uint(x);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0x7fc0u | tag;
-  const unsigned t = u >> 16;
-  return ((t & 1u) == tag) ? t : t + 1u;
+// Two bf16 partials in one dword, each carrying the use tag in its mantissa LSB: the fp32
+// value's truncation, moved up one ulp where its LSB disagrees with the tag (the nearest
+// bf16 with the right LSB: error < 1 ulp). Packed integer ops (perm, and, xor, add): this
+// conversion sits on the critical path of every BPTT step and wave64 VALU ops cost 4 cycles
+// (the per-value version with NaN selects made the publish phase ~1.6k cycles longer). The
+// +1 can carry out of the low half only from 0xFFFF (a negative NaN with a full payload),
+// which is first replaced by the canonical NaN 0x7FC0.
+__device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
+  unsigned d = __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+  if ((d & 0xffffu) == 0xffffu) d = (d & 0xffff0000u) | 0x7fc0u;
+  const unsigned x = (d & 0x00010001u) ^ tagmask;
+  return d + x;
 }
+
 __device__ __forceinline__ bool granule_tagged16(i32x4 v, unsigned tag) {
   const unsigned want = tag ? 0x00010001u : 0u;
   return (((unsigned)v[0] & 0x00010001u) == want) && (((unsigned)v[1] & 0x00010001u) == want) &&
@@ -1257,6 +1263,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
       if (s > 0) {
         const int ws = s % 3;
         const unsigned tg = tag_of(s);
+        const unsigned tagmask = tg ? 0x00010001u : 0u;
         const bool prow = (lane & 15) < R;
         bf16x8 bfr[G];
 #pragma unroll
@@ -1293,8 +1300,8 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
                 i32x4 v;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                  v[q] = (int)(bf16_tagged(q < 2 ? a0[2 * q] : a1[2 * q - 4], tg) |
-                               (bf16_tagged(q < 2 ? a0[2 * q + 1] : a1[2 * q - 3], tg) << 16));
+                  v[q] = (int)bf16x2_tagged(q < 2 ? a0[2 * q] : a1[2 * q - 4], q < 2 ? a0[2 * q + 1] : a1[2 * q - 3],
+                                            tagmask);
                 const unsigned off = ring_off16(ws, mem, pr, lane & 15, lane >> 4);
                 if (plain) store_b128(rs_ring, off, v);
                 else store_sc1_b128(rs_ring, off, v);
