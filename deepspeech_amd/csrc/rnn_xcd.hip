@@ -109,14 +109,17 @@ __device__ __forceinline__ bf16_t f2bf_x(float f) {
   return ((b & 0x7f80u) == 0x7f80u && (b & 0x7fu)) ? (bf16_t)0x7fc0 : b;
 }
 
+// no 16-bit half of the granule is the sentinel 0xFFFF: SWAR "has a zero half" test on the
+// complement, (~w - 0x00010001) & w & 0x80008000 (a few VALU ops per dword; this check runs
+// on every poll of the latency-critical exchange)
 __device__ __forceinline__ bool granule_ready(i32x4 v) {
-  bool ok = true;
+  unsigned any = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const unsigned w = (unsigned)v[i];
-    ok = ok && ((w & 0xffffu) != 0xffffu) && ((w >> 16) != 0xffffu);
+    any |= (~w - 0x00010001u) & w & 0x80008000u;
   }
-  return ok;
+  return any == 0;
 }
 
 __device__ __forceinline__ void store_granule(bool plain, __amdgpu_buffer_rsrc_t rs, bf16_t* base, unsigned off,
