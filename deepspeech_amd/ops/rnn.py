@@ -574,15 +574,24 @@ class FusedBiLayer(torch.autograd.Function):
         ugrp = arena.group_view([U_f, U_b], "grad") if (arena is not None and d1) else None
         if ugrp is not None and arena.first_write(U_f) and arena.first_write(U_b):
             # both directions' dU_d = dgh_d^T h_d as ONE batched GEMM into the packed slots
-            steps = dgh.shape[1]
-            g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
-            h3 = hx[:, :steps].reshape(2, steps * plan.NP, plan.H)
-            out = ugrp.view(2, GH, plan.H)
-            try:
-                torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
-            except (RuntimeError, TypeError):
-                out.copy_(torch.bmm(g3, h3))
-            arena.grad_done(U_f, U_b)
+            def du(ugrp=ugrp, dgh=dgh, hx=hx):
+                steps = dgh.shape[1]
+                g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
+                h3 = hx[:, :steps].reshape(2, steps * plan.NP, plan.H)
+                out = ugrp.view(2, GH, plan.H)
+                try:
+                    torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
+                except (RuntimeError, TypeError):
+                    out.copy_(torch.bmm(g3, h3))
+                arena.grad_done(U_f, U_b)
+            on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
+            if _defer_input_wgrad and on_side and ctx.idx == 0 and _TAIL_DU:
+                # the side stream already carries dW_0 + every deferred dW and ends after the
+                # conv front-end's backward on the main stream: balance by issuing the
+                # bottom layer's dU on the main stream behind the front-end (join_wgrad_streams)
+                _main_tail.append(du)
+            else:
+                du()
         else:
             for d, p in enumerate([U_f, U_b] if d1 else [U_f]):
                 g = _dU(dgh, hx, d, plan, p)
@@ -618,7 +627,9 @@ def wgrad_stream(device: torch.device) -> Optional["torch.cuda.Stream"]:
 # Trainer enables it for world_size == 1 only (DS2_DEFER_DW=0/1 overrides).
 _defer_input_wgrad = False
 _DEFER_MIN_LAYER = int(os.environ.get("DS2_DEFER_MIN_LAYER", "1"))
+_TAIL_DU = os.environ.get("DS2_TAIL_DU", "1") == "1"
 _deferred = []
+_main_tail = []     # GEMMs issued on the main stream once the whole backward is queued
 
 
 def set_input_wgrad_deferral(on: bool) -> None:
@@ -630,6 +641,7 @@ def set_input_wgrad_deferral(on: bool) -> None:
 def discard_deferred_wgrads() -> None:
     """Drop deferred GEMMs of an aborted backward (called at the start of a step)."""
     _deferred.clear()
+    _main_tail.clear()
 
 
 def flush_deferred_wgrads() -> None:
@@ -646,6 +658,8 @@ def join_wgrad_streams() -> None:
             with torch.cuda.stream(s):
                 flush_deferred_wgrads()
         flush_deferred_wgrads()
+    while _main_tail:
+        _main_tail.pop(0)()
     for idx, s in _side_streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
 
