@@ -11,12 +11,16 @@ of csrc/bn_act.hip (BNClip).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import _ext
 from .optim import arena_of, emit_grad
 from ..utils import trace as TR
+
+_HEAD_SIDE = os.environ.get("DS2_HEAD_SIDE", "1") == "1"
 
 BN_EPS = 1e-3
 BN_MOMENTUM = 0.01
@@ -273,7 +277,6 @@ def cl_supported(model, feats: torch.Tensor) -> bool:
 
 
 def frontend_hip(model, feats: torch.Tensor) -> torch.Tensor:
-    import os
     if cl_supported(model, feats) and os.environ.get("DS2_CONV", "hip") == "hip":
         c1, c2 = model.conv1, model.conv2
         return FrontendCL.apply(feats, c1.weight, c1.bias, c1.bn_gamma, c1.bn_beta,
@@ -309,9 +312,27 @@ class FusedHead(torch.autograd.Function):
         T, N, K = dout.shape
         d2 = dout.to(torch.bfloat16).reshape(T * N, K)
         dh = torch.mm(d2, w16).view(T, N, -1) if ctx.needs_input_grad[0] else None
+        # arena-managed weights: dW and the bias sum run on the weight-gradient side stream,
+        # so the top recurrent layer's BPTT starts right after dh (they were ~75 us on the
+        # critical path); the Trainer joins that stream before Adam
+        from .rnn import wgrad_stream
+        side = (wgrad_stream(d2.device) if (arena_of(weight) is not None and arena_of(bias) is not None
+                                            and _HEAD_SIDE) else None)
+        if side is None:
+            gw, gb = FusedHead._weight_grads(weight, bias, d2, h2)
+            return dh, gw, gb
+        side.wait_stream(torch.cuda.current_stream(d2.device))
+        with torch.cuda.stream(side):
+            d2.record_stream(side)
+            h2.record_stream(side)
+            gw, gb = FusedHead._weight_grads(weight, bias, d2, h2)
+        return dh, gw, gb
+
+    @staticmethod
+    def _weight_grads(weight, bias, d2, h2):
         from .optim import mm_into
         gw = mm_into(weight, d2.t(), h2)
         if gw is None:
             arena_of(weight).grad_done(weight)
         gb = emit_grad(bias, d2.sum(0, dtype=torch.float32))
-        return dh, gw, gb
+        return gw, gb
