@@ -171,6 +171,30 @@ def test_ctc_long_labels(cuda, Lmax, T):
     assert _rel(x.grad, xr.grad) < 2e-2
 
 
+def test_ctc_peaked_distributions(cuda):
+    """Confident (peaked) frames, log-probs down to ~-100 nats: the linear-domain recursion
+    with per-frame power-of-two rescaling must track the log-space reference."""
+    from deepspeech_amd.ops import ctc as CTC
+    torch.manual_seed(3)
+    T, N, K = 120, 4, 29
+    logits = (torch.randn(T, N, K) * 12).to(cuda)
+    lens = torch.tensor([120, 100, 77, 120], dtype=torch.int32)
+    Ls = [40, 30, 20, 55]
+    labels = torch.zeros(N, max(Ls), dtype=torch.int32)
+    for b, L in enumerate(Ls):
+        labels[b, :L] = torch.randint(0, K - 1, (L,))
+    lab_lens = torch.tensor(Ls, dtype=torch.int32)
+    x = logits.clone().requires_grad_(True)
+    loss = CTC.ctc_loss_hip(x, lens.to(cuda), labels.to(cuda), lab_lens.to(cuda))
+    loss.mean().backward()
+    xr = logits.clone().requires_grad_(True)
+    lr = R.ctc_loss_ref(xr, labels.to(cuda), lens.to(cuda), lab_lens.to(cuda))
+    lr.mean().backward()
+    assert torch.isfinite(loss).all() and float(loss.min()) > 100.0, loss
+    assert torch.allclose(loss, lr, rtol=1e-4, atol=1e-2), (loss, lr)
+    assert _rel(x.grad, xr.grad) < 1e-3
+
+
 def test_ctc_infeasible_zero(cuda):
     from deepspeech_amd.ops import ctc as CTC
     T, N, K = 4, 1, 29
