@@ -31,10 +31,20 @@ __device__ __forceinline__ float lse2(float a, float b) {
   if (m == NEG_INF) return NEG_INF;
   return m + __logf(__expf(a - m) + __expf(b - m));
 }
-__device__ __forceinline__ float lse3(float a, float b, float c) {
+
+// log2-domain lse of three values with ONE of the three exponentials known to be 2^0:
+// m = max, the other two are the median and the minimum (v_max3 / v_med3 / v_min3), so a
+// state costs 2 v_exp_f32 + 1 v_log_f32 (no ln<->log2 scaling, no branch).
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+__device__ __forceinline__ float lse3_2(float a, float b, float c) {
   const float m = fmaxf(fmaxf(a, b), c);
-  if (m == NEG_INF) return NEG_INF;
-  return m + __logf(__expf(a - m) + __expf(b - m) + __expf(c - m));
+  const float lo = fminf(fminf(a, b), c);
+  const float mid = __builtin_amdgcn_fmed3f(a, b, c);
+  const float mc = fmaxf(m, -1e30f);                   // all -inf: keep the differences finite
+  const float r = mc + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(mid - mc) +
+                                             __builtin_amdgcn_exp2f(lo - mc));
+  return (m == NEG_INF) ? NEG_INF : r;
 }
 
 template <typename LT>
@@ -105,7 +115,8 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
   auto put_row = [&](int t, const float* v) {
     float4* o = reinterpret_cast<float4*>(out + (size_t)t * SPS + s0);
 #pragma unroll
-    for (int j = 0; j < SPL / 4; ++j) o[j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    for (int j = 0; j < SPL / 4; ++j)   // rows in natural-log units for the gradient kernel
+      o[j] = make_float4(v[4 * j] * LN2, v[4 * j + 1] * LN2, v[4 * j + 2] * LN2, v[4 * j + 3] * LN2);
   };
   // lp rows are staged through LDS in chunks of 64 frames (one 128-B row per lane), so
   // the per-frame gathers are LDS reads: a global load in the frame loop would make the
@@ -121,8 +132,8 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
 #pragma unroll
       for (int q = 0; q < KPAD / 4; ++q) {
         const float4 v4 = src[q];
-        lps[lane][4 * q + 0] = v4.x; lps[lane][4 * q + 1] = v4.y;
-        lps[lane][4 * q + 2] = v4.z; lps[lane][4 * q + 3] = v4.w;
+        lps[lane][4 * q + 0] = v4.x * LOG2E; lps[lane][4 * q + 1] = v4.y * LOG2E;   // log2 units
+        lps[lane][4 * q + 2] = v4.z * LOG2E; lps[lane][4 * q + 3] = v4.w * LOG2E;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
@@ -156,7 +167,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
       for (int j = 0; j < SPL; ++j) {
         const float a1 = (j >= 1) ? v[j - 1] : p1;
         const float a2 = (j >= 2) ? v[j - 2] : (j == 1 ? p1 : p2);
-        const float r = lse3(v[j], a1, ((skip >> j) & 1u) ? a2 : NEG_INF);
+        const float r = lse3_2(v[j], a1, ((skip >> j) & 1u) ? a2 : NEG_INF);
         nv[j] = (s0 + j < SP) ? r + lcur[j] : NEG_INF;
       }
     } else {
@@ -167,7 +178,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
       for (int j = 0; j < SPL; ++j) {
         const float b1 = (j + 1 < SPL) ? v[j + 1] : n1;
         const float b2 = (j + 2 < SPL) ? v[j + 2] : (j + 1 < SPL ? n1 : n2);
-        const float r = lse3(v[j], b1, ((skip >> j) & 1u) ? b2 : NEG_INF);
+        const float r = lse3_2(v[j], b1, ((skip >> j) & 1u) ? b2 : NEG_INF);
         nv[j] = (s0 + j < SP) ? r + lcur[j] : NEG_INF;
       }
     }
@@ -180,7 +191,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
     float mine = NEG_INF;
 #pragma unroll
     for (int j = 0; j < SPL; ++j)
-      if (s0 + j == SP - 1 || s0 + j == SP - 2) mine = lse2(mine, v[j]);
+      if (s0 + j == SP - 1 || s0 + j == SP - 2) mine = lse2(mine, v[j] * LN2);
     // at most two lanes hold a term: combine with a max-shifted wave reduction
     const float m = wave_max(mine);
     float e = (m == NEG_INF) ? 0.f : __expf(mine - m);
