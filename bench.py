@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--bucket_mb", type=float, default=32.0)
     p.add_argument("--allreduce_bf16", action="store_true")
     p.add_argument("--profile_dir", type=str, default="", help="write a torch.profiler trace here")
+    p.add_argument("--force_dp", action="store_true",
+                   help="run the data-parallel machinery (process group, gradient buckets, "
+                        "collectives on the ordering stream) even on one GPU, to time its overhead")
     p.add_argument("--fp8", action="store_true",
                    help="fp8 e4m3 input projections (BASELINE config 5; NOT the headline bf16 number)")
     return p.parse_args()
@@ -57,7 +60,7 @@ def main():
     from deepspeech_amd.trainer import Trainer, LRSchedule
     from deepspeech_amd.ops import rnn as RNN
 
-    ctx = init_distributed("auto")
+    ctx = init_distributed("auto", force_group=args.force_dp)
     dev = ctx.device
     if dev.type != "cuda" and args.engine == "hip":
         args.engine = "ref"
@@ -69,7 +72,7 @@ def main():
     model.set_engine(args.engine, dtype, fp8=bool(args.fp8 and args.engine == "hip"))
     trainer = Trainer(model, LRSchedule(1e-4, 10 ** 9, 0.9), moving_avg_decay=0.9999,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
-                      allreduce_bf16=args.allreduce_bf16)
+                      allreduce_bf16=args.allreduce_bf16, force_buckets=args.force_dp)
     feed = FixedShapeBatches(args.batch_size, max_frames=args.frames, seed=1000 + ctx.rank, pool=4)
     batches = [to_device(feed.next(), dev) for _ in range(4)]
     audio_per_step = [float(b["seq_lens"].sum().item()) / 100.0 for b in batches]

@@ -56,8 +56,10 @@ def _add_model_flags(p: argparse.ArgumentParser) -> None:
     p.add_argument("--seq_bn", type=str, default="frozen", choices=["frozen", "batch", "none"],
                    help="sequence-wise BN on W.x: frozen (reference parity, moving stats "
                         "never updated), batch (DS2 paper), none")
-    p.add_argument("--ctc_collapse_repeated", type=str2bool, default=False,
-                   help="TF preprocess_collapse_repeated (reference uses True, quirk Q5)")
+    p.add_argument("--ctc_collapse_repeated", type=str2bool, default=True,
+                   help="TF preprocess_collapse_repeated: repeated labels ('LL') are merged before "
+                        "the CTC loss, as the reference always does (src/deepSpeech_NCHW.py:225, "
+                        "quirk Q5); False = standard CTC")
 
 
 def build_train_parser() -> argparse.ArgumentParser:
@@ -177,7 +179,7 @@ def parse_eval_args(argv=None) -> argparse.Namespace:
     apply_resume_params(args, params, EVAL_KEYS)
     # reference-defaults for keys that may be missing in a json written by another tool
     for k, v in (("cell", "rnn_relu"), ("stack_fix", True), ("seq_bn", "frozen"),
-                 ("ctc_collapse_repeated", False), ("moving_avg_decay", 0.9999)):
+                 ("ctc_collapse_repeated", True), ("moving_avg_decay", 0.9999)):
         if not hasattr(args, k):
             setattr(args, k, v)
     return args

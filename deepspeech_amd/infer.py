@@ -133,6 +133,9 @@ class StreamingRecognizer:
         if self.dev.type == "cuda":
             torch.cuda.synchronize(self.dev)
         self.compute_s += time.perf_counter() - t0
+        if m.engine == "hip":
+            from .ops import rnn as RNN
+            RNN.check_errors()        # after the chunk's sync: one 4-byte read
         return out
 
     # ---- HIP-graph path -------------------------------------------------------------

@@ -67,6 +67,10 @@ class ParamArena:
         self.p16 = torch.zeros(off, device=dev, dtype=torch.bfloat16) if bf16_shadow else None
         self._index = {}
         self._ready_cbs = []
+        # per-parameter "gradient written" events (enabled by the DP bucketer): recorded on
+        # whatever stream enqueued the gradient write, so a collective waits for exactly
+        # the producers of its bucket instead of joining whole streams
+        self._ready_events: Optional[List[torch.cuda.Event]] = None
         self._written = set()
         self._known_zero = set()
         for i, (p, (o, n)) in enumerate(zip(self.params, self.offsets)):
@@ -140,18 +144,33 @@ class ParamArena:
         return id(p) not in self._written
 
     def grad_done(self, *params) -> None:
-        """Report gradients written straight into ``main_grad`` (fires bucket hooks)."""
+        """Report gradients written straight into ``main_grad`` (fires bucket hooks). Call
+        right after enqueueing the write, on the stream that carries it."""
         for p in params:
             if p is None:
                 continue
             self._written.add(id(p))
             self._known_zero.discard(id(p))
             i = self._index[id(p)]
+            self.record_ready(i)
             for cb in self._ready_cbs:
                 cb(i)
 
     def on_grad_ready(self, cb) -> None:
         self._ready_cbs.append(cb)
+
+    def enable_ready_events(self) -> None:
+        if self.grad.is_cuda and self._ready_events is None:
+            self._ready_events = [torch.cuda.Event() for _ in self.params]
+
+    def record_ready(self, i: int) -> None:
+        """Mark parameter i's gradient as produced by the work enqueued so far on the
+        current stream."""
+        if self._ready_events is not None:
+            self._ready_events[i].record()
+
+    def ready_event(self, i: int) -> Optional["torch.cuda.Event"]:
+        return self._ready_events[i] if self._ready_events is not None else None
 
     def views(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
         return {n: buf[o:o + c].view_as(p) for n, p, (o, c) in zip(self.names, self.params, self.offsets)}

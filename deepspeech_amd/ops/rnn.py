@@ -32,7 +32,10 @@ from ..utils import trace as TR
 CELL_CODE = {"rnn_relu": 0, "gru": 1}
 GATES = {"rnn_relu": 1, "gru": 3}
 TIMEOUT_TICKS = int(float(os.environ.get("DS2_RNN_TIMEOUT_S", "20")) * 1e8)   # s_memrealtime = 100 MHz
-_pending_errors: List[torch.Tensor] = []
+# One persistent error word per device: every recurrence launch ORs its spin-timeout bits
+# into it (atomicOr in the kernels), check_errors() reads and clears it at a point where the
+# host synchronises anyway. Nothing accumulates per launch.
+_err_words = {}
 # diagnostic: when set to a list, each kernel launch appends (kind, plan, stamps[grid, 8])
 # recorded by the s_memtime build (csrc/rnn_persistent_stamps.hip)
 STAMP_LOG: Optional[list] = None
@@ -203,17 +206,27 @@ def make_plan(N: int, H: int, cell: str, ndir: int, cus: int, mode: Optional[str
                    cell=cell, ndir=ndir)
 
 
+def error_word(device: torch.device) -> torch.Tensor:
+    """The device's persistent recurrence error word (int32, 0 = no timeout so far)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    w = _err_words.get(idx)
+    if w is None:
+        w = torch.zeros(1, device=torch.device("cuda", idx), dtype=torch.int32)
+        _err_words[idx] = w
+    return w
+
+
 def check_errors(clear: bool = True) -> None:
     """Raise if any recurrence kernel since the last check hit its spin timeout.
-    Call at a point where the host synchronises anyway (e.g. when logging the loss)."""
-    global _pending_errors
-    errs = _pending_errors
-    if clear:
-        _pending_errors = []
-    for e in errs:
-        if int(e.item()) != 0:
+    Call at a point where the host synchronises anyway (e.g. when logging the loss, once
+    per eval batch, after each streaming chunk). Costs one 4-byte read per device."""
+    for idx, w in list(_err_words.items()):
+        v = int(w.item())
+        if v != 0:
+            if clear:
+                w.zero_()
             raise RuntimeError("persistent recurrence kernel timed out waiting for its peers "
-                               "(grid not co-resident?) — rerun with DS2_RNN_MODE=step")
+                               "(error bits 0x%x; grid not co-resident?) — rerun with DS2_RNN_MODE=step" % v)
 
 
 def _stamps(kind: str, plan: "RnnPlan", grid: int, dev) -> Optional[torch.Tensor]:
@@ -251,11 +264,11 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     if plan.kind == "xcd":
         # one launch: h0 slots zero, exchange slots 1..T sentinel 0xFFFF ("not yet
         # produced"), census words -1, error word 0
-        aux = torch.empty(4 + ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
-        err, census = aux[:1], aux[4:]
+        census = torch.empty(ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
+        err = error_word(dev)
         regions = ([hx[d, 0] for d in range(ndir)] + [hx[d, 1:] for d in range(ndir)] +
-                   [hs[d, 0] for d in range(ndir)] + [aux[:4], census])
-        C.multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [0, -1])
+                   [hs[d, 0] for d in range(ndir)] + [census])
+        C.multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [-1])
         if h0 is not None:
             hs[:, 0, :N].copy_(h0)
             hx[:, 0, :N].copy_(h0)
@@ -268,7 +281,6 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
                    CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
                    _stamps("fwd", plan, int(C.rnnx_info(H, GATES[plan.cell], plan.mt, ndir * plan.BG,
                                                          plan.xcd_map)["grid"]), dev))
-        _pending_errors.append(err)
         y = torch.add(y2[0], y2[1]) if d1 else y2[0]
         return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
     hx[:, 0].zero_()                         # h0
@@ -276,7 +288,7 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     if h0 is not None:
         hs[:, 0, :N].copy_(h0)
         hx[:, 0, :N].copy_(h0)
-    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    err = error_word(dev)
     flags = torch.zeros(ndir * plan.BG * plan.S, device=dev, dtype=torch.int32)
     C.rnn_fwd(gx, lens, U[0], U[1] if d1 else None,
               bh[0], bh[1] if d1 else None,
@@ -287,7 +299,6 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
               flags, err, T, N, plan.NP, H, plan.BG, steps, gstride, ndir,
               CELL_CODE[plan.cell], plan.nw, plan.mt, plan.persistent, TIMEOUT_TICKS,
               _stamps("fwd", plan, flags.numel(), dev))
-    _pending_errors.append(err)
     y = torch.add(y2[0], y2[1]) if d1 else y2[0]
     return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
 
@@ -308,11 +319,11 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
     dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
     has_g = gates.numel() > 0
     if plan.kind == "xcd":
-        aux = torch.empty(4 + ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
-        err, census = aux[:1], aux[4:]
+        census = torch.empty(ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
+        err = error_word(dev)
         parts = torch.empty(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
                             dtype=torch.float32) if want_bias else None
-        regions, pats = [aux[:4], census], [0, -1]
+        regions, pats = [census], [-1]
         if parts is not None:
             regions.append(parts)
             pats.append(0)
@@ -331,7 +342,6 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
                        CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
                        _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev),
                        ring[0], ring[1] if d1 else None)
-            _pending_errors.append(err)
             return dgx, dgh, parts
         C.multi_fill(regions + [dgh], pats + [-1])         # dgh: sentinel 0xFFFF pairs
         C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
@@ -342,9 +352,8 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
                    float(dgx_scale), census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
                    CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
                    _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev))
-        _pending_errors.append(err)
         return dgx, dgh, parts
-    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    err = error_word(dev)
     parts = torch.zeros(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
                         dtype=torch.float32) if want_bias else None
     carry = None if plan.persistent else torch.zeros(ndir, plan.NP, H, device=dev, dtype=torch.float32)
@@ -360,7 +369,6 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
               parts[0] if parts is not None else None,
               parts[1] if (parts is not None and plan.cell == "gru") else None,
               float(dgx_scale))
-    _pending_errors.append(err)
     return dgx, dgh, parts
 
 
@@ -560,6 +568,7 @@ class FusedBiLayer(torch.autograd.Function):
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
             if _defer_input_wgrad and on_side and ctx.idx >= _DEFER_MIN_LAYER:
                 _deferred.append(dw)              # run after the last recurrent layer's BPTT
+                _queue_end_of_backward()
             else:
                 dw()
             if ctx.idx == 0:
@@ -590,6 +599,7 @@ class FusedBiLayer(torch.autograd.Function):
                 # conv front-end's backward on the main stream: balance by issuing the
                 # bottom layer's dU on the main stream behind the front-end (join_wgrad_streams)
                 _main_tail.append(du)
+                _queue_end_of_backward()
             else:
                 du()
         else:
@@ -642,6 +652,7 @@ def discard_deferred_wgrads() -> None:
     """Drop deferred GEMMs of an aborted backward (called at the start of a step)."""
     _deferred.clear()
     _main_tail.clear()
+    _eob_queued[0] = False
 
 
 def flush_deferred_wgrads() -> None:
@@ -650,9 +661,11 @@ def flush_deferred_wgrads() -> None:
         _deferred.pop(0)()
 
 
-def join_wgrad_streams() -> None:
-    """Make the current stream wait for every pending side-stream weight gradient."""
-    if _deferred:                         # e.g. a backward that never reached layer 0
+def _drain_deferred() -> None:
+    """Issue every deferred weight-gradient GEMM: leftover input-weight GEMMs (a backward
+    that never reached layer 0) on the side stream, then the main-stream tail (the bottom
+    layer's dU behind the front-end backward)."""
+    if _deferred:
         for idx, s in _side_streams.items():
             s.wait_stream(torch.cuda.current_stream(idx))
             with torch.cuda.stream(s):
@@ -660,6 +673,37 @@ def join_wgrad_streams() -> None:
         flush_deferred_wgrads()
     while _main_tail:
         _main_tail.pop(0)()
+
+
+_eob_queued = [False]
+
+
+def _queue_end_of_backward() -> None:
+    """Drain the deferred GEMMs when the running backward finishes, whoever drives it
+    (Trainer.step, a bare loss.backward(), the --debug profiler): autograd runs final
+    callbacks on the caller's current streams once the whole graph has been executed,
+    so no gradient is left unwritten (lazy zeroing would otherwise keep a stale value)."""
+    if _eob_queued[0]:
+        return
+    _eob_queued[0] = True
+
+    def cb():
+        _eob_queued[0] = False
+        _drain_deferred()
+    try:
+        torch.autograd.Variable._execution_engine.queue_callback(cb)
+    except RuntimeError:                  # not inside a backward: drained by join_wgrad_streams
+        _eob_queued[0] = False
+
+
+def pending_deferred() -> int:
+    """Number of weight-gradient GEMMs still waiting to be issued (0 after a backward)."""
+    return len(_deferred) + len(_main_tail)
+
+
+def join_wgrad_streams() -> None:
+    """Make the current stream wait for every pending side-stream weight gradient."""
+    _drain_deferred()
     for idx, s in _side_streams.items():
         torch.cuda.current_stream(idx).wait_stream(s)
 

@@ -55,8 +55,10 @@ class DistContext:
         return float(t.item())
 
 
-def init_distributed(device_pref: str = "auto", timeout_s: int = 600) -> DistContext:
-    """Initialise from torchrun env vars; a no-op single-process context otherwise."""
+def init_distributed(device_pref: str = "auto", timeout_s: int = 600, force_group: bool = False) -> DistContext:
+    """Initialise from torchrun env vars; a no-op single-process context otherwise.
+    force_group: initialise a process group even at world size 1 (RCCL on the GPU), so the
+    data-parallel machinery can run and be timed on one device."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -69,12 +71,17 @@ def init_distributed(device_pref: str = "auto", timeout_s: int = 600) -> DistCon
     else:
         device = torch.device("cpu")
     ctx = DistContext(rank=rank, local_rank=local, world_size=world, device=device)
-    if world > 1:
+    if world > 1 or force_group:
         # RCCL ("nccl") on GPUs; DS2_DIST_BACKEND=gloo runs the same collectives through host
         # memory (ranks sharing one GPU, where RCCL refuses duplicate devices)
         backend = os.environ.get("DS2_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if "MASTER_PORT" not in os.environ:          # single process without torchrun
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), rank=rank, world_size=world)
         if use_cuda and backend == "nccl":
             kw["device_id"] = device
         if not dist.is_initialized():
@@ -84,5 +91,5 @@ def init_distributed(device_pref: str = "auto", timeout_s: int = 600) -> DistCon
 
 
 def shutdown(ctx: DistContext) -> None:
-    if ctx.enabled and dist.is_initialized():
+    if ctx.backend is not None and dist.is_initialized():
         dist.destroy_process_group()

@@ -12,6 +12,12 @@ MI355X-first choices:
     the last bucket (conv layers, ~0.1 MB) adds almost nothing after backward ends;
   * optional bf16 compression halves bytes on the links (sum in bf16, scaled in fp32
     afterwards by the optimizer's gscale = 1/world).
+  * stream ordering without joins: every gradient write records an event on the stream
+    that enqueued it (main stream for dx-adjacent work, the weight-gradient side stream
+    for dW/dU), and a bucket's collective is issued from a dedicated ordering stream that
+    waits on exactly its members' events. The main stream (running the next layer's
+    BPTT) never waits on the side stream mid-backward; it waits for the collectives only
+    in finish(), before the optimizer.
 The SUM is averaged by the optimizer (``gscale``), so no extra division kernel runs.
 """
 from __future__ import annotations
@@ -24,7 +30,9 @@ import torch.distributed as dist
 
 class GradBucketer:
     def __init__(self, arena, bucket_mb: float = 32.0, compress_bf16: bool = False,
-                 process_group=None, world_size: Optional[int] = None):
+                 process_group=None, world_size: Optional[int] = None, force: bool = False):
+        """force: run the bucketed collectives even at world size 1 (needs an initialised
+        process group; measures the DP machinery's own overhead on one GPU)."""
         self.arena = arena
         self.pg = process_group
         self.compress = compress_bf16
@@ -62,8 +70,12 @@ class GradBucketer:
         self._works = []
         self._shadow: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._handles = []
-        self.enabled = self.world > 1
+        self.enabled = self.world > 1 or (force and dist.is_initialized())
+        self._order_stream = None
         if self.enabled:
+            arena.enable_ready_events()
+            if arena.grad.is_cuda:
+                self._order_stream = torch.cuda.Stream(device=arena.grad.device)
             # autograd-accumulated grads fire the tensor hook; fused ops that write
             # main_grad directly report through the arena
             for i, p in enumerate(arena.params):
@@ -88,6 +100,9 @@ class GradBucketer:
                 if id(p) in written:
                     return
                 written.add(id(p))
+            # autograd accumulated this gradient on the current stream (the engine runs the
+            # hook under the producing op's stream)
+            self.arena.record_ready(i)
             self._ready(i)
         return hook
 
@@ -100,29 +115,41 @@ class GradBucketer:
         if self._launched[b]:
             return
         self._launched[b] = True
-        s, e, _ = self.buckets[b]
+        s, e, idx = self.buckets[b]
         g = self.arena.grad[s:e]
-        if g.is_cuda:
-            # a bucket may mix gradients produced on the current stream and on the
-            # recurrent layers' weight-gradient side stream: the collective (which waits on
-            # the current stream only) must see both
-            from ..ops.rnn import join_wgrad_streams
-            join_wgrad_streams()
+        os_ = self._order_stream
+        if os_ is None:
+            self._works.append((b, self._collective(b, g)))
+            return
+        # the collective (ProcessGroupNCCL waits on the CURRENT stream at issue time) is
+        # issued from the ordering stream, which waits on each member's producer event:
+        # gradients written on the side stream and on the main stream alike, nothing else
+        for i in idx:
+            ev = self.arena.ready_event(i)
+            if ev is not None and id(self.arena.params[i]) in self.arena._written:
+                os_.wait_event(ev)
+        with torch.cuda.stream(os_):
+            self._works.append((b, self._collective(b, g)))
+
+    def _collective(self, b: int, g: torch.Tensor):
         if self.compress:
             sh = self._shadow[b]
             if sh is None or sh.numel() != g.numel():
                 sh = torch.empty(g.numel(), device=g.device, dtype=torch.bfloat16)
                 self._shadow[b] = sh
             sh.copy_(g)
-            self._works.append((b, dist.all_reduce(sh, group=self.pg, async_op=True)))
-        else:
-            self._works.append((b, dist.all_reduce(g, group=self.pg, async_op=True)))
+            return dist.all_reduce(sh, group=self.pg, async_op=True)
+        return dist.all_reduce(g, group=self.pg, async_op=True)
 
     def finish(self) -> None:
         """Launch buckets whose params got no gradient (in index order on every rank),
         then wait for all all-reduces of this step."""
         if not self.enabled:
             return
+        if self._order_stream is not None and not all(self._launched):
+            # buckets still open hold parameters that got no gradient this step: their
+            # slices were zeroed on the current stream (Trainer: zero_unwritten)
+            self._order_stream.wait_stream(torch.cuda.current_stream(self.arena.grad.device))
         for b in range(len(self.buckets)):
             if not self._launched[b]:
                 self._launch(b)

@@ -80,6 +80,11 @@ def eval_once(model, args, data, num_iter: int, display: bool) -> float:
             b = to_device(hb, model.fc_weight.device)
             logits, lens = model(b["feats"], b["seq_lens"])
             preds = decode(logits, lens, args.decoder, args.beam_width)
+            if model.engine == "hip":
+                # decode() synchronised already: surface a recurrence timeout (undefined
+                # outputs) for this batch instead of reporting a CER computed from them
+                from .ops import rnn as RNN
+                RNN.check_errors()
             for i, p in enumerate(preds):
                 lab = hb.labels[i, : hb.label_lens[i]].tolist()
                 ref_s, hyp_s = ids_to_text(lab), ids_to_text(p)

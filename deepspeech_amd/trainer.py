@@ -51,7 +51,7 @@ def lr_schedule_from_args(args, steps_per_epoch: int) -> LRSchedule:
 class Trainer:
     def __init__(self, model: DeepSpeech2, lr_schedule: LRSchedule, moving_avg_decay: Optional[float] = 0.9999,
                  world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
-                 nan_policy: str = "abort", collapse_repeated: bool = False):
+                 nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False):
         self.model = model
         # bf16 compute shadows of the weights only for the HIP engine (fused ops read them)
         self.arena = ParamArena(model, bf16_shadow=(model.engine == "hip"))
@@ -59,14 +59,19 @@ class Trainer:
         self.lr_schedule = lr_schedule
         self.world = world_size
         self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb, compress_bf16=allreduce_bf16,
-                                     world_size=world_size)
+                                     world_size=world_size, force=force_buckets)
         if world_size > 1:
             broadcast_params(self.arena)
             self.arena.mark_dirty()
             if self.opt.ema is not None:
                 self.opt.ema.copy_(self.arena.flat)
         from .ops.rnn import set_input_wgrad_deferral
-        set_input_wgrad_deferral(world_size == 1)
+        # Deferring the input-weight gradients of layers >= 1 to the end of the BPTT chain
+        # measured within noise on one GPU (profiles/r1_s3_negative_results.md) and, with
+        # data parallelism, would hold ~40 % of the gradient bytes (every layer's W) back
+        # until backward ends instead of releasing one bucket per layer for overlap: on for
+        # the single-GPU path only (DS2_DEFER_DW=0/1 overrides)
+        set_input_wgrad_deferral(world_size == 1 and not self.bucketer.enabled)
         self.global_step = 0
         self.nan_policy = nan_policy
         self.collapse_repeated = collapse_repeated

@@ -251,7 +251,14 @@ def restore(trainer, directory_or_file: str) -> Optional[int]:
     load_model_from_tf(trainer.model, tensors, strict=True)
     _load_arena_slots(trainer, tensors)
     trainer.arena.mark_dirty()
-    step = int(data.get("global_step", step_from_path(path)))
-    trainer.global_step = step + 1 if data.get("format") else step
-    trainer.opt.t = int(data.get("adam_t", step + 1))
+    step = step_from_path(path)
+    if data.get("format"):
+        # snapshot() stores trainer.global_step as it stood after the saved step
+        # (Trainer.step already counted it), i.e. the index of the next step to run
+        trainer.global_step = int(data["global_step"])
+    else:
+        # file-name fallback: the reference saves model.ckpt-<step> right after running
+        # step <step> (src/deepSpeech_train.py:354-356), so <step>+1 runs next
+        trainer.global_step = step + 1
+    trainer.opt.t = int(data.get("adam_t", trainer.global_step))
     return step

@@ -101,9 +101,15 @@ def test_checkpoint_roundtrip_and_state_file(tmp_path):
     CK.restore(t2, str(tmp_path))
     assert torch.allclose(t.arena.flat, t2.arena.flat)
     assert torch.allclose(t.opt.m, t2.opt.m) and torch.allclose(t.opt.ema, t2.opt.ema)
-    assert t2.global_step == 4 and t2.opt.t == t.opt.t
+    assert t2.global_step == t.global_step == 3 and t2.opt.t == t.opt.t
+    assert t2.lr == t.lr
     l1, l2 = float(t.step(b)), float(t2.step(b))
     assert abs(l1 - l2) < 1e-4
+    # the continued trajectories agree after the update too (LR schedule, Adam t and the
+    # EMA's num_updates all restored at the same step)
+    assert t2.global_step == t.global_step
+    assert torch.allclose(t.arena.flat, t2.arena.flat, atol=1e-6)
+    assert torch.allclose(t.opt.ema, t2.opt.ema, atol=1e-6)
 
 
 def test_eval_restores_ema_weights(tmp_path):

@@ -133,3 +133,33 @@ def test_torchrun_gloo_two_ranks(tmp_path):
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "step 12" in r.stdout
+
+
+def _run_bench(nproc, extra_env, args, timeout=600):
+    import json
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % nproc,
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_json_contract():
+    """bench.py under torch.distributed.run with 2 ranks (gloo on CPU): one JSON line, whole-job
+    aggregate value (summed audio / max elapsed), n_gpus and dp degree reported."""
+    out = _run_bench(2, {"CUDA_VISIBLE_DEVICES": ""},
+                     ["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch_size", "2", "--frames", "200",
+                      "--num_hidden", "32", "--num_rnn_layers", "1", "--num_filters", "4"])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    # value is the job aggregate: per-GPU figure x world
+    assert abs(out["value"] - 2 * out["per_gpu_audio_sec_per_sec"]) <= 0.02 * out["value"]
+    # two ranks' audio (different seeds) summed over 2 steps: lengths are drawn from the
+    # top 100-frame bucket, (100, 200] frames at --frames 200 -> 4 utterances x 2 steps x (1, 2] s
+    total = out["value"] * out["ms_per_step"] * 2 / 1000.0
+    assert 8.0 < total <= 16.0 * 1.01, total

@@ -172,8 +172,12 @@ def test_ctc_long_labels(cuda, Lmax, T):
 
 
 def test_ctc_peaked_distributions(cuda):
-    """Confident (peaked) frames, log-probs down to ~-100 nats: the linear-domain recursion
-    with per-frame power-of-two rescaling must track the log-space reference."""
+    """Confident (peaked) frames, log-probs down to ~-100 nats. The kernel runs the alpha/beta
+    recursion in log2 units: the staged log-prob rows are scaled by LOG2E, each lattice state
+    takes a branch-free 3-way log-sum-exp (lse3_2: max3/med3/min3, two exp2 + one log2), and
+    the stored alpha/beta rows are rescaled by LN2 back to nats for the gradient. Large
+    log-prob gaps stress exactly that lse (exp2 underflow of the two smaller terms) and the
+    unit conversion; the result must track the natural-log reference."""
     from deepspeech_amd.ops import ctc as CTC
     torch.manual_seed(3)
     T, N, K = 120, 4, 29
