@@ -76,6 +76,8 @@ def main():
     feed = FixedShapeBatches(args.batch_size, max_frames=args.frames, seed=1000 + ctx.rank, pool=4)
     batches = [to_device(feed.next(), dev) for _ in range(4)]
     audio_per_step = [float(b["seq_lens"].sum().item()) / 100.0 for b in batches]
+    # analytic training FLOPs at each utterance's TRUE length (not the padded frame count)
+    flops_per_step = [sum(model.flops_per_step(1, int(t)) for t in b["seq_lens"].tolist()) for b in batches]
 
     def sync():
         if dev.type == "cuda":
@@ -95,10 +97,12 @@ def main():
         prof.__enter__()
     t0 = time.perf_counter()
     audio = 0.0
+    flops = 0.0
     loss = None
     for i in range(args.steps):
         loss = trainer.step(batches[i % len(batches)])
         audio += audio_per_step[i % len(batches)]
+        flops += flops_per_step[i % len(batches)]
     sync()
     ctx.barrier()
     sync()
@@ -115,7 +119,7 @@ def main():
     total_audio = ctx.all_reduce_sum(audio)
     ms = 1000.0 * elapsed / args.steps
     value = total_audio / elapsed
-    flops = model.flops_per_step(args.batch_size, args.frames) * ctx.world_size
+    flops = ctx.all_reduce_sum(flops)
     lossv = float(loss.float().item()) if loss is not None else float("nan")
     if ctx.is_main:
         out = {
@@ -141,7 +145,7 @@ def main():
             },
             "per_gpu_audio_sec_per_sec": round(value / ctx.world_size, 2),
             "utterances_per_sec": round(args.batch_size * ctx.world_size * args.steps / elapsed, 2),
-            "achieved_tflops": round(flops * args.steps / elapsed / 1e12, 2),
+            "achieved_tflops": round(flops / elapsed / 1e12, 2),
             "final_loss": round(lossv, 4),
         }
         print(json.dumps(out), flush=True)

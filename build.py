@@ -58,6 +58,21 @@ def _run(cmd):
     return r.stdout
 
 
+def _local_deps(src, seen=None):
+    """csrc files reached through #include "..." from ``src`` (transitively): an object is
+    rebuilt only when one of the files it actually includes changes."""
+    import re
+    seen = set() if seen is None else seen
+    with open(src, "r", errors="replace") as f:
+        text = f.read()
+    for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+        p = os.path.join(os.path.dirname(src), name)
+        if os.path.exists(p) and p not in seen:
+            seen.add(p)
+            _local_deps(p, seen)
+    return sorted(seen)
+
+
 def _compile(src, obj_dir, flags, deps):
     stem = os.path.splitext(os.path.basename(src))[0]
     key = _hash([src] + deps, flags)
@@ -77,9 +92,6 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         for f in os.listdir(BUILD):
             if f.endswith(".o"):
                 os.remove(os.path.join(BUILD, f))
-    # every TU may #include any other csrc file (e.g. the stamps build includes the kernel
-    # source), so all of csrc is a dependency of every object
-    headers = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip")))
     hip_srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
     common = ["-O3", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-I" + CSRC]
     if os.environ.get("DS2_DEBUG", "0") == "1":
@@ -93,7 +105,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         "-I" + py_inc, "-I" + os.path.join(ROCM, "include"), "-Wno-unused-result", "-Wno-deprecated-declarations"]
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        futs = [ex.submit(_compile, s, BUILD, hip_flags, headers) for s in hip_srcs]
+        futs = [ex.submit(_compile, s, BUILD, hip_flags, _local_deps(s)) for s in hip_srcs]
         futs.append(ex.submit(_compile, os.path.join(CSRC, "bindings.cpp"), BUILD, bind_flags, []))
         objs = [f.result() for f in futs]
     out = os.path.join(PKG, "_C" + EXT)

@@ -125,6 +125,15 @@ int ds2_bn_cl_apply(const void* y, const float* mean, const float* invstd, const
 int ds2_bn_cl_bwd(const void* dz, const void* y, const float* mean, const float* invstd, const float* gamma,
                   const float* beta, float* part, int nb, float* dgamma, float* dbeta, void* dy, int N, int T, int F,
                   int tmaj, hipStream_t st);
+int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev, int M, int N, int K,
+             int lda, int ldb, int ldc, int Ml, int Nl, int Kl, int a_col, int b_col, int epi, float alpha, int batch,
+             long long sA, long long sB, long long sC, int cfg, hipStream_t st);
+int ds2_gemm_tile(int cfg, int* bm, int* bn);
+int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens, const int* labels,
+                 const int* label_lens, float* loss, void* G, float* ws, int T, int N, int H, int K, int Lmax,
+                 int blank, int zero_inf, hipStream_t st);
+int ds2_fc_logits(const void* h, const void* W, const void* bias, void* logits, int out_bf16, int M, int H, int K,
+                  hipStream_t st);
 }
 
 namespace {
@@ -603,6 +612,99 @@ void fp8_quant2(at::Tensor a, at::Tensor b, double alpha, at::Tensor a8, at::Ten
         "fp8_quant2");
 }
 
+// --------------------------------------------------------------------------- GEMM (csrc/gemm.hip)
+// Operands are given as (possibly batched) matrices whose innermost dimension is unit-stride;
+// the leading dimension is the row stride. a_col / b_col select the column-major reading of
+// the csrc/gemm.hip header. epi 0: bf16 C = alpha*acc + bias; 1: fp32 C = alpha*acc;
+// 2: fp32 C += alpha*acc.
+int64_t ld_of(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.dim() == 2 || t.dim() == 3, name, " must be 2-D or batched 3-D");
+  TORCH_CHECK(t.stride(-1) == 1, name, " must have a unit-stride last dimension");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-B aligned");
+  const int64_t ld = t.dim() == 2 ? t.stride(0) : t.stride(1);
+  TORCH_CHECK(ld % 8 == 0, name, " row stride must be a multiple of 8 elements");
+  return ld;
+}
+
+void gemm(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t M, int64_t N, int64_t K, bool a_col,
+          bool b_col, int64_t epi, double alpha, int64_t cfg, OptT alpha_dev, int64_t Ml, int64_t Nl, int64_t Kl) {
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: bf16 operands");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm: epi 0..2");
+  TORCH_CHECK(C.scalar_type() == (epi == 0 ? at::kBFloat16 : at::kFloat), "gemm: C dtype does not match epi");
+  const int64_t lda = ld_of(A, "A"), ldb = ld_of(B, "B"), ldc = ld_of(C, "C");
+  const int64_t batch = A.dim() == 3 ? A.size(0) : 1;
+  TORCH_CHECK(B.dim() == A.dim() && C.dim() == A.dim(), "gemm: operands must all be 2-D or all 3-D");
+  if (batch > 1) TORCH_CHECK(B.size(0) == batch && C.size(0) == batch, "gemm: batch mismatch");
+  // stored extents: a col-mode operand may be padded to Ml/Nl columns and hold only Kl k-rows
+  const int64_t Mx = Ml ? Ml : M, Nx = Nl ? Nl : N, Kx = Kl ? Kl : K;
+  const int64_t ar = a_col ? Kx : M, ac = a_col ? Mx : K, br = b_col ? Kx : N, bc = b_col ? Nx : K;
+  TORCH_CHECK(A.size(-2) == ar && A.size(-1) == ac, "gemm: A shape");
+  TORCH_CHECK(B.size(-2) == br && B.size(-1) == bc, "gemm: B shape");
+  const float* ad = nullptr;
+  if (alpha_dev.has_value() && alpha_dev->defined()) {
+    TORCH_CHECK(alpha_dev->is_cuda() && alpha_dev->scalar_type() == at::kFloat && alpha_dev->numel() == 1,
+                "gemm: alpha_dev must be one fp32 device scalar");
+    ad = alpha_dev->data_ptr<float>();
+  }
+  TORCH_CHECK(C.size(-2) == M && C.size(-1) == N, "gemm: C shape");
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(epi == 0 && bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                "gemm: bias must be bf16 [N] (epi 0)");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(bias->data_ptr()) & 7) == 0, "gemm: bias 8-B aligned");
+    bp = bias->data_ptr();
+  }
+  const int64_t sA = batch > 1 ? A.stride(0) : 0, sB = batch > 1 ? B.stride(0) : 0, sC = batch > 1 ? C.stride(0) : 0;
+  check(ds2_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, ad, (int)M, (int)N, (int)K, (int)lda, (int)ldb,
+                 (int)ldc, (int)Ml, (int)Nl, (int)Kl, a_col ? 1 : 0, b_col ? 1 : 0, (int)epi, (float)alpha, (int)batch,
+                 sA, sB, sC, (int)cfg, cur_stream()),
+        "gemm");
+}
+
+// FC head + CTC (training): h [T, N, H] bf16, W [K, H] bf16, bias [K] bf16 -> loss [N] fp32,
+// G [T*N, 32] bf16 (per-utterance dloss/dlogits, zero-padded classes)
+void head_ctc(at::Tensor h, at::Tensor W, at::Tensor bias, at::Tensor lens, at::Tensor labels, at::Tensor label_lens,
+              at::Tensor loss, at::Tensor G, at::Tensor ws, int64_t blank, bool zero_inf) {
+  for (auto* t : {&h, &W, &bias, &lens, &labels, &label_lens, &loss, &G, &ws}) need_gpu(*t, "head_ctc operand");
+  TORCH_CHECK(h.dim() == 3 && h.scalar_type() == at::kBFloat16, "h: [T, N, H] bf16");
+  const int64_t T = h.size(0), N = h.size(1), H = h.size(2), K = W.size(0);
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 && W.dim() == 2 && W.size(1) == H, "W: [K, H] bf16");
+  TORCH_CHECK(bias.scalar_type() == at::kBFloat16 && bias.numel() == K, "bias: [K] bf16");
+  TORCH_CHECK(K <= 32 && H % 32 == 0, "head_ctc: K <= 32 classes and H % 32 == 0");
+  TORCH_CHECK(lens.scalar_type() == at::kInt && lens.numel() == N, "lens: [N] int32");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.dim() == 2 && labels.size(0) == N, "labels: [N, Lmax] int32");
+  TORCH_CHECK(label_lens.scalar_type() == at::kInt && label_lens.numel() == N, "label_lens: [N] int32");
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.numel() == N, "loss: [N] fp32");
+  TORCH_CHECK(G.scalar_type() == at::kBFloat16 && G.numel() == T * N * 32, "G: [T*N, 32] bf16");
+  const int64_t Lmax = labels.size(1);
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= ds2_ctc_ws_floats((int)T, (int)N, (int)Lmax),
+              "head_ctc: workspace too small");
+  check(ds2_head_ctc(h.data_ptr(), W.data_ptr(), bias.data_ptr(), lens.data_ptr<int>(), labels.data_ptr<int>(),
+                     label_lens.data_ptr<int>(), loss.data_ptr<float>(), G.data_ptr(), ws.data_ptr<float>(), (int)T,
+                     (int)N, (int)H, (int)K, (int)Lmax, (int)blank, zero_inf ? 1 : 0, cur_stream()),
+        "head_ctc");
+}
+
+// FC head alone: logits [M, K] (fp32 or bf16) = h [M, H] W^T + b
+void fc_logits(at::Tensor h, at::Tensor W, at::Tensor bias, at::Tensor logits) {
+  for (auto* t : {&h, &W, &bias, &logits}) need_gpu(*t, "fc_logits operand");
+  const int64_t H = h.size(-1), M = h.numel() / H, K = W.size(0);
+  TORCH_CHECK(h.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 && bias.scalar_type() == at::kBFloat16,
+              "fc_logits: bf16 h / W / bias");
+  TORCH_CHECK(W.size(1) == H && bias.numel() == K && logits.numel() == M * K && K <= 32 && H % 32 == 0,
+              "fc_logits: shapes");
+  check(ds2_fc_logits(h.data_ptr(), W.data_ptr(), bias.data_ptr(), logits.data_ptr(), is_bf16(logits), (int)M, (int)H,
+                      (int)K, cur_stream()),
+        "fc_logits");
+}
+
+py::tuple gemm_tile(int64_t cfg) {
+  int bm = 0, bn = 0;
+  TORCH_CHECK(ds2_gemm_tile((int)cfg, &bm, &bn) == 0, "gemm_tile: bad cfg");
+  return py::make_tuple(bm, bn);
+}
+
 // --------------------------------------------------------------------------- device info
 py::dict device_info(int64_t dev) {
   hipDeviceProp_t prop;
@@ -677,4 +779,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_cl_finalize", &bn_cl_finalize);
   m.def("bn_cl_apply", &bn_cl_apply);
   m.def("bn_cl_bwd", &bn_cl_bwd);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("a_col"), py::arg("b_col"), py::arg("epi"), py::arg("alpha"), py::arg("cfg"),
+        py::arg("alpha_dev") = py::none(), py::arg("Ml") = 0, py::arg("Nl") = 0, py::arg("Kl") = 0);
+  m.def("gemm_tile", &gemm_tile);
+  m.def("head_ctc", &head_ctc);
+  m.def("fc_logits", &fc_logits);
 }

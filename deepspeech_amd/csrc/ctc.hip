@@ -17,6 +17,15 @@
 //                         reduction, label states with per-wave LDS atomics, then
 //                         grad[t][k] = softmax_t(k) - occ_t(k). Frames past the length get 0.
 // Infeasible utterances (logP = -inf) get loss 0 and zero gradient when zero_inf != 0.
+//
+// Training path with the FC head fused in (ds2_head_ctc; reference FC + CTC at
+// src/deepSpeech_NCHW.py:188-198,225): the logits never reach memory.
+//   0. fc_lsm_kernel      logits = h W_fc^T + b on MFMA (16 frames per wave, W_fc in LDS),
+//                         log-softmax in registers, lp rows straight into the workspace
+//   2. ctc_recur_kernel   as above
+//   3. ctc_grad_lp_kernel gradient from lp (no logits re-read), written as a zero-padded
+//                         [T*N][32] bf16 matrix: the operand of the FC backward GEMMs
+//                         (dh = G W_fc, dW_fc = G^T h in csrc/gemm.hip)
 #include "common.h"
 
 using namespace ds2;
@@ -257,6 +266,147 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const LT* __restrict__ lo
   }
 }
 
+// ---------------------------------------------------------------- 0. FC + log-softmax
+// One wave per 16 frames (rows m = t*N + b of the time-major h). MFMA operands swapped
+// (D = W.h^T) so lane l ends with row m = l&15 and classes 4(l>>4)+j (+16): a row's 32
+// values sit in 4 lanes (l, l^16, l^32, l^48) and the row max / sum are two shuffles.
+constexpr int FC_WAVES = 4;
+template <typename OT>
+__global__ __launch_bounds__(FC_WAVES * 64) void fc_lsm_kernel(const bf16_t* __restrict__ h, const bf16_t* __restrict__ W,
+                                                             const bf16_t* __restrict__ bias,
+                                                             const int* __restrict__ lens, float* __restrict__ lp_ws,
+                                                             OT* __restrict__ logits, int T, int N, int H, int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int pitch = H * 2 + 16;                     // padded rows: 16 consecutive rows -> 16 distinct slots
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // stage W_fc (K <= 32 rows, zero rows past K) as [32][H] bf16
+  const int cpr = H / 8;
+  for (int q = tid; q < 32 * cpr; q += FC_WAVES * 64) {
+    const int r = q / cpr, c = q - r * cpr;
+    i32x4 v = {0, 0, 0, 0};
+    if (r < K) v = *reinterpret_cast<const i32x4*>(W + (size_t)r * H + 8 * c);
+    *reinterpret_cast<i32x4*>(smem + r * pitch + 16 * c) = v;
+  }
+  __syncthreads();
+  const int M = T * N;
+  const int blk = blockIdx.x * FC_WAVES + wave;
+  if (blk * 16 >= M) return;
+  const int mrow = blk * 16 + (lane & 15);
+  const bf16_t* hr = h + (size_t)min(mrow, M - 1) * H + 8 * (lane >> 4);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const unsigned char* w0 = smem + (lane & 15) * pitch + 16 * (lane >> 4);
+  const unsigned char* w1 = w0 + 16 * pitch;
+  const int KS = H / 32;
+  constexpr int CH = 5;                              // A fragments in flight per lane
+  for (int k0 = 0; k0 < KS; k0 += CH) {
+    bf16x8 af[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) af[i] = *reinterpret_cast<const bf16x8*>(hr + 32 * min(k0 + i, KS - 1));
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (k0 + i < KS) {
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(w0 + 64 * (k0 + i));
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(w1 + 64 * (k0 + i));
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0, af[i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, af[i], acc1, 0, 0, 0);
+      }
+    }
+  }
+  const int g = lane >> 4;
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n0 = 4 * g + j, n1 = 16 + 4 * g + j;
+    x[j] = n0 < K ? acc0[j] + bf2f(bias[n0]) : NEG_INF;
+    x[4 + j] = n1 < K ? acc1[j] + bf2f(bias[n1]) : NEG_INF;
+  }
+  float m = x[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) m = fmaxf(m, x[j]);
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float e = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e += __expf(x[j] - m);
+  e += __shfl_xor(e, 16, 64);
+  e += __shfl_xor(e, 32, 64);
+  const float lz = m + __logf(e);
+  if (mrow < M) {
+    const int t = mrow / N, b = mrow - (mrow / N) * N;
+    if (lp_ws && t < lens[b]) {
+      float4* o = reinterpret_cast<float4*>(lp_ws + ((size_t)b * T + t) * KPAD);
+      o[g] = make_float4(x[0] - lz, x[1] - lz, x[2] - lz, x[3] - lz);
+      o[4 + g] = make_float4(x[4] - lz, x[5] - lz, x[6] - lz, x[7] - lz);
+    }
+    if (logits) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (4 * g + j < K) st_grad<OT>(logits + (size_t)mrow * K + 4 * g + j, x[j]);
+        if (16 + 4 * g + j < K) st_grad<OT>(logits + (size_t)mrow * K + 16 + 4 * g + j, x[4 + j]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- 3'. gradient from lp
+// As ctc_grad_kernel, reading lp_t(k) from the workspace; G[t*N+b][0..31] = p - occ (bf16),
+// zero past the length / for infeasible utterances / in the padding classes.
+__global__ __launch_bounds__(256) void ctc_grad_lp_kernel(const int* __restrict__ lens, const int* __restrict__ labels,
+                                                        const int* __restrict__ label_lens,
+                                                        const float* __restrict__ lp_ws,
+                                                        const float* __restrict__ ab_ws,
+                                                        const float* __restrict__ logp_in, float* __restrict__ loss,
+                                                        bf16_t* __restrict__ G, int T, int N, int K, int Lmax, int SPS,
+                                                        int blank, int zero_inf) {
+  __shared__ float occ_s[4][KPAD];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + wv;
+  if (w >= T * N) return;
+  const int t = w / N, b = w % N;
+  const int len = min(lens[b], T);
+  const int L = label_lens[b];
+  const float logp = (len > 0 && L <= len) ? logp_in[b] : NEG_INF;
+  const bool feasible = logp > NEG_INF;
+  if (t == 0 && lane == 0) loss[b] = feasible ? -logp : (zero_inf ? 0.f : INFINITY);
+  bf16_t* g = G + (size_t)w * KPAD;
+  if (t >= len || !feasible) {
+    if (lane < KPAD) g[lane] = 0;
+    return;
+  }
+  float* occ = occ_s[wv];
+  if (lane < KPAD) occ[lane] = 0.f;
+  const float lpk = (lane < K) ? lp_ws[((size_t)b * T + t) * KPAD + lane] : NEG_INF;
+  const int SP = 2 * L + 1;
+  const float* A = ab_ws + ((size_t)b * T + t) * SPS;
+  const float* B = ab_ws + ((size_t)(N + b) * T + t) * SPS;
+  float blank_acc = 0.f;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  for (int base = 0; base < SP; base += 64) {
+    const int s = base + lane;
+    const bool in = s < SP;
+    const int c = in ? state_class(labels, b, Lmax, s, blank) : blank;
+    const float lc = __shfl(lpk, c, 64);
+    float e = 0.f;
+    if (in) {
+      const float ga = A[s] + B[s] - lc - logp;
+      e = (ga > -80.f) ? __expf(ga) : 0.f;
+    }
+    if (in && c != blank) atomicAdd(&occ[c], e);
+    else blank_acc += e;
+  }
+  blank_acc = wave_sum(blank_acc);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  if (lane < KPAD) {
+    float v = 0.f;
+    if (lane < K) {
+      const float p = __expf(lpk);
+      const float o = (lane == blank) ? blank_acc : occ[lane];
+      v = p - o;
+    }
+    g[lane] = f2bf(v);
+  }
+}
+
 template <int SPL>
 static void launch_recur(const int* lens, const int* labels, const int* label_lens, const float* lp_ws, float* ab_ws,
                          float* logp, int T, int N, int Lmax, int SPmax, int blank, hipStream_t st) {
@@ -308,6 +458,65 @@ int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const in
   else
     hipLaunchKernelGGL(ctc_grad_kernel<float>, g4, dim3(256), 0, st, (const float*)logits, lens, labels, label_lens,
                        ab_ws, logp, loss, (float*)grad, T, N, K, Lmax, SPS, blank, zero_inf);
+  return (int)hipGetLastError();
+}
+
+// W_fc staged in LDS: > 64 KB for H > 1000 needs the opt-in (160 KB per CU on gfx950)
+static int fc_attr(int lds) {
+  static int done = 0;
+  if (lds > 64 * 1024 && !done) {
+    hipError_t e = hipFuncSetAttribute((const void*)fc_lsm_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)fc_lsm_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    done = 1;
+  }
+  return lds > 160 * 1024 ? (int)hipErrorInvalidValue : 0;
+}
+
+// FC head + CTC for training: h [T*N][H] bf16 (time-major rows), W [K][H] bf16, bias [K] bf16.
+// Outputs loss [N] and G [T*N][32] bf16 (dloss_b/dlogits, zero-padded). ws as ds2_ctc_ws_floats.
+int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens, const int* labels,
+                 const int* label_lens, float* loss, void* G, float* ws, int T, int N, int H, int K, int Lmax,
+                 int blank, int zero_inf, hipStream_t st) {
+  if (K > KPAD || H % 32 != 0) return -20;
+  const int SPmax = 2 * Lmax + 1;
+  if (SPmax > 64 * 32) return -21;
+  const int spl = ctc_spl(SPmax);
+  const int SPS = 64 * spl;
+  float* lp_ws = ws;
+  float* ab_ws = lp_ws + (size_t)N * T * KPAD;
+  float* logp = ab_ws + 2 * (size_t)N * T * SPS;
+  const int M = T * N;
+  const int lds = 32 * (H * 2 + 16);
+  if (const int e = fc_attr(lds)) return e;
+  hipLaunchKernelGGL(fc_lsm_kernel<float>, dim3((M + 16 * FC_WAVES - 1) / (16 * FC_WAVES)), dim3(FC_WAVES * 64), lds,
+                     st, (const bf16_t*)h, (const bf16_t*)W, (const bf16_t*)bias, lens, lp_ws, (float*)nullptr, T, N,
+                     H, K);
+  if (spl == 4) launch_recur<4>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else if (spl == 8) launch_recur<8>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else if (spl == 16) launch_recur<16>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  else launch_recur<32>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  hipLaunchKernelGGL(ctc_grad_lp_kernel, dim3((M + 3) / 4), dim3(256), 0, st, lens, labels, label_lens, lp_ws, ab_ws,
+                     logp, loss, (bf16_t*)G, T, N, K, Lmax, SPS, blank, zero_inf);
+  return (int)hipGetLastError();
+}
+
+// FC head alone (inference): logits [T*N][K] (fp32 or bf16) = h W^T + b.
+int ds2_fc_logits(const void* h, const void* W, const void* bias, void* logits, int out_bf16, int M, int H, int K,
+                  hipStream_t st) {
+  if (K > KPAD || H % 32 != 0) return -20;
+  const int lds = 32 * (H * 2 + 16);
+  if (const int e = fc_attr(lds)) return e;
+  const dim3 grid((M + 16 * FC_WAVES - 1) / (16 * FC_WAVES));
+  if (out_bf16)
+    hipLaunchKernelGGL(fc_lsm_kernel<bf16_t>, grid, dim3(FC_WAVES * 64), lds, st, (const bf16_t*)h, (const bf16_t*)W,
+                       (const bf16_t*)bias, (const int*)nullptr, (float*)nullptr, (bf16_t*)logits, M, 1, H, K);
+  else
+    hipLaunchKernelGGL(fc_lsm_kernel<float>, grid, dim3(FC_WAVES * 64), lds, st, (const bf16_t*)h, (const bf16_t*)W,
+                       (const bf16_t*)bias, (const int*)nullptr, (float*)nullptr, (float*)logits, M, 1, H, K);
   return (int)hipGetLastError();
 }
 

@@ -299,6 +299,20 @@ class DeepSpeech2(nn.Module):
         h = self.recurrent(x, lens.to(x.device))
         return self.head(h), lens
 
+    def forward_loss(self, feats: torch.Tensor, seq_lens: torch.Tensor, targets: torch.Tensor,
+                     target_lens: torch.Tensor) -> torch.Tensor:
+        """Training forward: mean CTC loss of a batch. On the HIP engine the FC head and the
+        CTC loss are one fused op (ops/ctc.py FusedHeadCTC: the logits never reach memory);
+        otherwise forward() + loss()."""
+        if self.engine == "hip" and self.num_classes <= 32 and self.num_hidden % 32 == 0:
+            from ..ops import ctc as CTC
+            lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
+            x = self.frontend(feats.to(self.compute_dtype))
+            h = self.recurrent(x, lens.to(x.device))
+            return CTC.head_ctc_mean_loss_hip(h, self.fc_weight, self.fc_bias, lens, targets, target_lens)
+        logits, lens = self(feats, seq_lens)
+        return self.loss(logits, lens, targets, target_lens)
+
     # ------------------------------------------------------------------ loss
     def loss(self, logits: torch.Tensor, lens: torch.Tensor, targets: torch.Tensor,
              target_lens: torch.Tensor) -> torch.Tensor:

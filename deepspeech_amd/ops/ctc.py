@@ -67,6 +67,105 @@ class CTCMeanFused(CTCLossFused):
             return grad * (gloss / ctx.n), None, None, None, None, None
 
 
+class FusedHeadCTC(torch.autograd.Function):
+    """Mean CTC loss of the FC head's logits without materialising them (training path).
+
+    forward : csrc/ctc.hip ds2_head_ctc — FC on MFMA + log-softmax in registers -> lp
+              workspace -> alpha/beta recursion -> G = dloss_b/dlogits [T*N, 32] bf16
+    backward: scale = gloss / N as a DEVICE scalar folded into the GEMM epilogues (no sync)
+              dh     = scale * G W_fc          csrc/gemm.hip, critical path (feeds the top BPTT)
+              dW_fc  = scale * G^T h           csrc/gemm.hip, weight-gradient side stream
+              db_fc  = scale * sum_rows G      side stream
+    Reference: FC src/deepSpeech_NCHW.py:188-198, CTC :225 (blank = last class)."""
+
+    @staticmethod
+    def forward(ctx, h, weight, bias, lens, labels, label_lens, blank: int, zero_infinity: bool):
+        from .optim import arena_of
+        C = _ext.ext()
+        T, N, H = h.shape
+        K = weight.shape[0]
+        dev = h.device
+        h = h.to(torch.bfloat16).contiguous()
+        w16 = weight.bf16 if arena_of(weight) is not None else weight.detach().to(torch.bfloat16).contiguous()
+        b16 = bias.bf16 if arena_of(bias) is not None else bias.detach().to(torch.bfloat16).contiguous()
+        labels = labels.to(device=dev, dtype=torch.int32).contiguous()
+        if labels.dim() == 1:
+            labels = labels.view(N, -1)
+        if labels.shape[1] == 0:
+            labels = torch.zeros(N, 1, device=dev, dtype=torch.int32)
+        lens = lens.to(device=dev, dtype=torch.int32).contiguous()
+        label_lens = label_lens.to(device=dev, dtype=torch.int32).contiguous()
+        loss = torch.empty(N, device=dev, dtype=torch.float32)
+        G = torch.empty(T * N, 32, device=dev, dtype=torch.bfloat16)
+        ws = torch.empty(int(C.ctc_ws_floats(T, N, labels.shape[1])), device=dev, dtype=torch.float32)
+        C.head_ctc(h, w16, b16, lens, labels, label_lens, loss, G, ws, blank, zero_infinity)
+        ctx.save_for_backward(h, G, w16)
+        ctx.params = (weight, bias)
+        ctx.K = K
+        return loss.mean()
+
+    @staticmethod
+    def backward(ctx, gloss):
+        with TR.phase(TR.CTC_B):
+            return FusedHeadCTC._backward(ctx, gloss)
+
+    @staticmethod
+    def _backward(ctx, gloss):
+        from . import gemm as GM
+        from .optim import arena_of, emit_grad
+        from .rnn import wgrad_stream
+        h, G, w16 = ctx.saved_tensors
+        weight, bias = ctx.params
+        T, N, H = h.shape
+        K = ctx.K
+        M = T * N
+        scale = (gloss.to(torch.float32) / N).reshape(1).contiguous()
+        h2 = h.view(M, H)
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dh = torch.empty(M, H, device=h.device, dtype=torch.bfloat16)
+            # K = 32 padded classes; rows >= K of W_fc are never loaded (Kl) and meet G's zero columns
+            GM.gemm(G, w16, dh, M, H, 32, False, True, 0, 1.0, None, alpha_dev=scale, Kl=K)
+            dh = dh.view(T, N, H)
+        side = wgrad_stream(h.device) if (arena_of(weight) is not None and arena_of(bias) is not None) else None
+        if side is None:
+            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, scale, K)
+            return dh, gw, gb, None, None, None, None, None
+        side.wait_stream(torch.cuda.current_stream(h.device))
+        with torch.cuda.stream(side):
+            for t in (G, h2, scale):
+                t.record_stream(side)
+            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, scale, K)
+        return dh, gw, gb, None, None, None, None, None
+
+    @staticmethod
+    def _weight_grads(weight, bias, G, h2, scale, K):
+        from . import gemm as GM
+        from .optim import arena_of, emit_grad
+        M, H = h2.shape
+        a = arena_of(weight)
+        if a is not None:
+            # M = K rows stored; G is read as a [M_rows, 32]-column col-mode operand (Ml = 32)
+            GM.gemm(G, h2, weight.main_grad, K, H, M, True, True, 1 if a.first_write(weight) else 2, 1.0, None,
+                    alpha_dev=scale, Ml=32)
+            a.grad_done(weight)
+            gw = None
+        else:
+            out = torch.empty(K, H, device=h2.device, dtype=torch.float32)
+            GM.gemm(G, h2, out, K, H, M, True, True, 1, 1.0, None, alpha_dev=scale, Ml=32)
+            gw = out
+        gb = emit_grad(bias, G[:, :K].sum(0, dtype=torch.float32) * scale)
+        return gw, gb
+
+
+def head_ctc_mean_loss_hip(h: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, lens: torch.Tensor,
+                           labels: torch.Tensor, label_lens: torch.Tensor, blank: int = BLANK,
+                           zero_infinity: bool = True) -> torch.Tensor:
+    """FC head + mean CTC loss in one fused op (HIP engine training path)."""
+    with TR.phase(TR.CTC_F):
+        return FusedHeadCTC.apply(h, weight, bias, lens, labels, label_lens, blank, zero_infinity)
+
+
 def ctc_mean_loss_hip(logits: torch.Tensor, lens: torch.Tensor, labels: torch.Tensor,
                       label_lens: torch.Tensor, blank: int = BLANK, zero_infinity: bool = True) -> torch.Tensor:
     """Mean CTC loss over the batch (fp32 scalar)."""

@@ -294,8 +294,14 @@ class FusedHead(torch.autograd.Function):
         T, N, H = h.shape
         w16 = weight.bf16 if arena_of(weight) is not None else weight.to(torch.bfloat16)
         b16 = bias.bf16 if arena_of(bias) is not None else bias.to(torch.bfloat16)
-        h2 = h.to(torch.bfloat16).reshape(T * N, H)
-        out = torch.addmm(b16, h2, w16.t()).view(T, N, -1)
+        h2 = h.to(torch.bfloat16).reshape(T * N, H).contiguous()
+        K = w16.shape[0]
+        if K <= 32 and H % 32 == 0:
+            # csrc/ctc.hip fc_lsm_kernel: MFMA FC, W_fc staged in LDS, logits in bf16
+            out = torch.empty(T, N, K, device=h.device, dtype=torch.bfloat16)
+            _ext.ext().fc_logits(h2, w16.contiguous(), b16.contiguous(), out)
+        else:
+            out = torch.addmm(b16, h2, w16.t()).view(T, N, -1)
         ctx.save_for_backward(h2, w16)
         ctx.params = (weight, bias)
         return out

@@ -1,0 +1,170 @@
+"""Python front for the hand-written MFMA GEMM family (csrc/gemm.hip).
+
+Every GEMM of a recurrent layer runs here on the HIP engine (reference call sites
+src/custom_ops.py:59-67 for W.x / U.h, src/deepSpeech_NCHW.py:188-198 for the FC):
+
+  linear(x, W, b, alpha)   gx = alpha * x W^T + b            bf16 out (forward projection)
+  mm_nn(a, b)              a [M,K] . b [K,N]                  bf16 out (input gradient dx = dgx W)
+  mm_tn(a, b, out, acc)    a^T . b, a [K,M], b [K,N]          fp32 into ``out`` (weight gradients),
+                           batched over a leading dim          ``acc`` adds instead of overwriting
+
+Tile choice: per (shape, layout) from a small table measured on MI355X
+(tools/bench_gemm_ours.py), else a model that minimises the padded work of the last
+dispatch round. DS2_GEMM_CFG=<0..5> forces one tile for every call (tuning only).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _ext
+
+# cfg -> (BM, BN, workgroups per CU); LDS = 2 stages x (BM + BN) x 64 x 2 B
+_TILES = {0: (256, 256, 1), 1: (128, 256, 1), 2: (256, 128, 1), 3: (128, 128, 2), 4: (128, 128, 1),
+          5: (128, 128, 1)}
+# measured picks: (M, N, K, a_col, b_col, batch) -> cfg
+TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
+    # headline shapes (T2=241, N=32, H=800), tools/bench_gemm_ours.py on MI355X
+    (7712, 4800, 800, False, False, 1): 1,     # projection, layers 1-4: 93 us
+    (7712, 4800, 2400, False, False, 1): 1,    # projection, layer 0: 213 us
+    (7712, 800, 4800, False, True, 1): 2,
+    (7712, 2400, 4800, False, True, 1): 2,
+    (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
+}
+_FORCE = os.environ.get("DS2_GEMM_CFG")
+# DS2_GEMM selects which engine GEMM classes run here: "hip" (all), "torch" (none: library
+# GEMMs, A/B timing only) or a comma list of {proj, dx, wgrad}. Default "proj": measured in
+# the headline step on MI355X (profiles/r2_gemm_family.md) the forward projections win
+# against the TunableOp-tuned hipBLASLt picks (9.32 vs 9.41 ms/step), while the col-mode
+# (transposed-read) dx / weight-gradient kernels still lose (dx +0.42, wgrad +0.8 ms/step).
+# The FC head's GEMMs (FusedHeadCTC) always run here.
+_SPEC = os.environ.get("DS2_GEMM", "proj")
+_CLASSES = ({"proj", "dx", "wgrad"} if _SPEC == "hip" else set() if _SPEC == "torch"
+            else {c.strip() for c in _SPEC.split(",") if c.strip()})
+
+
+def enabled(cls: str = "wgrad") -> bool:
+    return cls in _CLASSES
+
+
+def _cdiv(a: int, b: int) -> int:
+    return -(-a // b)
+
+
+def choose_cfg(M: int, N: int, K: int, a_col: bool, b_col: bool, batch: int = 1, cus: int = 256) -> int:
+    if _FORCE is not None:
+        return int(_FORCE)
+    key = (M, N, K, a_col, b_col, batch)
+    if key in TUNED:
+        return TUNED[key]
+    best, best_cost = 0, None
+    for cfg, (bm, bn, per_cu) in _TILES.items():
+        if (a_col and bm < 128) or (b_col and bn < 128):
+            continue
+        tiles = _cdiv(M, bm) * _cdiv(N, bn) * batch
+        slots = cus * per_cu
+        rounds = _cdiv(tiles, slots)
+        # time ~ rounds x per-tile time; a tile of BMxBN on 1/per_cu of a CU takes
+        # bm*bn*per_cu "units"; smaller tiles pay a staging-efficiency penalty
+        eff = {0: 1.0, 1: 0.93, 2: 0.93, 3: 0.85, 4: 0.8, 5: 0.85}[cfg]
+        cost = rounds * bm * bn * per_cu / eff
+        if best_cost is None or cost < best_cost:
+            best, best_cost = cfg, cost
+    return best
+
+
+def _dev_cus(t: torch.Tensor) -> int:
+    return _ext.num_cus(t.device.index or 0)
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int, a_col: bool, b_col: bool,
+         epi: int, alpha: float = 1.0, bias: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
+         alpha_dev: Optional[torch.Tensor] = None, Ml: int = 0, Nl: int = 0, Kl: int = 0) -> torch.Tensor:
+    """Raw launch. A/B are the STORED matrices (unit-stride last dim): A [M,K] (row) or
+    [K,M] (col), B [N,K] (row) or [K,N] (col). alpha_dev: fp32 device scalar multiplied into
+    alpha. Ml/Nl: a col-mode operand padded in memory to Ml/Nl columns; Kl: a col-mode
+    operand holding only Kl k-rows (the rest must meet zeros in the other operand)."""
+    batch = A.shape[0] if A.dim() == 3 else 1
+    if cfg is None:
+        cfg = choose_cfg(M, N, K, a_col, b_col, batch, _dev_cus(A))
+    _ext.ext().gemm(A, B, C, bias, M, N, K, a_col, b_col, epi, float(alpha), cfg, alpha_dev, Ml, Nl, Kl)
+    return C
+
+
+def supported(M: int, N: int, K: int, a_col: bool = False, b_col: bool = False) -> bool:
+    return ((a_col and b_col) or K % 8 == 0) and N % 4 == 0 and (not a_col or M % 8 == 0) and \
+        (not b_col or N % 8 == 0)
+
+
+def linear(x2: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None, alpha: float = 1.0,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """alpha * x2 @ W^T + bias; x2 [M, K], W [N, K] (bf16, unit-stride rows); bf16 [M, N]."""
+    M, K = x2.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    return gemm(x2, W, out, M, N, K, False, False, 0, alpha, bias)
+
+
+def mm_nn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a [M, K] @ b [K, N] -> bf16 [M, N]."""
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    return gemm(a, b, out, M, N, K, False, True, 0)
+
+
+def _operand(t: torch.Tensor, row_if_unit_last: bool):
+    """(stored matrix with a unit-stride last dim, col flag) for a logical 2-D operand, or
+    None if neither dimension is unit-stride."""
+    if t.stride(-1) == 1:
+        return t, not row_if_unit_last
+    if t.stride(-2) == 1:
+        return t.transpose(-1, -2), row_if_unit_last
+    return None
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
+           alpha: float = 1.0, bias: Optional[torch.Tensor] = None) -> bool:
+    """out (=|+=) alpha * a @ b (+ bias) for 2-D (or batched 3-D) bf16 views of any unit-stride
+    orientation: a [M, K], b [K, N]; out fp32 (store / accumulate) or bf16 (store, optional
+    bias). Returns False (nothing launched) when the shape or strides are not covered."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+        return False
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    oa, ob = _operand(a, True), _operand(b, False)
+    if oa is None or ob is None or out.stride(-1) != 1:
+        return False
+    A, a_col = oa          # a [M,K] unit-stride K -> row mode (A(m,k) = A[m*lda+k])
+    B, b_col = ob          # b [K,N] unit-stride N -> col mode (B(n,k) = B[k*ldb+n])
+    if not supported(M, N, K, a_col, b_col):
+        return False
+    for t in (A, B, out):
+        if t.data_ptr() % 16 or (t.dim() >= 2 and t.stride(-2) % 8):
+            return False
+    if out.dtype == torch.bfloat16:
+        if accumulate:
+            return False
+        epi = 0
+    else:
+        epi = 2 if accumulate else 1
+        if bias is not None:
+            return False
+    gemm(A, B, out, M, N, K, a_col, b_col, epi, alpha, bias)
+    return True
+
+
+def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False,
+          alpha: float = 1.0) -> torch.Tensor:
+    """a^T @ b in fp32: a [(batch,) K, M], b [(batch,) K, N] -> out [(batch,) M, N] (written, or
+    added to when ``accumulate``)."""
+    K, M = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    if out is None:
+        shp = (a.shape[0], M, N) if a.dim() == 3 else (M, N)
+        out = torch.empty(shp, device=a.device, dtype=torch.float32)
+    return gemm(a, b, out, M, N, K, True, True, 2 if accumulate else 1, alpha)

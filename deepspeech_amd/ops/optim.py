@@ -210,13 +210,20 @@ def mm_into(p, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = N
     Arena-managed: the GEMM writes fp32 straight into ``p.main_grad`` (``out`` may name a
     larger group view of the gradient arena covering several packed parameters) and
     returns None; otherwise returns the fp32 product."""
+    from . import gemm as G
     arena = arena_of(p)
     if arena is None:
+        if G.enabled("wgrad") and a.is_cuda:
+            r = torch.empty(a.shape[0], b.shape[1], device=a.device, dtype=torch.float32)
+            if G.matmul(a, b, r):
+                return r
         try:
             return torch.mm(a, b, out_dtype=torch.float32)
         except (RuntimeError, TypeError):
             return torch.mm(a.float(), b.float())
     dst = out if out is not None else p.main_grad.view(a.shape[0], b.shape[1])
+    if G.enabled("wgrad") and G.matmul(a, b, dst, accumulate=not arena.first_write(p)):
+        return None
     if arena.first_write(p):
         try:
             torch.mm(a, b, out_dtype=torch.float32, out=dst)

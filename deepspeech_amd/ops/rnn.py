@@ -25,6 +25,7 @@ from typing import List, Optional
 import torch
 
 from . import _ext
+from . import gemm as GM
 from . import reference as R
 from .optim import arena_of, emit_grad, mm_into
 from ..utils import trace as TR
@@ -235,6 +236,30 @@ def _stamps(kind: str, plan: "RnnPlan", grid: int, dev) -> Optional[torch.Tensor
     t = torch.zeros(grid, 8, device=dev, dtype=torch.int64)
     STAMP_LOG.append((kind, plan, t))
     return t
+
+
+def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], alpha: float) -> torch.Tensor:
+    """gx = alpha * x2 W16^T + b16 (bf16): the hand-written MFMA GEMM (csrc/gemm.hip) with the
+    sequence-BN scale and the bias fused in its epilogue; library GEMM only for shapes the
+    kernel does not cover (K % 32 != 0) or under DS2_GEMM=torch."""
+    M, K = x2.shape
+    N = W16.shape[0]
+    if GM.enabled("proj") and x2.is_cuda:
+        out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+        if GM.matmul(x2, W16.t(), out, alpha=alpha, bias=b16):
+            return out
+    if b16 is None:
+        return torch.mm(x2, W16.t()) * alpha if alpha != 1.0 else torch.mm(x2, W16.t())
+    return torch.addmm(b16, x2, W16.t(), alpha=alpha)
+
+
+def _mm_bf16(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b in bf16 through csrc/gemm.hip (library GEMM for uncovered shapes)."""
+    if GM.enabled("dx") and a.is_cuda:
+        out = torch.empty(a.shape[0], b.shape[1], device=a.device, dtype=torch.bfloat16)
+        if GM.matmul(a, b, out):
+            return out
+    return torch.mm(a, b)
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -503,7 +528,7 @@ class FusedBiLayer(torch.autograd.Function):
         if fp8:
             gx = fp8_linear(x2, W16, b16, alpha).view(T, N, -1)
         else:
-            gx = torch.addmm(b16, x2, W16.t(), alpha=alpha).view(T, N, -1)
+            gx = _linear(x2, W16, b16, alpha).view(T, N, -1)
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
@@ -533,7 +558,7 @@ class FusedBiLayer(torch.autograd.Function):
         dgx, dgh, parts = _run_bwd(dy, lens, [U_f16, U_b16 if d1 else None], hx, hs, gates, plan,
                                    plan.ndir * GH, dgx_scale=ctx.alpha)
         dgx2 = dgx.view(T * N, plan.ndir * GH)
-        dx = torch.mm(dgx2, W16).view(T, N, D) if ctx.needs_input_grad[0] else None
+        dx = _mm_bf16(dgx2, W16).view(T, N, D) if ctx.needs_input_grad[0] else None
         # ---- weight gradients (off the critical path) ----
         # only arena-managed weights (gradients written to main_grad, nothing returned to
         # autograd) may be produced on another stream; the Trainer joins it before Adam
@@ -588,10 +613,11 @@ class FusedBiLayer(torch.autograd.Function):
                 g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
                 h3 = hx[:, :steps].reshape(2, steps * plan.NP, plan.H)
                 out = ugrp.view(2, GH, plan.H)
-                try:
-                    torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
-                except (RuntimeError, TypeError):
-                    out.copy_(torch.bmm(g3, h3))
+                if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out)):
+                    try:
+                        torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
+                    except (RuntimeError, TypeError):
+                        out.copy_(torch.bmm(g3, h3))
                 arena.grad_done(U_f, U_b)
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
             if _defer_input_wgrad and on_side and ctx.idx == 0 and _TAIL_DU:
@@ -734,11 +760,11 @@ def input_projection_hip(layer, x: torch.Tensor, lens: torch.Tensor) -> torch.Te
     x2 = x.reshape(T * N, D)
     if layer.seq_bn == "frozen":
         # moving stats are constant (mean 0, var 1): SBN is a scalar scale folded into the GEMM
-        gx = torch.addmm(b, x2, W.t(), alpha=sbn_scale())
+        gx = _linear(x2, W, b, sbn_scale())
     elif layer.seq_bn == "none":
-        gx = torch.addmm(b, x2, W.t())
+        gx = _linear(x2, W, b, 1.0)
     else:
-        y = (x2 @ W.t()).view(T, N, -1)
+        y = _linear(x2, W, None, 1.0).view(T, N, -1)
         outs = []
         GH = dirs[0].W.shape[0]
         for i, d in enumerate(dirs):
@@ -777,7 +803,7 @@ def recurrent_layer_infer(layer, x: torch.Tensor, lens: torch.Tensor, h0: Option
     if layer.seq_bn == "batch":
         gx = input_projection_hip(layer, x.to(torch.bfloat16), lens)
     else:
-        gx = torch.addmm(b16, x.to(torch.bfloat16).reshape(T * N, -1), W16.t(), alpha=alpha).view(T, N, -1)
+        gx = _linear(x.to(torch.bfloat16).reshape(T * N, -1), W16, b16, alpha).view(T, N, -1)
     lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
     y, (hx, hs, gates) = _run_fwd(gx.contiguous(), lens, U, bh, plan, h0=h0)
     return y, hs[:, T, :N].clone()

@@ -91,8 +91,7 @@ class Trainer:
         lazy = model.engine == "hip"
         discard_deferred_wgrads()
         self.arena.zero_grad(lazy=lazy)
-        logits, lens = model(batch["feats"], batch["seq_lens"])
-        loss = model.loss(logits, lens, batch["labels"], batch["label_lens"])
+        loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
         loss.backward()
         join_wgrad_streams()
         if lazy:

@@ -21,36 +21,26 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def _pair(cuda, cell, H, L, seq_bn="frozen"):
+def _pair(cuda, cell, H, L, seq_bn="frozen", C=32):
+    """fp32 reference engine + HIP engine copies. C = 32 filters: the hand-written
+    channels-last conv kernels (other widths take the library-conv path)."""
     torch.manual_seed(11)
-    ref = DeepSpeech2(num_filters=8, num_hidden=H, num_rnn_layers=L, cell=cell, seq_bn=seq_bn).to(cuda)
+    ref = DeepSpeech2(num_filters=C, num_hidden=H, num_rnn_layers=L, cell=cell, seq_bn=seq_bn).to(cuda)
     hip = copy.deepcopy(ref)
     ref.set_engine("ref", torch.float32)
     hip.set_engine("hip", torch.bfloat16)
     return ref, hip
 
 
-def _loss(model, batch):
+def _loss(model, batch, fused=False):
     model.train()
+    if fused:
+        return model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
     logits, lens = model(batch["feats"], batch["seq_lens"])
     return model.loss(logits, lens, batch["labels"], batch["label_lens"])
 
 
-@pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
-@pytest.mark.parametrize("use_arena", [True, False])
-def test_model_grads_match_reference(cuda, cell, use_arena):
-    from deepspeech_amd.ops import rnn as RNN
-    ref, hip = _pair(cuda, cell, H=64, L=2)
-    batch = to_device(FixedShapeBatches(6, max_frames=260, seed=3, pool=1).next(), cuda)
-    arena = ParamArena(hip, bf16_shadow=True) if use_arena else None
-    if arena is not None:
-        arena.zero_grad()
-    lh = _loss(hip, batch)
-    lh.backward()
-    lr = _loss(ref, batch)
-    lr.backward()
-    torch.cuda.synchronize()
-    RNN.check_errors()
+def _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=None):
     assert abs(float(lh) - float(lr)) / abs(float(lr)) < 3e-2, (float(lh), float(lr))
     gref = dict((n, p.grad) for n, p in ref.named_parameters())
     errs, bad = {}, []
@@ -64,14 +54,93 @@ def test_model_grads_match_reference(cuda, cell, use_arena):
             if errs[n] > 1e-6:
                 bad.append(n)
             continue
-        errs[n] = _rel(g, gr)
+        errs[n] = round(_rel(g, gr), 5)
         # bf16 activations end to end: the conv front-end sits below every recurrent
         # layer, so its gradients carry the most accumulated rounding
         # (ReLU-RNN: bf16 rounding also flips clip masks, so the front-end sees more)
-        tol = (0.12 if cell == "gru" else 0.2) if n.startswith("conv") else 0.06
+        tol = (tol_conv or (0.12 if cell == "gru" else 0.2)) if n.startswith("conv") else tol_rnn
         if errs[n] > tol:
             bad.append(n)
-    assert not bad, (bad, errs)
+    assert not bad, ("loss hip %.5f ref %.5f" % (float(lh), float(lr)), bad, errs)
+    return errs
+
+
+@pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
+@pytest.mark.parametrize("use_arena,fused", [(True, True), (True, False), (False, True)])
+def test_model_grads_match_reference(cuda, cell, use_arena, fused):
+    """fused=True: the training path (FC head + CTC fused, ops/ctc.py FusedHeadCTC);
+    fused=False: forward() logits (fc_logits kernel) + the standalone fused CTC."""
+    from deepspeech_amd.ops import rnn as RNN
+    ref, hip = _pair(cuda, cell, H=64, L=2)
+    batch = to_device(FixedShapeBatches(6, max_frames=260, seed=3, pool=1).next(), cuda)
+    arena = ParamArena(hip, bf16_shadow=True) if use_arena else None
+    if arena is not None:
+        arena.zero_grad()
+    lh = _loss(hip, batch, fused)
+    lh.backward()
+    if arena is not None:
+        RNN.join_wgrad_streams()
+    lr = _loss(ref, batch)
+    lr.backward()
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    _compare_grads(ref, hip, lh, lr, cell)
+
+
+@pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
+def test_headline_geometry_matches_reference(cuda, cell):
+    """The headline shape end to end (32 filters, H=800, 5 layers, batch 32, 10-s
+    utterances): HIP engine (bf16, every hand-written kernel, arena + side streams) vs the
+    fp32 reference engine. The per-parameter relative errors are in the assert message."""
+    from deepspeech_amd.ops import rnn as RNN
+    ref, hip = _pair(cuda, cell, H=800, L=5)
+    batch = to_device(FixedShapeBatches(32, max_frames=1000, seed=5, pool=1).next(), cuda)
+    arena = ParamArena(hip, bf16_shadow=True)
+    arena.zero_grad()
+    lh = _loss(hip, batch, True)
+    lh.backward()
+    RNN.join_wgrad_streams()
+    lr = _loss(ref, batch)
+    lr.backward()
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    # Every recurrent / FC parameter within 6 %. The conv front-end sits under 5 bf16
+    # layers of rounding: measured on MI355X (GRU) conv1.weight 7.2 %, conv1.bn_beta 13 %
+    # (a sum over 1.2 M positions with cancellation), conv2 within 6 %.
+    _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=0.15 if cell == "gru" else 0.25)
+
+
+def test_fused_head_ctc_matches_reference(cuda):
+    """FusedHeadCTC (MFMA FC + in-register log-softmax + CTC + GEMM backward) against the
+    fp32 FC + torch CTC, gradients of h, W_fc and b_fc."""
+    from deepspeech_amd.ops import ctc as CTC
+    from deepspeech_amd.ops import reference as R
+    torch.manual_seed(2)
+    T, N, H, K = 120, 8, 256, 29
+    h = (torch.randn(T, N, H, device=cuda) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(K, H, device=cuda) * 0.1)
+    b = torch.randn(K, device=cuda) * 0.1
+    lens = torch.tensor([120, 100, 77, 120, 31, 64, 119, 90], dtype=torch.int32, device=cuda)
+    Ls = [30, 25, 20, 1, 8, 15, 40, 2]
+    labels = torch.zeros(N, max(Ls), dtype=torch.int32)
+    for i, L in enumerate(Ls):
+        labels[i, :L] = torch.randint(0, K - 1, (L,))
+    labels = labels.to(cuda)
+    lab_lens = torch.tensor(Ls, dtype=torch.int32, device=cuda)
+    Wb, bb = W.to(torch.bfloat16).float(), b.to(torch.bfloat16).float()
+    hx = h.clone().requires_grad_(True)
+    Wx, bx = Wb.clone().requires_grad_(True), bb.clone().requires_grad_(True)
+    loss = CTC.head_ctc_mean_loss_hip(hx, Wx, bx, lens, labels, lab_lens)
+    (loss * 0.5).backward()
+    hr = h.float().clone().requires_grad_(True)
+    Wr, br = Wb.clone().requires_grad_(True), bb.clone().requires_grad_(True)
+    logits = hr @ Wr.t() + br
+    lr = R.ctc_loss_ref(logits, labels, lens, lab_lens).mean()
+    (lr * 0.5).backward()
+    assert abs(float(loss) - float(lr)) / float(lr) < 2e-3, (float(loss), float(lr))
+    assert _rel(hx.grad, hr.grad) < 2e-2
+    assert _rel(Wx.grad, Wr.grad) < 2e-2
+    assert _rel(bx.grad, br.grad) < 2e-2
 
 
 def test_arena_groups_pack_directions(cuda):
@@ -89,7 +158,7 @@ def test_hip_engine_trains(cuda):
     """A few fused Adam steps on one batch lower the CTC loss (HIP engine, arena path)."""
     from deepspeech_amd.trainer import Trainer, LRSchedule
     torch.manual_seed(0)
-    m = DeepSpeech2(num_filters=8, num_hidden=128, num_rnn_layers=2, cell="gru").to(cuda)
+    m = DeepSpeech2(num_filters=32, num_hidden=128, num_rnn_layers=2, cell="gru").to(cuda)
     m.set_engine("hip", torch.bfloat16)
     tr = Trainer(m, LRSchedule(3e-3, 1000, 0.9))
     batch = to_device(FixedShapeBatches(8, max_frames=300, seed=1, pool=1).next(), cuda)
