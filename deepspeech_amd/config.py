@@ -125,8 +125,16 @@ def build_train_parser() -> argparse.ArgumentParser:
     p.add_argument("--max_frames", type=int, default=1800,
                    help="drop utterances longer than this (frames)")
     p.add_argument("--fault_inject_step", type=int, default=-1,
-                   help="testing only: raise at this step on rank --fault_inject_rank")
+                   help="testing only: kill rank --fault_inject_rank at this step (first attempt of "
+                        "an elastic job only, so a torchrun restart runs through)")
     p.add_argument("--fault_inject_rank", type=int, default=0)
+    p.add_argument("--resume", type=str, default="none", choices=["none", "auto"],
+                   help="auto: continue from the latest checkpoint in train_dir instead of wiping it "
+                        "(implied when torchrun restarts the job: TORCHELASTIC_RESTART_COUNT > 0)")
+    p.add_argument("--activation_summaries", type=str2bool, default=True,
+                   help="activation histograms + sparsity at conv1/conv2/rnn/logits on summary steps")
+    p.add_argument("--summaries_on_dummy", type=str2bool, default=False,
+                   help="write summaries in --dummy mode too (the reference skips them there)")
     return p
 
 

@@ -132,6 +132,10 @@ int ds2_gemm_tile(int cfg, int* bm, int* bn);
 int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens, const int* labels,
                  const int* label_lens, float* loss, void* G, float* ws, int T, int N, int H, int K, int Lmax,
                  int blank, int zero_inf, hipStream_t st);
+int ds2_hist_nbucket();
+int ds2_hist_blocks(long long n);
+int ds2_hist_stats(const void* x, int bf16, long long n, unsigned* counts, float* part, int blocks, hipStream_t st);
+int ds2_nonfinite_watch(const float* loss, int* counter, int* first_bad, hipStream_t st);
 int ds2_fc_logits(const void* h, const void* W, const void* bias, void* logits, int out_bf16, int M, int H, int K,
                   hipStream_t st);
 }
@@ -699,6 +703,29 @@ void fc_logits(at::Tensor h, at::Tensor W, at::Tensor bias, at::Tensor logits) {
         "fc_logits");
 }
 
+// --------------------------------------------------------------------------- summaries (csrc/stats.hip)
+void hist_stats(at::Tensor x, at::Tensor counts, at::Tensor part) {
+  need_gpu(x, "x");
+  need_gpu(counts, "counts");
+  need_gpu(part, "part");
+  TORCH_CHECK(counts.scalar_type() == at::kInt && counts.numel() == ds2_hist_nbucket(), "counts: [nbucket] int32");
+  const int blocks = ds2_hist_blocks(x.numel());
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= 6 * blocks, "part: [blocks, 6] fp32");
+  check(ds2_hist_stats(x.data_ptr(), is_bf16(x), x.numel(), reinterpret_cast<unsigned*>(counts.data_ptr<int>()),
+                       part.data_ptr<float>(), blocks, cur_stream()),
+        "hist_stats");
+}
+
+void nonfinite_watch(at::Tensor loss, at::Tensor counter, at::Tensor first_bad) {
+  need_gpu(loss, "loss");
+  need_gpu(counter, "counter");
+  need_gpu(first_bad, "first_bad");
+  TORCH_CHECK(loss.scalar_type() == at::kFloat && loss.numel() == 1, "loss: fp32 scalar");
+  TORCH_CHECK(counter.scalar_type() == at::kInt && first_bad.scalar_type() == at::kInt, "int32 words");
+  check(ds2_nonfinite_watch(loss.data_ptr<float>(), counter.data_ptr<int>(), first_bad.data_ptr<int>(), cur_stream()),
+        "nonfinite_watch");
+}
+
 py::tuple gemm_tile(int64_t cfg) {
   int bm = 0, bn = 0;
   TORCH_CHECK(ds2_gemm_tile((int)cfg, &bm, &bn) == 0, "gemm_tile: bad cfg");
@@ -785,4 +812,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tile", &gemm_tile);
   m.def("head_ctc", &head_ctc);
   m.def("fc_logits", &fc_logits);
+  m.def("hist_stats", &hist_stats);
+  m.def("hist_nbucket", []() { return ds2_hist_nbucket(); });
+  m.def("hist_blocks", [](int64_t n) { return ds2_hist_blocks(n); });
+  m.def("nonfinite_watch", &nonfinite_watch);
 }

@@ -182,6 +182,11 @@ class DeepSpeech2(nn.Module):
         he_trunc_normal_(self.fc_weight, [num_classes, num_hidden])
         self.engine = "ref"
         self.compute_dtype = torch.float32
+        # activation summaries (reference _activation_summary at conv1 / conv2 / rnn / logits,
+        # src/deepSpeech_NCHW.py:134,158,183,199): when ``capture`` is set, the next forward
+        # keeps detached references to those activations in ``act_taps``
+        self.capture = False
+        self.act_taps: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ config
     def set_engine(self, engine: str, compute_dtype: torch.dtype = torch.float32, fp8: bool = False) -> "DeepSpeech2":
@@ -233,10 +238,16 @@ class DeepSpeech2(nn.Module):
         x = feats.unsqueeze(1)
         with TR.phase(TR.conv(1)):
             x = self.conv1.forward_ref(x)
+        self._tap("conv1", x)
         with TR.phase(TR.conv(2)):
             x = self.conv2.forward_ref(x)
+        self._tap("conv2", x)
         N, C, T2, F2 = x.shape
         return x.permute(2, 0, 1, 3).reshape(T2, N, C * F2)
+
+    def _tap(self, name: str, t: torch.Tensor) -> None:
+        if self.capture:
+            self.act_taps[name] = t.detach()
 
     def recurrent(self, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
         inp = x
@@ -250,6 +261,7 @@ class DeepSpeech2(nn.Module):
                 with TR.phase(TR.rnn_cell(i)):
                     out = layer.forward_ref(inp, lens)
             inp = out if self.stack_fix else x
+        self._tap("rnn", out)
         return out
 
     def arena_groups(self):
@@ -297,7 +309,9 @@ class DeepSpeech2(nn.Module):
             feats = feats.to(self.compute_dtype)
         x = self.frontend(feats)
         h = self.recurrent(x, lens.to(x.device))
-        return self.head(h), lens
+        logits = self.head(h)
+        self._tap("softmax_linear", logits)
+        return logits, lens
 
     def forward_loss(self, feats: torch.Tensor, seq_lens: torch.Tensor, targets: torch.Tensor,
                      target_lens: torch.Tensor) -> torch.Tensor:
@@ -309,6 +323,9 @@ class DeepSpeech2(nn.Module):
             lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
             x = self.frontend(feats.to(self.compute_dtype))
             h = self.recurrent(x, lens.to(x.device))
+            if self.capture:
+                with torch.no_grad():   # the fused head never materialises the logits
+                    self._tap("softmax_linear", self.head(h.detach()))
             return CTC.head_ctc_mean_loss_hip(h, self.fc_weight, self.fc_bias, lens, targets, target_lens)
         logits, lens = self(feats, seq_lens)
         return self.loss(logits, lens, targets, target_lens)

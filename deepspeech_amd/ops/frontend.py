@@ -218,6 +218,9 @@ class FrontendCL(torch.autograd.Function):
             mean2, inv2 = stats(part2, grid, N * T2 * F2, c2)
             out = torch.empty(T2, N, 32 * F2, **bf)
             C_.bn_cl_apply(y2, mean2, inv2, g2f, be2f, out, True)
+        if getattr(model, "capture", False):
+            model.act_taps["conv1"] = z1.detach()      # [N, T1, F1, C] channels-last
+            model.act_taps["conv2"] = out.detach()     # time-major [T2, N, C*F2]
         ctx.save_for_backward(x, y1, z1, y2, mean1, inv1, mean2, inv2, g1f, be1f, g2f, be2f, w2_16)
         ctx.params = (w1, b1, g1, be1, w2, b2, g2, be2)
         ctx.training = training
@@ -283,7 +286,12 @@ def frontend_hip(model, feats: torch.Tensor) -> torch.Tensor:
                                 c2.weight, c2.bias, c2.bn_gamma, c2.bn_beta, model)
     x = feats.unsqueeze(1)
     x = conv_block_hip(model.conv1, x, 0, 1)
-    return conv_block_hip(model.conv2, x, 1, 2)
+    if getattr(model, "capture", False):
+        model.act_taps["conv1"] = x.detach()
+    x = conv_block_hip(model.conv2, x, 1, 2)
+    if getattr(model, "capture", False):
+        model.act_taps["conv2"] = x.detach()
+    return x
 
 
 class FusedHead(torch.autograd.Function):

@@ -18,6 +18,7 @@ import os
 import sys
 import time
 from datetime import datetime
+from typing import Optional
 
 import numpy as np
 import torch
@@ -106,6 +107,40 @@ def write_debug_reports(prof, model, args, dev) -> None:
         f.write(P.format_table(out) + "\n")
 
 
+def resume_dir(args) -> Optional[str]:
+    """Directory to resume from: --checkpoint (reference semantics), or train_dir itself under
+    --resume auto / an elastic restart (torchrun --max-restarts) when it holds a checkpoint."""
+    if args.checkpoint is not None:
+        return args.checkpoint
+    restarted = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) > 0
+    if (args.resume == "auto" or restarted) and CK.latest_checkpoint(args.train_dir) is not None:
+        return args.train_dir
+    return None
+
+
+def write_summaries(events, step: int, trainer, model, args, lv: float, ema: float) -> None:
+    """Reference add_summaries (src/deepSpeech_train.py:401-416: learning rate, gradient and
+    variable histograms) + _activation_summary (src/helper_routines.py:15-28). Histograms are
+    computed on the device (csrc/stats.hip), one pass per tensor; tags use the TF variable
+    names of the checkpoint layout."""
+    from .utils.stats import histogram
+    events.scalars(step, {"ctc_loss(raw)": lv, "ctc_loss": ema, "learning_rate": trainer.lr})
+    tfname = {tn: tf for tf, tn, _, _ in CK.tf_name_map(model)}
+    grads = trainer.arena.views(trainer.arena.grad)
+    for n, p in model.named_parameters():
+        tag = tfname.get(n, n)
+        events.histogram_stats(step, tag, histogram(p.detach()))
+        if n in grads:
+            events.histogram_stats(step, tag + "/gradients", histogram(grads[n]))
+    if args.activation_summaries:
+        for name, t in model.act_taps.items():
+            st = histogram(t)
+            events.histogram_stats(step, name + "/activations", st)
+            events.scalars(step, {name + "/sparsity": st.zero_fraction})
+    model.act_taps.clear()
+    events.flush()
+
+
 def main(argv=None) -> int:
     args = C.parse_train_args(argv)
     ctx = init_distributed(args.device)
@@ -119,7 +154,7 @@ def main(argv=None) -> int:
         print("nchw: ", args.nchw)
         print("dummy: ", args.dummy)
         print("engine: ", args.engine, "->", engine, "| dtype:", dtype, "| world:", ctx.world_size)
-        if args.train_dir != args.checkpoint:
+        if args.train_dir != args.checkpoint and resume_dir(args) is None:
             clean_train_dir(args.train_dir)
         C.dump_param_json(args, args.train_dir)
         print("Running on platform: ", args.platform)
@@ -132,11 +167,13 @@ def main(argv=None) -> int:
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
                       allreduce_bf16=args.allreduce_dtype == "bf16", nan_policy=args.nan_policy)
     start = 0
-    if args.checkpoint is not None:
-        print("has checkpoint")
-        step = CK.restore(trainer, args.checkpoint)
+    rdir = resume_dir(args)
+    if rdir is not None:
+        print("has checkpoint", rdir)
+        step = CK.restore(trainer, rdir)
         if step is not None:
             start = trainer.global_step
+            trainer.watch.reset(start)
     else:
         print("does not have checkpoint")
     if ctx.is_main:
@@ -154,6 +191,19 @@ def main(argv=None) -> int:
     audio_since = 0.0
     loss = None
     prof = None
+    # per-step device time from events recorded after each step (no per-step sync); read at
+    # the host sync points -> p50/p95 step time and achieved TFLOP/s in metrics.jsonl
+    step_events = []           # (event, analytic training FLOPs of the step)
+    ev_prev = None
+    first_attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) == 0
+    sum_on = ctx.is_main and (not args.dummy or args.summaries_on_dummy) and args.summary_every > 0
+
+    def check_divergence():
+        bad = trainer.first_nonfinite_step()
+        if bad is not None and args.nan_policy == "abort":
+            raise FloatingPointError("Model diverged with loss = NaN (step %d)" % bad)
+        return bad
+
     for step in range(start, args.max_steps):
         t0 = time.time()
         hb = data.next()
@@ -168,8 +218,15 @@ def main(argv=None) -> int:
                            record_shapes=False)
             prof.__enter__()
         batch = to_device(hb, dev)
+        model.capture = sum_on and step % args.summary_every == 0
         loss = trainer.step(batch)
-        if args.fault_inject_step == step and ctx.rank == args.fault_inject_rank:
+        model.capture = False
+        if dev.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            fl = sum(model.flops_per_step(1, int(t)) for t in np.asarray(hb.seq_lens).tolist())
+            step_events.append((ev, fl))
+        if args.fault_inject_step == step and ctx.rank == args.fault_inject_rank and first_attempt:
             print("fault injection at step %d on rank %d" % (step, ctx.rank), flush=True)
             os._exit(17)
         steps_since += 1
@@ -184,16 +241,22 @@ def main(argv=None) -> int:
                 write_debug_reports(prof, model, args, dev)
             prof = None
         do_log = (step > 10 and step % args.log_every == 0) or step + 1 == args.max_steps
-        do_sum = ctx.is_main and step % args.summary_every == 0
+        do_sum = sum_on and step % args.summary_every == 0
         do_ckpt = ctx.is_main and (step % args.checkpoint_every == 0 or step + 1 == args.max_steps)
         if do_log or do_sum or do_ckpt:
             lv = float(loss.item())          # host sync point
             if engine == "hip":
                 from .ops import rnn as RNN
                 RNN.check_errors()
-            if lv != lv or lv in (float("inf"), float("-inf")):
-                if args.nan_policy == "abort":
-                    raise FloatingPointError("Model diverged with loss = NaN (step %d)" % step)
+            check_divergence()               # every step's loss was checked on the device
+            step_ms = []
+            step_fl = 0.0
+            for ev, fl in step_events:
+                if ev_prev is not None:
+                    step_ms.append(ev_prev.elapsed_time(ev))
+                    step_fl += fl
+                ev_prev = ev
+            step_events = []
             now = time.time()
             dur = (now - t_last) / max(1, steps_since)
             if step >= 10:
@@ -213,15 +276,20 @@ def main(argv=None) -> int:
                     print("%s: step %d, loss = %.2f (%.1f examples/sec; %.3f sec/batch; %.1f audio-sec/sec)"
                           % (datetime.now(), step, lv, ex_sec, sec_batch, aps), flush=True)
             if ctx.is_main:
-                metrics.write(step, loss=lv, loss_ema=ema, lr=trainer.lr)
+                rec = dict(loss=lv, loss_ema=ema, lr=trainer.lr)
+                if step_ms:
+                    ms = np.asarray(step_ms)
+                    rec.update(step_ms_p50=round(float(np.percentile(ms, 50)), 4),
+                               step_ms_p95=round(float(np.percentile(ms, 95)), 4),
+                               tflops=round(step_fl * ctx.world_size / (ms.sum() / 1e3) / 1e12, 3))
+                metrics.write(step, **rec)
             if do_sum:
-                events.scalars(step, {"ctc_loss(raw)": lv, "ctc_loss": ema, "learning_rate": trainer.lr})
-                if not args.dummy:
-                    for n, p in model.named_parameters():
-                        events.histogram(step, n, p.detach().float().cpu().numpy())
-                events.flush()
+                write_summaries(events, step, trainer, model, args, lv, ema)
             if do_ckpt:
                 ckpt.save(trainer, step)
+    if loss is not None:
+        float(loss.item())
+        check_divergence()
     if ckpt is not None:
         ckpt.wait()
     if events is not None:

@@ -28,6 +28,7 @@ from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
 from .ops.rnn import discard_deferred_wgrads, join_wgrad_streams
 from .parallel.grad_sync import GradBucketer, broadcast_params
 from .utils import trace as TR
+from .utils.stats import NonfiniteWatch
 
 
 @dataclass
@@ -77,6 +78,8 @@ class Trainer:
         self.collapse_repeated = collapse_repeated
         self.loss_ema: Optional[float] = None
         self.last_skip: Optional[torch.Tensor] = None
+        # per-step divergence record on the device (read at host sync points, never skipped)
+        self.watch = NonfiniteWatch(self.arena.flat.device)
 
     @property
     def lr(self) -> float:
@@ -92,6 +95,7 @@ class Trainer:
         discard_deferred_wgrads()
         self.arena.zero_grad(lazy=lazy)
         loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
+        self.watch.update(loss)
         loss.backward()
         join_wgrad_streams()
         if lazy:
@@ -107,6 +111,11 @@ class Trainer:
             self.opt.step(self.lr, self.global_step, gscale=gscale, skip_flag=skip)
         self.global_step += 1
         return loss.detach()
+
+    def first_nonfinite_step(self) -> Optional[int]:
+        """Global step of the first non-finite loss so far (None if none). Reads one device
+        word: call where the host synchronises anyway."""
+        return self.watch.first_bad_step()
 
     def update_loss_ema(self, loss_value: float, decay: float = 0.9) -> float:
         """tf.train.ExponentialMovingAverage(0.9) of the loss (src/deepSpeech_train.py:175-188)."""

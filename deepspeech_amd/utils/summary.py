@@ -99,6 +99,20 @@ def _histogram(values: np.ndarray) -> bytes:
     return h
 
 
+def _histogram_from_stats(st) -> bytes:
+    """HistogramProto of a utils.stats.HistStats (TF default buckets; empty buckets are merged
+    into their right neighbour, as TF's EncodeToProto does)."""
+    from .stats import limits
+    lim = limits()
+    nz = np.nonzero(st.counts)[0]
+    h = (_double_field(1, st.min) + _double_field(2, st.max) + _double_field(3, st.num) +
+         _double_field(4, st.sum) + _double_field(5, st.sum_sq))
+    if nz.size:
+        h += _bytes_field(6, struct.pack("<%dd" % nz.size, *lim[nz].tolist()))
+        h += _bytes_field(7, struct.pack("<%dd" % nz.size, *st.counts[nz].astype(np.float64).tolist()))
+    return h
+
+
 def _event(step: int, summary: Optional[bytes] = None, file_version: Optional[str] = None) -> bytes:
     e = _double_field(1, time.time()) + _int_field(2, step)
     if file_version is not None:
@@ -125,6 +139,11 @@ class EventWriter:
 
     def histogram(self, step: int, tag: str, values) -> None:
         s = _bytes_field(1, _bytes_field(1, tag.encode()) + _bytes_field(5, _histogram(values)))
+        self._f.write(frame_record(_event(step, summary=s)))
+
+    def histogram_stats(self, step: int, tag: str, st) -> None:
+        """Histogram from precomputed (device-side) statistics: utils.stats.HistStats."""
+        s = _bytes_field(1, _bytes_field(1, tag.encode()) + _bytes_field(5, _histogram_from_stats(st)))
         self._f.write(frame_record(_event(step, summary=s)))
 
     def flush(self) -> None:
@@ -204,4 +223,39 @@ def read_events(path: str):
                 for ff, wt2, v in vals:
                     if ff == 2 and wt2 == 5:
                         out.append((step, tag, struct.unpack("<f", v)[0]))
+    return out
+
+
+def read_histograms(path: str):
+    """Parse histograms back from an event file (tests): [(step, tag, dict)] with min, max,
+    num, sum, sum_sq, limits, counts."""
+    out = []
+    with open(path, "rb") as f:
+        data = f.read()
+    i = 0
+    while i < len(data):
+        (n,) = struct.unpack_from("<Q", data, i)
+        rec = data[i + 12: i + 12 + n]
+        i += 12 + n + 4
+        fields = _parse(rec)
+        step = next((v for f, wt, v in fields if f == 2 and wt == 0), 0)
+        for f, wt, summ in fields:
+            if f != 5:
+                continue
+            for vf, _, val in _parse(summ):
+                if vf != 1:
+                    continue
+                vals = _parse(val)
+                tag = next((v.decode() for ff, _, v in vals if ff == 1), "")
+                for ff, wt2, v in vals:
+                    if ff == 5 and wt2 == 2:
+                        h = {}
+                        for hf, hwt, hv in _parse(v):
+                            key = {1: "min", 2: "max", 3: "num", 4: "sum", 5: "sum_sq"}.get(hf)
+                            if key:
+                                h[key] = struct.unpack("<d", hv)[0]
+                            elif hf in (6, 7):
+                                arr = list(struct.unpack("<%dd" % (len(hv) // 8), hv))
+                                h["limits" if hf == 6 else "counts"] = arr
+                        out.append((step, tag, h))
     return out
