@@ -26,6 +26,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# platform environment (RCCL channel budget, kernel-argument placement, high-priority
+# collectives) before torch is imported: deepspeech_amd/utils/setenvs.py
+from deepspeech_amd.utils.setenvs import setenvs  # noqa: E402
+
+setenvs([])
 
 
 def parse():

@@ -25,13 +25,13 @@ ENGINE_ALIASES = ("tf", "mkl", "mkldnn_rnn", "cudnn_rnn")
 # (reference: src/deepSpeech_train.py:114-127) plus our extensions.
 RESUME_KEYS = (
     "num_hidden", "num_rnn_layers", "rnn_type", "num_filters", "use_fp16",
-    "temporal_stride", "initial_lr", "engine",
+    "temporal_stride", "initial_lr", "engine", "nchw",
     # extensions
     "cell", "stack_fix", "seq_bn", "dtype", "ctc_collapse_repeated",
 )
 EVAL_KEYS = (
     "num_hidden", "num_rnn_layers", "rnn_type", "num_filters", "use_fp16",
-    "moving_avg_decay",
+    "moving_avg_decay", "nchw",
     "cell", "stack_fix", "seq_bn", "ctc_collapse_repeated",
 )
 
@@ -101,7 +101,9 @@ def build_train_parser() -> argparse.ArgumentParser:
                    help="ref | hip (aliases: tf, mkl, mkldnn_rnn, cudnn_rnn)")
     p.add_argument("--debug", type=str2bool, default=False,
                    help="write a chrome trace + per-layer profile at step 20")
-    p.add_argument("--nchw", type=str2bool, default=True, help="layout hint (kept for compat)")
+    p.add_argument("--nchw", type=str2bool, default=True,
+                   help="True: the reference's NCHW graph (src/deepSpeech_NCHW.py); False: its NHWC graph "
+                        "(src/deepSpeech.py: moments+EMA conv BN, per-direction RNN stacks)")
     p.add_argument("--dummy", type=str2bool, default=False,
                    help="Use synthetic data rather than LibriSpeech data")
     # ---- extensions ---------------------------------------------------------------
@@ -230,6 +232,7 @@ def model_kwargs_from_args(args) -> Dict[str, Any]:
         bidirectional=bidir,
         stack_fix=getattr(args, "stack_fix", True),
         seq_bn=getattr(args, "seq_bn", "frozen"),
+        layout="nchw" if str2bool(getattr(args, "nchw", True)) else "nhwc",
     )
 
 

@@ -136,6 +136,7 @@ int ds2_hist_nbucket();
 int ds2_hist_blocks(long long n);
 int ds2_hist_stats(const void* x, int bf16, long long n, unsigned* counts, float* part, int blocks, hipStream_t st);
 int ds2_nonfinite_watch(const float* loss, int* counter, int* first_bad, hipStream_t st);
+int ds2_spin(long long ticks, int blocks, int threads, int lds_bytes, int* done, hipStream_t st);
 int ds2_fc_logits(const void* h, const void* W, const void* bias, void* logits, int out_bf16, int M, int H, int K,
                   hipStream_t st);
 }
@@ -816,4 +817,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("hist_nbucket", []() { return ds2_hist_nbucket(); });
   m.def("hist_blocks", [](int64_t n) { return ds2_hist_blocks(n); });
   m.def("nonfinite_watch", &nonfinite_watch);
+  m.def("spin", [](int64_t ticks, int64_t blocks, int64_t threads, int64_t lds_bytes, at::Tensor done) {
+    need_gpu(done, "done");
+    TORCH_CHECK(done.scalar_type() == at::kInt, "done: int32");
+    check(ds2_spin(ticks, (int)blocks, (int)threads, (int)lds_bytes, done.data_ptr<int>(), cur_stream()), "spin");
+  });
 }

@@ -95,9 +95,27 @@ __global__ __launch_bounds__(HIST_THREADS) void hist_stats_kernel(const T* __res
     if (h[i]) atomicAdd(&counts[i], h[i]);
 }
 
+// CU occupier for co-residency tests: every workgroup spins on s_memrealtime for `ticks`
+// (100 MHz) holding its CU slot, like an RCCL channel block for the length of a collective.
+__global__ void spin_kernel(long long ticks, int* done) {
+  extern __shared__ int spin_lds[];
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (threadIdx.x == 0) {
+    spin_lds[0] = 1;
+    atomicAdd(done, spin_lds[0]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int ds2_spin(long long ticks, int blocks, int threads, int lds_bytes, int* done, hipStream_t st) {
+  if (blocks <= 0 || threads <= 0 || threads > 1024 || lds_bytes < 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(spin_kernel, dim3(blocks), dim3(threads), lds_bytes, st, ticks, done);
+  return (int)hipGetLastError();
+}
 
 int ds2_hist_nbucket() { return NBUCKET; }
 int ds2_hist_npos() { return NPOS; }

@@ -74,26 +74,71 @@ def freq_out(F_in: int = FREQ_BINS) -> Tuple[int, int]:
     return f1, f2
 
 
-class ConvBlock(nn.Module):
-    """conv + bias + BatchNorm + clipped ReLU (src/deepSpeech_NCHW.py:110-158)."""
+NHWC_BN_EPS = 1e-5
+NHWC_BN_DECAY = 0.5
 
-    def __init__(self, cin: int, cout: int, kernel: Tuple[int, int], stride: Tuple[int, int]):
+
+class ConvBlock(nn.Module):
+    """conv + bias + BatchNorm + clipped ReLU.
+
+    bn='fused' (NCHW graph, src/deepSpeech_NCHW.py:110-158 / custom_ops.batch_norm2):
+        fused batch norm, eps 1e-3, batch statistics in training; running statistics
+        (momentum 0.01) in eval (quirk Q4: the reference also used batch stats in eval).
+    bn='moments_ema' (NHWC graph, src/deepSpeech.py:110-158 / custom_ops.batch_norm,
+        src/custom_ops.py:163-181): tf.nn.moments over (N, T, F) per channel, eps 1e-5,
+        ExponentialMovingAverage(decay 0.5, zero_debias) of the batch mean / variance,
+        whose debiased values normalise in eval."""
+
+    def __init__(self, cin: int, cout: int, kernel: Tuple[int, int], stride: Tuple[int, int], bn: str = "fused"):
         super().__init__()
+        if bn not in ("fused", "moments_ema"):
+            raise ValueError(bn)
         self.stride = stride
+        self.bn = bn
+        self.bn_eps = CONV_BN_EPS if bn == "fused" else NHWC_BN_EPS
         self.weight = nn.Parameter(torch.empty(cout, cin, *kernel))
         self.bias = nn.Parameter(torch.full((cout,), -0.05))
         self.bn_gamma = nn.Parameter(torch.ones(cout))
         self.bn_beta = nn.Parameter(torch.zeros(cout))
         self.register_buffer("running_mean", torch.zeros(cout))
         self.register_buffer("running_var", torch.ones(cout))
+        # zero-debiased EMA state of the moments (TF: <shadow>/biased, <shadow>/local_step)
+        self.register_buffer("ema_mean_biased", torch.zeros(cout))
+        self.register_buffer("ema_var_biased", torch.zeros(cout))
+        self.register_buffer("ema_steps", torch.zeros((), dtype=torch.float32))
         # TF HWIO shape for initialisation parity
         he_trunc_normal_(self.weight, [kernel[0], kernel[1], cin, cout])
 
+    @torch.no_grad()
+    def ema_update(self, mean: torch.Tensor, var: torch.Tensor) -> None:
+        """biased <- decay*biased + (1-decay)*value; local_step += 1 (TF zero-debias)."""
+        d = NHWC_BN_DECAY
+        self.ema_mean_biased.mul_(d).add_(mean.detach().float(), alpha=1 - d)
+        self.ema_var_biased.mul_(d).add_(var.detach().float(), alpha=1 - d)
+        self.ema_steps.add_(1.0)
+
+    def ema_moments(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Debiased EMA mean / variance (eval statistics of the moments_ema variant)."""
+        corr = 1.0 - NHWC_BN_DECAY ** self.ema_steps.clamp(min=1.0)
+        return self.ema_mean_biased / corr, self.ema_var_biased / corr
+
     def forward_ref(self, x: torch.Tensor) -> torch.Tensor:
         y = F.conv2d(x, self.weight.to(x.dtype), self.bias.to(x.dtype), stride=self.stride)
-        y = F.batch_norm(y, self.running_mean, self.running_var, self.bn_gamma.to(y.dtype),
-                         self.bn_beta.to(y.dtype), training=self.training, momentum=0.01,
-                         eps=CONV_BN_EPS)
+        if self.bn == "fused":
+            y = F.batch_norm(y, self.running_mean, self.running_var, self.bn_gamma.to(y.dtype),
+                             self.bn_beta.to(y.dtype), training=self.training, momentum=0.01,
+                             eps=CONV_BN_EPS)
+        else:
+            if self.training:
+                yf = y.float()
+                mean = yf.mean(dim=(0, 2, 3))
+                var = ((yf - mean.view(1, -1, 1, 1)) ** 2).mean(dim=(0, 2, 3))   # tf.nn.moments (biased)
+                self.ema_update(mean, var)
+            else:
+                mean, var = self.ema_moments()
+            inv = torch.rsqrt(var + NHWC_BN_EPS)
+            y = ((y - mean.view(1, -1, 1, 1).to(y.dtype)) * (inv * self.bn_gamma).view(1, -1, 1, 1).to(y.dtype)
+                 + self.bn_beta.view(1, -1, 1, 1).to(y.dtype))
         return R.clipped_relu(y)
 
 
@@ -141,6 +186,17 @@ class RecurrentLayer(nn.Module):
         y = R.seq_batch_norm(y, lens, self.seq_bn, d.sbn_mean, d.sbn_var, self.training)
         return y + d.b.to(y.dtype)
 
+    def forward_ref_split(self, x_f: torch.Tensor, x_b: torch.Tensor, lens: torch.Tensor):
+        """Per-direction stacks (NHWC graph): the forward direction reads the forward stack's
+        input, the backward direction the backward stack's; outputs are NOT summed."""
+        bh = lambda d: None if d.b_h is None else d.b_h.to(x_f.dtype)
+        gx_f = self.input_projection_ref(x_f, self.fw, lens)
+        y_f, _ = R.recurrent_scan(self.cell, gx_f, self.fw.U.to(x_f.dtype), bh(self.fw), lens)
+        gx_b = self.input_projection_ref(x_b, self.bw, lens)
+        y_br, _ = R.recurrent_scan(self.cell, R.reverse_sequence(gx_b, lens), self.bw.U.to(x_b.dtype), bh(self.bw),
+                                   lens)
+        return y_f, R.reverse_sequence(y_br, lens)
+
     def forward_ref(self, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
         gx_f = self.input_projection_ref(x, self.fw, lens)
         gx_b = self.input_projection_ref(x, self.bw, lens) if self.bw is not None else None
@@ -154,10 +210,22 @@ class DeepSpeech2(nn.Module):
     def __init__(self, num_filters: int = 32, num_hidden: int = 1024, num_rnn_layers: int = 2,
                  cell: str = "rnn_relu", bidirectional: bool = True, stack_fix: bool = True,
                  seq_bn: str = "frozen", num_classes: int = NUM_CLASSES,
-                 freq_bins: int = FREQ_BINS):
+                 freq_bins: int = FREQ_BINS, layout: str = "nchw"):
+        """layout 'nchw' = src/deepSpeech_NCHW.py (default, --nchw True); 'nhwc' =
+        src/deepSpeech.py (--nchw False): moments+EMA conv BN (eps 1e-5) and, when
+        bidirectional, two deep per-direction stacks (bidirectional_dynamic_rnn over a
+        MultiRNNCell each, src/deepSpeech.py:165-185) summed only at the top. The NHWC
+        graph's channels-last flatten of conv2 (feature f*C + c) is a fixed permutation of
+        the first layer's input columns; it is applied at the checkpoint boundary
+        (utils/checkpoint.py), the compute layout is shared."""
         super().__init__()
         if cell not in GATES:
             raise ValueError("cell must be one of %s" % list(GATES))
+        if layout not in ("nchw", "nhwc"):
+            raise ValueError("layout must be nchw or nhwc")
+        self.layout = layout
+        if layout == "nhwc":
+            stack_fix = True          # the NHWC graph's MultiRNNCell stacks correctly (no Q1)
         self.num_filters = num_filters
         self.num_hidden = num_hidden
         self.num_rnn_layers = num_rnn_layers
@@ -169,8 +237,9 @@ class DeepSpeech2(nn.Module):
         self.freq_bins = freq_bins
         _, f2 = freq_out(freq_bins)
         self.rnn_in = f2 * num_filters                     # 75*C = 2400 for 161 bins
-        self.conv1 = ConvBlock(1, num_filters, (20, 5), (2, 2))
-        self.conv2 = ConvBlock(num_filters, num_filters, (10, 5), (2, 1))
+        bn = "fused" if layout == "nchw" else "moments_ema"
+        self.conv1 = ConvBlock(1, num_filters, (20, 5), (2, 2), bn=bn)
+        self.conv2 = ConvBlock(num_filters, num_filters, (10, 5), (2, 1), bn=bn)
         layers = []
         for i in range(num_rnn_layers):
             # Q1: with stack_fix=False every layer consumes the conv output.
@@ -249,7 +318,23 @@ class DeepSpeech2(nn.Module):
         if self.capture:
             self.act_taps[name] = t.detach()
 
+    def direction_stacks(self) -> bool:
+        return self.layout == "nhwc" and self.bidirectional
+
     def recurrent(self, x: torch.Tensor, lens: torch.Tensor) -> torch.Tensor:
+        if self.direction_stacks():
+            x_f = x_b = x
+            for i, layer in enumerate(self.rnn):
+                if self.engine == "hip":
+                    from ..ops import rnn as RNN
+                    x_f, x_b = RNN.recurrent_layer_split_hip(layer, x_f, x_b, lens, i)
+                else:
+                    from ..utils import trace as TR
+                    with TR.phase(TR.rnn_cell(i)):
+                        x_f, x_b = layer.forward_ref_split(x_f, x_b, lens)
+            out = x_f + x_b
+            self._tap("rnn", out)
+            return out
         inp = x
         out = x
         for i, layer in enumerate(self.rnn):

@@ -26,11 +26,36 @@ BN_EPS = 1e-3
 BN_MOMENTUM = 0.01
 
 
+def bn_eval_stats(block, eps: float):
+    """(mean, invstd) for eval: running statistics (fused variant) or the debiased EMA of
+    the moments (moments_ema variant, NHWC graph)."""
+    if getattr(block, "bn", "fused") == "moments_ema":
+        m, v = block.ema_moments()
+        return m.float().contiguous(), torch.rsqrt(v.float() + eps).contiguous()
+    return block.running_mean.float().contiguous(), torch.rsqrt(block.running_var.float() + eps).contiguous()
+
+
+def bn_track(block, mean: torch.Tensor, invstd: torch.Tensor, eps: float) -> None:
+    """moments_ema variant: feed the batch moments (variance recovered from invstd) into the
+    zero-debiased EMA (the kernels' own running-stat update went to scratch buffers)."""
+    if getattr(block, "bn", "fused") == "moments_ema":
+        block.ema_update(mean, invstd.pow(-2) - eps)
+
+
+def _stat_buffers(block, dev):
+    """Running-stat buffers the kernels update in place: the block's own for the fused
+    variant, scratch for moments_ema (tracked by bn_track instead)."""
+    if getattr(block, "bn", "fused") == "moments_ema":
+        return torch.zeros(block.bn_gamma.numel(), device=dev), torch.ones(block.bn_gamma.numel(), device=dev)
+    return block.running_mean, block.running_var
+
+
 class BNClip(torch.autograd.Function):
     """out = clip(BN_train(y) * gamma + beta, 0, 20); layout 0 = NCHW, 1 = [T, N, C*F]."""
 
     @staticmethod
-    def forward(ctx, y, gamma, beta, run_mean, run_var, training: bool, layout: int, out_dtype, idx: int = 0):
+    def forward(ctx, y, gamma, beta, run_mean, run_var, training: bool, layout: int, out_dtype, idx: int = 0,
+                block=None):
         C_ = _ext.ext()
         y = y.contiguous()
         N, C, T, Fd = y.shape
@@ -38,12 +63,19 @@ class BNClip(torch.autograd.Function):
         gamma_p, beta_p = gamma, beta
         gamma = gamma.float().contiguous()
         beta = beta.float().contiguous()
+        eps = getattr(block, "bn_eps", BN_EPS)
         if training:
             nb = int(C_.bn_chunks(N, T, Fd))
             part = torch.empty(C * nb * 2, device=dev, dtype=torch.float32)
             mean = torch.empty(C, device=dev, dtype=torch.float32)
             invstd = torch.empty(C, device=dev, dtype=torch.float32)
-            C_.bn_stats(y, part, BN_EPS, mean, invstd, run_mean, run_var, BN_MOMENTUM)
+            if block is not None:
+                run_mean, run_var = _stat_buffers(block, dev)
+            C_.bn_stats(y, part, eps, mean, invstd, run_mean, run_var, BN_MOMENTUM)
+            if block is not None:
+                bn_track(block, mean, invstd, eps)
+        elif block is not None:
+            mean, invstd = bn_eval_stats(block, eps)
         else:
             mean = run_mean.float().contiguous()
             invstd = torch.rsqrt(run_var.float() + BN_EPS).contiguous()
@@ -78,7 +110,8 @@ class BNClip(torch.autograd.Function):
         dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
         dy = torch.empty_like(y)
         C_.bn_bwd(dout, y, mean, invstd, gamma, beta, part, dgamma, dbeta, dy, ctx.layout)
-        return dy, emit_grad(ctx.g_param, dgamma), emit_grad(ctx.b_param, dbeta), None, None, None, None, None, None
+        return (dy, emit_grad(ctx.g_param, dgamma), emit_grad(ctx.b_param, dbeta), None, None, None, None, None, None,
+                None)
 
 
 class ConvFused(torch.autograd.Function):
@@ -129,7 +162,7 @@ def conv_block_hip(block, x: torch.Tensor, layout: int, idx: int) -> torch.Tenso
         y = ConvFused.apply(x, block.weight, block.bias, tuple(block.stride), bool(block.training), idx)
     with TR.phase(TR.bn(idx)):
         return BNClip.apply(y, block.bn_gamma, block.bn_beta, block.running_mean, block.running_var,
-                            block.training, layout, dt, idx)
+                            block.training, layout, dt, idx, block)
 
 
 def _bf16_of(p: torch.Tensor) -> torch.Tensor:
@@ -188,14 +221,15 @@ class FrontendCL(torch.autograd.Function):
         ncu = _ext.num_cus(dev.index or 0)
 
         def stats(part, nb, M, blk):
+            eps = getattr(blk, "bn_eps", BN_EPS)
             if training:
                 mean = torch.empty(32, **f32)
                 inv = torch.empty(32, **f32)
-                C_.bn_cl_finalize(part, nb, float(M), BN_EPS, mean, inv, blk.running_mean, blk.running_var,
-                                  BN_MOMENTUM)
+                rm, rv = _stat_buffers(blk, dev)
+                C_.bn_cl_finalize(part, nb, float(M), eps, mean, inv, rm, rv, BN_MOMENTUM)
+                bn_track(blk, mean, inv, eps)
                 return mean, inv
-            return (blk.running_mean.float().contiguous(),
-                    torch.rsqrt(blk.running_var.float() + BN_EPS).contiguous())
+            return bn_eval_stats(blk, eps)
 
         g1f, be1f = g1.detach().float().contiguous(), be1.detach().float().contiguous()
         g2f, be2f = g2.detach().float().contiguous(), be2.detach().float().contiguous()

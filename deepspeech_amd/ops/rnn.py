@@ -832,3 +832,29 @@ def _recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int) -
     bh_f = fw.b_h if layer.cell == "gru" else None
     bh_b = bw.b_h if (layer.cell == "gru" and ndir == 2) else None
     return BiRecurrence.apply(gx, lens, U_f, U_b, bh_f, bh_b, plan)
+
+
+def _uni_layer_hip(layer, d, x: torch.Tensor, lens: torch.Tensor, idx: int) -> torch.Tensor:
+    """One direction of a layer as a one-direction fused layer over x (forward in time)."""
+    plan = plan_for(x.shape[1], layer.hidden, layer.cell, 1, x.device)
+    if layer.seq_bn in ("frozen", "none"):
+        alpha = sbn_scale() if layer.seq_bn == "frozen" else 1.0
+        return FusedBiLayer.apply(x, lens, plan, alpha, idx, bool(getattr(layer, "fp8", False)),
+                                  d.W, None, d.U, None, d.b, None, d.b_h, None)
+    gx = layer.input_projection_ref(x.to(torch.bfloat16), d, lens).to(torch.bfloat16)
+    bh = d.b_h if layer.cell == "gru" else None
+    return BiRecurrence.apply(gx, lens, d.U.to(torch.bfloat16), None, bh, None, plan)
+
+
+def recurrent_layer_split_hip(layer, x_f: torch.Tensor, x_b: torch.Tensor, lens: torch.Tensor, idx: int = 0):
+    """Per-direction stacks of the NHWC graph (src/deepSpeech.py:165-185, two MultiRNNCells
+    under bidirectional_dynamic_rnn): the forward direction of layer idx reads the forward
+    stack, the backward direction the backward stack, and the outputs stay separate. The
+    backward direction runs as a forward recurrence over the length-aware reversal of its
+    input (TF ReverseSequence semantics, ops/reference.py reverse_sequence)."""
+    with TR.phase(TR.rnn_cell(idx)):
+        lens = lens.to(device=x_f.device, dtype=torch.int32)
+        y_f = _uni_layer_hip(layer, layer.fw, x_f, lens, idx)
+        xr = R.reverse_sequence(x_b, lens)
+        y_b = R.reverse_sequence(_uni_layer_hip(layer, layer.bw, xr, lens, idx), lens)
+        return y_f, y_b

@@ -84,6 +84,16 @@ def init_distributed(device_pref: str = "auto", timeout_s: int = 600, force_grou
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), rank=rank, world_size=world)
         if use_cuda and backend == "nccl":
             kw["device_id"] = device
+        restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if restart is not None and world > 1:
+            # elastic job (torchrun): the agent hosts the store for every attempt. Keys of a
+            # relaunched attempt live under their own prefix, so no rank can read a peer
+            # address left by the killed attempt (observed: gloo connectFullMesh dialling a
+            # dead port after a --max-restarts relaunch)
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                                 is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
+            run_id = os.environ.get("TORCHELASTIC_RUN_ID", "ds2")
+            kw["store"] = dist.PrefixStore("ds2/%s/attempt_%s" % (run_id, restart), base)
         if not dist.is_initialized():
             dist.init_process_group(**kw)
         ctx.backend = backend

@@ -38,28 +38,72 @@ def _conv_from_tf(w: torch.Tensor) -> torch.Tensor:    # [H, W, I, O] -> [O, I, 
     return w.permute(3, 2, 0, 1).contiguous()
 
 
+def _nhwc_col_perm(model: DeepSpeech2):
+    """Column permutation between the compute layout of the first layer's input (NCHW
+    flatten of conv2: feature c*F2 + f, src/deepSpeech_NCHW.py:166-168) and the NHWC graph's
+    channels-last flatten (f*C + c, src/deepSpeech.py:163-167): (to_tf, from_tf) on W."""
+    C = model.num_filters
+    F2 = model.rnn_in // C
+    nhwc_of = torch.arange(C * F2).view(C, F2).t().reshape(-1)     # nhwc column j <- nchw column
+    inv = torch.empty_like(nhwc_of)
+    inv[nhwc_of] = torch.arange(C * F2)
+
+    def to_tf(w):
+        return w.index_select(-1, nhwc_of.to(w.device)).contiguous()
+
+    def from_tf(w):
+        return w.index_select(-1, inv.to(w.device)).contiguous()
+    return to_tf, from_tf
+
+
 def tf_name_map(model: DeepSpeech2) -> List[Tuple[str, str, Callable, Callable]]:
-    """[(tf_name, torch_name, to_tf, from_tf)] for every parameter and buffer."""
+    """[(tf_name, torch_name, to_tf, from_tf)] for every parameter and buffer.
+
+    NCHW graph (default): src/deepSpeech_NCHW.py + custom_ops.stacked_brnn scopes.
+    NHWC graph (layout 'nhwc', --nchw False): src/deepSpeech.py scopes — conv BN under 'bn'
+    with the zero-debiased moment EMAs, the RNN as two MultiRNNCells under
+    bidirectional_rnn/{fw,bw}/multi_rnn_cell/cell_<i> (rnn/multi_rnn_cell/... uni-dir), and
+    the first layer's W in channels-last input order."""
     ident = lambda t: t  # noqa: E731
+    nhwc = getattr(model, "layout", "nchw") == "nhwc"
     out = []
     for blk in ("conv1", "conv2"):
         out += [
             ("%s/weights" % blk, "%s.weight" % blk, _conv_to_tf, _conv_from_tf),
             ("%s/biases" % blk, "%s.bias" % blk, ident, ident),
-            ("%s/bn2/beta" % blk, "%s.bn_beta" % blk, ident, ident),
-            ("%s/bn2/gamma" % blk, "%s.bn_gamma" % blk, ident, ident),
-            ("%s/bn2/moving_mean" % blk, "%s.running_mean" % blk, ident, ident),
-            ("%s/bn2/moving_variance" % blk, "%s.running_var" % blk, ident, ident),
         ]
+        if nhwc:
+            ema = "%s/bn/moments/Squeeze%s/ExponentialMovingAverage"
+            out += [
+                ("%s/bn/beta" % blk, "%s.bn_beta" % blk, ident, ident),
+                ("%s/bn/gamma" % blk, "%s.bn_gamma" % blk, ident, ident),
+                ((ema % (blk, "")) + "/biased", "%s.ema_mean_biased" % blk, ident, ident),
+                ((ema % (blk, "_1")) + "/biased", "%s.ema_var_biased" % blk, ident, ident),
+                ((ema % (blk, "")) + "/local_step", "%s.ema_steps" % blk, ident, ident),
+            ]
+        else:
+            out += [
+                ("%s/bn2/beta" % blk, "%s.bn_beta" % blk, ident, ident),
+                ("%s/bn2/gamma" % blk, "%s.bn_gamma" % blk, ident, ident),
+                ("%s/bn2/moving_mean" % blk, "%s.running_mean" % blk, ident, ident),
+                ("%s/bn2/moving_variance" % blk, "%s.running_var" % blk, ident, ident),
+            ]
     cell_scope = "CustomRNNCell2" if model.cell == "rnn_relu" else "GRUCell"
+    perm = _nhwc_col_perm(model) if nhwc else None
     for i, layer in enumerate(model.rnn):
         for dname in (["fw", "bw"] if layer.bw is not None else ["fw"]):
-            if layer.bw is not None:
+            if nhwc:
+                if layer.bw is not None:
+                    scope = "bidirectional_rnn/%s/multi_rnn_cell/cell_%d/%s" % (dname, i, cell_scope)
+                else:
+                    scope = "rnn/multi_rnn_cell/cell_%d/%s" % (i, cell_scope)
+            elif layer.bw is not None:
                 scope = "rnn/brnn-%d/bidirectional_rnn/%s/%s" % (i, dname, cell_scope)
             else:
                 scope = "rnn/rnn-%d/%s" % (i, cell_scope)
             tp = "rnn.%d.%s" % (i, dname)
-            out += [("%s/W" % scope, tp + ".W", ident, ident),
+            w_to, w_from = (perm if (perm is not None and i == 0) else (ident, ident))
+            out += [("%s/W" % scope, tp + ".W", w_to, w_from),
                     ("%s/U" % scope, tp + ".U", ident, ident),
                     ("%s/%s" % (scope, "B" if model.cell == "rnn_relu" else "b_i"), tp + ".b", ident, ident),
                     ("%s/sbn/moving_mean" % scope, tp + ".sbn_mean", ident, ident),

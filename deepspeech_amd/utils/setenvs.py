@@ -11,6 +11,17 @@ SURVEY §5.6; the CLI shims deepSpeech_train.py / deepSpeech_test.py call this f
           TORCH_NCCL_HIGH_PRIORITY=1     RCCL on high-priority streams, so bucketed gradient
                                          all-reduces overlap BPTT instead of queuing behind it
           OMP_NUM_THREADS                host threads for the loader / featurizer (8)
+          NCCL_MAX_NCHANNELS=32          RCCL CU footprint (see below)
+
+RCCL channel budget. Each RCCL channel is one workgroup that stays resident for the whole
+collective. The persistent recurrence needs P*groups co-resident workgroups, one per CU:
+200 of the 256 CUs at the headline shape (8 groups x 25), and the weight-gradient GEMMs
+use the rest. If a bucket's all-reduce is in flight when a recurrence launches, its
+workgroups wait for CUs held by RCCL channels (they never deadlock: the collective does not
+depend on the recurrence, and every recurrence spin is bounded, tests/test_dp_gpu.py), so
+the channel count is what the recurrence can lose: 256 - 200 = 56 free CUs, minus room for
+the side-stream GEMM tiles -> at most 32 channels. 32 channels x ~2 channels per xGMI link
+direction still cover the 7 links of the 8-GPU mesh.
   knl/bdw the reference's Intel settings, kept for command-line compatibility.
 
 Existing values in the environment always win (setdefault), so a launcher can override.
@@ -26,6 +37,7 @@ PLATFORMS: Dict[str, Dict[str, str]] = {
         "HIP_FORCE_DEV_KERNARG": "1",
         "TORCH_NCCL_HIGH_PRIORITY": "1",
         "OMP_NUM_THREADS": "8",
+        "NCCL_MAX_NCHANNELS": "32",
     },
     "bdw": {
         "KMP_BLOCKTIME": "1", "KMP_SETTINGS": "1", "OMP_NUM_THREADS": "8", "MKL_NUM_THREADS": "8",

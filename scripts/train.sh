@@ -3,8 +3,8 @@
 # 40k steps, lr 1e-4, 32 conv filters). Set gpus=N for data parallel over N GPUs of this
 # node (torchrun, one process per GPU, RCCL over xGMI). restarts=K makes the job elastic:
 # torchrun relaunches all ranks up to K times after a failure and they resume from the
-# latest checkpoint in train_dir (deepspeech_amd/train.py resume_dir); that needs the c10d
-# rendezvous (the static --master-addr store keeps the dead attempt's keys).
+# latest checkpoint in train_dir (deepspeech_amd/train.py resume_dir); every attempt builds
+# its process group under its own store prefix (deepspeech_amd/parallel/dist.py).
 set -e
 source "$(dirname "$0")/_common.sh"
 echo "-----------------------------------"

@@ -1,0 +1,48 @@
+"""Data-parallel readiness on one GPU (no 8-GPU node needed); the 2-rank gradient path is
+tests/test_dp_gpu.py.
+
+* co-residency: the persistent recurrence (200 co-resident workgroups at the headline
+  shape) must complete without a spin timeout while RCCL-channel-shaped workgroups hold CUs,
+  whichever launches first (tools/coresidency.py);
+* the data-parallel step machinery (process group over RCCL at world size 1, gradient
+  buckets, collectives on the ordering stream) produces the same update as the plain step.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("blocks,lds", [(32, 16384), (64, 16384), (56, 100 * 1024)])
+def test_recurrence_coresident_with_channel_blocks(cuda, blocks, lds):
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import coresidency
+    res = coresidency.run([blocks], threads=256, lds=lds, spin_ms=2.0, iters=2)
+    for r in res:
+        assert r["timeout"] is None, r
+        # the layer may wait for the spinners' CUs but never longer than the spin itself
+        assert r["layer_ms"] < r["layer_ms_alone"] + 2.0 * r["spin_ms"] + 1.0, r
+
+
+def test_dp_machinery_world1_matches_plain_step(cuda):
+    """force_buckets: gradient buckets + collectives at world size 1 give the plain update."""
+    import copy
+    from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.parallel.dist import init_distributed
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    init_distributed("cuda", force_group=True)
+    torch.manual_seed(0)
+    base = DeepSpeech2(num_filters=32, num_hidden=128, num_rnn_layers=2, cell="gru").to(cuda)
+    batch = to_device(FixedShapeBatches(8, max_frames=300, seed=2, pool=1).next(), cuda)
+    outs = []
+    for force in (False, True):
+        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9), force_buckets=force)
+        for _ in range(2):
+            tr.step(batch)
+        torch.cuda.synchronize()
+        outs.append(tr.arena.flat.clone())
+    assert torch.allclose(outs[0], outs[1], atol=1e-6, rtol=0), (outs[0] - outs[1]).abs().max()

@@ -229,3 +229,32 @@ def test_step_is_bitwise_reproducible(cuda):
     assert l0 == l1, (l0, l1)
     assert torch.equal(g0, g1), (g0 - g1).abs().max()
     assert torch.equal(w0, w1)
+
+
+@pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
+def test_nhwc_graph_hip_matches_reference(cuda, cell):
+    """--nchw False graph on the HIP engine (moments+EMA conv BN in the channels-last
+    kernels, per-direction stacks as one-direction persistent layers over length-aware
+    reversals) against the fp32 reference engine; EMA state advanced identically."""
+    from deepspeech_amd.ops import rnn as RNN
+    torch.manual_seed(12)
+    ref = DeepSpeech2(num_filters=32, num_hidden=64, num_rnn_layers=3, cell=cell, layout="nhwc").to(cuda)
+    hip = copy.deepcopy(ref)
+    ref.set_engine("ref", torch.float32)
+    hip.set_engine("hip", torch.bfloat16)
+    batch = to_device(FixedShapeBatches(6, max_frames=260, seed=4, pool=1).next(), cuda)
+    arena = ParamArena(hip, bf16_shadow=True)
+    arena.zero_grad()
+    lh = _loss(hip, batch, True)
+    lh.backward()
+    RNN.join_wgrad_streams()
+    lr = _loss(ref, batch)
+    lr.backward()
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    _compare_grads(ref, hip, lh, lr, cell)
+    for blk in ("conv1", "conv2"):
+        a, b = getattr(hip, blk), getattr(ref, blk)
+        assert float(a.ema_steps) == float(b.ema_steps) == 1.0
+        assert _rel(a.ema_mean_biased, b.ema_mean_biased) < 2e-2
+        assert _rel(a.ema_var_biased, b.ema_var_biased) < 5e-2

@@ -124,9 +124,9 @@ def test_resume_auto_continues_instead_of_wiping(tmp_path):
 
 def test_torchrun_restart_resumes_after_rank_kill(tmp_path):
     """Rank 1 dies at step 5 of the first attempt; torchrun --max-restarts=1 relaunches both
-    ranks, which resume from train_dir's latest checkpoint (step 4) and finish. Elastic
-    restarts need the c10d rendezvous: the static (--master-addr) store keeps the dead
-    attempt's process-group keys and the relaunched ranks connect to stale addresses."""
+    ranks, which resume from train_dir's latest checkpoint (step 4) and finish. Each
+    attempt builds its process group under its own store prefix (parallel/dist.py): without
+    it a relaunched rank could dial a peer address left by the killed attempt."""
     from deepspeech_amd.utils import checkpoint as CK
     d = str(tmp_path / "tr")
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
