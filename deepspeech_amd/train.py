@@ -143,6 +143,8 @@ def write_summaries(events, step: int, trainer, model, args, lv: float, ema: flo
 
 def main(argv=None) -> int:
     args = C.parse_train_args(argv)
+    from .utils.setenvs import setenvs
+    setenvs(platform=args.platform if args.platform in ("mi355x", "knl", "bdw") else "mi355x")   # before HIP init
     ctx = init_distributed(args.device)
     dev = ctx.device
     engine = C.resolve_engine(args.engine, dev)
@@ -162,6 +164,10 @@ def main(argv=None) -> int:
 
     model = DeepSpeech2(**C.model_kwargs_from_args(args)).to(dev)
     model.set_engine(engine, dtype, fp8=(args.dtype == "fp8" and engine == "hip"))
+    # --engine mkldnn_rnn / cudnn_rnn (reference: MkldnnRNNCell, src/deepSpeech_NCHW.py:173-176)
+    # checkpoints keep the MKL-DNN single-blob RNN parameters (utils/mkldnn_blob.py)
+    if args.engine in ("mkldnn_rnn", "cudnn_rnn") and model.cell == "rnn_relu" and model.layout == "nchw":
+        model.param_layout = "mkldnn"
     data, steps_per_epoch = build_data(args, ctx, args.train_dir)
     trainer = Trainer(model, lr_schedule_from_args(args, steps_per_epoch), args.moving_avg_decay,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,

@@ -121,9 +121,23 @@ def model_to_tf(model: DeepSpeech2) -> Dict[str, torch.Tensor]:
     return {tf: to_tf(sd[tn].detach()) for tf, tn, to_tf, _ in tf_name_map(model)}
 
 
+def _in_dims(model: DeepSpeech2) -> List[int]:
+    return [layer.fw.W.shape[1] for layer in model.rnn]
+
+
+def normalize_layout(model: DeepSpeech2, tensors: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Accept the MKL-DNN single-blob RNN layout (engine=mkldnn_rnn / cudnn_rnn checkpoints,
+    src/mkldnn_rnn_op.py:16-45) by unpacking its blobs into the per-matrix names."""
+    from .mkldnn_blob import from_mkldnn_layout, is_mkldnn_checkpoint
+    if is_mkldnn_checkpoint(tensors):
+        return from_mkldnn_layout(tensors, model.num_hidden, _in_dims(model))
+    return tensors
+
+
 def load_model_from_tf(model: DeepSpeech2, tensors: Dict[str, torch.Tensor], strict: bool = True,
                        use_ema: bool = False) -> List[str]:
     """Copy TF-named tensors into the model; with use_ema, prefer '<name>/ExponentialMovingAverage'."""
+    tensors = normalize_layout(model, tensors)
     sd = dict(model.named_parameters())
     sd.update(dict(model.named_buffers()))
     missing = []
@@ -227,6 +241,12 @@ class CheckpointManager:
             out[k] = v.detach().to("cpu", copy=True)
         for k, v in _arena_slots(trainer).items():
             out[k] = v.detach().to("cpu", copy=True)
+        if getattr(trainer.model, "param_layout", "tf") == "mkldnn":
+            # engine=mkldnn_rnn / cudnn_rnn: the reference's MkldnnRNNCell blob per direction
+            from .mkldnn_blob import to_mkldnn_layout
+            tens = to_mkldnn_layout({k: v for k, v in out.items() if isinstance(v, torch.Tensor)})
+            out = {k: v for k, v in out.items() if not isinstance(v, torch.Tensor)}
+            out.update(tens)
         out["global_step"] = int(trainer.global_step)
         out["beta1_power"] = float(trainer.opt.b1 ** trainer.opt.t)
         out["beta2_power"] = float(trainer.opt.b2 ** trainer.opt.t)
@@ -291,7 +311,7 @@ def restore(trainer, directory_or_file: str) -> Optional[int]:
             print("No checkpoint file found")
             return None
     data = load_checkpoint_file(path)
-    tensors = {k: v for k, v in data.items() if isinstance(v, torch.Tensor)}
+    tensors = normalize_layout(trainer.model, {k: v for k, v in data.items() if isinstance(v, torch.Tensor)})
     load_model_from_tf(trainer.model, tensors, strict=True)
     _load_arena_slots(trainer, tensors)
     trainer.arena.mark_dirty()

@@ -12,6 +12,14 @@ SURVEY §5.6; the CLI shims deepSpeech_train.py / deepSpeech_test.py call this f
                                          all-reduces overlap BPTT instead of queuing behind it
           OMP_NUM_THREADS                host threads for the loader / featurizer (8)
           NCCL_MAX_NCHANNELS=32          RCCL CU footprint (see below)
+          GPU_MAX_HW_QUEUES=8            hardware queues per process. A data-parallel step uses
+                                         the main stream, the weight-gradient side stream, the
+                                         bucket-ordering stream and RCCL's streams: with HIP's
+                                         default of 4 queues two of them share one and the
+                                         weight-gradient GEMMs serialise behind the BPTT
+                                         (measured at world size 1 with the DP machinery forced
+                                         on: 10.01-10.08 ms/step at 4 queues, 9.39-9.43 at 8,
+                                         9.35-9.45 without DP; profiles/r2_dp_readiness.md)
 
 RCCL channel budget. Each RCCL channel is one workgroup that stays resident for the whole
 collective. The persistent recurrence needs P*groups co-resident workgroups, one per CU:
@@ -38,6 +46,7 @@ PLATFORMS: Dict[str, Dict[str, str]] = {
         "TORCH_NCCL_HIGH_PRIORITY": "1",
         "OMP_NUM_THREADS": "8",
         "NCCL_MAX_NCHANNELS": "32",
+        "GPU_MAX_HW_QUEUES": "8",
     },
     "bdw": {
         "KMP_BLOCKTIME": "1", "KMP_SETTINGS": "1", "OMP_NUM_THREADS": "8", "MKL_NUM_THREADS": "8",

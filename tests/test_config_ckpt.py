@@ -9,6 +9,7 @@ from deepspeech_amd import config as C
 from deepspeech_amd.models import DeepSpeech2
 from deepspeech_amd.trainer import LRSchedule, Trainer
 from deepspeech_amd.utils import checkpoint as CK
+from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
 
 
 REF_TRAIN_DEFAULTS = {
@@ -184,3 +185,36 @@ def test_setenvs_platforms(monkeypatch):
     assert os.environ["OMP_NUM_THREADS"] == "3"          # existing values win
     with pytest.raises(ValueError):
         S.setenvs([], platform="pentium")
+
+
+def test_mkldnn_blob_layout_roundtrip(tmp_path):
+    """engine=mkldnn_rnn checkpoints: one rnn_weights blob per layer/direction
+    (src/mkldnn_rnn_op.py:37), W | R | b_W | b_R order; weights, Adam and EMA slots round-trip."""
+    from deepspeech_amd.utils import mkldnn_blob as MB
+    from deepspeech_amd.trainer import Trainer, LRSchedule
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="rnn_relu")
+    m.param_layout = "mkldnn"
+    tr = Trainer(m, LRSchedule(1e-4, 100, 0.9))
+    b = to_device(FixedShapeBatches(2, max_frames=200, seed=0, pool=1).next(), torch.device("cpu"))
+    tr.step(b)
+    mgr = CK.CheckpointManager(str(tmp_path), async_save=False)
+    path = mgr.save(tr, 0)
+    data = CK.load_checkpoint_file(path)
+    key = "rnn/brnn-1/bidirectional_rnn/bw/MkldnnRNNCell/rnn_weights"
+    assert key in data and data[key].numel() == MB.params_size(16, 16)
+    assert key + "/Adam" in data and key + "/ExponentialMovingAverage" in data
+    assert not any("CustomRNNCell2" in k for k in data)
+    blob = data["rnn/brnn-0/bidirectional_rnn/fw/MkldnnRNNCell/rnn_weights"]
+    W = m.rnn[0].fw.W.detach()
+    assert torch.equal(blob[: W.numel()], W.reshape(-1))
+    assert torch.equal(blob[-16:], torch.zeros(16))          # b_R exported as zeros
+    m2 = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="rnn_relu")
+    tr2 = Trainer(m2, LRSchedule(1e-4, 100, 0.9))
+    CK.restore(tr2, str(tmp_path))
+    for (n, p), (_, q) in zip(m.named_parameters(), m2.named_parameters()):
+        assert torch.equal(p, q), n
+    assert torch.equal(tr.opt.m, tr2.opt.m) and torch.equal(tr.opt.ema, tr2.opt.ema)
+    # a recurrent bias split across b_W / b_R imports as their sum
+    W3, U3, b3 = MB.unpack(MB.pack(W, W[:, :16], torch.ones(16), torch.full((16,), 2.0)), 16, W.shape[1])
+    assert torch.equal(b3, torch.full((16,), 3.0))
