@@ -101,6 +101,12 @@ class DummyBucketWalk:
             n = self.remaining[i]
             self.remaining[i] = 0
             self.current += 1
+        return self.batch_for(i, n)
+
+    def batch_for(self, i: int, n: Optional[int] = None) -> Batch:
+        """One batch of bucket i (n utterances, default the batch size), as next() makes it."""
+        n = self.batch_size if n is None else n
+        B = self.batch_size
         T = UTT_LENGTHS[i]
         start = int(self.rng.integers(0, EXTRA + B * (UTT_LENGTHS[-1] - T)))
         feats = self.buffer[start: start + T * n].reshape(n, T, FREQ_BINS)

@@ -210,11 +210,25 @@ def main(argv=None) -> int:
             raise FloatingPointError("Model diverged with loss = NaN (step %d)" % bad)
         return bad
 
+    class _Src:       # host batches, labels collapsed like TF preprocess_collapse_repeated
+        def next(self):
+            hb_ = data.next()
+            return collapse_batch_labels(hb_) if args.ctc_collapse_repeated else hb_
+    src = _Src()
+    # GPU: batches are produced and uploaded by a background thread through a pinned ring
+    # (data/prefetch.py), overlapping the previous steps' kernels
+    prefetch = None
+    if dev.type == "cuda" and os.environ.get("DS2_PREFETCH", "1") == "1":
+        from .data.prefetch import DevicePrefetcher
+        prefetch = DevicePrefetcher(src, dev, depth=2)
+
     for step in range(start, args.max_steps):
         t0 = time.time()
-        hb = data.next()
-        if args.ctc_collapse_repeated:
-            hb = collapse_batch_labels(hb)
+        if prefetch is not None:
+            hb, batch = prefetch.next()
+        else:
+            hb = src.next()
+            batch = None
         data_time = time.time() - t0
         if args.debug and step == 20:
             from torch.profiler import ProfilerActivity, profile
@@ -223,7 +237,8 @@ def main(argv=None) -> int:
             prof = profile(activities=[ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if dev.type == "cuda" else []),
                            record_shapes=False)
             prof.__enter__()
-        batch = to_device(hb, dev)
+        if batch is None:
+            batch = to_device(hb, dev)
         model.capture = sum_on and step % args.summary_every == 0
         loss = trainer.step(batch)
         model.capture = False
@@ -300,6 +315,8 @@ def main(argv=None) -> int:
         ckpt.wait()
     if events is not None:
         events.close()
+    if prefetch is not None:
+        prefetch.close()
     if hasattr(data, "close"):
         data.close()
     shutdown(ctx)

@@ -32,7 +32,8 @@ the side-stream GEMM tiles -> at most 32 channels. 32 channels x ~2 channels per
 direction still cover the 7 links of the 8-GPU mesh.
   knl/bdw the reference's Intel settings, kept for command-line compatibility.
 
-Existing values in the environment always win (setdefault), so a launcher can override.
+Existing values in the environment win (setdefault), so a launcher can override — except
+GPU_MAX_HW_QUEUES, which is raised to at least 8 (a lower preset value is replaced).
 """
 from __future__ import annotations
 
@@ -76,7 +77,20 @@ def setenvs(argv: Optional[List[str]] = None, platform: Optional[str] = None) ->
         raise ValueError("unknown platform %r (expected one of %s)" % (plat, sorted(PLATFORMS)))
     applied = {}
     for k, v in PLATFORMS[plat].items():
-        if k not in os.environ:
+        if k in _AT_LEAST and k in os.environ:
+            # a floor, not a default: machines export HIP's own default of 4 queues, which
+            # is exactly what a DP step must not run with (see GPU_MAX_HW_QUEUES above)
+            try:
+                if int(os.environ[k]) >= int(v):
+                    continue
+            except ValueError:
+                pass
+            os.environ[k] = v
+            applied[k] = v
+        elif k not in os.environ:
             os.environ[k] = v
             applied[k] = v
     return applied
+
+
+_AT_LEAST = ("GPU_MAX_HW_QUEUES",)

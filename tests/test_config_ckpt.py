@@ -218,3 +218,14 @@ def test_mkldnn_blob_layout_roundtrip(tmp_path):
     # a recurrent bias split across b_W / b_R imports as their sum
     W3, U3, b3 = MB.unpack(MB.pack(W, W[:, :16], torch.ones(16), torch.full((16,), 2.0)), 16, W.shape[1])
     assert torch.equal(b3, torch.full((16,), 3.0))
+
+
+def test_setenvs_hw_queue_floor(monkeypatch):
+    """GPU_MAX_HW_QUEUES is raised to at least 8 (a DP step has > 4 streams), never lowered."""
+    from deepspeech_amd.utils import setenvs as S
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    S.setenvs([], platform="mi355x")
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "8"
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
+    S.setenvs([], platform="mi355x")
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "16"
