@@ -31,6 +31,8 @@
 //    resident, K split over the 8 waves, reduced through LDS.
 //  * Every spin is bounded by an s_memrealtime timeout that sets an error word and
 //    aborts the launch, so a grid that is not co-resident cannot hang the GPU.
+#include <type_traits>
+
 #include "common.h"
 
 using namespace ds2;
@@ -95,6 +97,16 @@ struct Stamps {
     if (!on) return;
     for (int k = 0; k < 6; ++k) dst[(size_t)blockIdx.x * 8 + base + k] = acc[k];
   }
+};
+
+// compile-time-off variant: the stamp accumulators would otherwise hold ~14 VGPRs of every
+// wave for the whole launch (enough to push a 3-waves-per-SIMD kernel into spilling)
+struct NoStamps {
+  unsigned long long acc[6];
+  bool on = false;
+  __device__ explicit NoStamps(bool) {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void store(unsigned long long*, int) {}
 };
 
 __device__ __forceinline__ unsigned xcc_id() {
@@ -226,6 +238,42 @@ __device__ __forceinline__ bool poll_mfma(__amdgpu_buffer_rsrc_t rs, const unsig
     mfma(kk, __builtin_bit_cast(bf16x8, need ? v[kk] : z));
   }
   return ok_all;
+}
+
+// Same contract as poll_mfma, but every granule is loaded up front and each retry round
+// re-issues ALL granules not yet consumed, back to back (no divergent branch around a load,
+// so no vmcnt(0) between them): a round costs ONE L2 round trip however many producers are
+// late. (poll_mfma reloads only the granule it is waiting on, so k-steps whose first load
+// came back early-stale cost one serial round trip each.) The MFMAs still run in k order,
+// so the accumulation order — and the result — is deterministic.
+template <int KB, typename MfmaFn>
+__device__ __forceinline__ bool poll_mfma_par(__amdgpu_buffer_rsrc_t rs, const unsigned (&off)[KB],
+                                              const bool (&kval)[KB], long long timeout, MfmaFn&& mfma) {
+  i32x4 v[KB];
+#pragma unroll
+  for (int kk = 0; kk < KB; ++kk) v[kk] = load_sc1_b128(rs, off[kk]);
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned done = 0;                     // wave-uniform: k-steps consumed (an in-order prefix)
+  constexpr unsigned FULL = (1u << KB) - 1u;
+  while (true) {
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      if (done == (1u << kk) - 1u) {
+        if (!kval[kk]) {
+          done |= 1u << kk;
+        } else if (__all(granule_ready(v[kk]))) {
+          mfma(kk, __builtin_bit_cast(bf16x8, v[kk]));
+          done |= 1u << kk;
+        }
+      }
+    }
+    if (done == FULL) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) return false;
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk)
+      if (!(done & (1u << kk))) v[kk] = load_sc1_b128(rs, off[kk]);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -361,7 +409,9 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
   bf16_t* hxd = a.hx[dir];
   const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
   Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
-  const int arow = min(r0 + (lane & 15), NP - 1);
+  // padding lanes of the 16-row fragment (row >= R) re-read row R-1: same cache line as a
+  // real lane, so the wave's poll moves only R rows (knob 512: old per-lane rows, A/B)
+  const int arow = (a.knobs & 512) ? min(r0 + (lane & 15), NP - 1) : r0 + min(lane & 15, R - 1);
 
   // The two roles run separate copies of the step loop (one LDS barrier per iteration in
   // both), so the memory wave's prefetch registers and the MFMA waves' resident U slice are
@@ -475,6 +525,260 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
   }
   if (wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
   if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
+}
+
+// ------------------------------------------------------------------------------------
+// forward, generation 4: K-quarter split with a register-resident cell epilogue.
+//
+// Stamps of generation 2 at the headline (cycles/step): poll+MFMA 3.1k, partial store 0.4k,
+// barrier 1.0k, epilogue 1.3k. Everything after the poll sits on the step's critical path,
+// and most of it is the 7-way K reduction (24 partial floats written per lane, 21 read
+// back per element) feeding 4 epilogue waves that run 2 elements each.
+//  * 8 MFMA waves: wave w owns unit half uh = w & 1 (16 of the workgroup's 32 units, all G
+//    gates, so G accumulator tiles) over K quarter kq = w >> 1 (k-steps kq, kq+4, ...).
+//  * Transpose-reduce: element j of a 16x16 tile (row 4*(lane>>4)+j, unit lane&15) is
+//    finalised by the wave with kq == j. Each wave stores the 3 elements it does not own
+//    (3*G floats per lane, lane-contiguous: conflict-free), ONE barrier, then reads the
+//    3 other quarters of its own element. Every lane then holds the full pre-activations
+//    of exactly one (row, unit) and runs the cell in registers: h_{t-1} stays in the
+//    lane across steps, gx and the recurrent bias are read before the exchange wait.
+//  * Wave 8 is the memory wave: gx one step ahead into an LDS ring, outputs two steps
+//    behind out of an LDS staging area (vmcnt retires in order per wave, so no MFMA wave
+//    ever waits behind a bulk store).
+// Same exchange protocol and buffers as generation 2 (sentinel hx slots, census-decided
+// plain/write-through stores), so the host-side plan is shared.
+// ------------------------------------------------------------------------------------
+constexpr int QW = 8;             // MFMA waves of the generation-4 forward
+constexpr int QTH = (QW + 1) * 64;
+
+template <int CELL, int KB, bool STAMPS>
+__global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
+  using StampT = typename std::conditional<STAMPS, Stamps, NoStamps>::type;
+  constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
+  constexpr int ROWS = 16;
+  constexpr int GP = G * UPW + 4;                 // gx ring row pitch: 4*GP = 16 (mod 64) banks
+  constexpr int OP = UPW + 4;                     // output staging row pitch
+  constexpr int RG = ROWS * G * (UPW / 8);        // gx granules per step (upper bound)
+  constexpr int RGL = (RG + 63) / 64;
+  __shared__ float red_s[2][2][4][3][G][64];      // [parity][uh][element j][source][gate][lane]
+  __shared__ float gxr_s[2][ROWS][GP];
+  __shared__ __attribute__((aligned(16))) float oh_s[2][ROWS][OP];
+  __shared__ __attribute__((aligned(16))) float oy_s[2][ROWS][OP];
+  __shared__ float4 og_s[(CELL == CELL_GRU) ? 2 : 1][(CELL == CELL_GRU) ? ROWS : 1][OP];
+  __shared__ int len_s[ROWS];
+  __shared__ int s_mode, s_abort;
+
+  int grp, mem;
+  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  DS2_DCHECK(grp < a.ngroups && mem < a.P && a.NP >= a.BG * a.R && a.R <= 16);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, KS = H / 32, N = a.N, NP = a.NP, R = a.R;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW;
+  const int uh = wave & 1, kq = wave >> 1;
+  const int erow = 4 * (lane >> 4) + (kq & 3);    // this lane's cell element (MFMA waves)
+  const int ec = 16 * uh + (lane & 15);
+  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  if (wave == 0) {
+    const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+
+  __syncthreads();   // len_s / census
+  if (s_abort) return;
+
+  // memory wave: gx granule q -> (row, gate, 8-unit chunk)
+  i32x4 gpre[RGL];
+  const int NRG = R * G * (UPW / 8);
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      const int qq = q < NRG ? q : 0;
+      const int row = qq / (G * 4), rem = qq - row * (G * 4), g = rem >> 2, c8 = rem & 3;
+      const int b = min(r0 + row, N - 1);
+      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+      gpre[j] = *reinterpret_cast<const i32x4*>(a.gx + ((size_t)t * N + b) * a.gstride + dir * G * H + g * H + u0 +
+                                                c8 * 8);
+    }
+  };
+  auto mw_put = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      if (q < NRG) {
+        const int row = q / (G * 4), rem = q - row * (G * 4), g = rem >> 2, c8 = rem & 3;
+        const bool act = s < len_s[row];
+        const bf16x8 v = __builtin_bit_cast(bf16x8, gpre[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gxr_s[s & 1][row][g * UPW + c8 * 8 + k] = act ? bf2f((bf16_t)v[k]) : 0.f;
+      }
+    }
+  };
+  // outputs of step s out of staging slot s&1: lane -> (row, 4 consecutive units) x 2
+  auto mw_store = [&](int s) {
+    f32x4 vh[2], vy[2];
+    float4 vg[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {         // all LDS reads first, then the stores
+      const int row = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
+      vh[j] = *reinterpret_cast<const f32x4*>(&oh_s[s & 1][row][c4]);
+      vy[j] = *reinterpret_cast<const f32x4*>(&oy_s[s & 1][row][c4]);
+      if (CELL == CELL_GRU)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vg[j][i] = og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c4 + i];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
+      if (row < R) {
+        const int b = r0 + row, u = u0 + c4;
+        *reinterpret_cast<f32x4*>(a.hsave[dir] + ((size_t)(s + 1) * NP + b) * H + u) = vh[j];
+        if (CELL == CELL_GRU) {
+          float4* gp = reinterpret_cast<float4*>(a.gates[dir]) + ((size_t)s * NP + b) * H + u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) gp[i] = vg[j][i];
+        }
+        if (b < N) {
+          const int L = len_s[row];
+          const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+          uint2 o;
+          o.x = (unsigned)f2bf(vy[j][0]) | ((unsigned)f2bf(vy[j][1]) << 16);
+          o.y = (unsigned)f2bf(vy[j][2]) | ((unsigned)f2bf(vy[j][3]) << 16);
+          *reinterpret_cast<uint2*>(a.y[dir] + ((size_t)t * N + b) * H + u) = o;
+        }
+      }
+    }
+  };
+  if (wave == QW) {
+    mw_load(0);
+    mw_put(0);
+    if (a.steps > 1) mw_load(1);
+  }
+  __syncthreads();   // gx ring slot 0
+  const bool plain = s_mode == 1;
+  const unsigned hx_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H * 2);
+  bf16_t* hxd = a.hx[dir];
+  const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
+  StampT st(a.stamps != nullptr && (wave == 0 || wave == QW) && lane == 0);
+
+  if (wave < QW) {
+    // resident U fragments: B[k][c] = U[g*H + u0 + 16*uh + c][ks*32 + k], ks = kq + 4*kk
+    bf16x8 uf[KB][G];
+    bool kval[KB];
+    float hreg = 0.f, bhr[G];
+    {
+      const bf16_t* Ud = a.U[dir];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) {
+        const int ks = kq + 4 * kk;
+        kval[kk] = ks < KS;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          if (kval[kk])
+            v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)(g * H + u0 + ec) * H + ks * 32 + 8 * (lane >> 4));
+          uf[kk][g] = v;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        bhr[g] = (CELL == CELL_GRU && a.bh[dir]) ? a.bh[dir][g * H + u0 + ec] : 0.f;
+      if (erow < R) hreg = a.hsave[dir][(size_t)(r0 + erow) * H + u0 + ec];   // slot 0 = h0
+    }
+    // padding lanes of the 16-row fragment re-read row R-1 (a real, polled row: same cache
+    // line as its own lane), so every lane can wait on its granule and use it unmasked
+    const int arow = r0 + min(lane & 15, R - 1);
+    const bool erow_ok = erow < R;
+    const int L = len_s[erow];
+    for (int s = 0; s < a.steps; ++s) {
+      st.mark(-1);
+      float gxv[G];                    // slot s&1 was filled before the previous barrier
+#pragma unroll
+      for (int g = 0; g < G; ++g) gxv[g] = gxr_s[s & 1][erow][g * UPW + ec];
+      unsigned off[KB];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk)
+        off[kk] = (unsigned)((((size_t)s * NP + arow) * H + min(kq + 4 * kk, KS - 1) * 32 + 8 * (lane >> 4)) * 2);
+      f32x4 acc[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, [&](int kk, bf16x8 af) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, uf[kk][g], acc[g], 0, 0, 0);
+      });
+      if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
+      st.mark(0);
+      // transpose-reduce: hand the three elements this wave does not finalise to their owners
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j == kq) continue;
+        const int src = kq < j ? kq : kq - 1;
+#pragma unroll
+        for (int g = 0; g < G; ++g) red_s[s & 1][uh][j][src][g][lane] = acc[g][j];
+      }
+      st.mark(1);
+      lds_barrier();
+      st.mark(2);
+      if (s_abort) break;
+      float pre[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float own = kq == 0 ? acc[g][0] : kq == 1 ? acc[g][1] : kq == 2 ? acc[g][2] : acc[g][3];
+        pre[g] = own + red_s[s & 1][uh][kq][0][g][lane] + red_s[s & 1][uh][kq][1][g][lane] +
+                 red_s[s & 1][uh][kq][2][g][lane];
+      }
+      const bool act = s < L;
+      float hn;
+      float4 gsv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (CELL == CELL_GRU) {
+        const float ghn = pre[2] + bhr[2];
+        const float r = sigmoidf_(gxv[0] + pre[0] + bhr[0]);
+        const float z = sigmoidf_(gxv[1] + pre[1] + bhr[1]);
+        const float n = tanhf_(gxv[2] + r * ghn);
+        hn = (1.f - z) * n + z * hreg;
+        if (act) gsv = make_float4(r, z, n, ghn);
+      } else {
+        hn = fminf(fmaxf(gxv[0] + pre[0], 0.f), RELU_CAP);
+      }
+      const float hnew = act ? hn : hreg;
+      hreg = hnew;
+      const unsigned hq = (unsigned)(unsigned short)f2bf_x(hnew);
+      // 16-B exchange granule = 8 consecutive units of one row = 8 consecutive lanes
+      const unsigned pr = hq | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)hq, 0x101, 0xf, 0xf, false) << 16);
+      const int q1 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x102, 0xf, 0xf, false);
+      const int q2 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x104, 0xf, 0xf, false);
+      const int q3 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x106, 0xf, 0xf, false);
+      if ((lane & 7) == 0 && erow_ok) {
+        const i32x4 v = {(int)pr, q1, q2, q3};
+        const unsigned off = (unsigned)((((size_t)(s + 1) * NP + r0 + erow) * H + u0 + ec) * 2);
+        store_granule(plain, rs_hx, hxd, off, v);
+      }
+      oh_s[s & 1][erow][ec] = hnew;
+      oy_s[s & 1][erow][ec] = act ? hn : 0.f;
+      if (CELL == CELL_GRU) og_s[(CELL == CELL_GRU) ? (s & 1) : 0][erow][ec] = gsv;
+      st.mark(4);
+    }
+  } else {
+    for (int s = 0; s < a.steps; ++s) {
+      st.mark(-1);
+      if (s + 1 < a.steps) mw_put(s + 1);
+      if (s >= 2) mw_store(s - 2);
+      if (s + 2 < a.steps) mw_load(s + 2);
+      st.mark(0);
+      lds_barrier();
+      st.mark(1);
+      if (s_abort) break;
+    }
+  }
+  __syncthreads();
+  if (wave == QW && !s_abort) {
+    if (a.steps >= 2) mw_store(a.steps - 2);
+    if (a.steps >= 1) mw_store(a.steps - 1);
+  }
+  if (STAMPS && wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
 }
 
 constexpr int GW = 7;             // gather waves of the backward kernel
@@ -1493,6 +1797,26 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
   a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->steps <= 0) return 0;
   const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
+  // generation 4 (K-quarter split, register epilogue) unless knob 256 asks for generation 2
+  const int kbq = (d->H / 32 + 3) / 4;
+  // (GRU at kbq = 8 spills under the 3-waves-per-SIMD register budget)
+  if (!(d->knobs & 256) && d->mt == 1 && kbq <= (d->cell == CELL_GRU ? 7 : 8)) {
+#define DS2_QL(C, K)                                                                                  \
+  if (a.stamps) hipLaunchKernelGGL((rnnq_fwd_kernel<C, K, true>), dim3(grid), dim3(QTH), 0, st, a);    \
+  else hipLaunchKernelGGL((rnnq_fwd_kernel<C, K, false>), dim3(grid), dim3(QTH), 0, st, a);
+#define DS2_QK(C, K) \
+  case K: DS2_QL(C, K) break;
+#define DS2_Q(C)                                                                                      \
+  switch (kbq) {                                                                                      \
+    DS2_QK(C, 1) DS2_QK(C, 2) DS2_QK(C, 3) DS2_QK(C, 4) DS2_QK(C, 5) DS2_QK(C, 6) DS2_QK(C, 7)        \
+    default: DS2_QL(C, 8) break;                                                                      \
+  }
+    if (d->cell == CELL_GRU) { DS2_Q(CELL_GRU) } else { DS2_Q(CELL_RELU) }
+#undef DS2_QL
+#undef DS2_QK
+#undef DS2_Q
+    return (int)hipGetLastError();
+  }
   const size_t smem = ds2_rnnx_smem(d->H, G, d->mt, 1);
   int rc;
 #define DS2_FWD(C, M)                                                                        \
