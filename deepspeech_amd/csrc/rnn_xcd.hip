@@ -577,6 +577,9 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   const int bg = grp % a.BG, dir = grp / a.BG;
   const int r0 = bg * R, u0 = mem * UPW;
   const int uh = wave & 1, kq = wave >> 1;
+  // Every wave finalises element j = kq of its tiles. (Measured: handing the R <= 8 rows'
+  // elements to 4 waves only, one per SIMD, so the other 4 go straight back to polling, was
+  // 10 % slower: the early pollers' retry loads compete with the epilogue.)
   const int erow = 4 * (lane >> 4) + (kq & 3);    // this lane's cell element (MFMA waves)
   const int ec = 16 * uh + (lane & 15);
   if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
@@ -744,7 +747,9 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
       }
       const float hnew = act ? hn : hreg;
       hreg = hnew;
-      const unsigned hq = (unsigned)(unsigned short)f2bf_x(hnew);
+      // hardware RNE conversion; 0xFFFF (the sentinel, a negative NaN) -> canonical NaN
+      unsigned hq = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)hnew);
+      hq = hq == 0xffffu ? 0x7fc0u : hq;
       // 16-B exchange granule = 8 consecutive units of one row = 8 consecutive lanes
       const unsigned pr = hq | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)hq, 0x101, 0xf, 0xf, false) << 16);
       const int q1 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x102, 0xf, 0xf, false);
