@@ -10,6 +10,10 @@ Explicit hipcc invocations (no hipify, no setuptools CUDA shim):
 
 Objects are cached under build/ keyed by a hash of (source, included headers, flags),
 so a no-op rebuild takes well under a second. ``python build.py --force`` rebuilds all.
+
+Same-box A/B of a compile-time change: ``python build.py --variant NAME -D SYMBOL`` links
+``ab/_C_NAME<EXT_SUFFIX>`` with the extra defines (the in-tree ``_C`` is left alone) and
+``DS2_EXT_SO=ab/_C_NAME...so`` makes a process load it instead (``scripts/ab_so.sh``).
 """
 from __future__ import annotations
 
@@ -84,7 +88,7 @@ def _compile(src, obj_dir, flags, deps):
     return obj
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines=(), variant: str = "") -> str:
     inc, torch_lib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     os.makedirs(BUILD, exist_ok=True)
@@ -98,6 +102,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         # device-side DS2_DCHECKs (csrc/common.h) print failing conditions; objects are keyed
         # by their flags, so debug and release objects coexist in build/
         common += ["-DDS2_DEBUG=1", "-g"]
+    common += ["-D" + d for d in defines]
     hip_flags = [HIPCC, "--offload-arch=" + ARCH, "-fno-gpu-rdc", "-munsafe-fp-atomics"] + common
     torch_defs = ["-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DUSE_ROCM=1",
                   "-D_GLIBCXX_USE_CXX11_ABI=%d" % abi]
@@ -109,8 +114,12 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         futs.append(ex.submit(_compile, os.path.join(CSRC, "bindings.cpp"), BUILD, bind_flags, []))
         objs = [f.result() for f in futs]
     out = os.path.join(PKG, "_C" + EXT)
-    link_key = _hash(objs, [ARCH])
     stamp = os.path.join(BUILD, "_C.link")
+    if variant:
+        os.makedirs(os.path.join(ROOT, "ab"), exist_ok=True)
+        out = os.path.join(ROOT, "ab", "_C_%s%s" % (variant, EXT))
+        stamp = os.path.join(BUILD, "_C_%s.link" % variant)
+    link_key = _hash(objs, [ARCH])
     if force or not os.path.exists(out) or not os.path.exists(stamp) or open(stamp).read() != link_key:
         tmp = out + ".tmp"
         _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", tmp] + objs + [
@@ -121,7 +130,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
             f.write(link_key)
     if verbose:
         print("built", out)
-    build_runtime(verbose=verbose)
+    if not variant:
+        build_runtime(verbose=verbose)
     return out
 
 
@@ -155,9 +165,13 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=0)
+    ap.add_argument("--variant", default="", help="link ab/_C_<variant> instead of the in-tree _C")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra -D for a variant")
     a = ap.parse_args()
+    if a.defines and not a.variant:
+        ap.error("-D needs --variant (the in-tree _C is always the default build)")
     try:
-        build(force=a.force, verbose=True, jobs=a.jobs)
+        build(force=a.force, verbose=True, jobs=a.jobs, defines=a.defines, variant=a.variant)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

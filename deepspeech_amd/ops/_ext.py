@@ -7,6 +7,7 @@ extension is missing or stale, :func:`ext` raises with the build command. Set
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -16,6 +17,15 @@ _err = None
 
 
 def _try_import():
+    path = os.environ.get("DS2_EXT_SO")
+    if path:
+        # same-box A/B of a compile-time variant (build.py --variant): load that file as _C
+        import sys
+        spec = importlib.util.spec_from_file_location("deepspeech_amd._C", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        sys.modules["deepspeech_amd._C"] = mod
+        return mod
     return importlib.import_module("deepspeech_amd._C")
 
 
