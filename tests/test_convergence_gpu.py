@@ -1,0 +1,64 @@
+"""Training-dynamics parity: 200 Adam steps of the HIP engine (bf16 compute, fused kernels,
+fp32 master weights in the arena) against the pure-PyTorch fp32 reference engine, same
+initial weights, same batches ("a 200-step synthetic
+loss-curve comparison, HIP-bf16 against ref-fp32, on a small model").
+
+Per-step gradients already match within bf16 tolerance (test_engine_gpu.py); this checks
+that the rounding does not accumulate into a different trajectory: windowed mean losses
+must track each other and both runs must actually learn (the reference's training loop:
+src/deepSpeech_train.py:292-380 — Adam, loss EMA, weight EMA).
+"""
+import copy
+
+import pytest
+import torch
+
+from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+from deepspeech_amd.models import DeepSpeech2
+from deepspeech_amd.trainer import LRSchedule, Trainer
+
+pytestmark = pytest.mark.gpu
+
+STEPS, WINDOW = 200, 20
+
+
+def _curves(cuda, cell, steps=STEPS, lr=5e-4):
+    torch.manual_seed(5)
+    ref = DeepSpeech2(num_filters=32, num_hidden=64, num_rnn_layers=2, cell=cell).to(cuda)
+    hip = copy.deepcopy(ref)
+    ref.set_engine("ref", torch.float32)
+    hip.set_engine("hip", torch.bfloat16)
+    # 4 fixed batches cycled: the model can fit them, so the loss has somewhere to go
+    batches = [to_device(FixedShapeBatches(8, max_frames=300, seed=s, pool=1).next(), cuda) for s in range(4)]
+    sched = LRSchedule(lr, 10 ** 9, 1.0)
+    t_ref = Trainer(ref, sched, moving_avg_decay=0.9999)
+    t_hip = Trainer(hip, sched, moving_avg_decay=0.9999)
+    lr_, lh_ = [], []
+    for i in range(steps):
+        b = batches[i % len(batches)]
+        lr_.append(t_ref.step(b).detach().float())
+        lh_.append(t_hip.step(b).detach().float())
+    torch.cuda.synchronize()
+    return torch.stack(lr_).cpu(), torch.stack(lh_).cpu(), t_ref, t_hip
+
+
+@pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
+def test_loss_curve_hip_bf16_tracks_ref_fp32(cuda, cell):
+    lr_, lh_, t_ref, t_hip = _curves(cuda, cell)
+    assert torch.isfinite(lr_).all() and torch.isfinite(lh_).all()
+    wr = lr_.view(-1, WINDOW).mean(1)
+    wh = lh_.view(-1, WINDOW).mean(1)
+    rel = ((wh - wr).abs() / wr).tolist()
+    table = " ".join("%.1f/%.1f" % (a, b) for a, b in zip(wr.tolist(), wh.tolist()))
+    # both engines learn the 4 batches ...
+    assert wr[-1] < 0.7 * wr[0] and wh[-1] < 0.7 * wh[0], "windowed ref/hip loss: " + table
+    # ... along the same trajectory: every 20-step window mean within 5 % (measured on
+    # MI355X: GRU 134 -> 1.2 with max window difference 0.2 %, weights 1.1 % apart; clipped
+    # ReLU 164 -> 1.0, 1.6 %, weights 7.7 %)
+    assert max(rel) < 0.05, "windowed ref/hip loss: %s (max rel diff %.3f)" % (table, max(rel))
+    # the master weights stay close too (fp32 arena in both; only the compute is bf16). The
+    # clipped-ReLU net drifts further: bf16 rounding flips clip masks, and Adam's normalised
+    # steps turn small gradient differences into full-size weight differences
+    w_rel = ((t_hip.arena.flat - t_ref.arena.flat).norm() / t_ref.arena.flat.norm()).item()
+    print("%s windowed ref/hip loss: %s; max rel %.4f; weights rel %.4f" % (cell, table, max(rel), w_rel))
+    assert w_rel < (0.05 if cell == "gru" else 0.12), w_rel
