@@ -127,7 +127,7 @@ class FusedHeadCTC(torch.autograd.Function):
             # K = 32 padded classes; rows >= K of W_fc are never loaded (Kl) and meet G's zero columns
             GM.gemm(G, w16, dh, M, H, 32, False, True, 0, 1.0, None, alpha_dev=scale, Kl=K)
             dh = dh.view(T, N, H)
-        side = wgrad_stream(h.device) if (arena_of(weight) is not None and arena_of(bias) is not None) else None
+        side = wgrad_stream(h.device, arena_of(weight)) if arena_of(bias) is not None else None
         if side is None:
             gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, scale, K)
             return dh, gw, gb, None, None, None, None, None

@@ -364,8 +364,8 @@ class FusedHead(torch.autograd.Function):
         # so the top recurrent layer's BPTT starts right after dh (they were ~75 us on the
         # critical path); the Trainer joins that stream before Adam
         from .rnn import wgrad_stream
-        side = (wgrad_stream(d2.device) if (arena_of(weight) is not None and arena_of(bias) is not None
-                                            and _HEAD_SIDE) else None)
+        side = (wgrad_stream(d2.device, arena_of(weight)) if (arena_of(bias) is not None and _HEAD_SIDE)
+                else None)
         if side is None:
             gw, gb = FusedHead._weight_grads(weight, bias, d2, h2)
             return dh, gw, gb

@@ -67,6 +67,10 @@ class ParamArena:
         self.p16 = torch.zeros(off, device=dev, dtype=torch.bfloat16) if bf16_shadow else None
         self._index = {}
         self._ready_cbs = []
+        # where / when this arena's weight-gradient GEMMs run (side stream, deferral, queues):
+        # per arena, so independent models in one process never share that state
+        from .rnn import WgradScheduler
+        self.wgrad = WgradScheduler()
         # per-parameter "gradient written" events (enabled by the DP bucketer): recorded on
         # whatever stream enqueued the gradient write, so a collective waits for exactly
         # the producers of its bucket instead of joining whole streams

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -562,7 +563,7 @@ class FusedBiLayer(torch.autograd.Function):
         # ---- weight gradients (off the critical path) ----
         # only arena-managed weights (gradients written to main_grad, nothing returned to
         # autograd) may be produced on another stream; the Trainer joins it before Adam
-        side = wgrad_stream(x16.device) if arena_of(ctx.params[0]) is not None else None
+        side = wgrad_stream(x16.device, arena_of(ctx.params[0]))
         if side is None:
             return FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx)
         # The layer below only needs dx: its BPTT (200 of the 256 CUs, latency-bound) runs
@@ -590,14 +591,15 @@ class FusedBiLayer(torch.autograd.Function):
             def dw(grp=grp, dgx2=dgx2, x2=x2):
                 mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
                 arena.grad_done(W_f, W_b if d1 else None)
+            sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
-            if _defer_input_wgrad and on_side and ctx.idx >= _DEFER_MIN_LAYER:
-                _deferred.append(dw)              # run after the last recurrent layer's BPTT
-                _queue_end_of_backward()
+            if sch.defer_input and on_side and ctx.idx >= sch.min_layer:
+                sch.deferred.append(dw)           # run after the last recurrent layer's BPTT
+                sch.queue_end_of_backward()
             else:
                 dw()
             if ctx.idx == 0:
-                flush_deferred_wgrads()
+                sch.flush()
         else:
             for d, p in enumerate([W_f, W_b] if d1 else [W_f]):
                 g = mm_into(p, dgx2[:, d * GH:(d + 1) * GH].t(), x2)
@@ -619,13 +621,14 @@ class FusedBiLayer(torch.autograd.Function):
                     except (RuntimeError, TypeError):
                         out.copy_(torch.bmm(g3, h3))
                 arena.grad_done(U_f, U_b)
+            sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
-            if _defer_input_wgrad and on_side and ctx.idx == 0 and _TAIL_DU:
+            if sch.defer_input and on_side and ctx.idx == 0 and sch.tail_du:
                 # the side stream already carries dW_0 + every deferred dW and ends after the
                 # conv front-end's backward on the main stream: balance by issuing the
-                # bottom layer's dU on the main stream behind the front-end (join_wgrad_streams)
-                _main_tail.append(du)
-                _queue_end_of_backward()
+                # bottom layer's dU on the main stream behind the front-end (WgradScheduler.join)
+                sch.main_tail.append(du)
+                sch.queue_end_of_backward()
             else:
                 du()
         else:
@@ -639,99 +642,120 @@ class FusedBiLayer(torch.autograd.Function):
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
 
 
-_side_streams = {}
+class WgradScheduler:
+    """Where and when one parameter arena's weight-gradient GEMMs run.
+
+    Owned by the :class:`~deepspeech_amd.ops.optim.ParamArena` whose gradients it produces
+    (``arena.wgrad``), so two trainers / models in one process (training beside eval or
+    streaming, two Trainers in a test) never share a side stream, a deferral switch or a
+    queue of pending GEMMs (this state used to be module-global).
+
+    * ``stream(device)``: side stream for the recurrent layers' (and head's / front-end's)
+      weight-gradient GEMMs (DS2_WGRAD_STREAM=0 keeps them on the current stream). The
+      Trainer joins it (:meth:`join`) before the optimizer reads the gradients.
+    * Input-weight gradients (dW = dgx^T x) of layers > 0 may be deferred until the last
+      recurrent layer's BPTT has been issued: the side stream then carries only the
+      recurrent dU GEMMs while the BPTT chain runs, which competes less with it (1 GPU:
+      10.40-10.47 vs 10.60-10.64 ms/step on the same boxes; deferring dU too was slower).
+      With data parallelism it would hold those gradient buckets back to the end of
+      backward, so the Trainer enables it for world_size == 1 only (DS2_DEFER_DW=0/1
+      overrides).
+    """
+
+    def __init__(self):
+        self.streams = {}
+        self.defer_input = False
+        self.min_layer = int(os.environ.get("DS2_DEFER_MIN_LAYER", "1"))
+        self.tail_du = os.environ.get("DS2_TAIL_DU", "1") == "1"
+        self.deferred = []
+        self.main_tail = []        # GEMMs issued on the main stream once the whole backward is queued
+        self._eob_queued = False
+        _schedulers.add(self)
+
+    def stream(self, device: torch.device) -> Optional["torch.cuda.Stream"]:
+        if device.type != "cuda" or os.environ.get("DS2_WGRAD_STREAM", "1") != "1":
+            return None
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        s = self.streams.get(idx)
+        if s is None:
+            s = torch.cuda.Stream(device=torch.device("cuda", idx))
+            self.streams[idx] = s
+        return s
+
+    def set_deferral(self, on: bool) -> None:
+        env = os.environ.get("DS2_DEFER_DW")
+        self.defer_input = (env == "1") if env in ("0", "1") else bool(on)
+
+    def discard(self) -> None:
+        """Drop deferred GEMMs of an aborted backward (called at the start of a step)."""
+        self.deferred.clear()
+        self.main_tail.clear()
+        self._eob_queued = False
+
+    def flush(self) -> None:
+        """Issue every deferred input-weight gradient GEMM (on the current stream)."""
+        while self.deferred:
+            self.deferred.pop(0)()
+
+    def drain(self) -> None:
+        """Issue every deferred weight-gradient GEMM: leftover input-weight GEMMs (a backward
+        that never reached layer 0) on the side stream, then the main-stream tail (the bottom
+        layer's dU behind the front-end backward)."""
+        if self.deferred:
+            for idx, s in self.streams.items():
+                s.wait_stream(torch.cuda.current_stream(idx))
+                with torch.cuda.stream(s):
+                    self.flush()
+            self.flush()
+        while self.main_tail:
+            self.main_tail.pop(0)()
+
+    def queue_end_of_backward(self) -> None:
+        """Drain the deferred GEMMs when the running backward finishes, whoever drives it
+        (Trainer.step, a bare loss.backward(), the --debug profiler): autograd runs final
+        callbacks on the caller's current streams once the whole graph has been executed,
+        so no gradient is left unwritten (lazy zeroing would otherwise keep a stale value)."""
+        if self._eob_queued:
+            return
+        self._eob_queued = True
+
+        def cb():
+            self._eob_queued = False
+            self.drain()
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(cb)
+        except RuntimeError:              # not inside a backward: drained by join()
+            self._eob_queued = False
+
+    def pending(self) -> int:
+        """Number of weight-gradient GEMMs still waiting to be issued (0 after a backward)."""
+        return len(self.deferred) + len(self.main_tail)
+
+    def join(self) -> None:
+        """Make the current stream wait for every pending side-stream weight gradient."""
+        self.drain()
+        for idx, s in self.streams.items():
+            torch.cuda.current_stream(idx).wait_stream(s)
 
 
-def wgrad_stream(device: torch.device) -> Optional["torch.cuda.Stream"]:
-    """Side stream for the recurrent layers' weight-gradient GEMMs (DS2_WGRAD_STREAM=0
-    keeps them on the current stream). Callers join it with :func:`join_wgrad_streams`
-    before the optimizer reads the gradients."""
-    if device.type != "cuda" or os.environ.get("DS2_WGRAD_STREAM", "1") != "1":
-        return None
-    s = _side_streams.get(device.index)
-    if s is None:
-        s = torch.cuda.Stream(device=device)
-        _side_streams[device.index] = s
-    return s
+_schedulers = weakref.WeakSet()
 
 
-# Input-weight gradients (dW = dgx^T x) of layers > 0 may be deferred until the last
-# recurrent layer's BPTT has been issued: the side stream then carries only the recurrent
-# dU GEMMs while the BPTT chain runs, which competes less with it (measured 1 GPU: 10.40-10.47
-# vs 10.60-10.64 ms/step on the same boxes; deferring dU too was slower). With data
-# parallelism it would hold those gradient buckets back to the end of backward, so the
-# Trainer enables it for world_size == 1 only (DS2_DEFER_DW=0/1 overrides).
-_defer_input_wgrad = False
-_DEFER_MIN_LAYER = int(os.environ.get("DS2_DEFER_MIN_LAYER", "1"))
-_TAIL_DU = os.environ.get("DS2_TAIL_DU", "1") == "1"
-_deferred = []
-_main_tail = []     # GEMMs issued on the main stream once the whole backward is queued
+def wgrad_stream(device: torch.device, arena=None) -> Optional["torch.cuda.Stream"]:
+    """The weight-gradient side stream of ``arena`` (None without an arena: plain autograd
+    gradients are returned to autograd on the current stream)."""
+    return arena.wgrad.stream(device) if arena is not None else None
 
 
-def set_input_wgrad_deferral(on: bool) -> None:
-    global _defer_input_wgrad
-    env = os.environ.get("DS2_DEFER_DW")
-    _defer_input_wgrad = (env == "1") if env in ("0", "1") else bool(on)
+def join_wgrad_streams(arena=None) -> None:
+    """Join ``arena``'s weight-gradient work (every live arena's when None: tests and tools
+    that drive a bare ``loss.backward()``)."""
+    for sch in ([arena.wgrad] if arena is not None else list(_schedulers)):
+        sch.join()
 
 
-def discard_deferred_wgrads() -> None:
-    """Drop deferred GEMMs of an aborted backward (called at the start of a step)."""
-    _deferred.clear()
-    _main_tail.clear()
-    _eob_queued[0] = False
-
-
-def flush_deferred_wgrads() -> None:
-    """Issue every deferred input-weight gradient GEMM (on the current stream)."""
-    while _deferred:
-        _deferred.pop(0)()
-
-
-def _drain_deferred() -> None:
-    """Issue every deferred weight-gradient GEMM: leftover input-weight GEMMs (a backward
-    that never reached layer 0) on the side stream, then the main-stream tail (the bottom
-    layer's dU behind the front-end backward)."""
-    if _deferred:
-        for idx, s in _side_streams.items():
-            s.wait_stream(torch.cuda.current_stream(idx))
-            with torch.cuda.stream(s):
-                flush_deferred_wgrads()
-        flush_deferred_wgrads()
-    while _main_tail:
-        _main_tail.pop(0)()
-
-
-_eob_queued = [False]
-
-
-def _queue_end_of_backward() -> None:
-    """Drain the deferred GEMMs when the running backward finishes, whoever drives it
-    (Trainer.step, a bare loss.backward(), the --debug profiler): autograd runs final
-    callbacks on the caller's current streams once the whole graph has been executed,
-    so no gradient is left unwritten (lazy zeroing would otherwise keep a stale value)."""
-    if _eob_queued[0]:
-        return
-    _eob_queued[0] = True
-
-    def cb():
-        _eob_queued[0] = False
-        _drain_deferred()
-    try:
-        torch.autograd.Variable._execution_engine.queue_callback(cb)
-    except RuntimeError:                  # not inside a backward: drained by join_wgrad_streams
-        _eob_queued[0] = False
-
-
-def pending_deferred() -> int:
-    """Number of weight-gradient GEMMs still waiting to be issued (0 after a backward)."""
-    return len(_deferred) + len(_main_tail)
-
-
-def join_wgrad_streams() -> None:
-    """Make the current stream wait for every pending side-stream weight gradient."""
-    _drain_deferred()
-    for idx, s in _side_streams.items():
-        torch.cuda.current_stream(idx).wait_stream(s)
+def pending_deferred(arena=None) -> int:
+    return sum(sch.pending() for sch in ([arena.wgrad] if arena is not None else list(_schedulers)))
 
 
 _plan_cache = {}

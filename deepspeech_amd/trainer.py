@@ -25,7 +25,6 @@ import torch
 
 from .models import DeepSpeech2
 from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
-from .ops.rnn import discard_deferred_wgrads, join_wgrad_streams
 from .parallel.grad_sync import GradBucketer, broadcast_params
 from .utils import trace as TR
 from .utils.stats import NonfiniteWatch
@@ -66,13 +65,13 @@ class Trainer:
             self.arena.mark_dirty()
             if self.opt.ema is not None:
                 self.opt.ema.copy_(self.arena.flat)
-        from .ops.rnn import set_input_wgrad_deferral
         # Deferring the input-weight gradients of layers >= 1 to the end of the BPTT chain
         # measured within noise on one GPU (profiles/r1_s3_negative_results.md) and, with
         # data parallelism, would hold ~40 % of the gradient bytes (every layer's W) back
         # until backward ends instead of releasing one bucket per layer for overlap: on for
         # the single-GPU path only (DS2_DEFER_DW=0/1 overrides)
-        set_input_wgrad_deferral(world_size == 1 and not self.bucketer.enabled)
+        # (per arena: another Trainer / model in this process keeps its own setting)
+        self.arena.wgrad.set_deferral(world_size == 1 and not self.bucketer.enabled)
         self.global_step = 0
         self.nan_policy = nan_policy
         self.collapse_repeated = collapse_repeated
@@ -92,12 +91,12 @@ class Trainer:
         # the HIP engine delivers every gradient through the arena (first write overwrites),
         # so the per-step memset of the whole gradient buffer is skipped
         lazy = model.engine == "hip"
-        discard_deferred_wgrads()
+        self.arena.wgrad.discard()
         self.arena.zero_grad(lazy=lazy)
         loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
         self.watch.update(loss)
         loss.backward()
-        join_wgrad_streams()
+        self.arena.wgrad.join()
         if lazy:
             self.arena.zero_unwritten()
         with TR.phase(TR.ALLREDUCE):
