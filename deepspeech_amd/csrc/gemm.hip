@@ -157,7 +157,44 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
 }
 
-template <int AC, int BC, int FM, int FN, int WM, int WN, int NS>
+// One tile's C-store: lane (row mb + 16i, columns nb + 16j .. +3). Buffer stores with an
+// exact per-lane count (rows / columns past M / N get an out-of-range offset and are dropped
+// by the resource's bounds check), so a persistent workgroup can count vmcnt across it.
+template <int FM, int FN>
+__device__ __forceinline__ void store_tile(const GemmArgs& g, const f32x4 (&acc)[FN][FM], const float (&bv)[FN][4],
+                                           float alpha, int mb, int nb) {
+  const size_t esz = g.epi == 0 ? 2 : 4;
+  const size_t cbytes = (size_t)g.M * g.ldc * esz;
+  char* Cz = (char*)g.C + (size_t)blockIdx.z * g.sC * esz;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(Cz, (unsigned)min(cbytes, (size_t)0xFFFFFFF0u));
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = nb + j * 16;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = mb + i * 16;
+      const unsigned off = (m < g.M && n < g.N) ? (unsigned)(((size_t)m * g.ldc + n) * esz) : 0xFFFFFFF0u;
+      const f32x4 v = acc[j][i];
+      if (g.epi == 0) {
+        const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[j][0]) | ((unsigned)f2bf(alpha * v[1] + bv[j][1]) << 16);
+        const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[j][2]) | ((unsigned)f2bf(alpha * v[3] + bv[j][3]) << 16);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                                 make_uint2(lo, hi)), rs, off, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                               make_float4(alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3])), rs, off, 0, 0);
+      }
+    }
+  }
+}
+
+// PERS: persistent grid (one workgroup per CU, a multiple of 8): XCD x = blockIdx % 8 owns the
+// contiguous tile-id range [x*Tx, (x+1)*Tx) of the grouped order and its workgroups stride
+// through it. At a tile seam the next tile's first NS-1 LDS stages go out BEFORE this tile's
+// C stores, so the next prologue's load latency hides under the epilogue (the per-tile fixed
+// cost was ~1/3 of the K = 800 projection). epi 2 (read-modify-write) is not persistent.
+template <int AC, int BC, int FM, int FN, int WM, int WN, int NS, bool PERS>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
   constexpr int NW = WM * WN, BM = WM * FM * 16, BN = WN * FN * 16;
   constexpr int A_BYTES = BM * BK * 2, STAGE_BYTES = (BM + BN) * BK * 2;
@@ -174,31 +211,42 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
   // once form a GROUP_M x (32/GROUP_M) block whose A rows and B columns share that XCD's L2
   // (row-major tile order streamed all of B through every XCD: MALL-bound, 25 % MFMA busy).
   constexpr int GROUP_M = 8;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int gsz = GROUP_M * ntn;
-  const int grp = id / gsz, first_m = grp * GROUP_M;
-  const int gm = min(ntm - first_m, GROUP_M);
-  if (gm <= 0) return;
-  const int within = id - grp * gsz;
-  const int tm = first_m + within % gm, tn = within / gm;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int id, id_end, id_step;
+  if constexpr (PERS) {
+    const int total = ntm * ntn, tx = (total + 7) >> 3, x = blockIdx.x & 7;
+    id = x * tx + (blockIdx.x >> 3);
+    id_end = min(total, (x + 1) * tx);
+    id_step = gridDim.x >> 3;
+  } else {
+    id = xcd_remap(blockIdx.x, gridDim.x);
+    id_end = id + 1;
+    id_step = 1;
+  }
+  auto coords = [&](int t, int& m0_, int& n0_) -> bool {
+    const int gsz = GROUP_M * ntn;
+    const int grp = t / gsz, first_m = grp * GROUP_M;
+    const int gm = min(ntm - first_m, GROUP_M);
+    if (gm <= 0) return false;
+    const int within = t - grp * gsz;
+    m0_ = (first_m + within % gm) * BM;
+    n0_ = (within / gm) * BN;
+    return true;
+  };
+  int m0, n0;
+  if (id >= id_end || !coords(id, m0, n0)) return;
   const bf16_t* A = g.A + (size_t)blockIdx.z * g.sA;
   const bf16_t* B = g.B + (size_t)blockIdx.z * g.sB;
   const int tid = threadIdx.x, lane = tid & 63, wave = uni(tid >> 6);
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int K = g.K;
   const int nkt = (K + BK - 1) / BK;
+  const float alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
 
   f32x4 acc[FN][FM];
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto stage_all = [&](int buf, int kt) {
+  auto stage_all = [&](int buf, int kt, int mm0, int nn0) {
     unsigned char* base = smem + buf * STAGE_BYTES;
-    stage<AC != 0, BM, NW>(base, A, g.lda, m0, g.Ml, kt * BK, AC ? g.Kl : K, wave, lane);
-    stage<BC != 0, BN, NW>(base + A_BYTES, B, g.ldb, n0, g.Nl, kt * BK, BC ? g.Kl : K, wave, lane);
+    stage<AC != 0, BM, NW>(base, A, g.lda, mm0, g.Ml, kt * BK, AC ? g.Kl : K, wave, lane);
+    stage<BC != 0, BN, NW>(base + A_BYTES, B, g.ldb, nn0, g.Nl, kt * BK, BC ? g.Kl : K, wave, lane);
   };
 
   // Pipeline (cdna_hip_programming.md §5 'Pipelining across barriers'), NS LDS stages:
@@ -234,98 +282,151 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
         acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][i], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  auto prologue_issue = [&](int mm0, int nn0) {
+    stage_all(0, 0, mm0, nn0);
+    if (NS == 3 && nkt > 1) stage_all(1, 1, mm0, nn0);
+  };
 
-  stage_all(0, 0);
-  if (NS == 3 && nkt > 1) {
-    stage_all(1, 1);
-    wait_vm<LPW>();
-  } else {
-    wait_vm<0>();
-  }
-  lds_barrier();
-  prep(0, smem);
-  read_half(smem, 0, af0, bf0);
-  int buf = 0;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = kt + NS - 1 < nkt;
-    if (more) {
-      const int nb = buf + NS - 1;
-      stage_all(nb >= NS ? nb - NS : nb, kt + NS - 1);
-    }
-    unsigned char* cur = smem + buf * STAGE_BYTES;
-    const bool half2 = kvalid(kt) > 32;
-    if (half2) read_half(cur, 1, af1, bf1);
-    mfma_half(af0, bf0);
-    const int nxt = (buf + 1 == NS) ? 0 : buf + 1;
-    if (kt + 1 < nkt) {
-      if (NS == 3 && more) wait_vm<LPW>();
+  prologue_issue(m0, n0);
+  bool first = true;
+  while (true) {
+    // stage 0 landed: behind it are stage 1 (NS = 3) and, after a seam, the previous tile's
+    // FM*FN C stores (vmcnt counts stores too and retires in order)
+    if (first) {
+      if (NS == 3 && nkt > 1) wait_vm<LPW>();
       else wait_vm<0>();
-      lds_barrier();
-      prep(kt + 1, smem + nxt * STAGE_BYTES);
-      read_half(smem + nxt * STAGE_BYTES, 0, af0, bf0);
+    } else {
+      if (NS == 3 && nkt > 1) wait_vm<LPW + FM * FN>();
+      else wait_vm<FM * FN>();
     }
-    if (half2) mfma_half(af1, bf1);
-    buf = nxt;
-  }
-
-  // epilogue: acc[j][i][e] = C[m][n + e], m = row of A fragment lane&15, n = 4 consecutive
-  const int mb = m0 + wm * FM * 16 + (lane & 15);
-  const int nb = n0 + wn * FN * 16 + 4 * (lane >> 4);
-  const float alpha = g.alpha_dev ? g.alpha * *g.alpha_dev : g.alpha;
+    first = false;
+    lds_barrier();
+    // this tile's bias columns, loaded now so their latency hides under the k-loop
+    // (unconditional, clamped loads: a conditional load gets a vmcnt(0) right behind it)
+    const int nb = n0 + wn * FN * 16 + 4 * (lane >> 4);
+    const bool has_bias = g.epi == 0 && g.bias != nullptr;
+    const bf16_t* bsrc = has_bias ? g.bias : B;
+    uint2 braw[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = nb + j * 16;
-    if (n >= g.N) continue;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (g.epi == 0 && g.bias) {
-      const uint2 b2 = *(const uint2*)(g.bias + n);
-      bv[0] = bf2f((bf16_t)(b2.x & 0xffff)); bv[1] = bf2f((bf16_t)(b2.x >> 16));
-      bv[2] = bf2f((bf16_t)(b2.y & 0xffff)); bv[3] = bf2f((bf16_t)(b2.y >> 16));
-    }
+    for (int j = 0; j < FN; ++j) braw[j] = *(const uint2*)(bsrc + min(nb + j * 16, g.N - 4));
+    prep(0, smem);
+    read_half(smem, 0, af0, bf0);
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = mb + i * 16;
-      if (m >= g.M) continue;
-      const f32x4 v = acc[j][i];
-      if (g.epi == 0) {
-        bf16_t* C = (bf16_t*)g.C + (size_t)blockIdx.z * g.sC + (size_t)m * g.ldc + n;
-        const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[0]) | ((unsigned)f2bf(alpha * v[1] + bv[1]) << 16);
-        const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[2]) | ((unsigned)f2bf(alpha * v[3] + bv[3]) << 16);
-        *(uint2*)C = make_uint2(lo, hi);
-      } else {
-        float* C = (float*)g.C + (size_t)blockIdx.z * g.sC + (size_t)m * g.ldc + n;
-        float4 o = make_float4(alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3]);
-        if (g.epi == 2) {
-          const float4 c = *(const float4*)C;
-          o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
-        }
-        *(float4*)C = o;
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int buf = 0;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const bool more = kt + NS - 1 < nkt;
+      if (more) {
+        const int nb = buf + NS - 1;
+        stage_all(nb >= NS ? nb - NS : nb, kt + NS - 1, m0, n0);
       }
+      unsigned char* cur = smem + buf * STAGE_BYTES;
+      const bool half2 = kvalid(kt) > 32;
+      if (half2) read_half(cur, 1, af1, bf1);
+      mfma_half(af0, bf0);
+      const int nxt = (buf + 1 == NS) ? 0 : buf + 1;
+      if (kt + 1 < nkt) {
+        if (NS == 3 && more) wait_vm<LPW>();
+        else wait_vm<0>();
+        lds_barrier();
+        prep(kt + 1, smem + nxt * STAGE_BYTES);
+        read_half(smem + nxt * STAGE_BYTES, 0, af0, bf0);
+      }
+      if (half2) mfma_half(af1, bf1);
+      buf = nxt;
+    }
+
+    // epilogue: acc[j][i][e] = C[m][n + e], m = row of A fragment lane&15, n = 4 consecutive
+    const int mb = m0 + wm * FM * 16 + (lane & 15);
+    float bv[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const uint2 b2 = braw[j];
+      const float on = has_bias ? 1.f : 0.f;
+      bv[j][0] = on * bf2f((bf16_t)(b2.x & 0xffff)); bv[j][1] = on * bf2f((bf16_t)(b2.x >> 16));
+      bv[j][2] = on * bf2f((bf16_t)(b2.y & 0xffff)); bv[j][3] = on * bf2f((bf16_t)(b2.y >> 16));
+    }
+    if constexpr (PERS) {
+      const int nid = id + id_step;
+      int nm0 = 0, nn0 = 0;
+      const bool next = nid < id_end && coords(nid, nm0, nn0);
+      if (next) {
+        lds_barrier();                 // every wave's last fragment reads of this tile retired
+        prologue_issue(nm0, nn0);      // next tile's loads fly under this tile's stores
+      }
+      store_tile<FM, FN>(g, acc, bv, alpha, mb, nb);
+      if (!next) break;
+      id = nid;
+      m0 = nm0;
+      n0 = nn0;
+      continue;
+    } else {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = nb + j * 16;
+        if (n >= g.N) continue;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = mb + i * 16;
+          if (m >= g.M) continue;
+          const f32x4 v = acc[j][i];
+          if (g.epi == 0) {
+            bf16_t* C = (bf16_t*)g.C + (size_t)blockIdx.z * g.sC + (size_t)m * g.ldc + n;
+            const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[j][0]) | ((unsigned)f2bf(alpha * v[1] + bv[j][1]) << 16);
+            const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[j][2]) | ((unsigned)f2bf(alpha * v[3] + bv[j][3]) << 16);
+            *(uint2*)C = make_uint2(lo, hi);
+          } else {
+            float* C = (float*)g.C + (size_t)blockIdx.z * g.sC + (size_t)m * g.ldc + n;
+            float4 o = make_float4(alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3]);
+            if (g.epi == 2) {
+              const float4 c = *(const float4*)C;
+              o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
+            }
+            *(float4*)C = o;
+          }
+        }
+      }
+      break;
     }
   }
 }
 
-template <int AC, int BC, int FM, int FN, int WM, int WN, int NS>
+template <int AC, int BC, int FM, int FN, int WM, int WN, int NS, bool PERS = false>
 int launch(const GemmArgs& a, int batch, hipStream_t st) {
   constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
   const int lds = (BM + BN) * BK * 2 * NS;
-  auto kern = gemm_kernel<AC, BC, FM, FN, WM, WN, NS>;
+  auto kern = gemm_kernel<AC, BC, FM, FN, WM, WN, NS, PERS>;
   static bool attr = false;
   if (!attr) {
     DS2_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr = true;
   }
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL(kern, dim3(tiles, 1, batch), dim3(WM * WN * 64), lds, st, a);
+  int grid = tiles;
+  if (PERS) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      DS2_HIP_CHECK(hipGetDevice(&dev));
+      DS2_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    grid = min(cus, (tiles + 7) & ~7);          // one workgroup per CU (>= 96 KB of LDS), x8 for the XCD map
+    grid = max(8, grid & ~7);
+  }
+  hipLaunchKernelGGL(kern, dim3(grid, 1, batch), dim3(WM * WN * 64), lds, st, a);
   return (int)hipGetLastError();
 }
 
 // tile configurations (BM x BN, waves, LDS stages):
 //   0 = 256x256 8w 2st (128 KB)   1 = 128x256 8w 3st (144 KB)   2 = 256x128 8w 3st (144 KB)
 //   3 = 128x128 4w 2st (64 KB, 2 per CU)   4 = 128x128 4w 3st (96 KB)   5 = 128x128 8w 3st (96 KB)
-constexpr int NCFG = 6;
+//   6/7/8 = persistent 0/1/2 (epilogue overlapped with the next tile's loads; epi 0/1 only)
+constexpr int NCFG = 9;
 template <int AC, int BC>
 int dispatch(const GemmArgs& a, int batch, int cfg, hipStream_t st) {
+  if (cfg >= 6 && a.epi == 2) return (int)hipErrorInvalidValue;
   switch (cfg) {
     case 0: return launch<AC, BC, 8, 4, 2, 4, 2>(a, batch, st);
     case 1: return launch<AC, BC, 4, 4, 2, 4, 3>(a, batch, st);
@@ -333,6 +434,9 @@ int dispatch(const GemmArgs& a, int batch, int cfg, hipStream_t st) {
     case 3: return launch<AC, BC, 4, 4, 2, 2, 2>(a, batch, st);
     case 4: return launch<AC, BC, 4, 4, 2, 2, 3>(a, batch, st);
     case 5: return launch<AC, BC, 2, 4, 4, 2, 3>(a, batch, st);
+    case 6: return launch<AC, BC, 8, 4, 2, 4, 2, true>(a, batch, st);
+    case 7: return launch<AC, BC, 4, 4, 2, 4, 3, true>(a, batch, st);
+    case 8: return launch<AC, BC, 4, 4, 4, 2, 3, true>(a, batch, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -343,7 +447,8 @@ extern "C" {
 
 // Returns the tile (BM, BN) of configuration cfg, or -1.
 int ds2_gemm_tile(int cfg, int* bm, int* bn) {
-  static const int T[NCFG][2] = {{256, 256}, {128, 256}, {256, 128}, {128, 128}, {128, 128}, {128, 128}};
+  static const int T[NCFG][2] = {{256, 256}, {128, 256}, {256, 128}, {128, 128}, {128, 128}, {128, 128},
+                                 {256, 256}, {128, 256}, {256, 128}};
   if (cfg < 0 || cfg >= NCFG) return -1;
   *bm = T[cfg][0];
   *bn = T[cfg][1];

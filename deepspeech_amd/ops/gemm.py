@@ -24,11 +24,15 @@ from . import _ext
 # cfg -> (BM, BN, workgroups per CU); LDS = 2 stages x (BM + BN) x 64 x 2 B
 _TILES = {0: (256, 256, 1), 1: (128, 256, 1), 2: (256, 128, 1), 3: (128, 128, 2), 4: (128, 128, 1),
           5: (128, 128, 1)}
+# 6/7/8: persistent versions of 0/1/2 (one workgroup per CU striding over tiles, the next
+# tile's loads under this tile's stores); explicit TUNED picks only (no read-modify-write)
+_PERSISTENT = {6: 0, 7: 1, 8: 2}
 # measured picks: (M, N, K, a_col, b_col, batch) -> cfg
 TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
     # headline shapes (T2=241, N=32, H=800), tools/bench_gemm_ours.py on MI355X
-    (7712, 4800, 800, False, False, 1): 1,     # projection, layers 1-4: 93 us
-    (7712, 4800, 2400, False, False, 1): 1,    # projection, layer 0: 213 us
+    # projections: persistent 128x256 (cfg 7) 84.2 / 196.3 us vs 87.1 / 200.8 (cfg 1), same box
+    (7712, 4800, 800, False, False, 1): 7,     # projection, layers 1-4
+    (7712, 4800, 2400, False, False, 1): 7,    # projection, layer 0
     (7712, 800, 4800, False, True, 1): 2,
     (7712, 2400, 4800, False, True, 1): 2,
     (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
@@ -89,6 +93,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
     batch = A.shape[0] if A.dim() == 3 else 1
     if cfg is None:
         cfg = choose_cfg(M, N, K, a_col, b_col, batch, _dev_cus(A))
+        if epi != 2 and cfg in (1, 2) and _FORCE is None:
+            cfg += 6        # the persistent twin: same tile, next tile's loads under the stores
     _ext.ext().gemm(A, B, C, bias, M, N, K, a_col, b_col, epi, float(alpha), cfg, alpha_dev, Ml, Nl, Kl)
     return C
 

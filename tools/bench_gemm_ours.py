@@ -17,7 +17,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from deepspeech_amd.ops import gemm as G  # noqa: E402
 
-NCFG = 6
+NCFG = 9
 
 
 def timeit(fn, iters=10):
