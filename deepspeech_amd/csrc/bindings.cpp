@@ -70,8 +70,10 @@ struct DS2RnnX {
   long long timeout;
   unsigned long long* stamps;
   void* ring[2];
+  void* ysum;
 };
 int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st);
+int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs);
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
 long long ds2_rnnx_ring_floats(int H, int BG, int R);
 int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st);
@@ -279,7 +281,7 @@ void rnnx_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_
               OptT y_b, at::Tensor hx_f, OptT hx_b, at::Tensor hs_f, OptT hs_b, OptT gates_f, OptT gates_b,
               at::Tensor census, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t R,
               int64_t steps, int64_t gstride, int64_t ndir, int64_t cell, int64_t mt, int64_t timeout,
-              int64_t xcd_map, int64_t knobs, OptT stamps) {
+              int64_t xcd_map, int64_t knobs, OptT stamps, OptT ysum) {
   need_gpu(gx, "gx");
   TORCH_CHECK(gx.scalar_type() == at::kBFloat16 && gx.numel() >= T * N * gstride, "gx must be bf16 [T, N, gstride]");
   TORCH_CHECK(lens.scalar_type() == at::kInt && lens.numel() == N, "lens must be int32 [N]");
@@ -300,6 +302,12 @@ void rnnx_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_
   d.hsave[1] = ptr_or_null<float>(hs_b, "hs_b");
   d.gates[0] = ptr_or_null<float>(gates_f, "gates_f");
   d.gates[1] = ptr_or_null<float>(gates_b, "gates_b");
+  d.ysum = nullptr;
+  if (ysum.has_value()) {
+    TORCH_CHECK(ysum->scalar_type() == at::kBFloat16 && ysum->numel() >= T * N * H && ysum->is_contiguous(),
+                "ysum must be contiguous bf16 [T, N, H]");
+    d.ysum = ysum->data_ptr();
+  }
   TORCH_CHECK(ndir == 1 || (d.U[1] && d.y[1] && d.ex[1] && d.hsave[1]), "backward-direction buffers missing");
   TORCH_CHECK(cell == 0 || (d.gates[0] && (ndir == 1 || d.gates[1])), "GRU needs gate buffers");
   check(ds2_rnnx_fwd(&d, cur_stream()), "rnnx_fwd");
@@ -770,7 +778,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("census"), py::arg("err"), py::arg("T"),
         py::arg("N"), py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("R"), py::arg("steps"), py::arg("gstride"),
         py::arg("ndir"), py::arg("cell"), py::arg("mt"), py::arg("timeout"), py::arg("xcd_map"), py::arg("knobs"),
-        py::arg("stamps") = py::none());
+        py::arg("stamps") = py::none(), py::arg("ysum") = py::none());
+  m.def("rnnx_fwd_fuses_sum", [](int64_t H, int64_t cell, int64_t mt, int64_t ndir, int64_t knobs) {
+    return ds2_rnnx_fwd_fuses_sum((int)H, (int)cell, (int)mt, (int)ndir, (int)knobs) != 0;
+  });
   m.def("rnnx_bwd", &rnnx_bwd, py::arg("dy"), py::arg("lens"), py::arg("U_f"), py::arg("U_b"), py::arg("hs_f"),
         py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("dgh_f"), py::arg("dgh_b"), py::arg("dgx"),
         py::arg("dbx_part"), py::arg("dbh_part"), py::arg("dgx_scale"), py::arg("census"), py::arg("err"),

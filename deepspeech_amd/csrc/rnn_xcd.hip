@@ -53,6 +53,7 @@ struct XFwd {
   const bf16_t* U[2];
   const float* bh[2];
   bf16_t* y[2];
+  bf16_t* ysum;           // gen 4, two directions: fused direction sum [T][N][H], sentinel-filled
   bf16_t* hx[2];          // [steps+1][NP][H]: slot 0 = h0, slots 1.. pre-filled with sentinel
   float* hsave[2];
   float* gates[2];
@@ -619,6 +620,19 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
       }
     }
   };
+  // fused direction sum: the other direction's value for this lane's 2 output granules of
+  // step s, loaded ahead (before the gx put) so the round trip hides under the put
+  unsigned long long yq[2] = {0ull, 0ull};
+  auto ysum_ptr = [&](int s, int j) -> unsigned long long* {
+    const int row = min((lane >> 3) + 8 * j, R - 1), c4 = (lane & 7) * 4;
+    const int b = min(r0 + row, N - 1), L = len_s[row];
+    const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+    return reinterpret_cast<unsigned long long*>(a.ysum + ((size_t)t * N + b) * H + u0 + c4);
+  };
+  auto mw_ysum_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) yq[j] = __hip_atomic_load(ysum_ptr(s, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   // outputs of step s out of staging slot s&1: lane -> (row, 4 consecutive units) x 2
   auto mw_store = [&](int s) {
     f32x4 vh[2], vy[2];
@@ -643,13 +657,61 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) gp[i] = vg[j][i];
         }
+      }
+    }
+    // y (or the fused direction sum) after the state stores: the gate registers are dead
+    // before any wait on the other direction
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
+      if (row < R) {
+        const int b = r0 + row, u = u0 + c4;
         if (b < N) {
           const int L = len_s[row];
           const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
           uint2 o;
           o.x = (unsigned)f2bf(vy[j][0]) | ((unsigned)f2bf(vy[j][1]) << 16);
           o.y = (unsigned)f2bf(vy[j][2]) | ((unsigned)f2bf(vy[j][3]) << 16);
-          *reinterpret_cast<uint2*>(a.y[dir] + ((size_t)t * N + b) * H + u) = o;
+          if (a.ysum == nullptr) {
+            *reinterpret_cast<uint2*>(a.y[dir] + ((size_t)t * N + b) * H + u) = o;
+          } else {
+            // Fused direction sum (reference: the fw + bw outputs summed by the caller,
+            // src/custom_ops.py:36-96). Position t is produced by the forward direction at
+            // step t and by the backward one at step L-1-t (padding positions: both at step
+            // t). The direction that produces it LATER (ties: the backward one) waits for the
+            // other's bf16 value in the sentinel-filled sum buffer and writes the bf16 sum,
+            // rounding exactly like bf16 + bf16 in torch; the earlier one writes its value
+            // through (sc1: the other direction's groups live on other XCDs). No cycle: the
+            // later side of a pair only waits for a step the earlier side reached first.
+            unsigned long long* p = ysum_ptr(s, j);
+            const int other = (s < L) ? (L - 1 - s) : s;
+            const bool later = s > other || (s == other && dir == 1);
+            auto canon = [](unsigned h) { return (h & 0xffffu) == 0xffffu ? 0x7fc0u : (h & 0xffffu); };
+            if (!later) {
+              o.x = canon(o.x) | (canon(o.x >> 16) << 16);
+              o.y = canon(o.y) | (canon(o.y >> 16) << 16);
+              __hip_atomic_store(p, ((unsigned long long)o.y << 32) | o.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+              const long long t0 = __builtin_amdgcn_s_memrealtime();
+              unsigned long long q = yq[j];           // usually already there (loaded ahead)
+              while (true) {
+                const unsigned w0 = (unsigned)q, w1 = (unsigned)(q >> 32);
+                const bool ready = ((~w0 - 0x00010001u) & w0 & 0x80008000u) == 0 &&
+                                   ((~w1 - 0x00010001u) & w1 & 0x80008000u) == 0;
+                if (ready) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { atomicOr(a.err, 4u); break; }
+                __builtin_amdgcn_s_sleep(2);
+                q = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+              const unsigned q0 = (unsigned)q, q1 = (unsigned)(q >> 32);
+              auto add2 = [](unsigned x, unsigned y) {      // two bf16 pairs -> rounded bf16 sums
+                const unsigned lo = f2bf(__uint_as_float(x << 16) + __uint_as_float(y << 16));
+                const unsigned hi = f2bf(__uint_as_float(x & 0xffff0000u) + __uint_as_float(y & 0xffff0000u));
+                return lo | (hi << 16);
+              };
+              *reinterpret_cast<uint2*>(p) = make_uint2(add2(o.x, q0), add2(o.y, q1));
+            }
+          }
         }
       }
     }
@@ -768,6 +830,7 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   } else {
     for (int s = 0; s < a.steps; ++s) {
       st.mark(-1);
+      if (a.ysum != nullptr && s >= 2) mw_ysum_load(s - 2);
       if (s + 1 < a.steps) mw_put(s + 1);
       if (s >= 2) mw_store(s - 2);
       if (s + 2 < a.steps) mw_load(s + 2);
@@ -779,8 +842,14 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   }
   __syncthreads();
   if (wave == QW && !s_abort) {
-    if (a.steps >= 2) mw_store(a.steps - 2);
-    if (a.steps >= 1) mw_store(a.steps - 1);
+    if (a.steps >= 2) {
+      if (a.ysum != nullptr) mw_ysum_load(a.steps - 2);
+      mw_store(a.steps - 2);
+    }
+    if (a.steps >= 1) {
+      if (a.ysum != nullptr) mw_ysum_load(a.steps - 1);
+      mw_store(a.steps - 1);
+    }
   }
   if (STAMPS && wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
   if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
@@ -1758,7 +1827,15 @@ struct DS2RnnX {
   long long timeout;
   unsigned long long* stamps;
   void* ring[2];         // bwd reduce-scatter exchange ring (fp32, sentinel-filled)
+  void* ysum;            // fwd gen 4: fused direction sum (sentinel-filled) or null
 };
+
+// 1 if the forward launch for these parameters is generation 4 (which can fuse the
+// direction sum into its output stores)
+int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs) {
+  const int kbq = (H / 32 + 3) / 4;
+  return ndir == 2 && !(knobs & 256) && mt == 1 && kbq <= (cell == CELL_GRU ? 7 : 8) ? 1 : 0;
+}
 
 // grid size of a launch (blocks with no role exit at once)
 int ds2_rnnx_grid(int H, int ngroups, int xcd_map) {
@@ -1799,13 +1876,16 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
     a.U[i] = (const bf16_t*)d->U[i]; a.bh[i] = d->bh[i]; a.y[i] = (bf16_t*)d->y[i];
     a.hx[i] = (bf16_t*)d->ex[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
   }
+  a.ysum = (bf16_t*)d->ysum;
   a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->steps <= 0) return 0;
   const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
   // generation 4 (K-quarter split, register epilogue) unless knob 256 asks for generation 2
   const int kbq = (d->H / 32 + 3) / 4;
   // (GRU at kbq = 8 spills under the 3-waves-per-SIMD register budget)
-  if (!(d->knobs & 256) && d->mt == 1 && kbq <= (d->cell == CELL_GRU ? 7 : 8)) {
+  const bool gen4 = !(d->knobs & 256) && d->mt == 1 && kbq <= (d->cell == CELL_GRU ? 7 : 8);
+  if (d->ysum != nullptr && (!gen4 || d->ndir != 2)) return -37;   // only gen 4 fuses the sum
+  if (gen4) {
 #define DS2_QL(C, K)                                                                                  \
   if (a.stamps) hipLaunchKernelGGL((rnnq_fwd_kernel<C, K, true>), dim3(grid), dim3(QTH), 0, st, a);    \
   else hipLaunchKernelGGL((rnnq_fwd_kernel<C, K, false>), dim3(grid), dim3(QTH), 0, st, a);

@@ -61,6 +61,7 @@ class RnnPlan:
 
 
 RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))   # diagnostic timing switches only
+_FUSE_DIRSUM = os.environ.get("DS2_FUSE_DIRSUM", "1") == "1"      # 0: separate torch.add (A/B)
 # BPTT exchange of the xcd kernels: "rs" = reduce-scatter of fp32 partial dh (generation 3),
 # "gather" = all-gather of dgh (generation 2)
 BWD_EXCHANGE = os.environ.get("DS2_RNN_BWD", "rs")
@@ -282,7 +283,13 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     dev = gx.device
     d1 = ndir == 2
     bf16 = torch.bfloat16
-    y2 = torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
+    # generation-4 forward fuses the direction sum into its output stores (sentinel-filled
+    # sum buffer, one direction writes through, the other adds): no torch.add launch and no
+    # per-direction output round trip
+    fuse = (plan.kind == "xcd" and d1 and _FUSE_DIRSUM and
+            bool(C.rnnx_fwd_fuses_sum(H, CELL_CODE[plan.cell], plan.mt, ndir, RNNX_KNOBS)))
+    y2 = None if fuse else torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
+    ysum = torch.empty(T, N, H, device=dev, dtype=bf16) if fuse else None
     hx = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=bf16)
     hs = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=torch.float32)
     gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
@@ -293,21 +300,22 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
         census = torch.empty(ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
         err = error_word(dev)
         regions = ([hx[d, 0] for d in range(ndir)] + [hx[d, 1:] for d in range(ndir)] +
-                   [hs[d, 0] for d in range(ndir)] + [census])
-        C.multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [-1])
+                   [hs[d, 0] for d in range(ndir)] + [census] + ([ysum] if fuse else []))
+        C.multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [-1] + ([-1] if fuse else []))
         if h0 is not None:
             hs[:, 0, :N].copy_(h0)
             hx[:, 0, :N].copy_(h0)
+        yf, yb = (ysum, ysum) if fuse else (y2[0], y2[1] if d1 else None)
         C.rnnx_fwd(gx, lens, U[0], U[1] if d1 else None, bh[0], bh[1] if d1 else None,
-                   y2[0], y2[1] if d1 else None, hx[0], hx[1] if d1 else None,
+                   yf, yb, hx[0], hx[1] if d1 else None,
                    hs[0], hs[1] if d1 else None,
                    gates[0] if gates is not None else None,
                    gates[1] if (gates is not None and d1) else None,
                    census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
                    CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
                    _stamps("fwd", plan, int(C.rnnx_info(H, GATES[plan.cell], plan.mt, ndir * plan.BG,
-                                                         plan.xcd_map)["grid"]), dev))
-        y = torch.add(y2[0], y2[1]) if d1 else y2[0]
+                                                         plan.xcd_map)["grid"]), dev), ysum)
+        y = ysum if fuse else (torch.add(y2[0], y2[1]) if d1 else y2[0])
         return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
     hx[:, 0].zero_()                         # h0
     hs[:, 0].zero_()
