@@ -19,6 +19,61 @@ namespace {
 
 constexpr int OPT_THREADS = 256;
 
+// One float4 group: loads issued for U groups before any math (U x 5 loads in flight per
+// lane), non-temporal: every byte is touched exactly once per step, so nothing is worth
+// keeping in L2 / MALL for the next kernel.
+#ifndef DS2_ADAM_NT
+#define DS2_ADAM_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_s(const T* p) {
+  if constexpr (DS2_ADAM_NT) return __builtin_nontemporal_load(p); else return *p;
+}
+template <typename T>
+__device__ __forceinline__ void st_s(T v, T* p) {
+  if constexpr (DS2_ADAM_NT) __builtin_nontemporal_store(v, p); else *p = v;
+}
+template <int U>
+__device__ __forceinline__ void adam_groups(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                            float* __restrict__ v, float* __restrict__ ema, bf16_t* __restrict__ p16,
+                                            long long i0, long long step, float lr_t, float b1, float b2, float eps,
+                                            float gscale, float ema_keep) {
+  f32x4 pp[U], gg[U], mm[U], vv[U], ee[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = i0 + u * step;
+    pp[u] = ld_s(reinterpret_cast<const f32x4*>(p) + i);
+    gg[u] = ld_s(reinterpret_cast<const f32x4*>(g) + i);
+    mm[u] = ld_s(reinterpret_cast<const f32x4*>(m) + i);
+    vv[u] = ld_s(reinterpret_cast<const f32x4*>(v) + i);
+    if (ema != nullptr) ee[u] = ld_s(reinterpret_cast<const f32x4*>(ema) + i);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = i0 + u * step;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = gg[u][j] * gscale;
+      mm[u][j] = b1 * mm[u][j] + (1.f - b1) * gj;
+      vv[u][j] = b2 * vv[u][j] + (1.f - b2) * gj * gj;
+      pp[u][j] -= lr_t * mm[u][j] / (sqrtf(vv[u][j]) + eps);
+    }
+    st_s(pp[u], reinterpret_cast<f32x4*>(p) + i);
+    st_s(mm[u], reinterpret_cast<f32x4*>(m) + i);
+    st_s(vv[u], reinterpret_cast<f32x4*>(v) + i);
+    if (ema != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ee[u][j] = pp[u][j] + ema_keep * (ee[u][j] - pp[u][j]);
+      st_s(ee[u], reinterpret_cast<f32x4*>(ema) + i);
+    }
+    if (p16 != nullptr) {
+      const unsigned lo = (unsigned)f2bf(pp[u][0]) | ((unsigned)f2bf(pp[u][1]) << 16);
+      const unsigned hi = (unsigned)f2bf(pp[u][2]) | ((unsigned)f2bf(pp[u][3]) << 16);
+      reinterpret_cast<uint2*>(p16)[i] = make_uint2(lo, hi);
+    }
+  }
+}
+
 __global__ __launch_bounds__(OPT_THREADS) void adam_ema_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ ema, bf16_t* __restrict__ p16, long long n, float lr_t, float b1, float b2, float eps,
@@ -26,44 +81,25 @@ __global__ __launch_bounds__(OPT_THREADS) void adam_ema_kernel(
   if (skip != nullptr && *skip) return;
   const long long n4 = n / 4;
   const long long stride = (long long)gridDim.x * OPT_THREADS;
-  for (long long i = (long long)blockIdx.x * OPT_THREADS + threadIdx.x; i < n4; i += stride) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    const float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gj = ga[j] * gscale;
-      ma[j] = b1 * ma[j] + (1.f - b1) * gj;
-      va[j] = b2 * va[j] + (1.f - b2) * gj * gj;
-      pa[j] -= lr_t * ma[j] / (sqrtf(va[j]) + eps);
-    }
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (ema != nullptr) {
-      float4 ee = reinterpret_cast<float4*>(ema)[i];
-      ee.x = pp.x + ema_keep * (ee.x - pp.x);
-      ee.y = pp.y + ema_keep * (ee.y - pp.y);
-      ee.z = pp.z + ema_keep * (ee.z - pp.z);
-      ee.w = pp.w + ema_keep * (ee.w - pp.w);
-      reinterpret_cast<float4*>(ema)[i] = ee;
-    }
-    if (p16 != nullptr) {
-      ushort4 h;
-      h.x = f2bf(pp.x); h.y = f2bf(pp.y); h.z = f2bf(pp.z); h.w = f2bf(pp.w);
-      reinterpret_cast<ushort4*>(p16)[i] = h;
-    }
-  }
+  long long i = (long long)blockIdx.x * OPT_THREADS + threadIdx.x;
+#ifndef DS2_ADAM_U
+#define DS2_ADAM_U 2      // float4 groups in flight per lane (A/B: build.py --variant ... -D DS2_ADAM_U=4)
+#endif
+  if (DS2_ADAM_U >= 4)
+    for (; i + 3 * stride < n4; i += 4 * stride)
+      adam_groups<4>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
+  if (DS2_ADAM_U >= 2)
+    for (; i + stride < n4; i += 2 * stride)
+      adam_groups<2>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
+  for (; i < n4; i += stride) adam_groups<1>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
   // tail
-  for (long long i = n4 * 4 + (long long)blockIdx.x * OPT_THREADS + threadIdx.x; i < n; i += stride) {
-    const float gj = g[i] * gscale;
-    m[i] = b1 * m[i] + (1.f - b1) * gj;
-    v[i] = b2 * v[i] + (1.f - b2) * gj * gj;
-    p[i] -= lr_t * m[i] / (sqrtf(v[i]) + eps);
-    if (ema != nullptr) ema[i] = p[i] + ema_keep * (ema[i] - p[i]);
-    if (p16 != nullptr) p16[i] = f2bf(p[i]);
+  for (long long k = n4 * 4 + (long long)blockIdx.x * OPT_THREADS + threadIdx.x; k < n; k += stride) {
+    const float gj = g[k] * gscale;
+    m[k] = b1 * m[k] + (1.f - b1) * gj;
+    v[k] = b2 * v[k] + (1.f - b2) * gj * gj;
+    p[k] -= lr_t * m[k] / (sqrtf(v[k]) + eps);
+    if (ema != nullptr) ema[k] = p[k] + ema_keep * (ema[k] - p[k]);
+    if (p16 != nullptr) p16[k] = f2bf(p[k]);
   }
 }
 
