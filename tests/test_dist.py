@@ -163,3 +163,21 @@ def test_bench_two_ranks_json_contract():
     # top 100-frame bucket, (100, 200] frames at --frames 200 -> 4 utterances x 2 steps x (1, 2] s
     total = out["value"] * out["ms_per_step"] * 2 / 1000.0
     assert 8.0 < total <= 16.0 * 1.01, total
+
+
+def test_allreduce_bandwidth_tool_two_ranks():
+    """tools/bench_allreduce.py (nccl-tests conventions) under torch.distributed.run, 2 CPU
+    ranks over gloo: one JSON line per size on rank 0 with busbw = algbw * 2(n-1)/n."""
+    import json
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tools", "bench_allreduce.py"), "--device", "cpu", "--sizes_mb", "1,2",
+           "--iters", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert [row["bytes"] for row in rows] == [2 ** 20, 2 * 2 ** 20]
+    for row in rows:
+        assert row["world"] == 2 and row["backend"] == "gloo"
+        assert abs(row["busbw_GBps"] - row["algbw_GBps"] * 2 * (2 - 1) / 2) <= 0.011
