@@ -328,3 +328,40 @@ def test_fp8_quant2_matches_torch(cuda):
         bad = (got != ref)
         assert bad.float().mean().item() < 1e-3
         assert ((got - ref).abs()[bad] <= ref.abs()[bad] * 0.125 + 1e-6).all()
+
+
+@pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
+def test_fused_direction_sum_bitwise(cuda, cell):
+    """The gen-4 forward's in-kernel direction sum (one direction writes its bf16 value, the
+    other adds) is bit-identical to y_fw + y_bw in bf16 via torch, variable lengths included."""
+    from deepspeech_amd.ops import rnn as RNN
+    torch.manual_seed(7)
+    N, H, T = 32, 800, 57
+    G = RNN.GATES[cell]
+    lens = torch.randint(T // 3, T + 1, (N,), dtype=torch.int32)
+    lens[0] = T
+    gx = (torch.randn(T, N, 2 * G * H) * 0.5).bfloat16().to(cuda)
+    Us = [(torch.randn(G * H, H) / math.sqrt(H)).bfloat16().to(cuda) for _ in range(2)]
+    bh = [(torch.randn(G * H) * 0.1).to(cuda) if cell == "gru" else None for _ in range(2)]
+    RNN._plan_cache.clear()
+    plan = RNN.plan_for(N, H, cell, 2, cuda)
+    assert plan.kind == "xcd"
+    C = _ext_mod().ext()
+    assert C.rnnx_fwd_fuses_sum(H, RNN.CELL_CODE[cell], plan.mt, 2, RNN.RNNX_KNOBS)
+    old = RNN._FUSE_DIRSUM
+    try:
+        ys = []
+        for fuse in (True, False):
+            RNN._FUSE_DIRSUM = fuse
+            y, _ = RNN._run_fwd(gx, lens.to(cuda), Us, bh, plan)
+            torch.cuda.synchronize()
+            RNN.check_errors()
+            ys.append(y.clone())
+    finally:
+        RNN._FUSE_DIRSUM = old
+    assert torch.equal(ys[0], ys[1])
+
+
+def _ext_mod():
+    from deepspeech_amd.ops import _ext
+    return _ext
