@@ -249,7 +249,7 @@ __device__ __forceinline__ bool poll_mfma(__amdgpu_buffer_rsrc_t rs, const unsig
 // so the accumulation order — and the result — is deterministic.
 template <int KB, typename MfmaFn>
 __device__ __forceinline__ bool poll_mfma_par(__amdgpu_buffer_rsrc_t rs, const unsigned (&off)[KB],
-                                              const bool (&kval)[KB], long long timeout, MfmaFn&& mfma) {
+                                              const bool (&kval)[KB], long long timeout, int nap, MfmaFn&& mfma) {
   i32x4 v[KB];
 #pragma unroll
   for (int kk = 0; kk < KB; ++kk) v[kk] = load_sc1_b128(rs, off[kk]);
@@ -270,7 +270,8 @@ __device__ __forceinline__ bool poll_mfma_par(__amdgpu_buffer_rsrc_t rs, const u
     }
     if (done == FULL) return true;
     if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) return false;
-    __builtin_amdgcn_s_sleep(1);
+    if (nap == 1) __builtin_amdgcn_s_sleep(1);           // retry back-off (0: busy re-poll)
+    else if (nap == 2) __builtin_amdgcn_s_sleep(3);
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk)
       if (!(done & (1u << kk))) v[kk] = load_sc1_b128(rs, off[kk]);
@@ -755,6 +756,9 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
     // padding lanes of the 16-row fragment re-read row R-1 (a real, polled row: same cache
     // line as its own lane), so every lane can wait on its granule and use it unmasked
     const int arow = r0 + min(lane & 15, R - 1);
+    // retry back-off: none by default (same-box A/B: 9.03 / 8.99 / 9.02 vs 9.08 / 9.04 / 9.05
+    // ms/step with s_sleep 1); knob bits 12-13 = 1: s_sleep 1, 2: s_sleep 3
+    const int nap = (a.knobs >> 12) & 3;
     const bool erow_ok = erow < R;
     const int L = len_s[erow];
     for (int s = 0; s < a.steps; ++s) {
@@ -769,7 +773,7 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
       f32x4 acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, [&](int kk, bf16x8 af) {
+      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, nap, [&](int kk, bf16x8 af) {
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, uf[kk][g], acc[g], 0, 0, 0);
       });
