@@ -1489,7 +1489,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
             if (pg7 + MW * i < P) {
               while (!(a.knobs & 4) && !granule_tagged16(v[i], want)) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
-                __builtin_amdgcn_s_sleep(1);
+                if (!(a.knobs & 16384)) __builtin_amdgcn_s_sleep(1);   // back-off (knob 16384: none; measured neutral)
                 v[i] = load_sc1_b128(rs_ring, off[i]);
               }
 #pragma unroll
@@ -1530,7 +1530,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
             if (pg7 + MW * (2 * i + h) < P) {
               while (!(a.knobs & 4) && !granule_tagged16(v[i], want)) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
-                __builtin_amdgcn_s_sleep(1);
+                if (!(a.knobs & 16384)) __builtin_amdgcn_s_sleep(1);   // back-off (knob 16384: none; measured neutral)
                 v[i] = load_sc1_b128(rs_ring, off[i]);
               }
 #pragma unroll
@@ -1570,7 +1570,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
             if (pg7 + MW * i < P) {
               while (!(a.knobs & 4) && !granule_tagged(v[i], want)) {   // knob 4: no wait (timing only)
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
-                __builtin_amdgcn_s_sleep(1);
+                if (!(a.knobs & 16384)) __builtin_amdgcn_s_sleep(1);   // back-off (knob 16384: none; measured neutral)
                 v[i] = load_sc1_b128(rs_ring, off[i]);
               }
               acc4 += __builtin_bit_cast(f32x4, v[i]);
