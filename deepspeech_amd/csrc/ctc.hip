@@ -169,9 +169,13 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
     float nv[SPL];
     if (!beta) {
       // neighbours s-1, s-2 of this lane's first two states live in the previous lane
-      float p1 = __shfl_up(v[SPL - 1], 1, 64);
-      float p2 = __shfl_up(v[SPL - 2], 1, 64);
-      if (lane == 0) { p1 = NEG_INF; p2 = NEG_INF; }
+      // previous lane's last two states: DPP wave_shr:1 (a VALU move, lane 0 keeps the
+      // NEG_INF 'old' operand) instead of ds_bpermute shuffles, whose LDS round trip sat on
+      // the frame recursion's dependency chain
+      const float p1 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(NEG_INF), __float_as_int(v[SPL - 1]),
+                                                                  0x138, 0xf, 0xf, false));
+      const float p2 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(NEG_INF), __float_as_int(v[SPL - 2]),
+                                                                  0x138, 0xf, 0xf, false));
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const float a1 = (j >= 1) ? v[j - 1] : p1;
@@ -180,9 +184,10 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
         nv[j] = (s0 + j < SP) ? r + lcur[j] : NEG_INF;
       }
     } else {
-      float n1 = __shfl_down(v[0], 1, 64);
-      float n2 = __shfl_down(v[1], 1, 64);
-      if (lane == 63) { n1 = NEG_INF; n2 = NEG_INF; }
+      const float n1 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(NEG_INF), __float_as_int(v[0]),
+                                                                  0x130, 0xf, 0xf, false));   // wave_shl:1
+      const float n2 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(NEG_INF), __float_as_int(v[1]),
+                                                                  0x130, 0xf, 0xf, false));
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const float b1 = (j + 1 < SPL) ? v[j + 1] : n1;
