@@ -7,6 +7,8 @@ from __future__ import annotations
 
 import torch
 
+_FC_SPLIT_MAX = int(__import__('os').environ.get('DS2_FC_SPLITK', '16'))   # 1: one unsplit GEMM (A/B)
+
 from .. import BLANK
 from . import _ext
 from ..utils import trace as TR
@@ -144,12 +146,30 @@ class FusedHeadCTC(torch.autograd.Function):
         from .optim import arena_of, emit_grad
         M, H = h2.shape
         a = arena_of(weight)
+        # dW_fc = G^T h: a [K x H] output (7 column tiles) over M = T*N tokens. Split over the
+        # token dimension as a batch of S partial GEMMs (7 -> 7*S workgroups; the unsplit
+        # call ran 110 us on 7 CUs beside the top BPTT) and sum the partials.
+        S = 1
+        while S < _FC_SPLIT_MAX and M % (2 * S) == 0:
+            S *= 2
+        if S > 1:
+            parts = torch.empty(S, K, H, device=h2.device, dtype=torch.float32)
+            GM.gemm(G.view(S, M // S, G.shape[1]), h2.view(S, M // S, H), parts, K, H, M // S, True, True, 1, 1.0,
+                    None, alpha_dev=scale, Ml=32)
         if a is not None:
-            # M = K rows stored; G is read as a [M_rows, 32]-column col-mode operand (Ml = 32)
-            GM.gemm(G, h2, weight.main_grad, K, H, M, True, True, 1 if a.first_write(weight) else 2, 1.0, None,
-                    alpha_dev=scale, Ml=32)
+            if S > 1:
+                if a.first_write(weight):
+                    torch.sum(parts, 0, out=weight.main_grad)
+                else:
+                    weight.main_grad.add_(parts.sum(0))
+            else:
+                # M = K rows stored; G is read as a [M_rows, 32]-column col-mode operand (Ml = 32)
+                GM.gemm(G, h2, weight.main_grad, K, H, M, True, True, 1 if a.first_write(weight) else 2, 1.0, None,
+                        alpha_dev=scale, Ml=32)
             a.grad_done(weight)
             gw = None
+        elif S > 1:
+            gw = parts.sum(0)
         else:
             out = torch.empty(K, H, device=h2.device, dtype=torch.float32)
             GM.gemm(G, h2, out, K, H, M, True, True, 1, 1.0, None, alpha_dev=scale, Ml=32)
