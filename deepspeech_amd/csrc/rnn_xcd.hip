@@ -1264,12 +1264,25 @@ struct XBwdRS {
 // (the per-value version with NaN selects made the publish phase ~1.6k cycles longer). The
 // +1 can carry out of the low half only from 0xFFFF (a negative NaN with a full payload),
 // which is first replaced by the canonical NaN 0x7FC0.
+#ifndef DS2_TAG_TRUNC
+// Hardware RNE pair conversion (one v_cvt_pk_bf16_f32), then the LSB set to the tag by an
+// XOR flip: |error| <= 1.5 bf16 ulp, 3 VALU ops per pair on the publish critical path
+// (the truncate-and-step variant below is < 1 ulp but 5-6 ops). No carry, so the 0xFFFF
+// special case is not needed.
+__device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  const bf2_t p = {(__bf16)lo, (__bf16)hi};
+  const unsigned d = __builtin_bit_cast(unsigned, p);
+  return d ^ ((d & 0x00010001u) ^ tagmask);
+}
+#else
 __device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
   unsigned d = __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
   if ((d & 0xffffu) == 0xffffu) d = (d & 0xffff0000u) | 0x7fc0u;
   const unsigned x = (d & 0x00010001u) ^ tagmask;
   return d + x;
 }
+#endif
 
 __device__ __forceinline__ bool granule_tagged16(i32x4 v, unsigned tag) {
   const unsigned want = tag ? 0x00010001u : 0u;
