@@ -1273,7 +1273,15 @@ __device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned t
   typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
   const bf2_t p = {(__bf16)lo, (__bf16)hi};
   const unsigned d = __builtin_bit_cast(unsigned, p);
+#ifdef DS2_TAG_ANDOR
   return d ^ ((d & 0x00010001u) ^ tagmask);
+#else
+  // one bitfield insert instead of and + or (gfx9 VOP3 takes no literal, so the compiler
+  // cannot fuse them into v_and_or_b32): r = (mask & tagmask) | (~mask & d)
+  unsigned r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(0x00010001u), "s"(tagmask), "v"(d));
+  return r;
+#endif
 }
 #else
 __device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
@@ -1682,6 +1690,55 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
         };
         if constexpr (PBF) {
           // unit pair p = wave + 7k: m-tiles 2p, 2p+1 -> one tagged-bf16 granule per lane
+          if (!(a.knobs & 40)) {
+            // pair by pair: MFMA chains 2k, 2k+1, then the pair's convert/tag/store, so the
+            // first granule leaves after 2G MFMAs. Measured against interleaving all MTU
+            // chains (k-step outer, every store after the last MFMA; DS2_PUB_PIPE): 3.14 vs
+            // 3.20 us/step, same box. No knob branch in here: a runtime `if` around the MFMAs
+            // made the compiler zero 8 accumulator VGPRs per pair ahead of the first MFMA.
+            constexpr int NP = MTU / 2;
+            unsigned offp[NP];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) offp[k] = ring_off16(ws, mem, wave + MW * k, lane & 15, lane >> 4);
+            // the store flavour is a compile-time branch of the whole loop (a runtime one per
+            // store cost a select + compare + 3 scalar branches per pair)
+            auto publish = [&](auto PLAIN) {
+            auto store_pair = [&](int k, const f32x4& a0, const f32x4& a1) {
+              if (prow && 2 * (wave + MW * k) + 1 < MTS) {
+                const i32x4 v = {(int)bf16x2_tagged(a0[0], a0[1], tagmask), (int)bf16x2_tagged(a0[2], a0[3], tagmask),
+                                 (int)bf16x2_tagged(a1[0], a1[1], tagmask), (int)bf16x2_tagged(a1[2], a1[3], tagmask)};
+                if constexpr (decltype(PLAIN)::value) store_b128(rs_ring, offp[k], v);
+                else store_sc1_b128(rs_ring, offp[k], v);
+              }
+            };
+#ifdef DS2_PUB_PIPE
+            f32x4 acc[MTU];
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+              for (int i = 0; i < MTU; ++i)
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], g ? acc[i] : f32x4{0.f, 0.f, 0.f, 0.f},
+                                                                 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < NP; ++k) store_pair(k, acc[2 * k], acc[2 * k + 1]);
+#else
+            // a pair past MTS multiplies the zero fragments loaded for it and is not stored
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+              f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k][0], bfr[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+              f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k + 1][0], bfr[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+              for (int g = 1; g < G; ++g) {
+                a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k][g], bfr[g], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k + 1][g], bfr[g], a1, 0, 0, 0);
+              }
+              store_pair(k, a0, a1);
+            }
+#endif
+            };
+            if (plain) publish(std::true_type{});
+            else publish(std::false_type{});
+          } else
 #pragma unroll
           for (int i = 0; i < MTU; i += 2) {
             const int pr = wave + MW * (i >> 1);
