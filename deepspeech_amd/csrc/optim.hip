@@ -33,6 +33,19 @@ template <typename T>
 __device__ __forceinline__ void st_s(T v, T* p) {
   if constexpr (DS2_ADAM_NT) __builtin_nontemporal_store(v, p); else *p = v;
 }
+// One element's update with every rounding spelled out (explicit fma / _rn products, nothing
+// left to the compiler's contraction choice), so the vector-group paths and the scalar tail
+// round identically: the result of an element does not depend on how the arena is split
+// into launches (Trainer's per-layer optimizer ranges are bitwise the single launch).
+__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float lr_t, float b1, float b2,
+                                      float eps, float gscale) {
+  const float gj = __fmul_rn(g, gscale);
+  m = __fmaf_rn(b1, m, __fmul_rn(1.f - b1, gj));
+  v = __fmaf_rn(b2, v, __fmul_rn(__fmul_rn(1.f - b2, gj), gj));
+  p = __fmaf_rn(-lr_t, __fdiv_rn(m, __fadd_rn(__fsqrt_rn(v), eps)), p);
+}
+__device__ __forceinline__ float ema1(float e, float p, float keep) { return __fmaf_rn(keep, __fsub_rn(e, p), p); }
+
 template <int U>
 __device__ __forceinline__ void adam_groups(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                             float* __restrict__ v, float* __restrict__ ema, bf16_t* __restrict__ p16,
@@ -53,17 +66,16 @@ __device__ __forceinline__ void adam_groups(float* __restrict__ p, const float* 
     const long long i = i0 + u * step;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float gj = gg[u][j] * gscale;
-      mm[u][j] = b1 * mm[u][j] + (1.f - b1) * gj;
-      vv[u][j] = b2 * vv[u][j] + (1.f - b2) * gj * gj;
-      pp[u][j] -= lr_t * mm[u][j] / (sqrtf(vv[u][j]) + eps);
+      float pj = pp[u][j], mj = mm[u][j], vj = vv[u][j];
+      adam1(pj, gg[u][j], mj, vj, lr_t, b1, b2, eps, gscale);
+      pp[u][j] = pj; mm[u][j] = mj; vv[u][j] = vj;
     }
     st_s(pp[u], reinterpret_cast<f32x4*>(p) + i);
     st_s(mm[u], reinterpret_cast<f32x4*>(m) + i);
     st_s(vv[u], reinterpret_cast<f32x4*>(v) + i);
     if (ema != nullptr) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ee[u][j] = pp[u][j] + ema_keep * (ee[u][j] - pp[u][j]);
+      for (int j = 0; j < 4; ++j) ee[u][j] = ema1(ee[u][j], pp[u][j], ema_keep);
       st_s(ee[u], reinterpret_cast<f32x4*>(ema) + i);
     }
     if (p16 != nullptr) {
@@ -94,12 +106,11 @@ __global__ __launch_bounds__(OPT_THREADS) void adam_ema_kernel(
   for (; i < n4; i += stride) adam_groups<1>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
   // tail
   for (long long k = n4 * 4 + (long long)blockIdx.x * OPT_THREADS + threadIdx.x; k < n; k += stride) {
-    const float gj = g[k] * gscale;
-    m[k] = b1 * m[k] + (1.f - b1) * gj;
-    v[k] = b2 * v[k] + (1.f - b2) * gj * gj;
-    p[k] -= lr_t * m[k] / (sqrtf(v[k]) + eps);
-    if (ema != nullptr) ema[k] = p[k] + ema_keep * (ema[k] - p[k]);
-    if (p16 != nullptr) p16[k] = f2bf(p[k]);
+    float pk = p[k], mk = m[k], vk = v[k];
+    adam1(pk, g[k], mk, vk, lr_t, b1, b2, eps, gscale);
+    p[k] = pk; m[k] = mk; v[k] = vk;
+    if (ema != nullptr) ema[k] = ema1(ema[k], pk, ema_keep);
+    if (p16 != nullptr) p16[k] = f2bf(pk);
   }
 }
 

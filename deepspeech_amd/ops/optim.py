@@ -166,12 +166,26 @@ class ParamArena:
     def enable_ready_events(self) -> None:
         if self.grad.is_cuda and self._ready_events is None:
             self._ready_events = [torch.cuda.Event() for _ in self.params]
+            self._ready_seq = 0
+            self._ready_at = [(0, 0)] * len(self.params)   # (record order, stream) per parameter
+
+    def ready_events_covering(self, idx) -> list:
+        """The fewest ready events whose completion implies every parameter in ``idx`` is
+        written: per recording stream, the latest-recorded member (streams run in order)."""
+        last = {}
+        for i in idx:
+            seq, st = self._ready_at[i]
+            if st not in last or seq > last[st][0]:
+                last[st] = (seq, i)
+        return [self._ready_events[i] for _, i in last.values()]
 
     def record_ready(self, i: int) -> None:
         """Mark parameter i's gradient as produced by the work enqueued so far on the
         current stream."""
         if self._ready_events is not None:
             self._ready_events[i].record()
+            self._ready_seq += 1
+            self._ready_at[i] = (self._ready_seq, torch.cuda.current_stream(self.grad.device).cuda_stream)
 
     def ready_event(self, i: int) -> Optional["torch.cuda.Event"]:
         return self._ready_events[i] if self._ready_events is not None else None
@@ -291,14 +305,36 @@ class FusedAdamEMA:
 
     @torch.no_grad()
     def step(self, lr: float, global_step: int, gscale: float = 1.0,
-             skip_flag: Optional[torch.Tensor] = None) -> None:
+             skip_flag: Optional[torch.Tensor] = None, parts=None) -> None:
+        """One Adam + EMA update of the whole arena.
+
+        ``parts`` (HIP only): list of ``(lo, hi, stream, wait)`` element ranges covering the
+        arena; range ``[lo, hi)`` is updated on ``stream`` (None = current) after that stream
+        waits on the events in ``wait``. The ranges share one Adam step count (one lr_t), so
+        the result is identical to the single launch; the split only lets the update of the
+        gradients that are final early run beside the work still producing the others."""
         self.t += 1
         lr_t = lr * math.sqrt(1.0 - self.b2 ** self.t) / (1.0 - self.b1 ** self.t)
         keep = self.ema_keep(global_step) if self.ema is not None else 0.0
         a = self.arena
         if self.use_hip:
-            _ext.ext().adam_ema(a.flat, a.grad, self.m, self.v, self.ema, self.p16, lr_t, self.b1, self.b2,
-                                self.eps, gscale, keep, skip_flag)
+            C = _ext.ext()
+            if parts is None:
+                C.adam_ema(a.flat, a.grad, self.m, self.v, self.ema, self.p16, lr_t, self.b1, self.b2,
+                           self.eps, gscale, keep, skip_flag)
+                return
+            for lo, hi, stream, wait in parts:
+                if hi <= lo:
+                    continue
+                sl = slice(lo, hi)
+                s = stream if stream is not None else torch.cuda.current_stream(a.flat.device)
+                for ev in wait:
+                    s.wait_event(ev)
+                with torch.cuda.stream(s):
+                    C.adam_ema(a.flat[sl], a.grad[sl], self.m[sl], self.v[sl],
+                               self.ema[sl] if self.ema is not None else None,
+                               self.p16[sl] if self.p16 is not None else None,
+                               lr_t, self.b1, self.b2, self.eps, gscale, keep, skip_flag)
             return
         if skip_flag is not None and int(skip_flag.item()) != 0:
             return

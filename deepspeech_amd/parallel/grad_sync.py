@@ -124,10 +124,12 @@ class GradBucketer:
         # the collective (ProcessGroupNCCL waits on the CURRENT stream at issue time) is
         # issued from the ordering stream, which waits on each member's producer event:
         # gradients written on the side stream and on the main stream alike, nothing else
-        for i in idx:
-            ev = self.arena.ready_event(i)
-            if ev is not None and id(self.arena.params[i]) in self.arena._written:
-                os_.wait_event(ev)
+        # one wait per producing stream (its latest-recorded member): every queued wait is a
+        # barrier packet the command processor handles in order, and they add up (measured
+        # with the per-layer optimizer ranges: one wait per member cost ~0.2 ms/step)
+        written = [i for i in idx if id(self.arena.params[i]) in self.arena._written]
+        for ev in self.arena.ready_events_covering(written):
+            os_.wait_event(ev)
         with torch.cuda.stream(os_):
             self._works.append((b, self._collective(b, g)))
 

@@ -18,6 +18,7 @@ No host synchronisation happens inside the step; the loss is returned as a devic
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -79,6 +80,58 @@ class Trainer:
         self.last_skip: Optional[torch.Tensor] = None
         # per-step divergence record on the device (read at host sync points, never skipped)
         self.watch = NonfiniteWatch(self.arena.flat.device)
+        # Per-layer optimizer (1 GPU, HIP engine). The arena is laid out in gradient-production
+        # order, and a recurrent layer's weights are never read again once its last weight
+        # gradient is written (the dx GEMM reading W_l is issued before dW_l, whose side-stream
+        # GEMM waits behind it). At the end of backward the main stream (conv front-end
+        # backward + dU_0) finishes before the side stream's deferred dW GEMMs, so instead
+        # of one whole-arena launch after both streams join, the main stream updates each
+        # layer's arena range as soon as that range's gradients are final: its own range
+        # [U_0, b_h0, conv] at once, then [W_0, b_0], [FC + layer L-1], [layer L-2], ... in
+        # the order the side stream finishes them — memory-bound updates beside the
+        # remaining compute-bound GEMMs. Measured slower on MI355X and therefore OFF by
+        # default (DS2_SPLIT_ADAM=1 enables it): same-box A/B 8.80-8.87 vs 8.68-8.71 ms/step
+        # (tools/host_overhead.py; one wait per range and stream; a per-parameter wait list
+        # was 9.0, a third "optimizer" stream 9.2). profiles/r1_s3_negative_results.md.
+        self._bounds = None
+        names = self.arena.names
+        if (os.environ.get("DS2_SPLIT_ADAM", "0") == "1" and model.engine == "hip"
+                and self.arena.flat.is_cuda and not self.bucketer.enabled and "rnn.0.fw.U" in names):
+            L = len(model.rnn)
+            cuts = [names.index("rnn.%d.fw.W" % i) for i in range(L - 2, -1, -1) if "rnn.%d.fw.W" % i in names]
+            cuts.append(names.index("rnn.0.fw.U"))
+            if cuts == sorted(cuts) and cuts[0] > 0:
+                self._bounds = [0] + cuts + [len(names)]
+                self.arena.enable_ready_events()
+
+    @property
+    def _split_at(self):
+        return None if self._bounds is None else self._bounds[-2]
+
+    def _optimizer_parts(self):
+        """(lo, hi, stream, events) ranges for FusedAdamEMA.step, or None (single launch).
+        Call after the backward is fully queued (and after zero_unwritten)."""
+        a = self.arena
+        b = self._bounds
+        if b is None:
+            return None
+        parts = []
+        nr = len(b) - 1
+        for r in range(nr):
+            members = []
+            for i in range(b[r], b[r + 1]):
+                if id(a.params[i]) in a._written:
+                    members.append(i)
+                elif r < nr - 1:
+                    return None        # zeroed / autograd-accumulated on the main stream
+            waits = a.ready_events_covering(members)
+            lo = a.offsets[b[r]][0]
+            hi = a.offsets[b[r + 1]][0] if b[r + 1] < len(a.params) else a.numel
+            parts.append((lo, hi, None, waits))
+        # issue order: the main stream's own range, W_0 (the side stream's first tail GEMM),
+        # then FC + layer L-1, L-2, ... (the deferred dW GEMMs' order)
+        order = [nr - 1, nr - 2] + list(range(nr - 2))
+        return [parts[r] for r in order]
 
     @property
     def lr(self) -> float:
@@ -96,6 +149,20 @@ class Trainer:
         loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
         self.watch.update(loss)
         loss.backward()
+        parts = None
+        if self._bounds is not None and self.nan_policy != "skip":
+            self.arena.wgrad.drain()
+            if lazy:
+                self.arena.zero_unwritten()
+            parts = self._optimizer_parts()
+            if parts is None and lazy:
+                lazy = False           # already zeroed
+        if parts is not None:
+            with TR.phase(TR.EMA):
+                self.opt.step(self.lr, self.global_step, gscale=1.0 / self.world, parts=parts)
+            self.arena.wgrad.join()
+            self.global_step += 1
+            return loss.detach()
         self.arena.wgrad.join()
         if lazy:
             self.arena.zero_unwritten()

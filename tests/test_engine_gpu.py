@@ -232,6 +232,32 @@ def test_step_is_bitwise_reproducible(cuda):
     assert torch.equal(w0, w1)
 
 
+def test_split_optimizer_matches_single_launch(cuda, monkeypatch):
+    """The split optimizer (Adam of the side-stream-produced arena prefix on the side stream,
+    the rest on the main stream, one shared step count) gives bitwise the weights, Adam
+    moments, EMA and bf16 shadows of the single whole-arena launch, over several steps."""
+    from deepspeech_amd.trainer import Trainer, LRSchedule
+    torch.manual_seed(0)
+    base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
+    batch = to_device(FixedShapeBatches(8, max_frames=300, seed=4, pool=1).next(), cuda)
+    out = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("DS2_SPLIT_ADAM", split)
+        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
+        assert (tr._split_at is not None) == (split == "1")
+        losses = [float(tr.step(batch)) for _ in range(3)]
+        if split == "1":
+            assert tr._optimizer_parts() is not None      # the split path is the one taken
+        torch.cuda.synchronize()
+        out[split] = (losses, tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone(),
+                      tr.arena.p16.clone())
+    a, b = out["1"], out["0"]
+    assert a[0] == b[0], (a[0], b[0])
+    for x, y, name in zip(a[1:], b[1:], ("flat", "m", "v", "ema", "p16")):
+        assert torch.equal(x, y), name
+
+
 @pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
 def test_nhwc_graph_hip_matches_reference(cuda, cell):
     """--nchw False graph on the HIP engine (moments+EMA conv BN in the channels-last

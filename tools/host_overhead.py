@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Host enqueue time vs GPU time of the headline training step.
+
+Times K steps twice: the host-side loop alone (time until the Python loop has enqueued
+all K steps, no synchronisation inside) and the full wall time to the final
+synchronize. If host time per step approaches the GPU time per step the step is
+launch-bound and host overhead adds straight to ms/step.
+  python tools/host_overhead.py --steps 30
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--num_hidden", type=int, default=800)
+    ap.add_argument("--num_rnn_layers", type=int, default=5)
+    a = ap.parse_args()
+    from deepspeech_amd.utils.setenvs import setenvs
+    setenvs([])
+    import torch
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+    from deepspeech_amd.trainer import Trainer, LRSchedule
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=32, num_hidden=a.num_hidden, num_rnn_layers=a.num_rnn_layers, cell="gru").to(dev)
+    m.set_engine("hip", torch.bfloat16)
+    tr = Trainer(m, LRSchedule(1e-4, 10 ** 9, 0.9))
+    batch = to_device(FixedShapeBatches(32, max_frames=1000, seed=0, pool=1).next(), dev)
+    for _ in range(5):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.step(batch)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print("host enqueue %.3f ms/step, wall %.3f ms/step (split=%s)" %
+          (1e3 * (t1 - t0) / a.steps, 1e3 * (t2 - t0) / a.steps, os.environ.get("DS2_SPLIT_ADAM", "1")))
+
+
+if __name__ == "__main__":
+    main()
