@@ -93,7 +93,8 @@ int ds2_bn_bwd(const void* dout, int dout_bf16, const void* y, int y_bf16, const
                const float* gamma, const float* beta, float* part, int nb, float* dgamma, float* dbeta, void* dy,
                int dy_bf16, int N, int C, int T, int F, int layout, hipStream_t st);
 int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
-                 float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, hipStream_t st);
+                 float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
+                 hipStream_t st);
 int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
@@ -435,7 +436,7 @@ void bn_bwd(at::Tensor dout, at::Tensor y, at::Tensor mean, at::Tensor invstd, a
 
 // --------------------------------------------------------------------------- optimizer
 void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, OptT p16, double lr_t, double b1,
-              double b2, double eps, double gscale, double ema_keep, OptT skip) {
+              double b2, double eps, double gscale, double ema_keep, OptT skip, int64_t max_grid) {
   need_gpu(p, "p");
   need_gpu(g, "g");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 arena expected");
@@ -444,7 +445,7 @@ void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, 
   check(ds2_adam_ema(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                      ptr_or_null<float>(ema, "ema"), ptr_or_null<void>(p16, "p16"), n, (float)lr_t, (float)b1,
                      (float)b2, (float)eps, (float)gscale, (float)ema_keep, ptr_or_null<const int>(skip, "skip"),
-                     cur_stream()),
+                     (int)max_grid, cur_stream()),
         "adam_ema");
 }
 

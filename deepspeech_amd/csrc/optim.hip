@@ -154,9 +154,14 @@ int grid_for(long long n) {
 
 extern "C" {
 
+// max_grid > 0 caps the grid (an update issued beside a persistent kernel that holds most
+// of the CUs: a few workgroups stream the range instead of queueing behind it)
 int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
-                 float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, hipStream_t st) {
-  hipLaunchKernelGGL(adam_ema_kernel, dim3(grid_for(n)), dim3(OPT_THREADS), 0, st, p, g, m, v, ema, (bf16_t*)p16, n,
+                 float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
+                 hipStream_t st) {
+  int grid = grid_for(n);
+  if (max_grid > 0 && grid > max_grid) grid = max_grid;
+  hipLaunchKernelGGL(adam_ema_kernel, dim3(grid), dim3(OPT_THREADS), 0, st, p, g, m, v, ema, (bf16_t*)p16, n,
                      lr_t, b1, b2, eps, gscale, ema_keep, skip);
   return (int)hipGetLastError();
 }

@@ -530,6 +530,9 @@ class FusedBiLayer(torch.autograd.Function):
         T, N, D = x.shape
         dirs_W = [W_f] + ([W_b] if W_b is not None else [])
         dirs_b = [b_f] + ([b_b] if b_b is not None else [])
+        arena = arena_of(W_f)
+        if arena is not None and idx >= 1:
+            arena.flush_update()                      # the previous step's update of layers >= 1
         W16 = _bf16_group(dirs_W)                     # [ndir*G*H, D]
         b16 = _bf16_group(dirs_b)                     # [ndir*G*H]
         x16 = x.to(torch.bfloat16).contiguous()
@@ -538,6 +541,8 @@ class FusedBiLayer(torch.autograd.Function):
             gx = fp8_linear(x2, W16, b16, alpha).view(T, N, -1)
         else:
             gx = _linear(x2, W16, b16, alpha).view(T, N, -1)
+        if arena is not None and idx == 0:
+            arena.launch_update()                     # streams beside this layer's recurrence
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]

@@ -124,6 +124,7 @@ def write_summaries(events, step: int, trainer, model, args, lv: float, ema: flo
     computed on the device (csrc/stats.hip), one pass per tensor; tags use the TF variable
     names of the checkpoint layout."""
     from .utils.stats import histogram
+    trainer.flush_optimizer()                  # variable histograms read the updated weights
     events.scalars(step, {"ctc_loss(raw)": lv, "ctc_loss": ema, "learning_rate": trainer.lr})
     tfname = {tn: tf for tf, tn, _, _ in CK.tf_name_map(model)}
     grads = trainer.arena.views(trainer.arena.grad)

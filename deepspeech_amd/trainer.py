@@ -104,6 +104,25 @@ class Trainer:
                 self._bounds = [0] + cuts + [len(names)]
                 self.arena.enable_ready_events()
 
+        # Overlapped optimizer (1 GPU, HIP engine, DS2_OVERLAP_OPT): at the end of a step only
+        # layer 0 + the conv front-end are updated; the update of the arena prefix [FC +
+        # layers L-1..1] is prepared with the same (lr_t, EMA decay) and runs during the next
+        # forward, beside layer 0's recurrence (ops.optim.DeferredUpdate). Same arithmetic,
+        # same order of reads and writes of every weight; flush_optimizer() completes it for
+        # any reader between steps (checkpoint, EMA swap, eval, the bench's last step).
+        self._defer_hi = None
+        self._defer_grid = int(os.environ.get("DS2_OVERLAP_OPT_GRID", "48"))
+        if (os.environ.get("DS2_OVERLAP_OPT", "0") == "1" and self._bounds is None and model.engine == "hip"
+                and self.arena.flat.is_cuda and not self.bucketer.enabled and len(model.rnn) >= 2
+                and "rnn.0.fw.W" in names
+                and all(getattr(l, "seq_bn", "frozen") in ("frozen", "none") for l in model.rnn)):
+            self._defer_hi = self.arena.offsets[names.index("rnn.0.fw.W")][0]
+
+    def flush_optimizer(self) -> None:
+        """Complete any deferred optimizer update (call before reading weights, EMA or Adam
+        state outside step())."""
+        self.arena.flush_update()
+
     @property
     def _split_at(self):
         return None if self._bounds is None else self._bounds[-2]
@@ -147,6 +166,9 @@ class Trainer:
         self.arena.wgrad.discard()
         self.arena.zero_grad(lazy=lazy)
         loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
+        # normally consumed inside the forward (layer 1); never let backward overwrite the
+        # gradients a pending update still has to read
+        self.arena.flush_update()
         self.watch.update(loss)
         loss.backward()
         parts = None
@@ -174,7 +196,14 @@ class Trainer:
             _, skip = self.opt.grad_norm_and_finite(gscale)
             self.last_skip = skip
         with TR.phase(TR.EMA):
-            self.opt.step(self.lr, self.global_step, gscale=gscale, skip_flag=skip)
+            if self._defer_hi is not None and skip is None:
+                from .ops.optim import DeferredUpdate
+                lr_t, keep = self.opt.prepare(self.lr, self.global_step)
+                self.opt.apply_range(self._defer_hi, self.arena.numel, lr_t, keep, gscale)
+                self.arena.pending_update = DeferredUpdate(self.opt, 0, self._defer_hi, lr_t, keep, gscale,
+                                                           self._defer_grid)
+            else:
+                self.opt.step(self.lr, self.global_step, gscale=gscale, skip_flag=skip)
         self.global_step += 1
         return loss.detach()
 
@@ -193,6 +222,7 @@ class Trainer:
 
     # ---- EMA weights for eval (reference evaluates the shadow variables) -------------
     def swap_ema(self) -> None:
+        self.flush_optimizer()
         if self.opt.ema is None:
             return
         tmp = self.arena.flat.clone()

@@ -241,6 +241,7 @@ def test_split_optimizer_matches_single_launch(cuda, monkeypatch):
     base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
     batch = to_device(FixedShapeBatches(8, max_frames=300, seed=4, pool=1).next(), cuda)
     out = {}
+    monkeypatch.setenv("DS2_OVERLAP_OPT", "0")
     for split in ("1", "0"):
         monkeypatch.setenv("DS2_SPLIT_ADAM", split)
         m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
@@ -315,3 +316,30 @@ def test_prefetcher_matches_direct_upload(cuda):
             assert torch.equal(dev[k], v), k
         assert hb.feats.shape[1] == dev["feats"].shape[1]
     pf.close()
+
+
+def test_overlapped_optimizer_matches_plain(cuda, monkeypatch):
+    """DS2_OVERLAP_OPT: the FC + layers >= 1 part of step s's Adam/EMA update runs during
+    step s+1's forward (beside layer 0's recurrence). Losses, weights, moments, EMA and bf16
+    shadows must be bitwise those of the plain end-of-step update."""
+    from deepspeech_amd.trainer import Trainer, LRSchedule
+    torch.manual_seed(0)
+    base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
+    batches = [to_device(FixedShapeBatches(8, max_frames=300, seed=s, pool=1).next(), cuda) for s in (5, 6)]
+    out = {}
+    for ov in ("1", "0"):
+        monkeypatch.setenv("DS2_OVERLAP_OPT", ov)
+        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
+        assert (tr._defer_hi is not None) == (ov == "1")
+        losses = [float(tr.step(batches[i % 2])) for i in range(4)]
+        if ov == "1":
+            assert tr.arena.pending_update is not None      # the overlapped path is taken
+        tr.flush_optimizer()
+        torch.cuda.synchronize()
+        out[ov] = (losses, tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone(),
+                   tr.arena.p16.clone())
+    a, b = out["1"], out["0"]
+    assert a[0] == b[0], (a[0], b[0])
+    for x, y, name in zip(a[1:], b[1:], ("flat", "m", "v", "ema", "p16")):
+        assert torch.equal(x, y), name

@@ -23,7 +23,7 @@ def main():
     p, g, m, v, e = (torch.randn(a.n, device=d) for _ in range(5))
     v.abs_()
     p16 = torch.empty(a.n, device=d, dtype=torch.bfloat16)
-    fn = lambda: C.adam_ema(p, g, m, v, e, p16, 1e-4, 0.9, 0.999, 1e-8, 1.0, 0.999, None)  # noqa: E731
+    fn = lambda: C.adam_ema(p, g, m, v, e, p16, 1e-4, 0.9, 0.999, 1e-8, 1.0, 0.999, None, 0)  # noqa: E731
     for _ in range(3):
         fn()
     s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
