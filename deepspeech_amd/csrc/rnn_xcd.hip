@@ -312,7 +312,8 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
   if (tid < G * UPW)
     bh_s[tid / UPW][tid % UPW] = (CELL == CELL_GRU && a.bh[dir]) ? a.bh[dir][(tid / UPW) * H + u0 + tid % UPW] : 0.f;
   if (wave == 0) {
-    const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if ((a.knobs & 32768) && m > 0) m = 0;      // knob 32768: force write-through (timing)
     if (lane == 0) { s_mode = m; s_abort = (m < 0); }
   }
 
@@ -551,12 +552,21 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
 // plain/write-through stores), so the host-side plan is shared.
 // ------------------------------------------------------------------------------------
 constexpr int QW = 8;             // MFMA waves of the generation-4 forward
+#ifndef DS2_WIDE_CH
+#define DS2_WIDE_CH 2             // wide layers (KL > 0): granules in flight per lane, 0 = all (CH 2/3/4/6/8 measured 5.67/5.75/5.77/6.16/7.49 us/step at H = 1280)
+#endif
 constexpr int QTH = (QW + 1) * 64;
 
-template <int CELL, int KB, bool STAMPS>
+// KL > 0 (wide layers, H = 1280 GRU: 10 k-steps per wave): the LAST KL k-steps of each
+// wave's U slice live in LDS instead of VGPRs (KB - KL register k-steps fit the 3-waves-per-
+// SIMD budget that KB = 8..10 would spill), read back as one conflict-free ds_read_b128 per
+// gate when the poll reaches that k-step.
+template <int CELL, int KB, bool STAMPS, int KL = 0>
 __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   using StampT = typename std::conditional<STAMPS, Stamps, NoStamps>::type;
   constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
+  constexpr int KR = KB - KL;                     // k-steps with register-resident U
+  static_assert(KL >= 0 && KR >= 1, "register k-steps");
   constexpr int ROWS = 16;
   constexpr int GP = G * UPW + 4;                 // gx ring row pitch: 4*GP = 16 (mod 64) banks
   constexpr int OP = UPW + 4;                     // output staging row pitch
@@ -569,6 +579,7 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   __shared__ float4 og_s[(CELL == CELL_GRU) ? 2 : 1][(CELL == CELL_GRU) ? ROWS : 1][OP];
   __shared__ int len_s[ROWS];
   __shared__ int s_mode, s_abort;
+  __shared__ bf16x8 ul_s[KL > 0 ? KL : 1][QW][G][64];   // LDS-resident U k-steps (KL > 0)
 
   int grp, mem;
   if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
@@ -586,7 +597,8 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   const int ec = 16 * uh + (lane & 15);
   if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
   if (wave == 0) {
-    const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if ((a.knobs & 32768) && m > 0) m = 0;      // knob 32768: force write-through (timing)
     if (lane == 0) { s_mode = m; s_abort = (m < 0); }
   }
 
@@ -731,7 +743,7 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
 
   if (wave < QW) {
     // resident U fragments: B[k][c] = U[g*H + u0 + 16*uh + c][ks*32 + k], ks = kq + 4*kk
-    bf16x8 uf[KB][G];
+    bf16x8 uf[KR][G];
     bool kval[KB];
     float hreg = 0.f, bhr[G];
     {
@@ -745,7 +757,8 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
           bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
           if (kval[kk])
             v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)(g * H + u0 + ec) * H + ks * 32 + 8 * (lane >> 4));
-          uf[kk][g] = v;
+          if (kk < KR) uf[kk < KR ? kk : 0][g] = v;
+          else ul_s[kk >= KR ? kk - KR : 0][wave][g][lane] = v;   // own slot: no barrier needed
         }
       }
 #pragma unroll
@@ -767,16 +780,34 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) gxv[g] = gxr_s[s & 1][erow][g * UPW + ec];
       unsigned off[KB];
+      if constexpr (KL > 0) {
+        // wide layers have KS == 4 * KB (host-checked): no clamp, and every k-step's granule
+        // is a constant 256 B past the first, so the loads take it as an immediate offset
+        // (one live VGPR instead of KB)
+        const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + kq * 32 + 8 * (lane >> 4)) * 2);
 #pragma unroll
-      for (int kk = 0; kk < KB; ++kk)
-        off[kk] = (unsigned)((((size_t)s * NP + arow) * H + min(kq + 4 * kk, KS - 1) * 32 + 8 * (lane >> 4)) * 2);
+        for (int kk = 0; kk < KB; ++kk) off[kk] = o0 + 256u * kk;
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk)
+          off[kk] = (unsigned)((((size_t)s * NP + arow) * H + min(kq + 4 * kk, KS - 1) * 32 + 8 * (lane >> 4)) * 2);
+      }
       f32x4 acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, nap, [&](int kk, bf16x8 af) {
+      auto mfma_k = [&](int kk, bf16x8 af) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, uf[kk][g], acc[g], 0, 0, 0);
-      });
+        for (int g = 0; g < G; ++g) {
+          const bf16x8 b = kk < KR ? uf[kk < KR ? kk : 0][g] : ul_s[kk >= KR ? kk - KR : 0][wave][g][lane];
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b, acc[g], 0, 0, 0);
+        }
+      };
+      bool ok;
+      if constexpr (KL > 0 && DS2_WIDE_CH > 0)
+        // wide layers: at most DS2_WIDE_CH granules in flight per lane (register budget)
+        ok = poll_mfma<KB, 1, DS2_WIDE_CH>(rs_hx, off, kval, true, a.timeout, mfma_k);
+      else
+        ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, nap, mfma_k);
       if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
       st.mark(0);
       // transpose-reduce: hand the three elements this wave does not finalise to their owners
@@ -932,7 +963,8 @@ __global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
   if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
 
   if (wave == 0) {
-    const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if ((a.knobs & 32768) && m > 0) m = 0;      // knob 32768: force write-through (timing)
     if (lane == 0) { s_mode = m; s_abort = (m < 0); }
   }
   for (int i = tid; i < ROWS * LP / 8; i += NTH) reinterpret_cast<i32x4*>(A)[i] = i32x4{0, 0, 0, 0};
@@ -1336,7 +1368,8 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
   for (int i = tid; i < ROWS * DGP; i += NTH) (&dg_s[0][0])[i] = 0;
   if (wave == 0) {
-    const int m = group_census(a.census, grp, mem, P, a.timeout, a.err);
+    int m = group_census(a.census, grp, mem, P, a.timeout, a.err);
+    if ((a.knobs & 32768) && m > 0) m = 0;      // knob 32768: force write-through (timing)
     if (lane == 0) { s_mode = m; s_abort = (m < 0); }
   }
 
@@ -1906,9 +1939,17 @@ struct DS2RnnX {
 
 // 1 if the forward launch for these parameters is generation 4 (which can fuse the
 // direction sum into its output stores)
-int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs) {
+// generation 4 serves k-steps per wave kbq <= 8 (ReLU) / <= 10 (GRU: beyond 7, the last
+// kbq - 7 of each wave's U k-steps are LDS-resident; knob 65536 keeps H = 1280 on gen 2)
+static bool gen4_ok(int H, int cell, int mt, int knobs) {
   const int kbq = (H / 32 + 3) / 4;
-  return ndir == 2 && !(knobs & 256) && mt == 1 && kbq <= (cell == CELL_GRU ? 7 : 8) ? 1 : 0;
+  if ((knobs & 256) || mt != 1) return false;
+  if (cell == CELL_GRU) return kbq <= 7 || (kbq <= 10 && (H / 32) % 4 == 0 && !(knobs & 65536));
+  return kbq <= 8;
+}
+
+int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs) {
+  return ndir == 2 && gen4_ok(H, cell, mt, knobs) ? 1 : 0;
 }
 
 // grid size of a launch (blocks with no role exit at once)
@@ -1956,8 +1997,9 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
   const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
   // generation 4 (K-quarter split, register epilogue) unless knob 256 asks for generation 2
   const int kbq = (d->H / 32 + 3) / 4;
-  // (GRU at kbq = 8 spills under the 3-waves-per-SIMD register budget)
-  const bool gen4 = !(d->knobs & 256) && d->mt == 1 && kbq <= (d->cell == CELL_GRU ? 7 : 8);
+  // (GRU at kbq = 8 spills under the 3-waves-per-SIMD register budget: kbq 8..10 keep
+  // kbq - 7 k-steps of U in LDS)
+  const bool gen4 = gen4_ok(d->H, d->cell, d->mt, d->knobs);
   if (d->ysum != nullptr && (!gen4 || d->ndir != 2)) return -37;   // only gen 4 fuses the sum
   if (gen4) {
 #define DS2_QL(C, K)                                                                                  \
@@ -1970,7 +2012,15 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
     DS2_QK(C, 1) DS2_QK(C, 2) DS2_QK(C, 3) DS2_QK(C, 4) DS2_QK(C, 5) DS2_QK(C, 6) DS2_QK(C, 7)        \
     default: DS2_QL(C, 8) break;                                                                      \
   }
-    if (d->cell == CELL_GRU) { DS2_Q(CELL_GRU) } else { DS2_Q(CELL_RELU) }
+#define DS2_QW(K, L)                                                                                  \
+  case K:                                                                                             \
+    if (a.stamps) hipLaunchKernelGGL((rnnq_fwd_kernel<CELL_GRU, K, true, L>), dim3(grid), dim3(QTH), 0, st, a); \
+    else hipLaunchKernelGGL((rnnq_fwd_kernel<CELL_GRU, K, false, L>), dim3(grid), dim3(QTH), 0, st, a); \
+    break;
+    if (d->cell == CELL_GRU && kbq > 7) {
+      switch (kbq) { DS2_QW(8, 1) DS2_QW(9, 2) default: DS2_QW(10, 3) }
+    } else if (d->cell == CELL_GRU) { DS2_Q(CELL_GRU) } else { DS2_Q(CELL_RELU) }
+#undef DS2_QW
 #undef DS2_QL
 #undef DS2_QK
 #undef DS2_Q
