@@ -37,6 +37,15 @@ TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
     (7712, 2400, 4800, False, True, 1): 2,
     (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
 }
+# (N, K, a_col, b_col) of bf16 projections where the library (hipBLASLt) measured faster than
+# every configuration here (tools/bench_gemm_ours.py --only proj, MI355X, M = 7712): GRU-1280
+# (config 5) 153 vs 182 us (K = 1280) and 260 vs 325 us (K = 2400); GRU-1760 305 vs 340 and
+# 390 vs 446 us. In the step: config 5 23.42 vs 24.12-24.19 ms/step; the reference's
+# 7 x bi-ReLU-1760 (N = 3520) 21.70-21.76 vs 22.10-22.22 (same box, alternating).
+# matmul() declines them so the caller's library path runs (DS2_GEMM_CFG forces ours).
+LIBRARY_WINS = {(7680, 1280, False, False), (7680, 2400, False, False),
+                (10560, 1760, False, False), (10560, 2400, False, False),
+                (3520, 1760, False, False), (3520, 2400, False, False)}
 _FORCE = os.environ.get("DS2_GEMM_CFG")
 # DS2_GEMM selects which engine GEMM classes run here: "hip" (all), "torch" (none: library
 # GEMMs, A/B timing only) or a comma list of {proj, dx, wgrad}. Default "proj": measured in
@@ -148,6 +157,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
     A, a_col = oa          # a [M,K] unit-stride K -> row mode (A(m,k) = A[m*lda+k])
     B, b_col = ob          # b [K,N] unit-stride N -> col mode (B(n,k) = B[k*ldb+n])
     if not supported(M, N, K, a_col, b_col):
+        return False
+    if _FORCE is None and (N, K, a_col, b_col) in LIBRARY_WINS:
         return False
     for t in (A, B, out):
         if t.data_ptr() % 16 or (t.dim() >= 2 and t.stride(-2) % 8):
