@@ -552,6 +552,9 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
 // plain/write-through stores), so the host-side plan is shared.
 // ------------------------------------------------------------------------------------
 constexpr int QW = 8;             // MFMA waves of the generation-4 forward
+#ifndef DS2_NARROW_CH
+#define DS2_NARROW_CH 0           // KL == 0: 0 = all granules in flight with wave-wide re-poll (poll_mfma_par)
+#endif
 #ifndef DS2_WIDE_CH
 #define DS2_WIDE_CH 2             // wide layers (KL > 0): granules in flight per lane, 0 = all (CH 2/3/4/6/8 measured 5.67/5.75/5.77/6.16/7.49 us/step at H = 1280)
 #endif
@@ -803,9 +806,9 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
         }
       };
       bool ok;
-      if constexpr (KL > 0 && DS2_WIDE_CH > 0)
+      if constexpr ((KL > 0 && DS2_WIDE_CH > 0) || (KL == 0 && DS2_NARROW_CH > 0))
         // wide layers: at most DS2_WIDE_CH granules in flight per lane (register budget)
-        ok = poll_mfma<KB, 1, DS2_WIDE_CH>(rs_hx, off, kval, true, a.timeout, mfma_k);
+        ok = poll_mfma<KB, 1, (KL > 0 ? DS2_WIDE_CH : DS2_NARROW_CH)>(rs_hx, off, kval, true, a.timeout, mfma_k);
       else
         ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, nap, mfma_k);
       if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
