@@ -10,7 +10,7 @@
 //                         s-1/s-2 (s+1/s+2) neighbours crossing a lane boundary come from a
 //                         cross-lane shuffle, so a frame costs no barrier and no LDS round
 //                         trip; the next frame's lp row is prefetched one frame ahead.
-//                         alpha/beta rows are streamed (float4 stores, 64*SPL row stride)
+//                         alpha/beta rows are streamed (float4/2 stores, 64*SPL row stride)
 //                         to ab_ws[2][N][T][64*SPL].
 //   3. ctc_grad_kernel    fully parallel over frames (one wave per (t, b)): occupancy
 //                         gamma_t(s) = alpha+beta-lp-logP, blank states summed with a wave
@@ -121,11 +121,21 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
   const float* lp = lp_ws + (size_t)b * T * KPAD;
   constexpr int SPS = 64 * SPL;                    // row stride: whole register tile, 16-B aligned
   float* out = ab_ws + ((size_t)beta * N + b) * (size_t)T * SPS;
-  auto put_row = [&](int t, const float* v) {
-    float4* o = reinterpret_cast<float4*>(out + (size_t)t * SPS + s0);
+  auto put_row = [&](int t, const float* v) {   // rows in natural-log units for the gradient kernel
+    float* o = out + (size_t)t * SPS + s0;       // 4*SPL-B aligned: widest store that divides it
+    if constexpr (SPL % 4 == 0) {
 #pragma unroll
-    for (int j = 0; j < SPL / 4; ++j)   // rows in natural-log units for the gradient kernel
-      o[j] = make_float4(v[4 * j] * LN2, v[4 * j + 1] * LN2, v[4 * j + 2] * LN2, v[4 * j + 3] * LN2);
+      for (int j = 0; j < SPL / 4; ++j)
+        reinterpret_cast<float4*>(o)[j] = make_float4(v[4 * j] * LN2, v[4 * j + 1] * LN2, v[4 * j + 2] * LN2,
+                                                      v[4 * j + 3] * LN2);
+    } else if constexpr (SPL % 2 == 0) {
+#pragma unroll
+      for (int j = 0; j < SPL / 2; ++j)
+        reinterpret_cast<float2*>(o)[j] = make_float2(v[2 * j] * LN2, v[2 * j + 1] * LN2);
+    } else {
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) o[j] = v[j] * LN2;
+    }
   };
   // lp rows are staged through LDS in chunks of 64 frames (one 128-B row per lane), so
   // the per-frame gathers are LDS reads: a global load in the frame loop would make the
@@ -423,10 +433,30 @@ static void launch_recur(const int* lens, const int* labels, const int* label_le
 
 extern "C" {
 
+// States per lane: the smallest instantiation that holds the longest label. The frame
+// recursion is latency/issue bound on ONE wave (2 v_exp + 1 v_log per state), so every
+// unused state slot costs time: 10-s utterances (~150 labels, 301 states) run SPL 5, not 8.
 static int ctc_spl(int SPmax) {
   const int need = (SPmax + 63) / 64;
+#ifdef DS2_CTC_SPL_POW2   // A/B build: power-of-two tile widths only (the round-1 set)
   for (int k : {4, 8, 16, 32}) if (k >= need) return k;
+#else
+  for (int k : {4, 5, 6, 8, 12, 16, 32}) if (k >= need) return k;
+#endif
   return -1;
+}
+
+static void launch_recur_spl(int spl, const int* lens, const int* labels, const int* label_lens, const float* lp_ws,
+                             float* ab_ws, float* logp, int T, int N, int Lmax, int SPmax, int blank, hipStream_t st) {
+  switch (spl) {
+    case 4: launch_recur<4>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st); break;
+    case 5: launch_recur<5>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st); break;
+    case 6: launch_recur<6>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st); break;
+    case 8: launch_recur<8>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st); break;
+    case 12: launch_recur<12>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st); break;
+    case 16: launch_recur<16>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st); break;
+    default: launch_recur<32>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st); break;
+  }
 }
 
 // workspace floats: lp [N][T][32] + alpha/beta [2][N][T][64*SPL] + logP [N]
@@ -453,10 +483,7 @@ int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const in
     hipLaunchKernelGGL(ctc_lsm_kernel<bf16_t>, g4, dim3(256), 0, st, (const bf16_t*)logits, lens, lp_ws, T, N, K);
   else
     hipLaunchKernelGGL(ctc_lsm_kernel<float>, g4, dim3(256), 0, st, (const float*)logits, lens, lp_ws, T, N, K);
-  if (spl == 4) launch_recur<4>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else if (spl == 8) launch_recur<8>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else if (spl == 16) launch_recur<16>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else launch_recur<32>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  launch_recur_spl(spl, lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
   if (logits_bf16)
     hipLaunchKernelGGL(ctc_grad_kernel<bf16_t>, g4, dim3(256), 0, st, (const bf16_t*)logits, lens, labels, label_lens,
                        ab_ws, logp, loss, (bf16_t*)grad, T, N, K, Lmax, SPS, blank, zero_inf);
@@ -500,10 +527,7 @@ int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens
   hipLaunchKernelGGL(fc_lsm_kernel<float>, dim3((M + 16 * FC_WAVES - 1) / (16 * FC_WAVES)), dim3(FC_WAVES * 64), lds,
                      st, (const bf16_t*)h, (const bf16_t*)W, (const bf16_t*)bias, lens, lp_ws, (float*)nullptr, T, N,
                      H, K);
-  if (spl == 4) launch_recur<4>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else if (spl == 8) launch_recur<8>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else if (spl == 16) launch_recur<16>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
-  else launch_recur<32>(lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
+  launch_recur_spl(spl, lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
   hipLaunchKernelGGL(ctc_grad_lp_kernel, dim3((M + 3) / 4), dim3(256), 0, st, lens, labels, label_lens, lp_ws, ab_ws,
                      logp, loss, (bf16_t*)G, T, N, K, Lmax, SPS, blank, zero_inf);
   return (int)hipGetLastError();

@@ -148,7 +148,7 @@ def test_ctc_fused(cuda, dtype):
     assert _rel(x.grad, xr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
 
 
-@pytest.mark.parametrize("Lmax,T", [(60, 150), (150, 241), (300, 700)])
+@pytest.mark.parametrize("Lmax,T", [(60, 150), (150, 241), (180, 400), (240, 500), (300, 700)])
 def test_ctc_long_labels(cuda, Lmax, T):
     """Lattices of 121..601 states: every register-tile width of the one-wave recursion."""
     from deepspeech_amd.ops import ctc as CTC
