@@ -43,18 +43,20 @@ __device__ __forceinline__ float lse2(float a, float b) {
 
 // log2-domain lse of three values with ONE of the three exponentials known to be 2^0:
 // m = max, the other two are the median and the minimum (v_max3 / v_med3 / v_min3), so a
-// state costs 2 v_exp_f32 + 1 v_log_f32 (no ln<->log2 scaling, no branch).
+// state costs 2 v_exp_f32 + 1 v_log_f32 (no ln<->log2 scaling, no branch). No all--inf
+// select either: the max is clamped to -1e30, so three -inf inputs give exactly -1e30 (fp32
+// ulp there ~7.6e22: adding log-probs keeps it at -1e30). The recursion carries -1e30 as its
+// "log 0", the gradient kernels' ga > -80 test maps it to 0 like -inf, and a logP below
+// -1e29 is returned as -inf (infeasible utterance).
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
-__device__ __forceinline__ float lse3_2(float a, float b, float c) {
-  const float m = fmaxf(fmaxf(a, b), c);
+__device__ __forceinline__ float lse3_rec(float a, float b, float c) {
+  const float m = fmaxf(fmaxf(fmaxf(a, b), c), -1e30f);
   const float lo = fminf(fminf(a, b), c);
   const float mid = __builtin_amdgcn_fmed3f(a, b, c);
-  const float mc = fmaxf(m, -1e30f);                   // all -inf: keep the differences finite
-  const float r = mc + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(mid - mc) +
-                                             __builtin_amdgcn_exp2f(lo - mc));
-  return (m == NEG_INF) ? NEG_INF : r;
+  return m + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(mid - m) + __builtin_amdgcn_exp2f(lo - m));
 }
+constexpr float LOG_ZERO_LIMIT = -1e29f;
 
 template <typename LT>
 __device__ __forceinline__ float ld_logit(const LT* p);
@@ -109,10 +111,12 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
 #pragma unroll
   for (int j = 0; j < SPL; ++j) {
     const int s = s0 + j;
-    cls[j] = (s < SP) ? state_class(labels, b, Lmax, s, blank) : blank;
-    DS2_DCHECK(cls[j] >= 0 && cls[j] < KPAD);      // label ids index the 32-wide lp rows
+    // states past the lattice read the staged rows' padding column KPAD, which holds -inf:
+    // their values stay -inf without a per-state select in the frame loop
+    cls[j] = (s < SP) ? state_class(labels, b, Lmax, s, blank) : KPAD;
+    DS2_DCHECK(cls[j] >= 0 && cls[j] <= KPAD);     // label ids index the 32-wide lp rows
     bool ok = false;
-    if (s < SP && cls[j] != blank) {
+    if (s < SP && cls[j] != blank) {   // (s >= SP: cls = KPAD, no skip transition)
       if (!beta) ok = s >= 2 && cls[j] != state_class(labels, b, Lmax, s - 2, blank);
       else ok = s + 2 < SP && cls[j] != state_class(labels, b, Lmax, s + 2, blank);
     }
@@ -141,6 +145,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
   // the per-frame gathers are LDS reads: a global load in the frame loop would make the
   // wave wait (vmcnt) behind its own streaming alpha/beta stores every frame.
   __shared__ float lps[64][KPAD + 1];
+  lps[lane][KPAD] = NEG_INF;                       // never overwritten by stage()
   const int dt = beta ? -1 : 1;
   const int t0 = beta ? len - 1 : 0;
   auto stage = [&](int c0) {   // frames c0 .. c0+63 (forward) or c0 .. c0-63 (backward)
@@ -190,8 +195,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
       for (int j = 0; j < SPL; ++j) {
         const float a1 = (j >= 1) ? v[j - 1] : p1;
         const float a2 = (j >= 2) ? v[j - 2] : (j == 1 ? p1 : p2);
-        const float r = lse3_2(v[j], a1, ((skip >> j) & 1u) ? a2 : NEG_INF);
-        nv[j] = (s0 + j < SP) ? r + lcur[j] : NEG_INF;
+        nv[j] = lse3_rec(v[j], a1, ((skip >> j) & 1u) ? a2 : NEG_INF) + lcur[j];
       }
     } else {
       const float n1 = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(NEG_INF), __float_as_int(v[0]),
@@ -202,8 +206,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
       for (int j = 0; j < SPL; ++j) {
         const float b1 = (j + 1 < SPL) ? v[j + 1] : n1;
         const float b2 = (j + 2 < SPL) ? v[j + 2] : (j + 1 < SPL ? n1 : n2);
-        const float r = lse3_2(v[j], b1, ((skip >> j) & 1u) ? b2 : NEG_INF);
-        nv[j] = (s0 + j < SP) ? r + lcur[j] : NEG_INF;
+        nv[j] = lse3_rec(v[j], b1, ((skip >> j) & 1u) ? b2 : NEG_INF) + lcur[j];
       }
     }
 #pragma unroll
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
     const float m = wave_max(mine);
     float e = (m == NEG_INF) ? 0.f : __expf(mine - m);
     e = wave_sum(e);
-    if (lane == 0) logp_out[b] = (m == NEG_INF) ? NEG_INF : m + __logf(e);
+    if (lane == 0) logp_out[b] = (m < LOG_ZERO_LIMIT) ? NEG_INF : m + __logf(e);
   }
 }
 

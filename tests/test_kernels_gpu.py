@@ -174,7 +174,7 @@ def test_ctc_long_labels(cuda, Lmax, T):
 def test_ctc_peaked_distributions(cuda):
     """Confident (peaked) frames, log-probs down to ~-100 nats. The kernel runs the alpha/beta
     recursion in log2 units: the staged log-prob rows are scaled by LOG2E, each lattice state
-    takes a branch-free 3-way log-sum-exp (lse3_2: max3/med3/min3, two exp2 + one log2), and
+    takes a branch-free 3-way log-sum-exp (lse3_rec: max3/med3/min3, two exp2 + one log2, -1e30 as log 0), and
     the stored alpha/beta rows are rescaled by LN2 back to nats for the gradient. Large
     log-prob gaps stress exactly that lse (exp2 underflow of the two smaller terms) and the
     unit conversion; the result must track the natural-log reference."""
