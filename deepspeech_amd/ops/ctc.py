@@ -121,23 +121,25 @@ class FusedHeadCTC(torch.autograd.Function):
         T, N, H = h.shape
         K = ctx.K
         M = T * N
-        scale = (gloss.to(torch.float32) / N).reshape(1).contiguous()
+        # the upstream gradient stays a device scalar (no host sync); 1/N goes into the host
+        # alpha of the critical-path dh GEMM, so no division kernel runs on the main stream
+        g32 = gloss.to(torch.float32).reshape(1).contiguous()
         h2 = h.view(M, H)
         dh = None
         if ctx.needs_input_grad[0]:
             dh = torch.empty(M, H, device=h.device, dtype=torch.bfloat16)
             # K = 32 padded classes; rows >= K of W_fc are never loaded (Kl) and meet G's zero columns
-            GM.gemm(G, w16, dh, M, H, 32, False, True, 0, 1.0, None, alpha_dev=scale, Kl=K)
+            GM.gemm(G, w16, dh, M, H, 32, False, True, 0, 1.0 / N, None, alpha_dev=g32, Kl=K)
             dh = dh.view(T, N, H)
         side = wgrad_stream(h.device, arena_of(weight)) if arena_of(bias) is not None else None
         if side is None:
-            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, scale, K)
+            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32 / N, K)
             return dh, gw, gb, None, None, None, None, None
         side.wait_stream(torch.cuda.current_stream(h.device))
         with torch.cuda.stream(side):
-            for t in (G, h2, scale):
+            for t in (G, h2, g32):
                 t.record_stream(side)
-            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, scale, K)
+            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32 / N, K)
         return dh, gw, gb, None, None, None, None, None
 
     @staticmethod

@@ -54,6 +54,7 @@ class Trainer:
                  world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
                  nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False):
         self.model = model
+        self._seed = {}            # (device, dtype) -> device scalar 1.0 (backward seed)
         # bf16 compute shadows of the weights only for the HIP engine (fused ops read them)
         self.arena = ParamArena(model, bf16_shadow=(model.engine == "hip"))
         self.opt = FusedAdamEMA(self.arena, lr=lr_schedule.initial_lr, ema_decay=moving_avg_decay)
@@ -170,7 +171,11 @@ class Trainer:
         # gradients a pending update still has to read
         self.arena.flush_update()
         self.watch.update(loss)
-        loss.backward()
+        # a cached device 1.0 as the backward seed: autograd would launch a fill for ones_like
+        one = self._seed.get((loss.device, loss.dtype))
+        if one is None:
+            one = self._seed[(loss.device, loss.dtype)] = torch.ones((), device=loss.device, dtype=loss.dtype)
+        loss.backward(one)
         parts = None
         if self._bounds is not None and self.nan_policy != "skip":
             self.arena.wgrad.drain()
