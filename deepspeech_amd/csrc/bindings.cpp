@@ -76,7 +76,6 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st);
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs);
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
 long long ds2_rnnx_ring_floats(int H, int BG, int R);
-int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st);
 int ds2_rnnx_grid(int H, int ngroups, int xcd_map);
 int ds2_rnnx_kb(int H, int G, int fwd);
 size_t ds2_rnnx_smem(int H, int G, int mt, int fwd);
@@ -347,19 +346,16 @@ void rnnx_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tens
   }
   d.dgx_scale = (float)dgx_scale;
   TORCH_CHECK(ndir == 1 || (d.U[1] && d.hsave[1] && d.ex[1]), "backward-direction buffers missing");
-  if (ring_f.has_value() && ring_f->defined()) {
-    // reduce-scatter BPTT (generation 3): dgh is a plain output, the exchange is the ring
-    const int64_t rf = ds2_rnnx_ring_floats((int)H, (int)BG, (int)R);
-    TORCH_CHECK(ring_f->scalar_type() == at::kFloat && ring_f->numel() >= rf, "ring_f must be fp32 [", rf, "]");
-    d.ring[0] = ring_f->data_ptr();
-    if (ndir == 2) {
-      TORCH_CHECK(ring_b.has_value() && ring_b->scalar_type() == at::kFloat && ring_b->numel() >= rf, "ring_b missing");
-      d.ring[1] = ring_b->data_ptr();
-    }
-    check(ds2_rnnx_bwd_rs(&d, cur_stream()), "rnnx_bwd_rs");
-    return;
+  // reduce-scatter BPTT (generation 3): dgh is a plain output, the exchange is the ring
+  TORCH_CHECK(ring_f.has_value() && ring_f->defined(), "rnnx_bwd needs the reduce-scatter ring");
+  const int64_t rf = ds2_rnnx_ring_floats((int)H, (int)BG, (int)R);
+  TORCH_CHECK(ring_f->scalar_type() == at::kFloat && ring_f->numel() >= rf, "ring_f must be fp32 [", rf, "]");
+  d.ring[0] = ring_f->data_ptr();
+  if (ndir == 2) {
+    TORCH_CHECK(ring_b.has_value() && ring_b->scalar_type() == at::kFloat && ring_b->numel() >= rf, "ring_b missing");
+    d.ring[1] = ring_b->data_ptr();
   }
-  check(ds2_rnnx_bwd(&d, cur_stream()), "rnnx_bwd");
+  check(ds2_rnnx_bwd_rs(&d, cur_stream()), "rnnx_bwd_rs");
 }
 
 py::dict rnnx_info(int64_t H, int64_t G, int64_t mt, int64_t ngroups, int64_t xcd_map) {

@@ -216,14 +216,23 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
   if (!beta) {
     // logP = lse(alpha_{len-1}(SP-1), alpha_{len-1}(SP-2))
     float mine = NEG_INF;
+    bool nan = false;
 #pragma unroll
     for (int j = 0; j < SPL; ++j)
-      if (s0 + j == SP - 1 || s0 + j == SP - 2) mine = lse2(mine, v[j] * LN2);
+      if (s0 + j == SP - 1 || s0 + j == SP - 2) {
+        nan = nan || (v[j] != v[j]);
+        mine = lse2(mine, v[j] * LN2);
+      }
     // at most two lanes hold a term: combine with a max-shifted wave reduction
     const float m = wave_max(mine);
     float e = (m == NEG_INF) ? 0.f : __expf(mine - m);
     e = wave_sum(e);
-    if (lane == 0) logp_out[b] = (m < LOG_ZERO_LIMIT) ? NEG_INF : m + __logf(e);
+    // A NaN log-prob (a diverged model: the log-softmax turns a NaN logit into a whole NaN
+    // frame, which every later frame of the recursion inherits) must reach the loss as NaN,
+    // not as an "infeasible" -inf that zero_infinity would hide: lse2 / wave_max use fmaxf,
+    // which drops NaN operands, so the final states are tested explicitly.
+    const bool any_nan = __any(nan);
+    if (lane == 0) logp_out[b] = any_nan ? __builtin_nanf("") : (m < LOG_ZERO_LIMIT) ? NEG_INF : m + __logf(e);
   }
 }
 
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const LT* __restrict__ lo
   const int len = min(lens[b], T);
   const int L = label_lens[b];
   const float logp = (len > 0 && L <= len) ? logp_in[b] : NEG_INF;
-  const bool feasible = logp > NEG_INF;
+  const bool feasible = !(logp == NEG_INF);        // NaN stays "feasible": it must reach the loss
   if (t == 0 && lane == 0) loss[b] = feasible ? -logp : (zero_inf ? 0.f : INFINITY);
   LT* g = grad + (size_t)w * K;
   if (t >= len || !feasible) {
@@ -384,7 +393,7 @@ __global__ __launch_bounds__(256) void ctc_grad_lp_kernel(const int* __restrict_
   const int len = min(lens[b], T);
   const int L = label_lens[b];
   const float logp = (len > 0 && L <= len) ? logp_in[b] : NEG_INF;
-  const bool feasible = logp > NEG_INF;
+  const bool feasible = !(logp == NEG_INF);        // NaN stays "feasible": it must reach the loss
   if (t == 0 && lane == 0) loss[b] = feasible ? -logp : (zero_inf ? 0.f : INFINITY);
   bf16_t* g = G + (size_t)w * KPAD;
   if (t >= len || !feasible) {

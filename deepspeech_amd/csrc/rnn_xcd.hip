@@ -63,24 +63,6 @@ struct XFwd {
   unsigned long long* stamps;   // optional [grid][8] phase cycle sums (diagnostics)
 };
 
-struct XBwd {
-  int T, N, NP, H, P, BG, R, steps, gstride, ngroups, xcd_map, knobs;
-  const int* lens;
-  const bf16_t* dy;
-  const bf16_t* U[2];
-  const float* hsave[2];
-  const float* gates[2];
-  bf16_t* dgh[2];         // [steps][NP][G*H] pre-filled with sentinel
-  bf16_t* dgx;
-  float* dbx_part[2];     // [BG][G*H]
-  float* dbh_part[2];
-  float dgx_scale;
-  unsigned* census;
-  unsigned* err;
-  long long timeout;
-  unsigned long long* stamps;
-};
-
 // Phase stamps (diagnostics; a null stamps pointer costs one uniform branch per phase).
 struct Stamps {
   unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
@@ -893,358 +875,17 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
 }
 
-constexpr int GW = 7;             // gather waves of the backward kernel
 #ifndef DS2_BWD_CH
 #define DS2_BWD_CH 3              // R > 8 reduce-scatter gather: producers' granules in flight per lane (0 = all; H = 1280 BPTT 6.78 -> 6.63 us/step at 3, 6.65 at 2 and 4)
 #endif
-constexpr int GTH = GW * 64;
 
-// Batched sentinel gather of NGR 16-B granules (row-major, GPR per row) into LDS rows of
-// pitch LP elements (backward kernel: its 3H-wide exchange row is swept coalesced, a full
-// 128-B line per 8 lanes, which beats per-fragment polling there). Returns false on timeout.
-template <int GMAX>   // granules in flight per thread
-__device__ __forceinline__ bool gather_tile(__amdgpu_buffer_rsrc_t rs, size_t base_elem, int row_stride, int GPR,
-                                            int NGR, bf16_t* lds, int LP, int gt, long long timeout, int nap = 1) {
-  const long long t0 = __builtin_amdgcn_s_memrealtime();
-  bool ok = true;
-  for (int q0 = 0; q0 < NGR; q0 += GTH * GMAX) {
-    i32x4 v[GMAX];
-    unsigned off[GMAX];
-#pragma unroll
-    for (int j = 0; j < GMAX; ++j) {
-      const int q = q0 + gt + j * GTH;
-      const int qq = q < NGR ? q : NGR - 1;
-      const int row = qq / GPR, c8 = qq - row * GPR;
-      off[j] = (unsigned)((base_elem + (size_t)row * row_stride + c8 * 8) * 2);
-      v[j] = load_sc1_b128(rs, off[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < GMAX; ++j) {
-      const int q = q0 + gt + j * GTH;
-      if (q < NGR) {
-        while (!granule_ready(v[j])) {
-          if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { ok = false; break; }
-          for (int z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(1);   // poll back-off (L2 traffic)
-          v[j] = load_sc1_b128(rs, off[j]);
-        }
-        const int row = q / GPR, c8 = q - row * GPR;
-        *reinterpret_cast<i32x4*>(lds + row * LP + c8 * 8) = v[j];
-      }
-    }
-  }
-  return ok;
-}
-
-// ------------------------------------------------------------------------------------
-// backward (BPTT). Structure of generation 2 (measured faster for the 3H-wide exchange
-// than the forward's per-fragment polling): waves 0..6 sweep dgh_{s+1} into an LDS A tile,
-// barrier, all 8 waves run the K-split MFMA, barrier, epilogue. Wave 7 does the memory
-// duties while the others gather. The A tile is dynamic LDS (K zero-padded to 8*KB*32).
-// ------------------------------------------------------------------------------------
-template <int CELL, int MT, int KB>
-__global__ __launch_bounds__(NTH) void rnnx_bwd_kernel(XBwd a) {
-  constexpr int G = (CELL == CELL_GRU) ? 3 : 1;
-  constexpr int ROWS = 16 * MT;
-  constexpr int EPT = ROWS * UPW / ETH;
-  constexpr int OPL = ROWS * UPW / 64;            // elements per memory-wave lane
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ float red_s[MW][ROWS][UPW + 1];
-  __shared__ __attribute__((aligned(16))) bf16_t st_s[ROWS][G * UPW];
-  __shared__ float dyr_s[2][ROWS][UPW];           // prefetch ring (memory wave -> epilogue)
-  __shared__ float hpr_s[2][ROWS][UPW];
-  __shared__ float4 gr_s[2][(CELL == CELL_GRU) ? ROWS : 1][UPW];
-  __shared__ float ox_s[2][ROWS][G][UPW];         // dgx staging by step parity (epilogue -> memory wave)
-  __shared__ int len_s[ROWS];
-  __shared__ int s_mode, s_abort;
-
-  int grp, mem;
-  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
-  DS2_DCHECK(grp < a.ngroups && mem < a.P && a.NP >= a.BG * a.R && a.R <= 16);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int H = a.H, GH = G * H, KS = GH / 32, N = a.N, NP = a.NP, R = a.R;
-  const int LP = KB * MW * 32 + 8;                // A pitch (K zero-padded to KB*7*32)
-  const int bg = grp % a.BG, dir = grp / a.BG;
-  const int r0 = bg * R, u0 = mem * UPW;
-  bf16_t* A = reinterpret_cast<bf16_t*>(smem);     // [ROWS][LP]
-  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
-
-  if (wave == 0) {
-    int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
-    if ((a.knobs & 32768) && m > 0) m = 0;      // knob 32768: force write-through (timing)
-    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
-  }
-  for (int i = tid; i < ROWS * LP / 8; i += NTH) reinterpret_cast<i32x4*>(A)[i] = i32x4{0, 0, 0, 0};
-
-  // resident U column fragments of the MFMA waves (0..6): k-step ks = wave + kk*7
-  // B[k][c] = U[k][u0 + 16*nt + c], k over all G*H (zero past it)
-  bf16x8 uf[KB][2];
-  {
-    const bf16_t* Ud = a.U[dir];
-#pragma unroll
-    for (int kk = 0; kk < KB; ++kk) {
-      const int ks = wave + kk * MW;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (wave < MW && ks < KS) {
-          const int k0 = ks * 32 + 8 * (lane >> 4);
-          const bf16_t* p = Ud + (size_t)k0 * H + u0 + 16 * nt + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (short)p[(size_t)j * H];
-        }
-        uf[kk][nt] = v;
-      }
-    }
-  }
-
-  float carry[EPT];
-  float sbx[EPT][G];
-  float sbh[EPT];
-#pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    carry[i] = 0.f;
-    sbh[i] = 0.f;
-#pragma unroll
-    for (int g = 0; g < G; ++g) sbx[i][g] = 0.f;
-  }
-  __syncthreads();   // len_s
-
-  // memory wave: per-step inputs (dy, gates, h_prev) two steps ahead, dgx stores
-  float pdy[OPL], php[OPL];
-  float4 pg[OPL];
-  auto mw_load = [&](int s) {
-#pragma unroll
-    for (int j = 0; j < OPL; ++j) {
-      const int e = lane + 64 * j;
-      const int row = e >> 5, c = e & 31;
-      const int bp = min(r0 + row, NP - 1), bn = min(r0 + row, N - 1), u = u0 + c;
-      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
-      pdy[j] = bf2f(a.dy[((size_t)t * N + bn) * H + u]);
-      if (CELL == CELL_GRU) {
-        pg[j] = reinterpret_cast<const float4*>(a.gates[dir])[((size_t)s * NP + bp) * H + u];
-        php[j] = a.hsave[dir][((size_t)s * NP + bp) * H + u];
-      } else {
-        php[j] = a.hsave[dir][((size_t)(s + 1) * NP + bp) * H + u];     // h_s itself
-      }
-    }
-  };
-  auto mw_put = [&](int s) {
-    const int slot = s & 1;
-#pragma unroll
-    for (int j = 0; j < OPL; ++j) {
-      const int e = lane + 64 * j;
-      const int row = e >> 5, c = e & 31;
-      const bool act = s < len_s[row];
-      dyr_s[slot][row][c] = act ? pdy[j] : 0.f;
-      hpr_s[slot][row][c] = act ? php[j] : 0.f;
-      if (CELL == CELL_GRU) gr_s[slot][(CELL == CELL_GRU) ? row : 0][c] = act ? pg[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  auto mw_store = [&](int s) {          // dgx of step s from the staging area
-#pragma unroll
-    for (int j = 0; j < OPL; ++j) {
-      const int e = lane + 64 * j;
-      const int row = e >> 5, c = e & 31;
-      const int b = r0 + row, u = u0 + c;
-      if (row < R && b < N) {
-        const int L = len_s[row];
-        const bool act = s < L;
-        const int t = act ? ((dir == 0) ? s : (L - 1 - s)) : s;
-        bf16_t* dst = a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + u;
-#pragma unroll
-        for (int g = 0; g < G; ++g) dst[g * H] = f2bf(ox_s[s & 1][row][g][c] * a.dgx_scale);
-      }
-    }
-  };
-  if (s_abort) return;
-  if (wave == MEMW && a.steps > 0) mw_load(a.steps - 1);
-  const bool plain = s_mode == 1;
-  const unsigned dgh_bytes = (unsigned)((size_t)a.steps * NP * GH * 2);
-  bf16_t* dghd = a.dgh[dir];
-  const __amdgpu_buffer_rsrc_t rs_dgh = make_rsrc(dghd, dgh_bytes);
-  Stamps st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
-
-  // Role-split step loops (see the forward kernel): the memory wave's prefetch registers
-  // and the workers' U slice + in-flight gather granules are never live together.
-  if (wave < MW) {
-    for (int s = a.steps - 1; s >= 0; --s) {
-      st.mark(-1);
-      const bool has_next = s + 1 < a.steps;
-      {
-        // 4 granules in flight per thread measured fastest (6: +12 %); knobs (diagnostics):
-        // bit 0 -> 6 in flight, bits 4..7 -> poll back-off naps
-        const int nap = ((a.knobs >> 4) & 15) + 1;
-        const bool ok = !has_next ||
-            (!(a.knobs & 1) ? gather_tile<4>(rs_dgh, ((size_t)(s + 1) * NP + r0) * GH, GH, GH / 8, R * (GH / 8), A, LP,
-                                            tid, a.timeout, nap)
-                           : gather_tile<6>(rs_dgh, ((size_t)(s + 1) * NP + r0) * GH, GH, GH / 8, R * (GH / 8), A, LP,
-                                            tid, a.timeout, nap));
-        if (!ok) {
-          s_abort = 1;
-          atomicOr(a.err, 1u);
-        }
-      }
-      st.mark(0);
-      lds_barrier();                                                        // #1
-      st.mark(1);
-      if (s_abort) break;
-      // (M) partial dh_rec over this wave's k-steps
-      if (has_next) {
-        f32x4 acc[MT][2];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) { acc[m][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[m][1] = acc[m][0]; }
-        bf16x8 af[MT][KB];
-#pragma unroll
-        for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
-            af[m][kk] = *reinterpret_cast<const bf16x8*>(A + (m * 16 + (lane & 15)) * LP + (wave + kk * MW) * 32 +
-                                                         8 * (lane >> 4));
-#pragma unroll
-        for (int kk = 0; kk < KB; ++kk)
-#pragma unroll
-          for (int m = 0; m < MT; ++m) {
-            acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][0], acc[m][0], 0, 0, 0);
-            acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], uf[kk][1], acc[m][1], 0, 0, 0);
-          }
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) red_s[wave][m * 16 + (lane >> 4) * 4 + j][nt * 16 + (lane & 15)] = acc[m][nt][j];
-      }
-      st.mark(2);
-      lds_barrier();                                                        // #2
-      st.mark(3);
-      // (E) cell backward; the exchange copy (dgh_s) goes out first
-      if (wave < EW) {
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) {
-          const int e = tid + i * ETH;
-          const int row = e >> 5, c = e & 31;
-          if (row < R) {
-            float dhrec = 0.f;
-            if (has_next) {
-#pragma unroll
-              for (int w = 0; w < MW; ++w) dhrec += red_s[w][row][c];
-            }
-            const bool act = s < len_s[row];
-            const float dh = dyr_s[s & 1][row][c] + carry[i] + dhrec;
-            const float hp = hpr_s[s & 1][row][c];
-            float ghv[G], gxs[G];
-            float cnew = 0.f;
-            if (CELL == CELL_GRU) {
-              const float4 gv = gr_s[s & 1][(CELL == CELL_GRU) ? row : 0][c];
-              const float r = gv.x, z = gv.y, n = gv.z, ghn = gv.w;
-              const float dn = dh * (1.f - z);
-              const float dz = dh * (hp - n);
-              cnew = dh * z;
-              const float dan = dn * (1.f - n * n);
-              const float dr = dan * ghn;
-              const float dghn = dan * r;
-              const float daz = dz * z * (1.f - z);
-              const float dar = dr * r * (1.f - r);
-              ghv[0] = dar; ghv[1] = daz; ghv[2] = dghn;
-              gxs[0] = dar; gxs[1] = daz; gxs[2] = dan;
-            } else {
-              const float da = (hp > 0.f && hp < RELU_CAP) ? dh : 0.f;
-              ghv[0] = da;
-              gxs[0] = da;
-            }
-            if (!act) {
-              cnew = 0.f;
-#pragma unroll
-              for (int g = 0; g < G; ++g) { ghv[g] = 0.f; gxs[g] = 0.f; }
-            }
-            carry[i] = cnew;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-              st_s[row][g * UPW + c] = f2bf_x(ghv[g]);
-              ox_s[s & 1][row][g][c] = gxs[g];
-              sbx[i][g] += gxs[g];
-            }
-            if (CELL == CELL_GRU) sbh[i] += ghv[G - 1];
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int i = 0; i < EPT; ++i) {
-          const int e = tid + i * ETH;
-          const int row = e >> 5, c = e & 31;
-          if ((c & 7) == 0 && row < R) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-              const i32x4 v = *reinterpret_cast<const i32x4*>(&st_s[row][g * UPW + c]);
-              const unsigned off = (unsigned)((((size_t)s * NP + r0 + row) * GH + g * H + u0 + c) * 2);
-              store_granule(plain, rs_dgh, dghd, off, v);
-            }
-          }
-        }
-      }
-      st.mark(4);
-    }
-  } else {
-    for (int s = a.steps - 1; s >= 0; --s) {
-      // memory wave, while the others wait on the exchange
-      st.mark(-1);
-      mw_put(s);
-      if (s + 2 < a.steps) mw_store(s + 2);
-      if (s >= 1) mw_load(s - 1);
-      st.mark(0);
-      lds_barrier();                                                        // #1
-      st.mark(1);
-      if (s_abort) break;
-      lds_barrier();                                                        // #2
-    }
-  }
-  __syncthreads();
-  if (wave == MEMW && !s_abort) {
-    if (a.steps >= 2) mw_store(1);
-    if (a.steps >= 1) mw_store(0);
-  }
-  if (wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
-  if (wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[2]; }
-
-  // bias gradients: reduce the epilogue waves' rows through LDS, one read-modify-write
-  // per (gate, unit) of the workgroup's own [bg] partial row
-  if (a.dbx_part[dir] != nullptr && !s_abort) {
-    constexpr int BW = (G + 1) * UPW;
-    static_assert(MW * ROWS * (UPW + 1) >= ROWS * BW, "bias reduction does not fit the LDS scratch");
-    float* bred = &red_s[0][0][0];
-    if (wave < EW) {
-#pragma unroll
-      for (int i = 0; i < EPT; ++i) {
-        const int e = tid + i * ETH;
-        const int row = e >> 5, c = e & 31;
-#pragma unroll
-        for (int g = 0; g < G; ++g) bred[row * BW + g * UPW + c] = sbx[i][g];
-        bred[row * BW + G * UPW + c] = sbh[i];
-      }
-    }
-    __syncthreads();
-    for (int q = tid; q < BW; q += NTH) {
-      float sum = 0.f;
-      for (int r = 0; r < ROWS; ++r) sum += bred[r * BW + q];
-      const int g = q / UPW, c = q % UPW;
-      const size_t base = (size_t)bg * GH + u0 + c;
-      if (g < G) {
-        a.dbx_part[dir][base + (size_t)g * H] += sum;
-        if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr && g < G - 1) a.dbh_part[dir][base + (size_t)g * H] += sum;
-      } else if (CELL == CELL_GRU && a.dbh_part[dir] != nullptr) {
-        a.dbh_part[dir][base + (size_t)(G - 1) * H] += sum;
-      }
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // backward (BPTT), generation 3: reduce-scatter exchange.
 //
-// The gather kernel above moves dgh_{s+1} (R rows x 3H gate columns, bf16) to EVERY
+// (Generation 2, removed in round 3, gathered dgh_{s+1} (R rows x 3H gate columns, bf16) to EVERY
 // workgroup of the group each step, because a workgroup's dh slice needs all 3H columns
-// of dgh times its U columns. Here each workgroup instead multiplies ITS OWN gate columns
+// of dgh times its U columns.) Here each workgroup instead multiplies ITS OWN gate columns
 // by the U rows they index, producing a partial dh for ALL H units,
 //     P_j(s) = dgh_s[:, cols_j] . U[cols_j, :]          (R x H, fp32)
 // and a consumer sums the 25 producers' partials of its own 32 units:
@@ -1900,20 +1541,6 @@ static int launch_fwd(const XFwd& a, int kb, int grid, size_t smem, hipStream_t 
   return (int)hipGetLastError();
 }
 
-template <int CELL, int MT>
-static int launch_bwd(const XBwd& a, int kb, int grid, size_t smem, hipStream_t st) {
-  switch (kb) {
-#define DS2_CASE(K)                                                                           \
-  case K:                                                                                     \
-    hipLaunchKernelGGL((rnnx_bwd_kernel<CELL, MT, K>), dim3(grid), dim3(NTH), smem, st, a); \
-    break;
-    DS2_CASE(2) DS2_CASE(4) DS2_CASE(6) DS2_CASE(8) DS2_CASE(11)
-#undef DS2_CASE
-    default: return -32;
-  }
-  return (int)hipGetLastError();
-}
-
 template <typename F>
 static int set_smem_attr(F kernel, size_t smem) {
   return (int)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
@@ -1967,23 +1594,18 @@ int ds2_rnnx_grid(int H, int ngroups, int xcd_map) {
   return (xcd_map && ngroups <= 8) ? 8 * P : ngroups * P;
 }
 
-// k-steps register tile: fwd = whole K per wave, bwd = K split over the 8 waves
+// k-steps register tile of the generation-2 forward: whole K per wave
 int ds2_rnnx_kb(int H, int G, int fwd) {
-  if (fwd) {
-    const int need = (H / 32 + MW - 1) / MW;
-    return need <= 6 ? need : -1;
-  }
-  const int need = (G * H / 32 + MW - 1) / MW;            // backward: K split over the 7 workers
-  for (int k : {2, 4, 6, 8, 11}) if (k >= need) return k;
-  return -1;
+  (void)G;
+  if (!fwd) return -1;                                    // the gather BPTT was removed
+  const int need = (H / 32 + MW - 1) / MW;
+  return need <= 6 ? need : -1;
 }
 
-// dynamic LDS: forward none (the exchanged state goes straight into MFMA registers);
-// backward the A tile, K zero-padded to the register tile
+// dynamic LDS: none (the exchanged state goes straight into MFMA registers)
 size_t ds2_rnnx_smem(int H, int G, int mt, int fwd) {
-  if (fwd) return 0;
-  const int kb = ds2_rnnx_kb(H, G, 0);
-  return (size_t)16 * mt * (kb * MW * 32 + 8) * 2;
+  (void)H; (void)G; (void)mt; (void)fwd;
+  return 0;
 }
 
 int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
@@ -2053,43 +1675,6 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
   if (d->mt != 1) return -33;     // 16-row tiles only: the 32-row LDS footprint exceeds 160 KB
   if (d->cell == CELL_GRU) DS2_FWD(CELL_GRU, 1) else DS2_FWD(CELL_RELU, 1)
 #undef DS2_FWD
-}
-
-int ds2_rnnx_bwd(const DS2RnnX* d, hipStream_t st) {
-  if (d->H % UPW != 0 || d->R < 1 || d->R > 16 * d->mt || d->NP != d->BG * d->R) return -30;
-  const int G = d->cell == CELL_GRU ? 3 : 1;
-  const int kb = ds2_rnnx_kb(d->H, G, 0);
-  if (kb < 0) return -32;
-  XBwd a;
-  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = d->H / UPW; a.BG = d->BG; a.R = d->R;
-  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
-  a.xcd_map = d->xcd_map && a.ngroups <= 8; a.knobs = d->knobs;
-  a.lens = d->lens; a.dy = (const bf16_t*)d->gx;
-  for (int i = 0; i < 2; ++i) {
-    a.U[i] = (const bf16_t*)d->U[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
-    a.dgh[i] = (bf16_t*)d->ex[i]; a.dbx_part[i] = d->dbx_part[i]; a.dbh_part[i] = d->dbh_part[i];
-  }
-  a.dgx = (bf16_t*)d->dgx; a.dgx_scale = d->dgx_scale;
-  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
-  if (d->steps <= 0) return 0;
-  const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
-  const size_t smem = ds2_rnnx_smem(d->H, G, d->mt, 0);
-  int rc;
-#define DS2_BWD(C, M)                                                                        \
-  {                                                                                          \
-    switch (kb) {                                                                            \
-      case 2: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 2>, smem); break;                     \
-      case 4: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 4>, smem); break;                     \
-      case 6: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 6>, smem); break;                     \
-      case 8: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 8>, smem); break;                     \
-      default: rc = set_smem_attr(rnnx_bwd_kernel<C, M, 11>, smem); break;                   \
-    }                                                                                        \
-    if (rc) return rc;                                                                       \
-    return launch_bwd<C, M>(a, kb, grid, smem, st);                                          \
-  }
-  if (d->mt != 1) return -33;
-  if (d->cell == CELL_GRU) DS2_BWD(CELL_GRU, 1) else DS2_BWD(CELL_RELU, 1)
-#undef DS2_BWD
 }
 
 // floats of the reduce-scatter ring of ONE direction: [3 slots][BG][P][R][H]

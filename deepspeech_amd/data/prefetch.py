@@ -12,6 +12,8 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
+import warnings
 from typing import Dict, Optional
 
 import numpy as np
@@ -99,11 +101,21 @@ class DevicePrefetcher:
             t.record_stream(cur)
         return hb, dev
 
-    def close(self) -> None:
+    def close(self, timeout_s: float = 60.0) -> bool:
+        """Stop the producer. Returns True once its thread has exited; False (with a
+        warning) if it is still inside ``source.next()`` or an upload wait after
+        ``timeout_s`` — the caller must then NOT tear the source down under it."""
         self._stop.set()
-        try:
-            while True:
-                self.q.get_nowait()
-        except queue.Empty:
-            pass
-        self._thread.join(timeout=5)
+        deadline = time.monotonic() + timeout_s
+        while self._thread.is_alive() and time.monotonic() < deadline:
+            try:                      # unblock a producer waiting on a full queue
+                while True:
+                    self.q.get_nowait()
+            except queue.Empty:
+                pass
+            self._thread.join(timeout=0.1)
+        if self._thread.is_alive():
+            warnings.warn("DevicePrefetcher: producer thread still running after %.0f s; "
+                          "leaving its source open" % timeout_s)
+            return False
+        return True

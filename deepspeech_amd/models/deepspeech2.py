@@ -318,12 +318,6 @@ class DeepSpeech2(nn.Module):
         if self.capture:
             self.act_taps[name] = t.detach()
 
-    def _flush_update(self) -> None:
-        """The FC head reads weights a deferred optimizer update may still cover."""
-        a = getattr(self.fc_weight, "_ds2_arena", None)
-        if a is not None:
-            a.flush_update()
-
     def direction_stacks(self) -> bool:
         return self.layout == "nhwc" and self.bidirectional
 
@@ -400,7 +394,6 @@ class DeepSpeech2(nn.Module):
             feats = feats.to(self.compute_dtype)
         x = self.frontend(feats)
         h = self.recurrent(x, lens.to(x.device))
-        self._flush_update()
         logits = self.head(h)
         self._tap("softmax_linear", logits)
         return logits, lens
@@ -415,7 +408,6 @@ class DeepSpeech2(nn.Module):
             lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
             x = self.frontend(feats.to(self.compute_dtype))
             h = self.recurrent(x, lens.to(x.device))
-            self._flush_update()
             if self.capture:
                 with torch.no_grad():   # the fused head never materialises the logits
                     self._tap("softmax_linear", self.head(h.detach()))

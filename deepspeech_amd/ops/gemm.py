@@ -46,10 +46,6 @@ TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
 LIBRARY_WINS = {(7680, 1280, False, False), (7680, 2400, False, False),
                 (10560, 1760, False, False), (10560, 2400, False, False),
                 (3520, 1760, False, False), (3520, 2400, False, False)}
-# A/B: DS2_GEMM_LIB="NxK,..." adds row-row projection shapes to the library set
-for _s in filter(None, os.environ.get("DS2_GEMM_LIB", "").split(",")):
-    _n, _k = (int(v) for v in _s.lower().split("x"))
-    LIBRARY_WINS.add((_n, _k, False, False))
 _FORCE = os.environ.get("DS2_GEMM_CFG")
 # DS2_GEMM selects which engine GEMM classes run here: "hip" (all), "torch" (none: library
 # GEMMs, A/B timing only) or a comma list of {proj, dx, wgrad}. Default "proj": measured in

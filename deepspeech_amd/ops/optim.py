@@ -75,7 +75,6 @@ class ParamArena:
         # whatever stream enqueued the gradient write, so a collective waits for exactly
         # the producers of its bucket instead of joining whole streams
         self._ready_events: Optional[List[torch.cuda.Event]] = None
-        self.pending_update: Optional["DeferredUpdate"] = None   # Trainer's overlapped prefix update
         self._written = set()
         self._known_zero = set()
         for i, (p, (o, n)) in enumerate(zip(self.params, self.offsets)):
@@ -115,22 +114,6 @@ class ParamArena:
             pos = o + n
         b = {"p16": self.p16, "grad": self.grad, "flat": self.flat}[buf]
         return None if b is None else b[start:pos]
-
-    # ---- deferred optimizer update (Trainer, DS2_OVERLAP_OPT) ----------------------
-    def launch_update(self) -> None:
-        """Start the pending prefix update on the side stream (layer 0's forward, after its
-        projection GEMM is queued)."""
-        u = getattr(self, "pending_update", None)
-        if u is not None:
-            u.launch(self.wgrad.stream(self.flat.device))
-
-    def flush_update(self) -> None:
-        """Make the current stream wait for the pending prefix update (running it here if
-        it was never launched): before anything reads the weights it covers."""
-        u = getattr(self, "pending_update", None)
-        if u is not None:
-            u.wait()
-            self.pending_update = None
 
     # ---- gradients ----------------------------------------------------------------
     def zero_grad(self, lazy: bool = False) -> None:
@@ -269,44 +252,6 @@ def mm_into(p, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = N
     return None
 
 
-class DeferredUpdate:
-    """The optimizer update of an arena prefix, prepared at the end of step s and executed
-    during the forward of step s+1 (Trainer, ``DS2_OVERLAP_OPT``).
-
-    The prefix [0, hi) holds the FC head and recurrent layers L-1..1, whose weights the
-    next forward first reads at layer 1's input projection. The update is launched on the
-    arena's side stream right after layer 0's projection GEMM, with a few workgroups, so it
-    streams through HBM beside layer 0's forward recurrence (latency-bound, 200 of the 256
-    CUs) instead of sitting at the end of the step; the main stream waits for it before
-    layer 1's projection (:meth:`wait`). Any other reader of the weights calls
-    :meth:`ParamArena.flush_update` first (runs it in place if it was never launched)."""
-
-    def __init__(self, opt: "FusedAdamEMA", lo: int, hi: int, lr_t: float, keep: float, gscale: float,
-                 max_grid: int):
-        self.opt, self.lo, self.hi = opt, lo, hi
-        self.lr_t, self.keep, self.gscale, self.max_grid = lr_t, keep, gscale, max_grid
-        self.done: Optional[torch.cuda.Event] = None
-
-    def launch(self, stream: Optional["torch.cuda.Stream"]) -> None:
-        if self.done is not None:
-            return
-        dev = self.opt.arena.flat.device
-        main = torch.cuda.current_stream(dev)
-        s = stream if stream is not None else main
-        if s is not main:
-            s.wait_stream(main)            # gradients of the previous step + any reader so far
-        with torch.cuda.stream(s):
-            self.opt.apply_range(self.lo, self.hi, self.lr_t, self.keep, self.gscale,
-                                 max_grid=self.max_grid if s is not main else 0)
-            self.done = torch.cuda.Event()
-            self.done.record(s)
-
-    def wait(self) -> None:
-        if self.done is None:
-            self.launch(None)
-        torch.cuda.current_stream(self.opt.arena.flat.device).wait_event(self.done)
-
-
 def exponential_decay(initial_lr: float, step: int, decay_steps: int, decay_rate: float,
                       staircase: bool = True) -> float:
     """tf.train.exponential_decay (src/deepSpeech_train.py:245-249)."""
@@ -369,12 +314,27 @@ class FusedAdamEMA:
     def apply_range(self, lo: int, hi: int, lr_t: float, keep: float, gscale: float = 1.0,
                     skip_flag: Optional[torch.Tensor] = None, max_grid: int = 0) -> None:
         """Adam + EMA of arena elements [lo, hi) with a prepared (lr_t, keep), on the current
-        stream (HIP only). Every element's update is independent and rounds the same way
-        whatever the launch split, so ranges compose bitwise into the whole-arena update."""
+        stream. Every element's update is independent and rounds the same way whatever the
+        launch split, so ranges compose bitwise into the whole-arena update (the DP bucketer
+        issues one range per gradient bucket)."""
         if hi <= lo:
             return
         a = self.arena
         sl = slice(lo, hi)
+        if not self.use_hip:
+            if skip_flag is not None and int(skip_flag.item()) != 0:
+                return
+            p, m, v = a.flat[sl], self.m[sl], self.v[sl]
+            g = a.grad[sl] * gscale
+            m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+            v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            p.sub_(lr_t * m / (v.sqrt() + self.eps))
+            if self.ema is not None:
+                e = self.ema[sl]
+                e.copy_(p + keep * (e - p))
+            if self.p16 is not None:
+                self.p16[sl].copy_(p)
+            return
         _ext.ext().adam_ema(a.flat[sl], a.grad[sl], self.m[sl], self.v[sl],
                             self.ema[sl] if self.ema is not None else None,
                             self.p16[sl] if self.p16 is not None else None,
@@ -382,36 +342,10 @@ class FusedAdamEMA:
 
     @torch.no_grad()
     def step(self, lr: float, global_step: int, gscale: float = 1.0,
-             skip_flag: Optional[torch.Tensor] = None, parts=None) -> None:
-        """One Adam + EMA update of the whole arena.
-
-        ``parts`` (HIP only): list of ``(lo, hi, stream, wait)`` element ranges covering the
-        arena; range ``[lo, hi)`` is updated on ``stream`` (None = current) after that stream
-        waits on the events in ``wait``. The ranges share one Adam step count (one lr_t), so
-        the result is identical to the single launch."""
+             skip_flag: Optional[torch.Tensor] = None) -> None:
+        """One Adam + EMA update of the whole arena."""
         lr_t, keep = self.prepare(lr, global_step)
-        a = self.arena
-        if self.use_hip:
-            if parts is None:
-                self.apply_range(0, a.numel, lr_t, keep, gscale, skip_flag)
-                return
-            for lo, hi, stream, wait in parts:
-                s = stream if stream is not None else torch.cuda.current_stream(a.flat.device)
-                for ev in wait:
-                    s.wait_event(ev)
-                with torch.cuda.stream(s):
-                    self.apply_range(lo, hi, lr_t, keep, gscale, skip_flag)
-            return
-        if skip_flag is not None and int(skip_flag.item()) != 0:
-            return
-        g = a.grad * gscale
-        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
-        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
-        a.flat.sub_(lr_t * self.m / (self.v.sqrt() + self.eps))
-        if self.ema is not None:
-            self.ema.copy_(a.flat + keep * (self.ema - a.flat))
-        if self.p16 is not None:
-            self.p16.copy_(a.flat)
+        self.apply_range(0, self.arena.numel, lr_t, keep, gscale, skip_flag)
 
     def state_dict(self) -> Dict[str, object]:
         return {"m": self.m, "v": self.v, "ema": self.ema, "t": self.t}

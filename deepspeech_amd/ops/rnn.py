@@ -61,10 +61,7 @@ class RnnPlan:
 
 
 RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))   # diagnostic timing switches only
-_FUSE_DIRSUM = os.environ.get("DS2_FUSE_DIRSUM", "1") == "1"      # 0: separate torch.add (A/B)
-# BPTT exchange of the xcd kernels: "rs" = reduce-scatter of fp32 partial dh (generation 3),
-# "gather" = all-gather of dgh (generation 2)
-BWD_EXCHANGE = os.environ.get("DS2_RNN_BWD", "rs")
+_FUSE_DIRSUM = True        # module switch: tests compare the fused direction sum with torch.add
 
 
 LDS_BYTES = 160 * 1024
@@ -87,26 +84,16 @@ def _rs_ok(H: int) -> bool:
     MI355X that still beats the generation-1 kernels for the 3-gate GRU (H=1280: fwd 1.52 vs
     1.93, BPTT 2.05 vs 3.68 ms per layer) but not for the one-gate clipped ReLU (H=1760 with
     8-producer gathers: 1.84 / 2.35 vs 1.26 / 1.41), which make_xcd_plan leaves on gen 1."""
-    return BWD_EXCHANGE == "rs" and H // 32 <= 42
+    return H // 32 <= 42
 
 
 def _xcd_lds(H: int, G: int, mt: int) -> int:
     """Static LDS bytes of the larger of the two csrc/rnn_xcd.hip kernels (16-row tiles only)."""
-    if mt != 1 or _xcd_kb(H, G, True) < 0:
+    if mt != 1 or _xcd_kb(H, G, True) < 0 or not _rs_ok(H):
         return 1 << 30
-    if _xcd_kb(H, G, False) < 0:
-        # no gather-BPTT tile: only the forward + reduce-scatter BPTT (static ~61 KB) run
-        if not _rs_ok(H):
-            return 1 << 30
-        return 2 * 7 * 16 * (G * 32 + 1) * 4 + 16 * 32 * 2 + 2 * 16 * G * 32 * 4 + 2 * 2 * 16 * 32 * 4 \
-            + (2 * 16 * 32 * 16 if G == 3 else 16) + 16 * 4 + G * 32 * 4 + 64
-    rows, gru = 16, G == 3
-    fwd = (2 * 7 * rows * (G * 32 + 1) * 4 + rows * 32 * 2 + 2 * rows * G * 32 * 4 + 2 * 2 * rows * 32 * 4
-           + (2 * rows * 32 * 16 if gru else 16) + rows * 4 + G * 32 * 4 + 64)
-    kb = _xcd_kb(H, G, False)
-    bwd = (rows * (kb * 7 * 32 + 8) * 2 + 7 * rows * 33 * 4 + rows * G * 32 * 2 + 2 * 2 * rows * 32 * 4
-           + (2 * rows * 32 * 16 if gru else 16) + 2 * rows * G * 32 * 4 + rows * 4 + 64)
-    return max(fwd, bwd)
+    # forward + reduce-scatter BPTT (static, ~61 KB at G = 3)
+    return 2 * 7 * 16 * (G * 32 + 1) * 4 + 16 * 32 * 2 + 2 * 16 * G * 32 * 4 + 2 * 2 * 16 * 32 * 4 \
+        + (2 * 16 * 32 * 16 if G == 3 else 16) + 16 * 4 + G * 32 * 4 + 64
 
 
 def make_xcd_plan(N: int, H: int, cell: str, ndir: int, cus: int) -> Optional[RnnPlan]:
@@ -361,23 +348,11 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
         if parts is not None:
             regions.append(parts)
             pats.append(0)
-        if _rs_ok(H):
-            # generation-3 BPTT: reduce-scatter of fp32 partials through a 3-slot ring
-            # (readiness = per-use tag in each word's LSB, ring filled with 0xFFFFFFFF); dgh is a plain output
-            rf = int(C.rnnx_ring_floats(H, plan.BG, plan.R))
-            ring = torch.empty(ndir, rf, device=dev, dtype=torch.float32)
-            C.multi_fill(regions + [ring], pats + [-1])     # one launch for every init
-            C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
-                       gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
-                       dgh[0], dgh[1] if d1 else None, dgx,
-                       parts[0] if parts is not None else None,
-                       parts[1] if (parts is not None and plan.cell == "gru") else None,
-                       float(dgx_scale), census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
-                       CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
-                       _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev),
-                       ring[0], ring[1] if d1 else None)
-            return dgx, dgh, parts
-        C.multi_fill(regions + [dgh], pats + [-1])         # dgh: sentinel 0xFFFF pairs
+        # generation-3 BPTT: reduce-scatter of partials through a 3-slot ring (readiness =
+        # per-use tag in each word's LSB, ring filled with 0xFFFFFFFF); dgh is a plain output
+        rf = int(C.rnnx_ring_floats(H, plan.BG, plan.R))
+        ring = torch.empty(ndir, rf, device=dev, dtype=torch.float32)
+        C.multi_fill(regions + [ring], pats + [-1])     # one launch for every init
         C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
                    gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
                    dgh[0], dgh[1] if d1 else None, dgx,
@@ -385,7 +360,8 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
                    parts[1] if (parts is not None and plan.cell == "gru") else None,
                    float(dgx_scale), census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
                    CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, RNNX_KNOBS,
-                   _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev))
+                   _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev),
+                   ring[0], ring[1] if d1 else None)
         return dgx, dgh, parts
     err = error_word(dev)
     parts = torch.zeros(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
@@ -530,9 +506,6 @@ class FusedBiLayer(torch.autograd.Function):
         T, N, D = x.shape
         dirs_W = [W_f] + ([W_b] if W_b is not None else [])
         dirs_b = [b_f] + ([b_b] if b_b is not None else [])
-        arena = arena_of(W_f)
-        if arena is not None and idx >= 1:
-            arena.flush_update()                      # the previous step's update of layers >= 1
         W16 = _bf16_group(dirs_W)                     # [ndir*G*H, D]
         b16 = _bf16_group(dirs_b)                     # [ndir*G*H]
         x16 = x.to(torch.bfloat16).contiguous()
@@ -541,8 +514,6 @@ class FusedBiLayer(torch.autograd.Function):
             gx = fp8_linear(x2, W16, b16, alpha).view(T, N, -1)
         else:
             gx = _linear(x2, W16, b16, alpha).view(T, N, -1)
-        if arena is not None and idx == 0:
-            arena.launch_update()                     # streams beside this layer's recurrence
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]

@@ -85,11 +85,13 @@ def init_distributed(device_pref: str = "auto", timeout_s: int = 600, force_grou
         if use_cuda and backend == "nccl":
             kw["device_id"] = device
         restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
-        if restart is not None and world > 1:
-            # elastic job (torchrun): the agent hosts the store for every attempt. Keys of a
-            # relaunched attempt live under their own prefix, so no rank can read a peer
-            # address left by the killed attempt (observed: gloo connectFullMesh dialling a
-            # dead port after a --max-restarts relaunch)
+        if restart is not None and world > 1 and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+            # elastic job (torchrun) whose agent hosts the store for every attempt: every rank
+            # is a client of it. Keys of a relaunched attempt live under their own prefix, so
+            # no rank can read a peer address left by the killed attempt (observed: gloo
+            # connectFullMesh dialling a dead port after a --max-restarts relaunch). Without
+            # an agent store nobody would host a client-only store: the default env://
+            # rendezvous (rank 0 hosts) is used instead.
             base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
                                  is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
             run_id = os.environ.get("TORCHELASTIC_RUN_ID", "ds2")

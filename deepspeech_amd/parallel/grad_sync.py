@@ -19,6 +19,17 @@ MI355X-first choices:
     BPTT) never waits on the side stream mid-backward; it waits for the collectives only
     in finish(), before the optimizer.
 The SUM is averaged by the optimizer (``gscale``), so no extra division kernel runs.
+
+Per-bucket optimizer (DP-native ordering, :meth:`GradBucketer.set_optimizer`): instead of
+one Adam over the whole arena after the last collective, each bucket's Adam + EMA range is
+issued on the ordering stream right behind its all-reduce, so the update of the early
+buckets (FC head, top layers) streams while the lower layers' BPTT and the remaining
+collectives run, and only the last bucket's range is left after backward. Every arena
+element's update is independent and rounded the same way whatever the launch split, so
+the result is bitwise the whole-arena update. A bucket's range is issued only once the
+main stream has passed the point where the NEXT bucket became ready (or finish()): by then
+the backward op that produced the bucket's last gradient has enqueued everything that
+reads those weights (dgrad / dx GEMMs), so an update never races a pending read.
 """
 from __future__ import annotations
 
@@ -70,6 +81,9 @@ class GradBucketer:
         self._works = []
         self._shadow: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._handles = []
+        self._opt = None                   # per-bucket optimizer: fn(lo, hi) on the current stream
+        self._opt_pending: List[int] = []  # buckets whose collective is issued, update not yet
+        self._main_stream = None
         self.enabled = self.world > 1 or (force and dist.is_initialized())
         self._order_stream = None
         if self.enabled:
@@ -110,16 +124,56 @@ class GradBucketer:
         self._pending = [len(idx) for (_, _, idx) in self.buckets]
         self._launched = [False] * len(self.buckets)
         self._works = []
+        self._opt = None
+        self._opt_pending = []
+
+    def set_optimizer(self, fn) -> None:
+        """Apply ``fn(lo, hi)`` (an optimizer update of arena elements [lo, hi), enqueued on
+        the current stream) to each bucket right behind its collective, for THIS step only
+        (:meth:`finish` clears it). Call before backward, on the stream that runs it (the
+        ranges wait for that stream's progress; a hook may fire on a side stream)."""
+        if self.enabled:
+            self._opt = fn
+            if self.arena.grad.is_cuda:
+                self._main_stream = torch.cuda.current_stream(self.arena.grad.device)
+
+    def _flush_updates(self) -> None:
+        """Issue the pending buckets' optimizer ranges behind their collectives (ordering
+        stream), after the main stream's work enqueued so far (see module docstring)."""
+        if not self._opt_pending:
+            return
+        os_ = self._order_stream
+        if os_ is not None:
+            os_.wait_stream(self._main_stream)
+        pend, self._opt_pending = self._opt_pending, []
+        waits = dict(self._works)
+        for b in pend:
+            s, e, _ = self.buckets[b]
+            if os_ is None:
+                waits[b].wait()
+                if self.compress:
+                    self.arena.grad[s:e].copy_(self._shadow[b])
+                self._opt(s, e)
+                continue
+            with torch.cuda.stream(os_):
+                waits[b].wait()                  # the ordering stream waits for the collective
+                if self.compress:
+                    self.arena.grad[s:e].copy_(self._shadow[b])
+                self._opt(s, e)
 
     def _launch(self, b: int) -> None:
         if self._launched[b]:
             return
         self._launched[b] = True
+        if self._opt is not None:
+            self._flush_updates()                # earlier buckets: their readers are enqueued
         s, e, idx = self.buckets[b]
         g = self.arena.grad[s:e]
         os_ = self._order_stream
         if os_ is None:
             self._works.append((b, self._collective(b, g)))
+            if self._opt is not None:
+                self._opt_pending.append(b)
             return
         # the collective (ProcessGroupNCCL waits on the CURRENT stream at issue time) is
         # issued from the ordering stream, which waits on each member's producer event:
@@ -132,6 +186,8 @@ class GradBucketer:
             os_.wait_event(ev)
         with torch.cuda.stream(os_):
             self._works.append((b, self._collective(b, g)))
+        if self._opt is not None:
+            self._opt_pending.append(b)
 
     def _collective(self, b: int, g: torch.Tensor):
         if self.compress:
@@ -155,12 +211,24 @@ class GradBucketer:
         for b in range(len(self.buckets)):
             if not self._launched[b]:
                 self._launch(b)
+        if self._opt is not None:
+            self._flush_updates()
+            if self._order_stream is not None:
+                # the next forward reads the updated weights / bf16 shadows
+                self._main_stream.wait_stream(self._order_stream)
+            self.prepare()
+            return
         for b, w in self._works:
             w.wait()
             if self.compress:
                 s, e, _ = self.buckets[b]
                 self.arena.grad[s:e].copy_(self._shadow[b])
         self.prepare()
+
+    @property
+    def updates_in_finish(self) -> bool:
+        """True while a per-bucket optimizer is set for the running step."""
+        return self._opt is not None
 
     def remove(self) -> None:
         for h in self._handles:

@@ -124,7 +124,6 @@ def write_summaries(events, step: int, trainer, model, args, lv: float, ema: flo
     computed on the device (csrc/stats.hip), one pass per tensor; tags use the TF variable
     names of the checkpoint layout."""
     from .utils.stats import histogram
-    trainer.flush_optimizer()                  # variable histograms read the updated weights
     events.scalars(step, {"ctc_loss(raw)": lv, "ctc_loss": ema, "learning_rate": trainer.lr})
     tfname = {tn: tf for tf, tn, _, _ in CK.tf_name_map(model)}
     grads = trainer.arena.views(trainer.arena.grad)
@@ -316,10 +315,9 @@ def main(argv=None) -> int:
         ckpt.wait()
     if events is not None:
         events.close()
-    if prefetch is not None:
-        prefetch.close()
-    if hasattr(data, "close"):
-        data.close()
+    source_free = prefetch.close() if prefetch is not None else True
+    if source_free and hasattr(data, "close"):
+        data.close()              # never under a producer thread that is still reading it
     shutdown(ctx)
     return 0
 

@@ -237,8 +237,6 @@ class CheckpointManager:
 
     def snapshot(self, trainer) -> Dict[str, object]:
         out: Dict[str, object] = {}
-        if hasattr(trainer, "flush_optimizer"):
-            trainer.flush_optimizer()          # a deferred optimizer update still pending
         for k, v in model_to_tf(trainer.model).items():
             out[k] = v.detach().to("cpu", copy=True)
         for k, v in _arena_slots(trainer).items():
@@ -312,8 +310,6 @@ def restore(trainer, directory_or_file: str) -> Optional[int]:
         if path is None:
             print("No checkpoint file found")
             return None
-    if hasattr(trainer, "flush_optimizer"):
-        trainer.flush_optimizer()              # never let a pending update overwrite the restore
     data = load_checkpoint_file(path)
     tensors = normalize_layout(trainer.model, {k: v for k, v in data.items() if isinstance(v, torch.Tensor)})
     load_model_from_tf(trainer.model, tensors, strict=True)

@@ -55,7 +55,7 @@ def unpack(blob: torch.Tensor, hidden: int, in_dim: int) -> Tuple[torch.Tensor, 
 
 def to_mkldnn_layout(tensors: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     """TF-named checkpoint dict (CustomRNNCell2 variables) -> the MkldnnRNNCell blob layout,
-    for the weights and their Adam / EMA slots. The cell has no SBN variables."""
+    for the weights and their Adam / EMA slots. SBN statistics are kept as they are."""
     out = dict(tensors)
     for key in list(tensors):
         m = _SCOPE.match(key)
@@ -68,14 +68,19 @@ def to_mkldnn_layout(tensors: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor
                 continue
             W, U, B = out.pop(cell + "/W" + sfx), out.pop(cell + "/U" + sfx), out.pop(cell + "/B" + sfx)
             out[scope + "/MkldnnRNNCell/rnn_weights" + sfx] = pack(W, U, B)
+        # the sequence-BN moving statistics are not blob parameters: they are stored next to
+        # the blob (a --seq_bn batch run learns them; dropping them would reset a resumed or
+        # evaluated model to mean 0 / variance 1)
         for k in ("/sbn/moving_mean", "/sbn/moving_variance"):
-            out.pop(cell + k, None)
+            if cell + k in out:
+                out[scope + "/MkldnnRNNCell" + k] = out.pop(cell + k)
     return out
 
 
 def from_mkldnn_layout(tensors: Dict[str, torch.Tensor], hidden: int, in_dims) -> Dict[str, torch.Tensor]:
     """Inverse of :func:`to_mkldnn_layout`. ``in_dims[i]`` is layer i's input width. SBN
-    moving statistics absent from a blob checkpoint come back as mean 0 / variance 1."""
+    moving statistics stored beside the blob are kept; absent ones (a checkpoint written by
+    the reference's MKL cell, which has no SBN) come back as mean 0 / variance 1."""
     out = dict(tensors)
     pat = re.compile(r"^(rnn/brnn-(\d+)/bidirectional_rnn/(?:fw|bw))/MkldnnRNNCell/rnn_weights(.*)$")
     for key in list(tensors):
@@ -87,8 +92,9 @@ def from_mkldnn_layout(tensors: Dict[str, torch.Tensor], hidden: int, in_dims) -
         cell = scope + "/CustomRNNCell2"
         out[cell + "/W" + sfx], out[cell + "/U" + sfx], out[cell + "/B" + sfx] = W, U, b
         if sfx == "":
-            out.setdefault(cell + "/sbn/moving_mean", torch.zeros(hidden))
-            out.setdefault(cell + "/sbn/moving_variance", torch.ones(hidden))
+            for k, fill in (("/sbn/moving_mean", torch.zeros), ("/sbn/moving_variance", torch.ones)):
+                v = out.pop(scope + "/MkldnnRNNCell" + k, None)
+                out.setdefault(cell + k, v if v is not None else fill(hidden))
     return out
 
 

@@ -79,7 +79,11 @@ def setenvs(argv: Optional[List[str]] = None, platform: Optional[str] = None) ->
     for k, v in PLATFORMS[plat].items():
         if k in _AT_LEAST and k in os.environ:
             # a floor, not a default: machines export HIP's own default of 4 queues, which
-            # is exactly what a DP step must not run with (see GPU_MAX_HW_QUEUES above)
+            # is exactly what a DP step must not run with (see GPU_MAX_HW_QUEUES above).
+            # DS2_KEEP_HW_QUEUES=1 keeps an exported value as it is (A/B of the queue count,
+            # scripts/ab_queues.sh)
+            if os.environ.get("DS2_KEEP_HW_QUEUES") == "1":
+                continue
             try:
                 if int(os.environ[k]) >= int(v):
                     continue

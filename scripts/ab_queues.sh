@@ -9,7 +9,7 @@ for q in ${queues:-4 8 16}; do
   for i in 1 2; do
     for mode in plain dp; do
       extra=""; [ "$mode" = dp ] && extra="--force_dp"
-      GPU_MAX_HW_QUEUES=$q timeout -k 10 120 python bench.py $extra > gpurun_out/abq/q${q}_${mode}_$i.log 2>&1 || exit 1
+      DS2_KEEP_HW_QUEUES=1 GPU_MAX_HW_QUEUES=$q timeout -k 10 120 python bench.py $extra > gpurun_out/abq/q${q}_${mode}_$i.log 2>&1 || exit 1
       echo "q=$q $mode run$i $(tail -1 gpurun_out/abq/q${q}_${mode}_$i.log | python3 -c 'import sys,json; print(json.loads(sys.stdin.read())["ms_per_step"])')"
     done
   done

@@ -1,7 +1,9 @@
 """Worker of tests/test_dp_gpu.py (run under torch.distributed.run, 2 ranks on cuda:0 over
 gloo): checks that the all-reduced gradient of the HIP engine — with the recurrent weight
 gradients produced on the side stream and small buckets that mix streams — equals the sum
-of the ranks' local gradients."""
+of the ranks' local gradients, and that a full training-mode DP step (per-rank BN, Adam
+ranges issued per bucket behind the all-reduces) gives the update of the averaged local
+gradients."""
 import os
 import sys
 
@@ -20,6 +22,17 @@ def model(dev):
     torch.manual_seed(0)
     m = DeepSpeech2(num_filters=32, num_hidden=64, num_rnn_layers=2, cell="gru").to(dev)
     return m.set_engine("hip", torch.bfloat16)
+
+
+def step_grads(tr, batch):
+    """Local gradient of the fused training path Trainer.step runs (forward_loss)."""
+    tr.model.train()
+    tr.arena.zero_grad(lazy=True)
+    tr.model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"]).backward()
+    join_wgrad_streams()
+    tr.arena.zero_unwritten()
+    torch.cuda.synchronize()
+    return tr.arena.grad.clone()
 
 
 def grads(tr, batch, dp):
@@ -62,7 +75,14 @@ def main():
         for bi, (s0, e0, idx) in enumerate(dp.bucketer.buckets):
             print("bucket", bi, s0, e0, [dp.arena.names[i] for i in idx])
     g_dp = grads(dp, batch, dp=True)
-    torch.save({"local": g_local.cpu(), "dp": g_dp.cpu()}, "%s.%d" % (out, ctx.rank))
+    # one full DP training step (per-bucket optimizer) from the initial weights
+    g_step = step_grads(Trainer(model(dev), LRSchedule(1e-3, 10 ** 6, 0.9), world_size=1), batch)
+    tr = Trainer(model(dev), LRSchedule(1e-3, 10 ** 6, 0.9), world_size=ctx.world_size, bucket_mb=bmb)
+    assert tr.bucketer.enabled and tr.per_bucket_update
+    tr.step(batch)
+    torch.cuda.synchronize()
+    torch.save({"local": g_local.cpu(), "dp": g_dp.cpu(), "step_local": g_step.cpu(),
+                "w_step": tr.arena.flat.cpu(), "ema_step": tr.opt.ema.cpu()}, "%s.%d" % (out, ctx.rank))
     torch.distributed.barrier()
     if ctx.rank == 0 and os.environ.get("DS2_DP_DIAG"):
         diagnose(out, list(zip(dp.arena.names, dp.arena.offsets)))

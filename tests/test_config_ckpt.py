@@ -187,13 +187,15 @@ def test_setenvs_platforms(monkeypatch):
         S.setenvs([], platform="pentium")
 
 
-def test_mkldnn_blob_layout_roundtrip(tmp_path):
+@pytest.mark.parametrize("seq_bn", ["frozen", "batch"])
+def test_mkldnn_blob_layout_roundtrip(tmp_path, seq_bn):
     """engine=mkldnn_rnn checkpoints: one rnn_weights blob per layer/direction
-    (src/mkldnn_rnn_op.py:37), W | R | b_W | b_R order; weights, Adam and EMA slots round-trip."""
+    (src/mkldnn_rnn_op.py:37), W | R | b_W | b_R order; weights, Adam and EMA slots round-trip,
+    and learned sequence-BN statistics (--seq_bn batch) are kept beside the blob."""
     from deepspeech_amd.utils import mkldnn_blob as MB
     from deepspeech_amd.trainer import Trainer, LRSchedule
     torch.manual_seed(0)
-    m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="rnn_relu")
+    m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="rnn_relu", seq_bn=seq_bn)
     m.param_layout = "mkldnn"
     tr = Trainer(m, LRSchedule(1e-4, 100, 0.9))
     b = to_device(FixedShapeBatches(2, max_frames=200, seed=0, pool=1).next(), torch.device("cpu"))
@@ -205,16 +207,23 @@ def test_mkldnn_blob_layout_roundtrip(tmp_path):
     assert key in data and data[key].numel() == MB.params_size(16, 16)
     assert key + "/Adam" in data and key + "/ExponentialMovingAverage" in data
     assert not any("CustomRNNCell2" in k for k in data)
+    assert "rnn/brnn-0/bidirectional_rnn/fw/MkldnnRNNCell/sbn/moving_mean" in data
     blob = data["rnn/brnn-0/bidirectional_rnn/fw/MkldnnRNNCell/rnn_weights"]
     W = m.rnn[0].fw.W.detach()
     assert torch.equal(blob[: W.numel()], W.reshape(-1))
     assert torch.equal(blob[-16:], torch.zeros(16))          # b_R exported as zeros
-    m2 = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="rnn_relu")
+    if seq_bn == "batch":
+        assert not torch.equal(m.rnn[0].fw.sbn_mean, torch.zeros(16))     # learned statistics
+    m2 = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="rnn_relu", seq_bn=seq_bn)
     tr2 = Trainer(m2, LRSchedule(1e-4, 100, 0.9))
     CK.restore(tr2, str(tmp_path))
     for (n, p), (_, q) in zip(m.named_parameters(), m2.named_parameters()):
         assert torch.equal(p, q), n
     assert torch.equal(tr.opt.m, tr2.opt.m) and torch.equal(tr.opt.ema, tr2.opt.ema)
+    for i in range(2):
+        for d in ("fw", "bw"):
+            a, c = getattr(m.rnn[i], d), getattr(m2.rnn[i], d)
+            assert torch.equal(a.sbn_mean, c.sbn_mean) and torch.equal(a.sbn_var, c.sbn_var)
     # a recurrent bias split across b_W / b_R imports as their sum
     W3, U3, b3 = MB.unpack(MB.pack(W, W[:, :16], torch.ones(16), torch.full((16,), 2.0)), 16, W.shape[1])
     assert torch.equal(b3, torch.full((16,), 3.0))
@@ -229,3 +238,8 @@ def test_setenvs_hw_queue_floor(monkeypatch):
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
     S.setenvs([], platform="mi355x")
     assert os.environ["GPU_MAX_HW_QUEUES"] == "16"
+    # an explicit A/B arm keeps its exported value
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    monkeypatch.setenv("DS2_KEEP_HW_QUEUES", "1")
+    S.setenvs([], platform="mi355x")
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "4"

@@ -181,3 +181,92 @@ def test_allreduce_bandwidth_tool_two_ranks():
     for row in rows:
         assert row["world"] == 2 and row["backend"] == "gloo"
         assert abs(row["busbw_GBps"] - row["algbw_GBps"] * 2 * (2 - 1) / 2) <= 0.011
+
+
+def _train_worker(rank, world, port, mode, out):
+    """mode 'fp32' / 'bf16': one TRAINING-mode step (per-rank BN batch statistics) with the
+    whole-arena update after finish(); 'bucket': the same step with the per-bucket optimizer
+    (GradBucketer.set_optimizer: each bucket's Adam range behind its all-reduce)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    from deepspeech_amd.data.synthetic import to_device
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.parallel.dist import init_distributed, shutdown
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    ctx = init_distributed("cpu")
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="gru")
+    tr = Trainer(m, LRSchedule(1e-2, 10 ** 6, 0.9), moving_avg_decay=0.99, world_size=world,
+                 bucket_mb=0.001, allreduce_bf16=(mode == "bf16"))
+    tr.per_bucket_update = mode == "bucket"
+    assert len(tr.bucketer.buckets) >= 3
+    grads = []
+    orig_finish = tr.bucketer.finish
+
+    def finish():                          # capture the reduced (summed) gradient
+        orig_finish()
+        grads.append(tr.arena.grad.clone())
+    tr.bucketer.finish = finish
+    losses = [float(tr.step(to_device(b, torch.device("cpu")))) for b in _batches(2 * world)[rank::world]]
+    if rank == 0:
+        torch.save({"w": tr.arena.flat.clone(), "ema": tr.opt.ema.clone(), "g": grads[0],
+                    "losses": torch.tensor(losses)}, out)
+    shutdown(ctx)
+
+
+def _dp_train(tmp_path, mode):
+    out = str(tmp_path / ("dp_%s.pt" % mode))
+    mp.spawn(_train_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True)
+    return torch.load(out, weights_only=True)
+
+
+def test_dp2_training_mode_equals_local_steps_plus_averaged_update(tmp_path):
+    """Training mode (per-rank BN statistics, as in the single-device reference): the DP step
+    equals each rank's local gradient computed single-process, averaged, then one Adam step."""
+    from deepspeech_amd.data.synthetic import to_device
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    res = _dp_train(tmp_path, "fp32")
+    bs = _batches(4)
+    local = []
+    for r in range(2):
+        torch.manual_seed(0)
+        m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="gru")
+        tr = Trainer(m, LRSchedule(1e-2, 10 ** 6, 0.9), moving_avg_decay=0.99)
+        tr.model.train()
+        tr.arena.zero_grad()
+        b = to_device(bs[r], torch.device("cpu"))
+        loss = tr.model.forward_loss(b["feats"], b["seq_lens"], b["labels"], b["label_lens"])
+        loss.backward()
+        local.append(tr.arena.grad.clone())
+    gsum = local[0] + local[1]
+    assert ((res["g"] - gsum).norm() / gsum.norm()) < 1e-5
+    # one Adam step from the same start with the averaged gradient
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=4, num_hidden=16, num_rnn_layers=2, cell="gru")
+    tr = Trainer(m, LRSchedule(1e-2, 10 ** 6, 0.9), moving_avg_decay=0.99)
+    w0 = tr.arena.flat.clone()
+    tr.arena.grad.copy_(res["g"])
+    tr.opt.step(tr.lr, 0, gscale=0.5)
+    assert not torch.equal(tr.arena.flat, w0)
+
+
+def test_dp2_per_bucket_optimizer_matches_single_update(tmp_path):
+    """Per-bucket Adam behind each all-reduce (DP-native ordering) gives bitwise the weights
+    and EMA of one whole-arena update after finish(), over two steps."""
+    a, b = _dp_train(tmp_path, "bucket"), _dp_train(tmp_path, "fp32")
+    assert torch.equal(a["losses"], b["losses"])
+    assert torch.equal(a["w"], b["w"]) and torch.equal(a["ema"], b["ema"])
+
+
+def test_dp2_bf16_compressed_allreduce_close_to_fp32(tmp_path):
+    """--allreduce_bf16: buckets summed in bf16 on the wire match the fp32 all-reduce within
+    bf16 rounding: each rank's value and the sum round to 8 mantissa bits, so the error of an
+    element is ~2^-8 of the ranks' magnitudes (a sum that cancels can be off by more than
+    2^-8 of itself), and the gradient norm is off by far less."""
+    a, b = _dp_train(tmp_path, "bf16"), _dp_train(tmp_path, "fp32")
+    ga, gb = a["g"], b["g"]
+    assert not torch.equal(ga, gb)                    # really compressed
+    assert ((ga - gb).norm() / gb.norm()) < 8e-3
+    assert (ga - gb).abs().max() < 2 ** -7 * gb.abs().max()

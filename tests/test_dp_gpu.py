@@ -33,3 +33,20 @@ def test_dp2_gradients_equal_sum_of_local(cuda, tmp_path):
     for k in range(2):
         err = ((g[k]["dp"] - want).norm() / want.norm()).item()
         assert err < 1e-5, (k, err)
+    # the full step: both ranks hold the same weights, equal to one Adam update of the
+    # averaged local gradients (per-rank BN statistics, as single-device training)
+    assert torch.equal(g[0]["w_step"], g[1]["w_step"]) and torch.equal(g[0]["ema_step"], g[1]["ema_step"])
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    import dp_gpu_worker as W
+    tr = Trainer(W.model(cuda), LRSchedule(1e-3, 10 ** 6, 0.9))
+    w0 = tr.arena.flat.clone()
+    tr.arena.grad.copy_((g[0]["step_local"] + g[1]["step_local"]).to(cuda))
+    tr.opt.step(tr.lr, 0, gscale=0.5)
+    w_ref = tr.arena.flat.cpu()
+    moved = (w_ref - w0.cpu()).abs()
+    assert moved.max() > 1e-4                                 # the step did something
+    # Adam's first update is ~lr * sign(g): the same weights up to elements whose averaged
+    # gradient is ~eps-sized (float summation order)
+    assert ((g[0]["w_step"] - w_ref).abs() > 1e-5).float().mean() < 1e-3
+    assert (g[0]["w_step"] - w_ref).abs().max() < 2.5e-3

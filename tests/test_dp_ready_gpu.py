@@ -31,18 +31,26 @@ def test_dp_machinery_world1_matches_plain_step(cuda):
     import copy
     from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
     from deepspeech_amd.models import DeepSpeech2
-    from deepspeech_amd.parallel.dist import init_distributed
+    from deepspeech_amd.parallel.dist import init_distributed, shutdown
     from deepspeech_amd.trainer import LRSchedule, Trainer
-    init_distributed("cuda", force_group=True)
-    torch.manual_seed(0)
-    base = DeepSpeech2(num_filters=32, num_hidden=128, num_rnn_layers=2, cell="gru").to(cuda)
-    batch = to_device(FixedShapeBatches(8, max_frames=300, seed=2, pool=1).next(), cuda)
-    outs = []
-    for force in (False, True):
-        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
-        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9), force_buckets=force)
-        for _ in range(2):
-            tr.step(batch)
-        torch.cuda.synchronize()
-        outs.append(tr.arena.flat.clone())
-    assert torch.allclose(outs[0], outs[1], atol=1e-6, rtol=0), (outs[0] - outs[1]).abs().max()
+    ctx = init_distributed("cuda", force_group=True)
+    try:
+        torch.manual_seed(0)
+        base = DeepSpeech2(num_filters=32, num_hidden=128, num_rnn_layers=2, cell="gru").to(cuda)
+        batch = to_device(FixedShapeBatches(8, max_frames=300, seed=2, pool=1).next(), cuda)
+        outs = []
+        # plain step; buckets + one update after finish(); buckets + per-bucket Adam ranges
+        for force, per_bucket in ((False, False), (True, False), (True, True)):
+            m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+            tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9), force_buckets=force)
+            tr.per_bucket_update = per_bucket
+            assert tr.bucketer.enabled == force
+            for _ in range(2):
+                tr.step(batch)
+            torch.cuda.synchronize()
+            outs.append((tr.arena.flat.clone(), tr.opt.ema.clone(), tr.arena.p16.clone()))
+        for o in outs[1:]:
+            for x, y in zip(outs[0], o):
+                assert torch.equal(x, y), (x.float() - y.float()).abs().max()
+    finally:
+        shutdown(ctx)           # later GPU tests must not run with a live RCCL group

@@ -113,6 +113,55 @@ def test_headline_geometry_matches_reference(cuda, cell):
     _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=0.15 if cell == "gru" else 0.35)
 
 
+@pytest.mark.parametrize("cell,H", [("gru", 1280), ("rnn_relu", 1760)])
+def test_wide_layer_models_match_reference(cuda, cell, H):
+    """Engine-level parity of the wide-layer configurations: BASELINE config 5's BiGRU-1280
+    and the reference's own 1760-unit clipped-ReLU stack (src/train.sh:42), two layers each,
+    batch 32 (the plans, GEMM routes and recurrence kernels of those geometries)."""
+    from deepspeech_amd.ops import rnn as RNN
+    ref, hip = _pair(cuda, cell, H=H, L=2)
+    batch = to_device(FixedShapeBatches(32, max_frames=600, seed=8, pool=1).next(), cuda)
+    arena = ParamArena(hip, bf16_shadow=True)
+    arena.zero_grad()
+    lh = _loss(hip, batch, True)
+    lh.backward()
+    RNN.join_wgrad_streams()
+    lr = _loss(ref, batch)
+    lr.backward()
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=0.15 if cell == "gru" else 0.35)
+
+
+def test_frontend_backward_headline_same_upstream(cuda):
+    """The conv front-end at the headline geometry (32 filters, batch 32, 10-s utterances)
+    with the SAME upstream gradient fed to the HIP kernels (bf16) and the fp32 reference:
+    isolates the front-end's own error from the bf16 drift accumulated through five
+    recurrent layers (test_headline_geometry_matches_reference allows 15-35 % there)."""
+    ref, hip = _pair(cuda, "gru", H=64, L=1)
+    batch = to_device(FixedShapeBatches(32, max_frames=1000, seed=5, pool=1).next(), cuda)
+    ref.train()
+    hip.train()
+    xr = ref.frontend(batch["feats"])
+    xh = hip.frontend(batch["feats"].to(torch.bfloat16))
+    assert xr.shape == xh.shape
+    assert _rel(xh, xr) < 1e-2
+    torch.manual_seed(1)
+    # an upstream gradient with a common component (like a loss gradient), so the BN beta /
+    # bias sums do not cancel down to rounding noise
+    dy = (torch.randn_like(xr) + 0.3) * 1e-3
+    xr.backward(dy)
+    xh.backward(dy.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    gref = dict(ref.named_parameters())
+    errs = {}
+    for n, p in hip.named_parameters():
+        if not n.startswith("conv") or n.endswith(".bias"):
+            continue                   # conv biases: identically zero under train-mode BN
+        errs[n] = _rel(p.grad, gref[n].grad)
+    assert errs and max(errs.values()) < 2e-2, errs
+
+
 def test_fused_head_ctc_matches_reference(cuda):
     """FusedHeadCTC (MFMA FC + in-register log-softmax + CTC + GEMM backward) against the
     fp32 FC + torch CTC, gradients of h, W_fc and b_fc."""
@@ -232,33 +281,6 @@ def test_step_is_bitwise_reproducible(cuda):
     assert torch.equal(w0, w1)
 
 
-def test_split_optimizer_matches_single_launch(cuda, monkeypatch):
-    """The split optimizer (Adam of the side-stream-produced arena prefix on the side stream,
-    the rest on the main stream, one shared step count) gives bitwise the weights, Adam
-    moments, EMA and bf16 shadows of the single whole-arena launch, over several steps."""
-    from deepspeech_amd.trainer import Trainer, LRSchedule
-    torch.manual_seed(0)
-    base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
-    batch = to_device(FixedShapeBatches(8, max_frames=300, seed=4, pool=1).next(), cuda)
-    out = {}
-    monkeypatch.setenv("DS2_OVERLAP_OPT", "0")
-    for split in ("1", "0"):
-        monkeypatch.setenv("DS2_SPLIT_ADAM", split)
-        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
-        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
-        assert (tr._split_at is not None) == (split == "1")
-        losses = [float(tr.step(batch)) for _ in range(3)]
-        if split == "1":
-            assert tr._optimizer_parts() is not None      # the split path is the one taken
-        torch.cuda.synchronize()
-        out[split] = (losses, tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone(),
-                      tr.arena.p16.clone())
-    a, b = out["1"], out["0"]
-    assert a[0] == b[0], (a[0], b[0])
-    for x, y, name in zip(a[1:], b[1:], ("flat", "m", "v", "ema", "p16")):
-        assert torch.equal(x, y), name
-
-
 @pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
 def test_nhwc_graph_hip_matches_reference(cuda, cell):
     """--nchw False graph on the HIP engine (moments+EMA conv BN in the channels-last
@@ -316,30 +338,3 @@ def test_prefetcher_matches_direct_upload(cuda):
             assert torch.equal(dev[k], v), k
         assert hb.feats.shape[1] == dev["feats"].shape[1]
     pf.close()
-
-
-def test_overlapped_optimizer_matches_plain(cuda, monkeypatch):
-    """DS2_OVERLAP_OPT: the FC + layers >= 1 part of step s's Adam/EMA update runs during
-    step s+1's forward (beside layer 0's recurrence). Losses, weights, moments, EMA and bf16
-    shadows must be bitwise those of the plain end-of-step update."""
-    from deepspeech_amd.trainer import Trainer, LRSchedule
-    torch.manual_seed(0)
-    base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
-    batches = [to_device(FixedShapeBatches(8, max_frames=300, seed=s, pool=1).next(), cuda) for s in (5, 6)]
-    out = {}
-    for ov in ("1", "0"):
-        monkeypatch.setenv("DS2_OVERLAP_OPT", ov)
-        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
-        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
-        assert (tr._defer_hi is not None) == (ov == "1")
-        losses = [float(tr.step(batches[i % 2])) for i in range(4)]
-        if ov == "1":
-            assert tr.arena.pending_update is not None      # the overlapped path is taken
-        tr.flush_optimizer()
-        torch.cuda.synchronize()
-        out[ov] = (losses, tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone(),
-                   tr.arena.p16.clone())
-    a, b = out["1"], out["0"]
-    assert a[0] == b[0], (a[0], b[0])
-    for x, y, name in zip(a[1:], b[1:], ("flat", "m", "v", "ema", "p16")):
-        assert torch.equal(x, y), name

@@ -101,17 +101,11 @@ def test_birnn_xcd_geometries(cuda, N, H):
     _rnn_case(cuda, "gru", N=N, H=H, T=33, ndir=2, mode="auto", seed=9)
 
 
-@pytest.mark.parametrize("exchange", ["rs", "gather"])
 @pytest.mark.parametrize("cell,N,H", [("gru", 32, 800), ("rnn_relu", 32, 800), ("gru", 40, 256), ("gru", 7, 96), ("gru", 32, 1280), ("rnn_relu", 32, 1760)])
-def test_bptt_exchanges(cuda, exchange, cell, N, H):
-    # generation-3 reduce-scatter BPTT and generation-2 all-gather BPTT against the reference
-    from deepspeech_amd.ops import rnn as RNN
-    old = RNN.BWD_EXCHANGE
-    RNN.BWD_EXCHANGE = exchange
-    try:
-        _rnn_case(cuda, cell, N=N, H=H, T=45, ndir=2, mode="auto", seed=21)
-    finally:
-        RNN.BWD_EXCHANGE = old
+def test_bptt_exchanges(cuda, cell, N, H):
+    # the BPTT kernel each geometry's plan selects (reduce-scatter generation 3, or the
+    # generation-1 kernels past 42 workgroups per group) against the reference
+    _rnn_case(cuda, cell, N=N, H=H, T=45, ndir=2, mode="auto", seed=21)
 
 
 def test_unirnn_gru(cuda):

@@ -35,3 +35,32 @@ def test_device_nonfinite_watch(cuda):
     for v in (1.0, float("inf"), float("nan")):
         w.update(torch.tensor(v, device=cuda))
     assert w.first_bad_step() == 101
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_nan_logits_reach_the_loss_and_the_watch(cuda, fused):
+    """A diverged model (NaN in the head's output) must produce a NaN loss even with
+    zero_infinity, so the per-step watch (and --nan_policy abort) sees it. The CTC kernels
+    used to treat NaN log-likelihoods as infeasible utterances (loss 0, zero gradient)."""
+    from deepspeech_amd.ops import ctc as CTC
+    torch.manual_seed(0)
+    T, N, H, K = 40, 4, 64, 29
+    lens = torch.full((N,), T, dtype=torch.int32, device=cuda)
+    labels = torch.randint(0, 28, (N, 8), dtype=torch.int32, device=cuda)
+    label_lens = torch.full((N,), 8, dtype=torch.int32, device=cuda)
+    if fused:
+        h = torch.randn(T, N, H, device=cuda).bfloat16()
+        h[7, 2, 5] = float("nan")                   # one utterance's hidden state diverged
+        w = torch.randn(K, H, device=cuda) * 0.1
+        b = torch.zeros(K, device=cuda)
+        loss = CTC.head_ctc_mean_loss_hip(h, w, b, lens, labels, label_lens)
+    else:
+        logits = torch.randn(T, N, K, device=cuda)
+        logits[7, 2, 3] = float("nan")
+        loss = CTC.ctc_mean_loss_hip(logits, lens, labels, label_lens)
+    assert torch.isnan(loss).item()
+    w = S.NonfiniteWatch(cuda)
+    w.reset(7)
+    w.update(torch.tensor(1.0, device=cuda))
+    w.update(loss.detach())
+    assert w.first_bad_step() == 8
