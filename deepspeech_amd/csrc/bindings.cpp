@@ -98,8 +98,13 @@ int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
 int ds2_fp8_quant_blocks(long long na, long long nb_el);
-int ds2_fp8_quant2(const void* a, long long na, const void* b, long long nb_el, float alpha, void* a8, void* b8,
-                   float* part, float* scales, hipStream_t st);
+int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev,
+              const float* alpha_dev2, int M, int N, int K, int lda, int ldb, int ldc, int fp8, int a_col, int b_col,
+              int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws, int cus,
+              hipStream_t st);
+int ds2_gemm8_splits(int K, int fp8, int S);
+int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
+                   void* a8, void* b8, float* part, float* scales, hipStream_t st);
 int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                    hipStream_t st);
 int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
@@ -599,8 +604,9 @@ void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
 // --------------------------------------------------------------------------- fp8 quantisation
 int64_t fp8_quant_blocks(int64_t na, int64_t nb) { return ds2_fp8_quant_blocks(na, nb); }
 
-// per-tensor e4m3fn quantisation of two bf16 operands; scales[0] = amax_a/448,
-// scales[1] = amax_b/448 * alpha (device-side, for the scaled GEMM)
+// per-tensor e4m3fn quantisation of two bf16 operands a [rows_a, K], b [rows_b, K] into
+// a8 [rows_a, Kp], b8 [rows_b, Kp] (columns >= K zero); scales[0] = amax_a/448,
+// scales[1] = amax_b/448 * alpha (device-side, for the fp8 GEMM's epilogue)
 void fp8_quant2(at::Tensor a, at::Tensor b, double alpha, at::Tensor a8, at::Tensor b8, at::Tensor part,
                 at::Tensor scales) {
   need_gpu(a, "a");
@@ -611,15 +617,84 @@ void fp8_quant2(at::Tensor a, at::Tensor b, double alpha, at::Tensor a8, at::Ten
   need_gpu(scales, "scales");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "bf16 operands expected");
   TORCH_CHECK(a8.scalar_type() == at::kFloat8_e4m3fn && b8.scalar_type() == at::kFloat8_e4m3fn, "e4m3fn outputs");
-  TORCH_CHECK(a8.numel() == a.numel() && b8.numel() == b.numel(), "size mismatch");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+              "a [rows_a, K], b [rows_b, K] contiguous");
+  const int64_t K = a.size(1), Kp = a8.size(-1);
+  TORCH_CHECK(a8.dim() == 2 && b8.dim() == 2 && a8.is_contiguous() && b8.is_contiguous() && a8.size(0) == a.size(0) &&
+                  b8.size(0) == b.size(0) && b8.size(1) == Kp && Kp >= K && K % 8 == 0 && Kp % 8 == 0,
+              "a8 [rows_a, Kp], b8 [rows_b, Kp], Kp >= K, K % 8 == 0");
   TORCH_CHECK(scales.scalar_type() == at::kFloat && scales.numel() >= 2, "scales: 2 floats");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0,
               "16-B aligned operands expected");
-  const int nb = ds2_fp8_quant_blocks(a.numel(), b.numel());
+  const int nb = ds2_fp8_quant_blocks(a.size(0) * Kp, b.size(0) * Kp);
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= 2 * nb, "part: 2*blocks floats");
-  check(ds2_fp8_quant2(a.data_ptr(), a.numel(), b.data_ptr(), b.numel(), (float)alpha, a8.data_ptr(), b8.data_ptr(),
-                       part.data_ptr<float>(), scales.data_ptr<float>(), cur_stream()),
+  check(ds2_fp8_quant2(a.data_ptr(), a.size(0), b.data_ptr(), b.size(0), (int)K, (int)Kp, (float)alpha, a8.data_ptr(),
+                       b8.data_ptr(), part.data_ptr<float>(), scales.data_ptr<float>(), cur_stream()),
         "fp8_quant2");
+}
+
+// --------------------------------------------------------------------------- GEMM (csrc/gemm8.hip)
+// C = epi(alpha * alpha_dev * alpha_dev2 * A B^T) on the STORED operands: A [(batch,) M, K] or,
+// a_col, [(batch,) K, M]; B [(batch,) N, K] or, b_col, [(batch,) K, N]; unit-stride rows.
+// bf16 (row-mode K % 32 == 0) or fp8 e4m3fn (row mode, K % 128 == 0). C bf16 (epi 0, + bias)
+// or fp32 (epi 1 store, 2 accumulate). splits > 1: split-K through ws (fp32).
+static const float* dev_scalar(const OptT& t, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() >= 1, name, " must be an fp32 device scalar");
+  return t->data_ptr<float>();
+}
+
+static int dev_cus() {
+  static int cus_of[64] = {0};
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "hipGetDevice");
+  if (!cus_of[dev])
+    TORCH_CHECK(hipDeviceGetAttribute(&cus_of[dev], hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
+                "CU count");
+  return cus_of[dev];
+}
+
+void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, double alpha, OptT alpha_dev,
+           OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws) {
+  const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(fp8 ? B.scalar_type() == at::kFloat8_e4m3fn
+                  : (A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16),
+              "gemm8: bf16 or fp8 e4m3fn operands (both the same)");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm8: epi 0..2");
+  TORCH_CHECK(C.scalar_type() == (epi == 0 ? at::kBFloat16 : at::kFloat), "gemm8: C dtype does not match epi");
+  TORCH_CHECK(B.dim() == A.dim() && C.dim() == A.dim() && (A.dim() == 2 || A.dim() == 3), "gemm8: 2-D or batched 3-D");
+  for (const at::Tensor* t : {&A, &B, &C}) {
+    TORCH_CHECK(t->is_cuda() && t->stride(-1) == 1, "gemm8: unit-stride rows");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "gemm8: 16-B aligned operands");
+  }
+  const int64_t batch = A.dim() == 3 ? A.size(0) : 1;
+  if (batch > 1) TORCH_CHECK(B.size(0) == batch && C.size(0) == batch, "gemm8: batch mismatch");
+  const int64_t M = a_col ? A.size(-1) : A.size(-2), K = a_col ? A.size(-2) : A.size(-1);
+  const int64_t N = b_col ? B.size(-1) : B.size(-2), Kb = b_col ? B.size(-2) : B.size(-1);
+  TORCH_CHECK(Kb == K && C.size(-2) == M && C.size(-1) == N, "gemm8: shapes");
+  const int64_t lda = A.stride(-2), ldb = B.stride(-2), ldc = C.stride(-2);
+  const void* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(epi == 0 && bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N,
+                "gemm8: bias must be bf16 [N] (epi 0)");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(bias->data_ptr()) & 7) == 0, "gemm8: bias 8-B aligned");
+    bp = bias->data_ptr();
+  }
+  float* wsp = nullptr;
+  const int S = ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)std::max<int64_t>(1, splits));
+  if (S > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined() && ws->is_cuda() && ws->scalar_type() == at::kFloat &&
+                    ws->numel() >= (int64_t)S * batch * M * N,
+                "gemm8: split-K needs an fp32 workspace of ", S * batch * M * N, " floats");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(ws->data_ptr()) & 15) == 0, "gemm8: 16-B aligned workspace");
+    wsp = ws->data_ptr<float>();
+  }
+  const int64_t sA = batch > 1 ? A.stride(0) : 0, sB = batch > 1 ? B.stride(0) : 0, sC = batch > 1 ? C.stride(0) : 0;
+  check(ds2_gemm8(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, dev_scalar(alpha_dev, "alpha_dev"),
+                  dev_scalar(alpha_dev2, "alpha_dev2"), (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc,
+                  fp8 ? 1 : 0, a_col ? 1 : 0, b_col ? 1 : 0, (int)epi, (float)alpha, (int)batch, sA, sB, sC, S, wsp,
+                  dev_cus(), cur_stream()),
+        "gemm8");
 }
 
 // --------------------------------------------------------------------------- GEMM (csrc/gemm.hip)
@@ -801,6 +876,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("device_info", &device_info);
   m.def("fp8_quant_blocks", &fp8_quant_blocks);
   m.def("fp8_quant2", &fp8_quant2);
+  m.def("gemm8", &gemm8, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("epi"),
+        py::arg("alpha") = 1.0, py::arg("alpha_dev") = py::none(), py::arg("alpha_dev2") = py::none(),
+        py::arg("a_col") = false, py::arg("b_col") = false, py::arg("splits") = 1, py::arg("ws") = py::none());
+  m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
   m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),
         py::arg("blank"), py::arg("score") = py::none());

@@ -148,6 +148,11 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
   lps[lane][KPAD] = NEG_INF;                       // never overwritten by stage()
   const int dt = beta ? -1 : 1;
   const int t0 = beta ? len - 1 : 0;
+  // A NaN log-prob (a diverged model: the log-softmax turns a NaN logit into a whole NaN
+  // frame) must reach the loss as NaN, not as an "infeasible" -inf that zero_infinity hides.
+  // The recursion cannot carry it (lse3_rec's fmaxf / fminf drop NaN operands, so a NaN
+  // frame decays to "log 0"), so the staged rows are tested instead: off the frame chain.
+  bool nan = false;
   auto stage = [&](int c0) {   // frames c0 .. c0+63 (forward) or c0 .. c0-63 (backward)
     const int t = c0 + dt * lane;
     __builtin_amdgcn_wave_barrier();
@@ -156,6 +161,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
 #pragma unroll
       for (int q = 0; q < KPAD / 4; ++q) {
         const float4 v4 = src[q];
+        nan = nan || (v4.x != v4.x) || (v4.y != v4.y) || (v4.z != v4.z) || (v4.w != v4.w);
         lps[lane][4 * q + 0] = v4.x * LOG2E; lps[lane][4 * q + 1] = v4.y * LOG2E;   // log2 units
         lps[lane][4 * q + 2] = v4.z * LOG2E; lps[lane][4 * q + 3] = v4.w * LOG2E;
       }
@@ -216,22 +222,14 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
   if (!beta) {
     // logP = lse(alpha_{len-1}(SP-1), alpha_{len-1}(SP-2))
     float mine = NEG_INF;
-    bool nan = false;
 #pragma unroll
     for (int j = 0; j < SPL; ++j)
-      if (s0 + j == SP - 1 || s0 + j == SP - 2) {
-        nan = nan || (v[j] != v[j]);
-        mine = lse2(mine, v[j] * LN2);
-      }
+      if (s0 + j == SP - 1 || s0 + j == SP - 2) mine = lse2(mine, v[j] * LN2);
     // at most two lanes hold a term: combine with a max-shifted wave reduction
     const float m = wave_max(mine);
     float e = (m == NEG_INF) ? 0.f : __expf(mine - m);
     e = wave_sum(e);
-    // A NaN log-prob (a diverged model: the log-softmax turns a NaN logit into a whole NaN
-    // frame, which every later frame of the recursion inherits) must reach the loss as NaN,
-    // not as an "infeasible" -inf that zero_infinity would hide: lse2 / wave_max use fmaxf,
-    // which drops NaN operands, so the final states are tested explicitly.
-    const bool any_nan = __any(nan);
+    const bool any_nan = __any(nan);          // a NaN frame anywhere in the utterance
     if (lane == 0) logp_out[b] = any_nan ? __builtin_nanf("") : (m < LOG_ZERO_LIMIT) ? NEG_INF : m + __logf(e);
   }
 }

@@ -1,0 +1,567 @@
+// 256x256-tile, 8-phase MFMA GEMM for the recurrent layers' big GEMMs (gfx950), bf16 or
+// fp8 e4m3 operands, fp32 accumulation.
+//
+//   C[m][n] = epi( alpha * alpha_dev[0] * alpha_dev2[0] * sum_k A[m][k] B[n][k] )
+//   A row-major [M][K] (lda), B row-major [N][K] (ldb) — both K-contiguous ("NT").
+//   epi 0: bf16 C = . + bias[n] (bf16, optional);  1: fp32 C = .;  2: fp32 C += .
+//
+// Reference call sites: the hoisted input projection x W^T of CustomRNNCell2
+// (src/custom_ops.py:59-61) for every direction at once, and the input gradient
+// dx = dgx W (autograd of the same op, src/deepSpeech_train.py:287) on a K-contiguous W^T.
+//
+// Structure (cdna_hip_programming.md §5 "The 256^2 8-phase template"): one workgroup of 8
+// waves per CU computes a 256x256 C tile; K advances in 128-byte k-tiles (64 bf16 or 128
+// fp8 elements) staged global -> LDS by global_load_lds_dwordx4 into two LDS buffers (2 x
+// 64 KB: A rows 0-127 | A rows 128-255 | B rows 0-127 | B rows 128-255, "half-tiles" of
+// 16 KB). A k-tile is consumed in 4 phases, one 128x128 C quadrant each, in the order
+// Q(0,0) Q(0,1) Q(1,1) Q(1,0): a phase reads only the A half qm and the B half qn, so a
+// half-tile of the buffer is free again one phase after its last reader (A0 after Q(0,1),
+// B1 after Q(1,1), A1 / B0 after Q(1,0)) and the next-but-one k-tile streams into it while
+// the current k-tile is still being multiplied. Each phase:
+//     ds_read the wave's register subtile (8 A and/or 4 B ds_read_b128)
+//     issue one half-tile of a later k-tile (2 glds per wave)
+//     [phases 3 and 7: s_waitcnt vmcnt(4) — every half-tile but the two just issued landed]
+//     s_barrier ; 16 MFMAs of the wave's 64x32 share of the quadrant ; s_barrier
+// Iteration = 2 k-tiles (even k-tile in buffer 0, odd in buffer 1) = 8 phases; stage plan:
+//     phase 0, 1: odd k-tile t+1's A1, B0 (buffer 1; its A0, B1 were issued a phase 6, 7 earlier)
+//     phase 2..5: k-tile t+2's A0, B1, A1, B0 (buffer 0, each one phase after its last read)
+//     phase 6, 7: k-tile t+3's A0, B1 (buffer 1)
+// so a staged half-tile is retired by the vmcnt of phase 3 / 7 and first read in the phase
+// after it (RAW: LDS-DMA data is ordered for ds_read only by the issuing waves' vmcnt and a
+// barrier every reader has passed), and is rewritten only after the barrier that follows
+// every wave's last read of it (WAR). No __syncthreads in the loop: its vmcnt(0) would
+// drain the in-flight half-tiles; every other global access sits outside the loop.
+//
+// LDS images: 128-B rows, 16-B chunk c of row r at position c ^ ((r >> 1) & 7) (the swizzle
+// goes on the per-lane glds SOURCE address: glds writes lane-linear), conflict-free for the
+// 16-row x one-chunk ds_read_b128 of a 16x16x32 operand. Operands are swapped in the MFMA
+// (D' = B A^T), so a lane ends with 4 consecutive C columns of one row: one 8-B (bf16) /
+// 16-B (fp32) store per fragment.
+// fp8: one v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit E8M0 block scales: the
+// per-tensor scales are folded into alpha_dev / alpha_dev2) per fragment per k-tile in
+// place of the bf16 pair: same LDS bytes, same cycles, twice the K per k-tile. A lane's 32
+// fp8 of a row are the two 16-B chunks the bf16 k-substeps 0 and 1 read; A and B use the
+// same k assignment, so the product is the full sum over the k-tile.
+// Persistent grid: one workgroup per CU (a multiple of 8); XCD x = blockIdx % 8 walks the
+// contiguous tile-id range [x*Tx, (x+1)*Tx) of a grouped order (8 m-tiles x all n-tiles,
+// m fastest), so the tiles an XCD holds at once share A rows and B columns in its L2.
+// Tails: K % 32 == 0 (bf16; a last k-tile of 32 skips its second k-substep) or K % 128 == 0
+// (fp8: the quantiser pads K with zeros); rows past M / N are clamped on load and masked on
+// store.
+//
+// Column-mode operands (bf16): an operand stored [K][M] (A) or [K][N] (B), M / N contiguous —
+// the input gradient dx = dgx W reads W [6H][D] as its B, the weight gradients dW = dgx^T x
+// and dU = dgh^T h read both operands that way. Its half-tile is a [64 k][128 cols] image
+// (256-B k-rows, 16-B chunk c of k-row k at c ^ 2((k & 3) | ((k >> 1) & 4)), 4 k-rows per
+// glds wave-instruction), read as MFMA fragments with ds_read_b64_tr_b16 (8 k of one column
+// per lane from two 4-row transposed reads). k-rows past K come back as zeros from the
+// bounds-checked buffer load, so any K works.
+// Split-K (S > 1): work unit = (tile, k-slice); each unit stores its raw fp32 partial tile to
+// a workspace [S][batch][M][N] and splitk_reduce_kernel sums the S partials in slice order
+// (deterministic, no atomics) and applies the epilogue. For the tall-skinny shapes (dx with
+// D = 800: 124 256^2 tiles; dW / dU: 76-80) that would otherwise leave most CUs idle.
+#include <algorithm>
+#include <type_traits>
+
+#include "common.h"
+
+using namespace ds2;
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+struct G8Args {
+  const unsigned char* A;
+  const unsigned char* B;
+  void* C;
+  const bf16_t* bias;
+  const float* alpha_dev;
+  const float* alpha_dev2;
+  long long sA, sB, sC;   // batch strides: bytes (A, B), elements (C)
+  int M, N, Kb;           // Kb: reduction length in BYTES (2K for bf16, K for fp8)
+  int lda, ldb, ldc;      // lda / ldb in bytes, ldc in elements
+  int epi;
+  float alpha;
+  int S, kps;             // split-K: S k-slices of kps k-tiles each (S = 1: no split)
+  float* ws;              // S > 1: fp32 partials [S][batch][M][N]
+  int batch;
+};
+
+constexpr int NWV = 8;
+constexpr int NTHR = NWV * 64;
+constexpr int ROWB = 128;               // bytes of a staged row (one k-tile)
+constexpr int HALF = 128 * ROWB;        // 16 KB
+constexpr int BUFB = 4 * HALF;          // A0 A1 B0 B1
+constexpr int LDS_BYTES = 2 * BUFB;     // 128 KB
+constexpr int GROUP_M = 8;
+
+__device__ __forceinline__ int rsw(int r) { return (r >> 1) & 7; }
+
+// Per-lane byte offsets of a half-tile's two glds (k-tile 0): rows [row0, row0 + 128) of an
+// operand (clamped to lim - 1), the lane's swizzled 16-B chunk. A k-tile adds kb0.
+__device__ __forceinline__ void half_offsets(unsigned (&o)[2], int ld, int row0, int lim, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = wave + NWV * j;                 // 1-KB wave-instruction: rows 8i .. 8i+7
+    const int r = 8 * i + (lane >> 3);
+    const int c = (lane & 7) ^ rsw(r);
+    o[j] = (unsigned)(min(row0 + r, lim - 1) * ld + 16 * c);
+  }
+}
+
+// one half-tile through the operand's buffer resource (32-bit offsets: 2 VGPRs per half
+// instead of 64-bit pointers). Chunks past the row's end (a ragged last bf16 k-tile) read
+// the next row, or zeros past the operand (bounds-checked), and are never multiplied.
+__device__ __forceinline__ void stage_half(unsigned char* dst, __amdgpu_buffer_rsrc_t rs, const unsigned (&o)[2],
+                                           unsigned kb0, int wave) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + (wave + NWV * j) * 1024), 16, o[j] + kb0, 0, 0,
+                                             0);
+}
+
+__device__ __forceinline__ i32x4 rd16(const unsigned char* half, int r, int chunk) {
+  return *(const i32x4*)(half + r * ROWB + ((chunk ^ rsw(r)) << 4));
+}
+
+// s_barrier that is also a compiler memory barrier (the builtin is IntrNoMem: LLVM may move
+// LDS reads and the glds issue across it); lgkmcnt is not waited here — the compiler puts
+// its own counted lgkmcnt in front of each MFMA that consumes a ds_read result
+__device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); }
+
+// ---- column-mode operands ([K][cols] storage) ----
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+__device__ __forceinline__ int csw(int k) { return 2 * ((k & 3) | ((k >> 1) & 4)); }
+
+// per-lane byte offsets of a col half-tile's two glds (k-tile 0): k-rows 4i + lane / 16,
+// columns [col0, col0 + 128) clamped to the last full 16-B chunk below lim (lim % 8 == 0)
+__device__ __forceinline__ void half_offsets_col(unsigned (&o)[2], int ld, int col0, int lim, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = wave + NWV * j;
+    const int kr = 4 * i + (lane >> 4);
+    const int c = (lane & 15) ^ csw(kr);
+    o[j] = (unsigned)(kr * ld + 2 * min(col0 + 8 * c, lim - 8));
+  }
+}
+
+// LDS byte offsets (within a col half-tile) of the two transposed 4-row reads that give a
+// lane its 8 k of fragment column block rb, k-substep 0 (substep 1: + 32 k-rows = 8 KB)
+__device__ __forceinline__ void col_frag_offsets(unsigned& o0, unsigned& o1, int rb, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c = (rb * 16 + 4 * p) >> 3;
+  const int k0 = 8 * g + q;
+  o0 = (unsigned)(k0 * 256 + ((c ^ csw(k0)) << 4) + 8 * (p & 1));
+  o1 = (unsigned)((k0 + 4) * 256 + ((c ^ csw(k0 + 4)) << 4) + 8 * (p & 1));
+}
+
+__device__ __forceinline__ s16x4 rdtr(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p);
+}
+
+__device__ __forceinline__ i32x8 col_frag(const unsigned char* half, unsigned o0, unsigned o1) {
+  const s16x4 a = rdtr(half + o0), b = rdtr(half + o1);
+  const s16x4 c = rdtr(half + o0 + 8192), d = rdtr(half + o1 + 8192);
+  const i32x4 lo = __builtin_bit_cast(i32x4, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+  const i32x4 hi = __builtin_bit_cast(i32x4, __builtin_shufflevector(c, d, 0, 1, 2, 3, 4, 5, 6, 7));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+
+// wave's register subtile: 4 A fragments (rows wr*64 + 16i) or 2 B fragments (rows wc*32 +
+// 16j) of one half, both k-substeps (chunks g and 4 + g of the row, g = lane / 16)
+struct Frag {
+  i32x8 v;       // k-substep 0 in elements 0..3, k-substep 1 in 4..7 (one register tuple)
+};
+__device__ __forceinline__ i32x8 cat(i32x4 lo, i32x4 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 lo8(i32x8 v) {
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 0, 1, 2, 3));
+}
+__device__ __forceinline__ bf16x8 hi8(i32x8 v) {
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v, v, 4, 5, 6, 7));
+}
+
+template <bool FP8, int UNUSED>
+__device__ __forceinline__ void mfma_tile(f32x4 (&acc)[2][4], const Frag (&a)[4], const Frag (&b)[2], bool full) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (FP8) {
+        acc[j][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b[j].v, a[i].v, acc[j][i], 0, 0, 0, 0x7f7f7f7f,
+                                                                     0, 0x7f7f7f7f);
+      } else {
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lo8(b[j].v), lo8(a[i].v), acc[j][i], 0, 0, 0);
+      }
+    }
+  if constexpr (!FP8) {
+    if (full) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hi8(b[j].v), hi8(a[i].v), acc[j][i], 0, 0, 0);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  // pin the cluster here: the MFMAs are pure, and without a use at this point IR-level code
+  // motion sinks them past the barriers to the end of the k-loop (all fragments of all 8
+  // phases then stay live: spills)
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[j][i]));
+}
+
+template <bool FP8, int AC, int BC>
+__global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
+  static_assert(!FP8 || (!AC && !BC), "fp8 operands are K-contiguous");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;         // wave's 64-row x 32-col share of a quadrant
+  const int ntm = (g.M + 255) / 256, ntn = (g.N + 255) / 256;
+  const int S = g.S;
+  const int total = ntm * ntn * S, tx = (total + 7) >> 3, xg = blockIdx.x & 7;
+  int id = xg * tx + (blockIdx.x >> 3);
+  const int id_end = min(total, (xg + 1) * tx), id_step = gridDim.x >> 3;
+  const int nkt_all = (g.Kb + ROWB - 1) / ROWB;
+  // a last k-tile of 32 bf16 with a row-mode operand: its second k-substep holds the next
+  // row's data there (a col-mode operand's k-rows past K load as zeros), so it is skipped
+  const bool ragged = !FP8 && !(AC && BC) && (g.Kb % ROWB) != 0;
+  const int K = g.Kb / (FP8 ? 1 : 2);
+  // bounds of the buffer resources: a row-mode operand holds its rows, a col-mode one K k-rows
+  // (k-rows past K then load as zeros)
+  const __amdgpu_buffer_rsrc_t rsA =
+      make_rsrc(g.A + (size_t)blockIdx.z * g.sA, (unsigned)((size_t)(AC ? K : g.M) * g.lda));
+  const __amdgpu_buffer_rsrc_t rsB =
+      make_rsrc(g.B + (size_t)blockIdx.z * g.sB, (unsigned)((size_t)(BC ? K : g.N) * g.ldb));
+  float alpha = g.alpha;
+  if (g.alpha_dev) alpha *= *g.alpha_dev;
+  if (g.alpha_dev2) alpha *= *g.alpha_dev2;
+  if (S > 1) alpha = 1.f;                          // partials are raw sums; the reduce scales
+  const int g16 = lane >> 4, r16 = lane & 15;
+
+  // fragment addresses. Row mode: row r = base + 16i + lane % 16 has swizzle (r >> 1) & 7 =
+  // (lane % 16 >> 1) & 7 for every fragment of the wave (bases are multiples of 16), so each
+  // lane needs one byte offset per k-substep and every read is base + immediate. Col mode:
+  // two offsets per fragment (the swizzle depends on the column block).
+  const int sw = rsw(r16);
+  const int c_lo = (g16 ^ sw) << 4, c_hi = ((4 + g16) ^ sw) << 4;
+  unsigned ca0[4], ca1[4], cb0[2], cb1[2];
+  if constexpr (AC) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) col_frag_offsets(ca0[i], ca1[i], wr * 4 + i, lane);
+  }
+  if constexpr (BC) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) col_frag_offsets(cb0[j], cb1[j], wc * 2 + j, lane);
+  }
+
+  for (; id < id_end; id += id_step) {
+    const int tile = id / S, ks = id - tile * S;
+    const int gsz = GROUP_M * ntn, grp = tile / gsz, first_m = grp * GROUP_M;
+    const int gm = min(ntm - first_m, GROUP_M), within = tile - grp * gsz;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+    const int kt0 = ks * g.kps;                      // this unit's k-tiles [kt0, kt0 + nkt)
+    const int nkt = max(0, min(nkt_all - kt0, g.kps));
+
+    unsigned oA0[2], oA1[2], oB0[2], oB1[2];
+    if constexpr (AC) {
+      half_offsets_col(oA0, g.lda, m0, g.M, wave, lane);
+      half_offsets_col(oA1, g.lda, m0 + 128, g.M, wave, lane);
+    } else {
+      half_offsets(oA0, g.lda, m0, g.M, wave, lane);
+      half_offsets(oA1, g.lda, m0 + 128, g.M, wave, lane);
+    }
+    if constexpr (BC) {
+      half_offsets_col(oB0, g.ldb, n0, g.N, wave, lane);
+      half_offsets_col(oB1, g.ldb, n0 + 128, g.N, wave, lane);
+    } else {
+      half_offsets(oB0, g.ldb, n0, g.N, wave, lane);
+      half_offsets(oB1, g.ldb, n0 + 128, g.N, wave, lane);
+    }
+    // half-tile h of local k-tile t into buffer t & 1: h 0/1 = A rows 0-127 / 128-255, 2/3 = B.
+    // A k-tile advances 128 bytes along a row-mode operand's rows, 64 k-rows of a col one.
+    auto stage = [&](int t, int h) {
+      if (t >= nkt) return;
+      unsigned char* dst = smem + (t & 1) * BUFB + h * HALF;
+      const int kt = kt0 + t;
+      const unsigned ka = AC ? (unsigned)(kt * 64) * (unsigned)g.lda : (unsigned)(kt * ROWB);
+      const unsigned kb = BC ? (unsigned)(kt * 64) * (unsigned)g.ldb : (unsigned)(kt * ROWB);
+      if (h == 0) stage_half(dst, rsA, oA0, ka, wave);
+      else if (h == 1) stage_half(dst, rsA, oA1, ka, wave);
+      else if (h == 2) stage_half(dst, rsB, oB0, kb, wave);
+      else stage_half(dst, rsB, oB1, kb, wave);
+    };
+    auto read_a = [&](Frag (&a)[4], int buf, int qm) {
+      if constexpr (AC) {
+        const unsigned char* h = smem + buf * BUFB + qm * HALF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i].v = col_frag(h, ca0[i], ca1[i]);
+      } else {
+        const unsigned char* h = smem + (wr * 64 + r16) * ROWB + buf * BUFB + qm * HALF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          a[i].v = cat(*(const i32x4*)(h + i * 16 * ROWB + c_lo), *(const i32x4*)(h + i * 16 * ROWB + c_hi));
+      }
+    };
+    auto read_b = [&](Frag (&b)[2], int buf, int qn) {
+      if constexpr (BC) {
+        const unsigned char* h = smem + buf * BUFB + (2 + qn) * HALF;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j].v = col_frag(h, cb0[j], cb1[j]);
+      } else {
+        const unsigned char* h = smem + 2 * HALF + (wc * 32 + r16) * ROWB + buf * BUFB + qn * HALF;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          b[j].v = cat(*(const i32x4*)(h + j * 16 * ROWB + c_lo), *(const i32x4*)(h + j * 16 * ROWB + c_hi));
+      }
+    };
+
+    f32x4 acc[2][2][2][4];
+#pragma unroll
+    for (int a0 = 0; a0 < 2; ++a0)
+#pragma unroll
+      for (int a1 = 0; a1 < 2; ++a1)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[a0][a1][j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: k-tile 0 whole, k-tile 1's A0 and B1 (the halves its phases 6, 7 would stage)
+    stage(0, 0); stage(0, 2); stage(0, 3); stage(0, 1);
+    stage(1, 0); stage(1, 3);
+    // a vmcnt count names the glds issued AFTER the retire point, so a skipped stage (past
+    // the last k-tile) needs the smaller count, never the steady-state one
+    if (nkt > 1) wait_vm<4>();
+    else wait_vm<0>();
+    bar();
+
+    Frag fa[4], fb[2];
+    // One phase: quadrant Q(qm, qn) of the k-tile in buffer buf, staging half-tile sh of
+    // k-tile st (skipped past the last k-tile), optionally retiring all but the last two
+    // half-tiles (wait: 0 none, 1 = vmcnt(4) if half-tile st exists, else vmcnt(0)).
+    auto phase = [&](auto BUF, auto QM, auto QN, auto RA, auto RB, int st, int sh, int wait, bool full) {
+      constexpr int bf = decltype(BUF)::value, qm = decltype(QM)::value, qn = decltype(QN)::value;
+      if constexpr (decltype(RB)::value) read_b(fb, bf, qn);
+      if constexpr (decltype(RA)::value && decltype(RB)::value) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (decltype(RA)::value) read_a(fa, bf, qm);
+      stage(st, sh);
+      if (wait) {
+        if (st < nkt) wait_vm<4>();
+        else wait_vm<0>();
+      }
+      bar();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_tile<FP8, 0>(acc[qm][qn], fa, fb, full);
+      __builtin_amdgcn_sched_barrier(0);   // the cluster stays between its barriers
+      bar();
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    int t0 = 0;
+    for (; t0 + 1 < nkt; t0 += 2) {
+      const bool full1 = !(ragged && kt0 + t0 + 1 == nkt_all - 1);
+      // even k-tile t0 (buffer 0): Q(0,0) Q(0,1) Q(1,1) Q(1,0)
+      phase(I0{}, I0{}, I0{}, T_{}, T_{}, t0 + 1, 1, 0, true);
+      phase(I0{}, I0{}, I1{}, F_{}, T_{}, t0 + 1, 2, 0, true);
+      phase(I0{}, I1{}, I1{}, T_{}, F_{}, t0 + 2, 0, 0, true);
+      phase(I0{}, I1{}, I0{}, F_{}, T_{}, t0 + 2, 3, 1, true);   // retires k-tile t0 + 1
+      // odd k-tile t0 + 1 (buffer 1)
+      phase(I1{}, I0{}, I0{}, T_{}, T_{}, t0 + 2, 1, 0, full1);
+      phase(I1{}, I0{}, I1{}, F_{}, T_{}, t0 + 2, 2, 0, full1);
+      phase(I1{}, I1{}, I1{}, T_{}, F_{}, t0 + 3, 0, 0, full1);
+      phase(I1{}, I1{}, I0{}, F_{}, T_{}, t0 + 3, 3, 1, full1);   // retires k-tile t0 + 2
+    }
+    if (t0 < nkt) {                     // an odd k-tile count: the last (even) k-tile alone
+      const bool full0 = !(ragged && kt0 + t0 == nkt_all - 1);
+      phase(I0{}, I0{}, I0{}, T_{}, T_{}, nkt, 0, 0, full0);
+      phase(I0{}, I0{}, I1{}, F_{}, T_{}, nkt, 0, 0, full0);
+      phase(I0{}, I1{}, I1{}, T_{}, F_{}, nkt, 0, 0, full0);
+      phase(I0{}, I1{}, I0{}, F_{}, T_{}, nkt, 0, 0, full0);
+    }
+
+    // epilogue: lane holds C[m][n .. n+3], m = .. + lane % 16, n = .. + 4 (lane / 16). A
+    // split unit stores its raw fp32 partial into workspace slice ks (fp32, ld = N).
+    const bool part = S > 1;
+    const int epi = part ? 1 : g.epi;
+    const int ldc = part ? g.N : g.ldc;
+    const size_t esz = epi == 0 ? 2 : 4;
+    char* Cz = part ? (char*)(g.ws + ((size_t)ks * g.batch + blockIdx.z) * (size_t)g.M * g.N)
+                    : (char*)g.C + (size_t)blockIdx.z * g.sC * esz;
+    const bool has_bias = epi == 0 && g.bias != nullptr;
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g16;
+        if (n >= g.N) continue;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (has_bias) {
+          const uint2 b2 = *(const uint2*)(g.bias + n);
+          bv[0] = bf2f((bf16_t)(b2.x & 0xffff)); bv[1] = bf2f((bf16_t)(b2.x >> 16));
+          bv[2] = bf2f((bf16_t)(b2.y & 0xffff)); bv[3] = bf2f((bf16_t)(b2.y >> 16));
+        }
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = m0 + qm * 128 + wr * 64 + 16 * i + r16;
+            if (m >= g.M) continue;
+            const f32x4 v = acc[qm][qn][j][i];
+            const size_t off = (size_t)m * ldc + n;
+            if (epi == 0) {
+              const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[0]) | ((unsigned)f2bf(alpha * v[1] + bv[1]) << 16);
+              const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[2]) | ((unsigned)f2bf(alpha * v[3] + bv[3]) << 16);
+              *(uint2*)(Cz + off * 2) = make_uint2(lo, hi);
+            } else {
+              float4 o = make_float4(alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3]);
+              float4* cp = (float4*)(Cz + off * 4);
+              if (epi == 2) {
+                const float4 c = *cp;
+                o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
+              }
+              *cp = o;
+            }
+          }
+      }
+    // the next tile's prologue restages buffer 0: every wave's last reads were retired by
+    // the final phase's barrier, and the stores above only read registers
+  }
+}
+
+// C = epi(alpha * sum_s ws[s]): float4 per thread over [batch][M][N] (N % 4 == 0)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int batch, int M,
+                                                            int N, void* C, int ldc, long long sC, int epi, float alpha,
+                                                            const float* alpha_dev, const float* alpha_dev2,
+                                                            const bf16_t* __restrict__ bias) {
+  if (alpha_dev) alpha *= *alpha_dev;
+  if (alpha_dev2) alpha *= *alpha_dev2;
+  const long long n4 = (long long)N / 4, per = (long long)M * n4, total = per * batch;
+  const size_t slice = (size_t)batch * M * N;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total; q += (long long)gridDim.x * 256) {
+    const long long z = q / per, r = q - z * per;
+    const int m = (int)(r / n4), n = (int)(r - (long long)m * n4) * 4;
+    const size_t src = ((size_t)z * M + m) * N + n;
+    float4 acc = *(const float4*)(ws + src);
+    for (int s = 1; s < S; ++s) {
+      const float4 v = *(const float4*)(ws + (size_t)s * slice + src);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    const size_t dst = (size_t)z * sC + (size_t)m * ldc + n;
+    if (epi == 0) {
+      float b[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bias) {
+        const uint2 b2 = *(const uint2*)(bias + n);
+        b[0] = bf2f((bf16_t)(b2.x & 0xffff)); b[1] = bf2f((bf16_t)(b2.x >> 16));
+        b[2] = bf2f((bf16_t)(b2.y & 0xffff)); b[3] = bf2f((bf16_t)(b2.y >> 16));
+      }
+      const unsigned lo = (unsigned)f2bf(alpha * acc.x + b[0]) | ((unsigned)f2bf(alpha * acc.y + b[1]) << 16);
+      const unsigned hi = (unsigned)f2bf(alpha * acc.z + b[2]) | ((unsigned)f2bf(alpha * acc.w + b[3]) << 16);
+      *(uint2*)((bf16_t*)C + dst) = make_uint2(lo, hi);
+    } else {
+      float4 o = make_float4(alpha * acc.x, alpha * acc.y, alpha * acc.z, alpha * acc.w);
+      float4* cp = (float4*)((float*)C + dst);
+      if (epi == 2) {
+        const float4 c = *cp;
+        o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
+      }
+      *cp = o;
+    }
+  }
+}
+
+template <bool FP8, int AC, int BC>
+int launch8(const G8Args& a, int cus, hipStream_t st) {
+  auto kern = gemm8_kernel<FP8, AC, BC>;
+  static bool attr = false;
+  if (!attr) {
+    DS2_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    attr = true;
+  }
+  const int units = ((a.M + 255) / 256) * ((a.N + 255) / 256) * a.S;
+  int grid = min(cus, (units + 7) & ~7);
+  grid = max(8, grid & ~7);
+  hipLaunchKernelGGL(kern, dim3(grid, 1, a.batch), dim3(NTHR), LDS_BYTES, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// fp8: A / B hold e4m3 bytes (K elements per row, K % 128 == 0, row mode only); bf16: row-mode
+// operands need K % 32 == 0, col-mode ones (a_col: A stored [K][M]; b_col: B stored [K][N])
+// M % 8 / N % 8 == 0 and any K. lda / ldb / ldc in elements, batch strides likewise.
+// S > 1: split-K over S k-slices through ws (fp32, >= S * batch * M * N floats).
+int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev,
+              const float* alpha_dev2, int M, int N, int K, int lda, int ldb, int ldc, int fp8, int a_col, int b_col,
+              int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws, int cus,
+              hipStream_t st) {
+  const int es = fp8 ? 1 : 2;
+  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || N % 4 != 0 || S < 1) return (int)hipErrorInvalidValue;
+  if (fp8 && (a_col || b_col || K % 128 != 0)) return (int)hipErrorInvalidValue;
+  if (!fp8 && (!a_col || !b_col) && K % 32 != 0) return (int)hipErrorInvalidValue;
+  if ((a_col && M % 8) || (b_col && N % 8)) return (int)hipErrorInvalidValue;
+  if (((lda * es) % 16) || ((ldb * es) % 16) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16))
+    return (int)hipErrorInvalidValue;
+  // 32-bit buffer offsets: each operand (one batch member) under 2 GB
+  if ((long long)(a_col ? K : M) * lda * es >= (1LL << 31) || (long long)(b_col ? K : N) * ldb * es >= (1LL << 31))
+    return (int)hipErrorInvalidValue;
+  if (epi < 0 || epi > 2 || (epi != 0 && bias)) return (int)hipErrorInvalidValue;
+  if (S > 1 && !ws) return (int)hipErrorInvalidValue;
+  G8Args a;
+  a.A = (const unsigned char*)A;
+  a.B = (const unsigned char*)B;
+  a.C = C;
+  a.bias = (const bf16_t*)bias;
+  a.alpha_dev = alpha_dev;
+  a.alpha_dev2 = alpha_dev2;
+  a.sA = sA * es;
+  a.sB = sB * es;
+  a.sC = sC;
+  a.M = M; a.N = N; a.Kb = K * es;
+  a.lda = lda * es; a.ldb = ldb * es; a.ldc = ldc;
+  a.epi = epi;
+  a.alpha = alpha;
+  a.batch = batch;
+  const int nkt = (K * es + ROWB - 1) / ROWB;
+  a.kps = (nkt + S - 1) / S;
+  a.S = (nkt + a.kps - 1) / a.kps;                // no empty slice
+  a.ws = ws;
+  int rc;
+  if (fp8) rc = launch8<true, 0, 0>(a, cus, st);
+  else if (!a_col && !b_col) rc = launch8<false, 0, 0>(a, cus, st);
+  else if (!a_col && b_col) rc = launch8<false, 0, 1>(a, cus, st);
+  else if (a_col && b_col) rc = launch8<false, 1, 1>(a, cus, st);
+  else rc = launch8<false, 1, 0>(a, cus, st);
+  if (rc || a.S == 1) return rc;
+  const long long quads = (long long)batch * M * (N / 4);
+  const int grid = (int)std::min<long long>((quads + 255) / 256, 4LL * cus);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, (const float*)ws, a.S, batch, M, N, C, ldc,
+                     sC, epi, alpha, alpha_dev, alpha_dev2, (const bf16_t*)bias);
+  return (int)hipGetLastError();
+}
+
+// k-slices ds2_gemm8 actually uses for a requested S (no empty slice)
+int ds2_gemm8_splits(int K, int fp8, int S) {
+  const int nkt = (K * (fp8 ? 1 : 2) + ROWB - 1) / ROWB;
+  const int kps = (nkt + S - 1) / S;
+  return (nkt + kps - 1) / kps;
+}
+
+}  // extern "C"

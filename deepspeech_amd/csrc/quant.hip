@@ -1,7 +1,7 @@
 // Per-tensor fp8 (OCP e4m3fn) quantisation of the two operands of a projection GEMM
 // (BASELINE config 5, `--fp8`): amax -> scale = amax / 448 -> saturating cast, for the input
-// activations AND the weights in two launches, scales left on the device for
-// hipBLASLt's scaled GEMM (no host sync).
+// activations AND the weights in two launches, scales left on the device for the fp8 MFMA
+// GEMM (csrc/gemm8.hip folds them into its epilogue; no host sync).
 //
 // The torch-level version (abs, amax, divide, clamp, float round trip, cast, for each
 // operand) was ~10 launches and ~0.9 ms per config-5 step (profiles/r1_s3_config5_fp8.md),
@@ -61,9 +61,11 @@ __device__ __forceinline__ unsigned char to_e4m3(float f) {
   return *reinterpret_cast<const unsigned char*>(&q);
 }
 
-__global__ __launch_bounds__(QT) void quant2_kernel(const bf16_t* __restrict__ a, long long na,
-                                                    const bf16_t* __restrict__ b, long long nb_el, int nb,
-                                                    const float* __restrict__ part, float alpha,
+// Casts [rows][K] bf16 to [rows][Kp] e4m3 (Kp >= K, K % 8 == 0): the padding columns are
+// written as zeros, so a GEMM can run over Kp (gemm8's fp8 k-tiles are 128 deep).
+__global__ __launch_bounds__(QT) void quant2_kernel(const bf16_t* __restrict__ a, long long rows_a,
+                                                    const bf16_t* __restrict__ b, long long rows_b, int K, int Kp,
+                                                    int nb, const float* __restrict__ part, float alpha,
                                                     unsigned char* __restrict__ a8, unsigned char* __restrict__ b8,
                                                     float* __restrict__ scales) {
   __shared__ float sh[QT / 64];
@@ -83,22 +85,25 @@ __global__ __launch_bounds__(QT) void quant2_kernel(const bf16_t* __restrict__ a
   }
   const bf16_t* x = second ? b : a;
   unsigned char* y = second ? b8 : a8;
-  const long long n = second ? nb_el : na;
+  const long long rows = second ? rows_b : rows_a;
   const float inv = 1.f / (second ? sb : sa);
   const int blk = second ? blockIdx.x - nb : blockIdx.x;
-  const long long n8 = n / 8;
+  const int cpr = Kp / 8;                      // 8-element output chunks per row
+  const long long n8 = rows * cpr;
   for (long long i = (long long)blk * QT + threadIdx.x; i < n8; i += (long long)nb * QT) {
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
+    const long long r = i / cpr;
+    const int c = (int)(i - r * cpr);
     unsigned lo = 0, hi = 0;
+    if (8 * c < K) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + r * K + 8 * c);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lo |= (unsigned)to_e4m3(bf2f((bf16_t)v[j]) * inv) << (8 * j);
-      hi |= (unsigned)to_e4m3(bf2f((bf16_t)v[4 + j]) * inv) << (8 * j);
+      for (int j = 0; j < 4; ++j) {
+        lo |= (unsigned)to_e4m3(bf2f((bf16_t)v[j]) * inv) << (8 * j);
+        hi |= (unsigned)to_e4m3(bf2f((bf16_t)v[4 + j]) * inv) << (8 * j);
+      }
     }
     *reinterpret_cast<uint2*>(y + i * 8) = make_uint2(lo, hi);
   }
-  for (long long i = n8 * 8 + (long long)blk * QT + threadIdx.x; i < n; i += (long long)nb * QT)
-    y[i] = to_e4m3(bf2f(x[i]) * inv);
 }
 
 }  // namespace
@@ -112,14 +117,18 @@ int ds2_fp8_quant_blocks(long long na, long long nb_el) {
   return (int)(nb < 1 ? 1 : nb);
 }
 
-// a, b: bf16 (16-B aligned); a8, b8: fp8 e4m3fn outputs; part: 2*nb floats; scales: 2 floats
-int ds2_fp8_quant2(const void* a, long long na, const void* b, long long nb_el, float alpha, void* a8, void* b8,
-                   float* part, float* scales, hipStream_t st) {
-  const int nb = ds2_fp8_quant_blocks(na, nb_el);
+// a [rows_a][K], b [rows_b][K]: bf16 (16-B aligned, K % 8 == 0); a8 [rows_a][Kp], b8
+// [rows_b][Kp]: fp8 e4m3fn outputs, Kp % 8 == 0, columns >= K zero; part: 2*nb floats;
+// scales: {amax_a / 448, amax_b / 448 * alpha}
+int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
+                   void* a8, void* b8, float* part, float* scales, hipStream_t st) {
+  if (K % 8 || Kp % 8 || Kp < K) return (int)hipErrorInvalidValue;
+  const long long na = rows_a * K, nb_el = rows_b * K;
+  const int nb = ds2_fp8_quant_blocks(rows_a * Kp, rows_b * Kp);
   hipLaunchKernelGGL(amax2_kernel, dim3(2 * nb), dim3(QT), 0, st, (const bf16_t*)a, na, (const bf16_t*)b, nb_el, nb,
                      part);
-  hipLaunchKernelGGL(quant2_kernel, dim3(2 * nb), dim3(QT), 0, st, (const bf16_t*)a, na, (const bf16_t*)b, nb_el, nb,
-                     (const float*)part, alpha, (unsigned char*)a8, (unsigned char*)b8, scales);
+  hipLaunchKernelGGL(quant2_kernel, dim3(2 * nb), dim3(QT), 0, st, (const bf16_t*)a, rows_a, (const bf16_t*)b, rows_b,
+                     K, Kp, nb, (const float*)part, alpha, (unsigned char*)a8, (unsigned char*)b8, scales);
   return (int)hipGetLastError();
 }
 

@@ -185,3 +185,86 @@ def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, 
         shp = (a.shape[0], M, N) if a.dim() == 3 else (M, N)
         out = torch.empty(shp, device=a.device, dtype=torch.float32)
     return gemm(a, b, out, M, N, K, True, True, 2 if accumulate else 1, alpha)
+
+
+# ---------------------------------------------------------------------------------------
+# csrc/gemm8.hip: 256x256-tile 8-phase MFMA GEMM on the STORED operands, C = epi(alpha * s1 * s2
+# * A B^T): A [M, K] row-major or (a_col) [K, M]; B [N, K] or (b_col) [K, N]; bf16 (a row-mode
+# operand needs K % 32 == 0) or fp8 e4m3fn (row mode, K % 128 == 0). Persistent grid of one
+# 8-wave workgroup per CU; split-K (deterministic slice-order reduce) for grids of few tiles.
+
+def gemm8_supported(M: int, N: int, K: int, fp8: bool = False, a_col: bool = False, b_col: bool = False) -> bool:
+    if M <= 0 or N <= 0 or N % 4 or (a_col and M % 8) or (b_col and N % 8):
+        return False
+    if fp8:
+        return not (a_col or b_col) and K % 128 == 0
+    return (a_col and b_col) or K % 32 == 0
+
+
+def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_slice: int = 1024) -> int:
+    """k-slices so that tiles x slices covers the CUs: a 256^2 tile is one workgroup, and the
+    skinny shapes (dx at D = 800: 124 tiles, dW / dU: 76-80) would leave half the chip idle.
+    A slice keeps >= min_slice of K (the prologue / epilogue per unit is ~2 k-tiles)."""
+    tiles = _cdiv(M, 256) * _cdiv(N, 256) * batch
+    best = 1
+    for s in range(1, 9):
+        if K // s < min_slice:
+            break
+        best = s
+        if tiles * s >= cus:
+            break
+    return best
+
+
+def gemm8(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = 0, alpha: float = 1.0,
+          bias: Optional[torch.Tensor] = None, alpha_dev: Optional[torch.Tensor] = None,
+          alpha_dev2: Optional[torch.Tensor] = None, a_col: bool = False, b_col: bool = False,
+          splits: Optional[int] = None) -> torch.Tensor:
+    """out (=, or += for epi 2) alpha * alpha_dev * alpha_dev2 * A @ B^T (+ bias) on the stored
+    operands (see the section comment); out bf16 (epi 0) or fp32 (epi 1 / 2). splits=None picks
+    the k-slice count from the shape (gemm8_splits)."""
+    batch = A.shape[0] if A.dim() == 3 else 1
+    M = A.shape[-1] if a_col else A.shape[-2]
+    K = A.shape[-2] if a_col else A.shape[-1]
+    N = B.shape[-1] if b_col else B.shape[-2]
+    if splits is None:
+        splits = gemm8_splits(M, N, K, batch, _dev_cus(A))
+    C = _ext.ext()
+    S = int(C.gemm8_splits(K, A.dtype == torch.float8_e4m3fn, splits)) if splits > 1 else 1
+    ws = torch.empty(S * batch * M * N, device=A.device, dtype=torch.float32) if S > 1 else None
+    C.gemm8(A, B, out, bias, epi, float(alpha), alpha_dev, alpha_dev2, a_col, b_col, S, ws)
+    return out
+
+
+def linear8(x2: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None, alpha: float = 1.0,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """alpha * x2 @ W^T + bias in bf16 through gemm8 (x2 [M, K], W [N, K])."""
+    if out is None:
+        out = torch.empty(x2.shape[0], W.shape[0], device=x2.device, dtype=torch.bfloat16)
+    return gemm8(x2, W, out, 0, alpha, bias, splits=1)
+
+
+def fp8_pad(K: int) -> int:
+    """Reduction length of an fp8 gemm8 operand: K rounded up to the 128-deep k-tile."""
+    return -(-K // 128) * 128
+
+
+def linear_fp8(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], alpha: float) -> torch.Tensor:
+    """alpha * x2 @ W16^T + b16 with both operands quantised per tensor to OCP fp8 e4m3
+    (csrc/quant.hip: amax, scale, saturating cast into K-padded copies, scales on the device)
+    and multiplied by gemm8's fp8 path (v_mfma_scale_f32_16x16x128_f8f6f4: twice the bf16
+    MFMA rate); the two scales and alpha are applied in the epilogue. bf16 output."""
+    C = _ext.ext()
+    x2 = x2.contiguous()
+    W16 = W16.contiguous()
+    M, K = x2.shape
+    N = W16.shape[0]
+    Kp = fp8_pad(K)
+    f8 = torch.float8_e4m3fn
+    x8 = torch.empty(M, Kp, device=x2.device, dtype=f8)
+    w8 = torch.empty(N, Kp, device=x2.device, dtype=f8)
+    nb = int(C.fp8_quant_blocks(M * Kp, N * Kp))
+    ws = torch.empty(2 * nb + 2, device=x2.device, dtype=torch.float32)
+    C.fp8_quant2(x2, W16, float(alpha), x8, w8, ws[:2 * nb], ws[2 * nb:])
+    out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    return gemm8(x8, w8, out, 0, 1.0, b16, ws[2 * nb:2 * nb + 1], ws[2 * nb + 1:2 * nb + 2], splits=1)

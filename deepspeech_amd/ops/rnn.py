@@ -426,31 +426,21 @@ FP8_MAX = 448.0      # OCP e4m3 (gfx950 MFMA fp8 is OCP e4m3fn, not MI300's fnuz
 
 
 def fp8_linear(x2: torch.Tensor, W16: torch.Tensor, b16: torch.Tensor, alpha: float) -> torch.Tensor:
-    """alpha * x2 @ W16^T + b16 with both operands quantised to fp8 e4m3 (per-tensor
-    amax scaling, scales kept on the device: no host sync) and run as a hipBLASLt scaled
-    GEMM on the CDNA4 fp8 MFMA path; bf16 output. Forward-only precision reduction: the
-    backward GEMMs keep the bf16 copies (fp8 'mixed precision', BASELINE config 5)."""
-    if x2.shape[1] % 16 or W16.shape[0] % 16:
-        # hipBLASLt fp8 GEMMs need K and N multiples of 16: such layers stay bf16
-        return torch.addmm(b16, x2, W16.t(), alpha=alpha)
-    f8 = torch.float8_e4m3fn
+    """alpha * x2 @ W16^T + b16 with both operands quantised to fp8 e4m3 (per-tensor amax
+    scaling, scales kept on the device: no host sync) and multiplied on the CDNA4 fp8 MFMA
+    path of the hand-written gemm8 kernel (ops/gemm.py linear_fp8); bf16 output. Forward-only
+    precision reduction: the backward GEMMs keep the bf16 copies (fp8 'mixed precision',
+    BASELINE config 5). CPU: the same arithmetic in torch (dequantised fp32 product)."""
     if x2.is_cuda:
-        # csrc/quant.hip: amax + scale + saturating cast of both operands in two launches
-        C = _ext.ext()
-        x2 = x2.contiguous()
-        W16 = W16.contiguous()
-        x8 = torch.empty(x2.shape, device=x2.device, dtype=f8)
-        w8 = torch.empty(W16.shape, device=x2.device, dtype=f8)
-        nb = int(C.fp8_quant_blocks(x2.numel(), W16.numel()))
-        ws = torch.empty(2 * nb + 2, device=x2.device, dtype=torch.float32)
-        C.fp8_quant2(x2, W16, float(alpha), x8, w8, ws[:2 * nb], ws[2 * nb:])
-        return torch._scaled_mm(x8, w8.t(), scale_a=ws[2 * nb], scale_b=ws[2 * nb + 1], bias=b16,
-                                out_dtype=torch.bfloat16)
+        if x2.shape[1] % 8 or W16.shape[0] % 4:
+            return torch.addmm(b16, x2, W16.t(), alpha=alpha)      # outside the kernels' contract
+        return GM.linear_fp8(x2, W16, b16, alpha)
+    f8 = torch.float8_e4m3fn
     sx = (x2.abs().amax().float() / FP8_MAX).clamp(min=1e-12)
     sw = (W16.abs().amax().float() / FP8_MAX).clamp(min=1e-12)
-    x8 = (x2.float() / sx).clamp(-FP8_MAX, FP8_MAX).to(f8)
-    w8 = (W16.float() / sw).clamp(-FP8_MAX, FP8_MAX).to(f8)
-    return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw * alpha, bias=b16, out_dtype=torch.bfloat16)
+    xq = (x2.float() / sx).clamp(-FP8_MAX, FP8_MAX).to(f8).float() * sx
+    wq = (W16.float() / sw).clamp(-FP8_MAX, FP8_MAX).to(f8).float() * sw
+    return (alpha * (xq @ wq.t()) + b16.float()).to(torch.bfloat16)
 
 
 def _bf16_group(params):

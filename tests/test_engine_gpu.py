@@ -133,33 +133,77 @@ def test_wide_layer_models_match_reference(cuda, cell, H):
     _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=0.15 if cell == "gru" else 0.35)
 
 
+class _RoundGrad(torch.autograd.Function):
+    """Identity forward; backward rounds the incoming gradient to bf16 (a kernel that
+    stores that gradient in bf16)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def _st_round(t):
+    """Value rounded to bf16 (a bf16 activation store), gradient passed straight through."""
+    return t + (t.to(torch.bfloat16).to(t.dtype) - t).detach()
+
+
+def _frontend_emulated(model, feats, dout):
+    """float64 reference of the channels-last HIP front-end (ops/frontend.py FrontendCL) that
+    stores what the kernels store in bf16 — the input, both weights, the conv outputs y1 / y2,
+    the BN+clip outputs, and the backward's dy2, dz1, dy1 — so its gradients differ from the
+    kernels' only by accumulation order. Returns the float64 parameter gradients."""
+    import torch.nn.functional as F
+    from deepspeech_amd.ops import reference as R
+    c1, c2 = model.conv1, model.conv2
+    leaves = {n: p.detach().double().requires_grad_(True) for n, p in
+              (("conv1.weight", c1.weight), ("conv1.bn_gamma", c1.bn_gamma), ("conv1.bn_beta", c1.bn_beta),
+               ("conv2.weight", c2.weight), ("conv2.bn_gamma", c2.bn_gamma), ("conv2.bn_beta", c2.bn_beta))}
+
+    def block(x, blk, pre):
+        y = F.conv2d(x, _st_round(leaves[pre + ".weight"]), blk.bias.detach().double(), stride=blk.stride)
+        y = _RoundGrad.apply(y)                           # dy (BN backward output) stored bf16
+        mean = y.mean(dim=(0, 2, 3), keepdim=True)        # statistics of the fp32 epilogue sums
+        var = ((y - mean) ** 2).mean(dim=(0, 2, 3), keepdim=True)
+        ys = _st_round(y)                                 # y stored bf16
+        z = (ys - mean) * torch.rsqrt(var + blk.bn_eps) * leaves[pre + ".bn_gamma"].view(1, -1, 1, 1) \
+            + leaves[pre + ".bn_beta"].view(1, -1, 1, 1)
+        return _st_round(R.clipped_relu(z))              # BN + clip output stored bf16
+
+    x = feats.to(torch.bfloat16).double().unsqueeze(1)
+    z1 = _RoundGrad.apply(block(x, c1, "conv1"))         # dz1 (conv2 dgrad output) stored bf16
+    z2 = block(z1, c2, "conv2")
+    N, C, T2, F2 = z2.shape
+    out = z2.permute(2, 0, 1, 3).reshape(T2, N, C * F2)
+    out.backward(dout.double())
+    return {n: t.grad for n, t in leaves.items()}
+
+
 def test_frontend_backward_headline_same_upstream(cuda):
     """The conv front-end at the headline geometry (32 filters, batch 32, 10-s utterances)
-    with the SAME upstream gradient fed to the HIP kernels (bf16) and the fp32 reference:
-    isolates the front-end's own error from the bf16 drift accumulated through five
-    recurrent layers (test_headline_geometry_matches_reference allows 15-35 % there)."""
+    with the SAME upstream gradient fed to the HIP kernels and to a float64 reference that
+    stores in bf16 exactly where the kernels do. Against the plain fp32 engine the conv1
+    gradients of this random problem differ by 7 % (weight) and 26 % (BN beta): the BN2
+    backward output is zero-mean per channel, so conv1's gradients are sums that cancel
+    to far below their terms and the bf16 storage of dz1 / dy1 dominates them. With that
+    storage emulated, what is left is the kernels' own arithmetic: every front-end
+    gradient within 2 %, so a kernel error of ~10 % cannot hide behind bf16 drift."""
     ref, hip = _pair(cuda, "gru", H=64, L=1)
     batch = to_device(FixedShapeBatches(32, max_frames=1000, seed=5, pool=1).next(), cuda)
-    ref.train()
     hip.train()
-    xr = ref.frontend(batch["feats"])
     xh = hip.frontend(batch["feats"].to(torch.bfloat16))
-    assert xr.shape == xh.shape
-    assert _rel(xh, xr) < 1e-2
     torch.manual_seed(1)
-    # an upstream gradient with a common component (like a loss gradient), so the BN beta /
-    # bias sums do not cancel down to rounding noise
-    dy = (torch.randn_like(xr) + 0.3) * 1e-3
-    xr.backward(dy)
-    xh.backward(dy.to(torch.bfloat16))
+    # an upstream gradient with a common component, like a loss gradient
+    dout = ((torch.randn(xh.shape, device=cuda) + 0.3) * 1e-3).to(torch.bfloat16)
+    xh.backward(dout)
     torch.cuda.synchronize()
-    gref = dict(ref.named_parameters())
-    errs = {}
-    for n, p in hip.named_parameters():
-        if not n.startswith("conv") or n.endswith(".bias"):
-            continue                   # conv biases: identically zero under train-mode BN
-        errs[n] = _rel(p.grad, gref[n].grad)
-    assert errs and max(errs.values()) < 2e-2, errs
+    want = _frontend_emulated(hip, batch["feats"], dout)
+    got = dict(hip.named_parameters())
+    errs = {n: _rel(got[n].grad.double(), g) for n, g in want.items()}
+    assert max(errs.values()) < 2e-2, errs
 
 
 def test_fused_head_ctc_matches_reference(cuda):

@@ -86,3 +86,127 @@ def test_row_stride_views():
     W = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
     out = G.linear(x, W)
     assert _rel(out, x.float() @ W.float().t()) < 6e-3
+
+
+# ------------------------------------------------------------------ csrc/gemm8.hip (8-phase 256^2)
+@pytest.mark.parametrize("M,N,K", [(7712, 4800, 800), (7712, 800, 4800), (300, 328, 96), (517, 1040, 2400),
+                                   (256, 256, 64), (255, 260, 32), (33, 4, 160), (7712, 7680, 1280)])
+def test_gemm8_bf16_bias_alpha(M, N, K):
+    """bf16 A B^T with the bf16 epilogue: ragged M / N tiles, odd k-tile counts, a last
+    k-tile of 32 (K % 64 == 32), a single k-tile, and more tiles than CUs."""
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV).to(BF)
+    W = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = torch.randn(N, device=DEV).to(BF)
+    out = G.linear8(x, W, b, alpha=0.75)
+    ref = 0.75 * (x.float() @ W.float().t()) + b.float()
+    assert _rel(out, ref) < 6e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(4800, 800, 7712), (136, 264, 96), (1000, 2400, 4800)])
+def test_gemm8_fp32_store_accumulate_batched(M, N, K):
+    """fp32 epilogues (store, then accumulate) on row-stride views and a batch of 2, with an
+    asymmetric operand pair so a swapped / transposed store cannot pass."""
+    torch.manual_seed(K)
+    a = torch.randn(2, M, K, device=DEV).to(BF)
+    b = (torch.randn(2, N, K, device=DEV) + 0.1).to(BF)
+    ref = a.float() @ b.float().transpose(1, 2)
+    out = torch.full((2, M, N), float("nan"), device=DEV)
+    G.gemm8(a, b, out, 1, 0.5, splits=1)
+    assert _rel(out, 0.5 * ref) < 2e-5 * K ** 0.5 + 1e-4
+    G.gemm8(a, b, out, 2, 1.0, splits=1)
+    assert _rel(out, 1.5 * ref) < 2e-5 * K ** 0.5 + 1e-4
+    # a row-strided operand view (every other row of a taller matrix)
+    big = torch.randn(2 * M, K, device=DEV).to(BF)
+    o2 = torch.empty(M, N, device=DEV)
+    G.gemm8(big[::2], b[0], o2, 1, splits=1)
+    assert _rel(o2, big[::2].float() @ b[0].float().t()) < 2e-5 * K ** 0.5 + 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(7712, 4800, 800), (7712, 7680, 2400), (300, 328, 96), (64, 256, 1280)])
+def test_gemm8_fp8_projection(M, N, K):
+    """fp8 e4m3 per-tensor quantised projection (K padded to the 128-deep k-tile): equals
+    the fp32 product of the DEQUANTISED operands to fp32 accumulation error, and the bf16
+    product to fp8 rounding error."""
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device=DEV).to(BF)
+    W = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = torch.randn(N, device=DEV).to(BF)
+    out = G.linear_fp8(x, W, b, 0.9)
+    sx = x.float().abs().max() / 448.0
+    sw = W.float().abs().max() / 448.0
+    xq = (x.float() / sx).to(torch.float8_e4m3fn).float() * sx
+    wq = (W.float() / sw).to(torch.float8_e4m3fn).float() * sw
+    ref_q = 0.9 * (xq @ wq.t()) + b.float()
+    # bf16 output rounding, and e4m3 ties the HIP cast and torch's round differently
+    assert _rel(out, ref_q) < 1.5e-2
+    ref = 0.9 * (x.float() @ W.float().t()) + b.float()
+    assert _rel(out, ref) < 6e-2                         # e4m3: 3 mantissa bits
+
+
+def test_gemm8_rejects_unsupported_k():
+    a = torch.randn(64, 48, device=DEV).to(BF)
+    with pytest.raises(RuntimeError):
+        G.gemm8(a, a, torch.empty(64, 64, device=DEV, dtype=BF), 0)
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(7712, 800, 4800), (7712, 2400, 4800), (300, 328, 96), (136, 264, 7712)])
+def test_gemm8_dx_col_b(splits, M, N, K):
+    """dx = dgx W with W read as stored ([K][N], N contiguous: column mode, transposed LDS
+    reads), bf16 output, optionally split over k-slices (deterministic reduce)."""
+    torch.manual_seed(N + K + splits)
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(K, N, device=DEV) * 0.05 + 0.01).to(BF)
+    out = G.gemm8(a, w, torch.empty(M, N, device=DEV, dtype=BF), 0, 1.0, b_col=True, splits=splits)
+    assert _rel(out, a.float() @ w.float()) < 6e-3
+
+
+@pytest.mark.parametrize("splits", [1, 2, 5])
+@pytest.mark.parametrize("M,N,K", [(4800, 800, 7712), (2400, 800, 7712), (136, 264, 96), (192, 256, 390),
+                                   (136, 128, 8), (800, 32, 300)])
+def test_gemm8_wgrad_col_col(splits, M, N, K):
+    """Weight gradients a^T b with both operands stored [K][M] / [K][N] (column mode), fp32
+    store then accumulate, any K (k-rows past K load as zeros), split-K."""
+    torch.manual_seed(M + K + splits)
+    a = torch.randn(K, M, device=DEV).to(BF)
+    b = (torch.randn(K, N, device=DEV) + 0.1).to(BF)
+    ref = a.float().t() @ b.float()
+    out = torch.full((M, N), float("nan"), device=DEV)
+    G.gemm8(a, b, out, 1, 1.0, a_col=True, b_col=True, splits=splits)
+    assert _rel(out, ref) < 2e-5 * K ** 0.5 + 1e-4
+    G.gemm8(a, b, out, 2, 0.5, a_col=True, b_col=True, splits=splits)
+    assert _rel(out, 1.5 * ref) < 2e-5 * K ** 0.5 + 1e-4
+
+
+def test_gemm8_wgrad_batched_directions():
+    """dU of both directions as one batched call (batch stride over the directions)."""
+    torch.manual_seed(3)
+    K, M, N = 7712, 2400, 800
+    a = torch.randn(2, K, M, device=DEV).to(BF)
+    b = torch.randn(2, K, N, device=DEV).to(BF)
+    out = torch.empty(2, M, N, device=DEV)
+    G.gemm8(a, b, out, 1, 1.0, a_col=True, b_col=True)
+    ref = a.float().transpose(1, 2) @ b.float()
+    assert _rel(out, ref) < 2e-5 * K ** 0.5 + 1e-4
+
+
+def test_gemm8_row_a_col_b_ragged_k():
+    """A row-mode operand with K % 64 == 32 beside a column-mode one: the last k-tile's
+    second k-substep is skipped (its row-mode chunks hold the next row's data)."""
+    torch.manual_seed(4)
+    M, N, K = 520, 264, 800
+    a = torch.randn(M, K, device=DEV).to(BF)
+    w = torch.randn(K, N, device=DEV).to(BF)
+    out = G.gemm8(a, w, torch.empty(M, N, device=DEV, dtype=BF), 0, 1.0, b_col=True, splits=1)
+    assert _rel(out, a.float() @ w.float()) < 6e-3
+
+
+def test_gemm8_split_reproducible():
+    """Split-K is bitwise reproducible (slice-order reduce, no atomics)."""
+    torch.manual_seed(5)
+    a = torch.randn(7712, 4800, device=DEV).to(BF)
+    b = torch.randn(7712, 800, device=DEV).to(BF)
+    o1 = G.gemm8(a, b, torch.empty(4800, 800, device=DEV), 1, 1.0, a_col=True, b_col=True, splits=4)
+    o2 = G.gemm8(a, b, torch.empty(4800, 800, device=DEV), 1, 1.0, a_col=True, b_col=True, splits=4)
+    assert torch.equal(o1, o2)
