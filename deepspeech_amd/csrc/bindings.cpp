@@ -100,11 +100,12 @@ int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
 int ds2_fp8_quant_blocks(long long na, long long nb_el);
 int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev,
               const float* alpha_dev2, int M, int N, int K, int lda, int ldb, int ldc, int fp8, int a_col, int b_col,
-              int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws, int cus,
-              hipStream_t st);
+              int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
+              unsigned* cnt, int cus, hipStream_t st);
 int ds2_gemm8_splits(int K, int fp8, int S);
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
                    void* a8, void* b8, float* part, float* scales, hipStream_t st);
+int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st);
 int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                    hipStream_t st);
 int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
@@ -587,6 +588,18 @@ void ctc_greedy(at::Tensor logits, at::Tensor lens, at::Tensor labels, at::Tenso
 
 // --------------------------------------------------------------------------- multi-fill
 // fill each (contiguous tensor, 32-bit pattern) region in ONE launch (<= 8 regions)
+// out [C, R] = in [R, C]^T (bf16, unit-stride rows)
+void transpose_bf16(at::Tensor in, at::Tensor out) {
+  need_gpu(in, "in");
+  need_gpu(out, "out");
+  TORCH_CHECK(in.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16, "transpose_bf16: bf16");
+  TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && in.stride(1) == 1 && out.stride(1) == 1, "transpose_bf16: 2-D rows");
+  TORCH_CHECK(out.size(0) == in.size(1) && out.size(1) == in.size(0), "transpose_bf16: out must be [C, R]");
+  check(ds2_transpose_bf16(in.data_ptr(), out.data_ptr(), (int)in.size(0), (int)in.size(1), (int)in.stride(0),
+                           (int)out.stride(0), cur_stream()),
+        "transpose_bf16");
+}
+
 void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
   TORCH_CHECK(ts.size() == patterns.size() && ts.size() <= 8, "multi_fill: <= 8 (tensor, pattern) pairs");
   void* ptrs[8];
@@ -655,7 +668,7 @@ static int dev_cus() {
 }
 
 void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, double alpha, OptT alpha_dev,
-           OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws) {
+           OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws, OptT cnt, int64_t max_grid) {
   const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
   TORCH_CHECK(fp8 ? B.scalar_type() == at::kFloat8_e4m3fn
                   : (A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16),
@@ -681,6 +694,7 @@ void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, dou
     bp = bias->data_ptr();
   }
   float* wsp = nullptr;
+  unsigned* cntp = nullptr;
   const int S = ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)std::max<int64_t>(1, splits));
   if (S > 1) {
     TORCH_CHECK(ws.has_value() && ws->defined() && ws->is_cuda() && ws->scalar_type() == at::kFloat &&
@@ -688,12 +702,17 @@ void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, dou
                 "gemm8: split-K needs an fp32 workspace of ", S * batch * M * N, " floats");
     TORCH_CHECK((reinterpret_cast<uintptr_t>(ws->data_ptr()) & 15) == 0, "gemm8: 16-B aligned workspace");
     wsp = ws->data_ptr<float>();
+    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * batch;
+    TORCH_CHECK(cnt.has_value() && cnt->defined() && cnt->is_cuda() && cnt->scalar_type() == at::kInt &&
+                    cnt->numel() >= tiles,
+                "gemm8: split-K needs ", tiles, " zeroed int32 tile counters (one buffer per stream)");
+    cntp = reinterpret_cast<unsigned*>(cnt->data_ptr<int>());
   }
   const int64_t sA = batch > 1 ? A.stride(0) : 0, sB = batch > 1 ? B.stride(0) : 0, sC = batch > 1 ? C.stride(0) : 0;
   check(ds2_gemm8(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, dev_scalar(alpha_dev, "alpha_dev"),
                   dev_scalar(alpha_dev2, "alpha_dev2"), (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc,
                   fp8 ? 1 : 0, a_col ? 1 : 0, b_col ? 1 : 0, (int)epi, (float)alpha, (int)batch, sA, sB, sC, S, wsp,
-                  dev_cus(), cur_stream()),
+                  cntp, max_grid > 0 ? (int)std::min<int64_t>(max_grid, dev_cus()) : dev_cus(), cur_stream()),
         "gemm8");
 }
 
@@ -876,9 +895,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("device_info", &device_info);
   m.def("fp8_quant_blocks", &fp8_quant_blocks);
   m.def("fp8_quant2", &fp8_quant2);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("gemm8", &gemm8, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("epi"),
         py::arg("alpha") = 1.0, py::arg("alpha_dev") = py::none(), py::arg("alpha_dev2") = py::none(),
-        py::arg("a_col") = false, py::arg("b_col") = false, py::arg("splits") = 1, py::arg("ws") = py::none());
+        py::arg("a_col") = false, py::arg("b_col") = false, py::arg("splits") = 1, py::arg("ws") = py::none(),
+        py::arg("cnt") = py::none(), py::arg("max_grid") = 0);
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
   m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),

@@ -54,3 +54,59 @@ extern "C" int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long
   hipLaunchKernelGGL(multi_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, st, f);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// bf16 transpose out[c][r] = in[r][c] ([R][C] -> [C][R], both row-major, unit-stride rows):
+// the K-contiguous W^T shadow of a recurrent layer's [W_fw; W_bw] that the input-gradient
+// GEMM dx = dgx W reads as a row-major operand (csrc/gemm.hip measured faster on it than on
+// W's column-major reading). 64 x 64 tiles through LDS: 16-B row reads of the input
+// (8 bf16 per lane) and 16-B row writes of the output; the LDS tile is padded by one
+// 4-byte word per row so the column gathers of the write pass spread over the banks.
+namespace {
+
+constexpr int TT = 64;
+
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                             int R, int C, int ldi, int ldo) {
+  __shared__ bf16_t tile[TT][TT + 2];
+  const int tc = blockIdx.x * TT, tr = blockIdx.y * TT;
+  const int t = threadIdx.x;
+  // read: 64 rows x 8 chunks of 8 bf16 = 512 chunks, 2 per thread
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = t + 256 * k, r = q >> 3, c8 = (q & 7) * 8;
+    const int gr = tr + r, gc = tc + c8;
+    bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (gr < R && gc + 8 <= C) v = *reinterpret_cast<const bf16x8*>(in + (size_t)gr * ldi + gc);
+    else if (gr < R)
+      for (int j = 0; j < 8; ++j) v[j] = gc + j < C ? (short)in[(size_t)gr * ldi + gc + j] : (short)0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[r][c8 + j] = (bf16_t)v[j];
+  }
+  __syncthreads();
+  // write: output rows = input columns
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = t + 256 * k, c = q >> 3, r8 = (q & 7) * 8;
+    const int oc = tc + c, orr = tr + r8;
+    if (oc >= C) continue;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (short)tile[r8 + j][c];
+    if (orr + 8 <= R) *reinterpret_cast<bf16x8*>(out + (size_t)oc * ldo + orr) = v;
+    else
+      for (int j = 0; j < 8; ++j)
+        if (orr + j < R) out[(size_t)oc * ldo + orr + j] = (bf16_t)v[j];
+  }
+}
+
+}  // namespace
+
+extern "C" int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st) {
+  if (R <= 0 || C <= 0 || ldi < C || ldo < R || ldi % 8 || ldo % 8 || (reinterpret_cast<uintptr_t>(in) & 15) ||
+      (reinterpret_cast<uintptr_t>(out) & 15))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3((C + TT - 1) / TT, (R + TT - 1) / TT), dim3(256), 0, st,
+                     (const bf16_t*)in, (bf16_t*)out, R, C, ldi, ldo);
+  return (int)hipGetLastError();
+}

@@ -57,9 +57,10 @@
 // per lane from two 4-row transposed reads). k-rows past K come back as zeros from the
 // bounds-checked buffer load, so any K works.
 // Split-K (S > 1): work unit = (tile, k-slice); each unit stores its raw fp32 partial tile to
-// a workspace [S][batch][M][N] and splitk_reduce_kernel sums the S partials in slice order
-// (deterministic, no atomics) and applies the epilogue. For the tall-skinny shapes (dx with
-// D = 800: 124 256^2 tiles; dW / dU: 76-80) that would otherwise leave most CUs idle.
+// a workspace [S][batch][M][N], and the tile's last-arriving slice sums the S partials in
+// slice order (deterministic) and applies the epilogue, in the same launch. For the
+// tall-skinny shapes (dx with D = 800: 124 256^2 tiles; dW / dU: 76-80) that would
+// otherwise leave most CUs idle.
 #include <algorithm>
 #include <type_traits>
 
@@ -86,6 +87,7 @@ struct G8Args {
   float alpha;
   int S, kps;             // split-K: S k-slices of kps k-tiles each (S = 1: no split)
   float* ws;              // S > 1: fp32 partials [S][batch][M][N]
+  unsigned* cnt;          // S > 1: per-tile arrival counters [batch][tiles], zero between launches
   int batch;
 };
 
@@ -250,7 +252,6 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
   float alpha = g.alpha;
   if (g.alpha_dev) alpha *= *g.alpha_dev;
   if (g.alpha_dev2) alpha *= *g.alpha_dev2;
-  if (S > 1) alpha = 1.f;                          // partials are raw sums; the reduce scales
   const int g16 = lane >> 4, r16 = lane & 15;
 
   // fragment addresses. Row mode: row r = base + 16i + lane % 16 has swizzle (r >> 1) & 7 =
@@ -398,90 +399,102 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
     // epilogue: lane holds C[m][n .. n+3], m = .. + lane % 16, n = .. + 4 (lane / 16). A
     // split unit stores its raw fp32 partial into workspace slice ks (fp32, ld = N).
     const bool part = S > 1;
-    const int epi = part ? 1 : g.epi;
-    const int ldc = part ? g.N : g.ldc;
-    const size_t esz = epi == 0 ? 2 : 4;
-    char* Cz = part ? (char*)(g.ws + ((size_t)ks * g.batch + blockIdx.z) * (size_t)g.M * g.N)
-                    : (char*)g.C + (size_t)blockIdx.z * g.sC * esz;
-    const bool has_bias = epi == 0 && g.bias != nullptr;
+    // the final epilogue: lane's fragment (qm, qn, j, i) holds C[m][n .. n+3]
+    auto finish = [&](auto&& value) {
+      const int epi = g.epi;
+      const size_t esz = epi == 0 ? 2 : 4;
+      char* Cz = (char*)g.C + (size_t)blockIdx.z * g.sC * esz;
+      const bool has_bias = epi == 0 && g.bias != nullptr;
 #pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
+      for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g16;
-        if (n >= g.N) continue;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (has_bias) {
-          const uint2 b2 = *(const uint2*)(g.bias + n);
-          bv[0] = bf2f((bf16_t)(b2.x & 0xffff)); bv[1] = bf2f((bf16_t)(b2.x >> 16));
-          bv[2] = bf2f((bf16_t)(b2.y & 0xffff)); bv[3] = bf2f((bf16_t)(b2.y >> 16));
-        }
-#pragma unroll
-        for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int m = m0 + qm * 128 + wr * 64 + 16 * i + r16;
-            if (m >= g.M) continue;
-            const f32x4 v = acc[qm][qn][j][i];
-            const size_t off = (size_t)m * ldc + n;
-            if (epi == 0) {
-              const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[0]) | ((unsigned)f2bf(alpha * v[1] + bv[1]) << 16);
-              const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[2]) | ((unsigned)f2bf(alpha * v[3] + bv[3]) << 16);
-              *(uint2*)(Cz + off * 2) = make_uint2(lo, hi);
-            } else {
-              float4 o = make_float4(alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3]);
-              float4* cp = (float4*)(Cz + off * 4);
-              if (epi == 2) {
-                const float4 c = *cp;
-                o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
-              }
-              *cp = o;
-            }
+        for (int j = 0; j < 2; ++j) {
+          const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g16;
+          if (n >= g.N) continue;
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (has_bias) {
+            const uint2 b2 = *(const uint2*)(g.bias + n);
+            bv[0] = bf2f((bf16_t)(b2.x & 0xffff)); bv[1] = bf2f((bf16_t)(b2.x >> 16));
+            bv[2] = bf2f((bf16_t)(b2.y & 0xffff)); bv[3] = bf2f((bf16_t)(b2.y >> 16));
           }
+#pragma unroll
+          for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int m = m0 + qm * 128 + wr * 64 + 16 * i + r16;
+              if (m >= g.M) continue;
+              const f32x4 v = value(qm, qn, j, i, m, n);
+              const size_t off = (size_t)m * g.ldc + n;
+              if (epi == 0) {
+                const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[0]) | ((unsigned)f2bf(alpha * v[1] + bv[1]) << 16);
+                const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[2]) | ((unsigned)f2bf(alpha * v[3] + bv[3]) << 16);
+                *(uint2*)(Cz + off * 2) = make_uint2(lo, hi);
+              } else {
+                float4 o = make_float4(alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3]);
+                float4* cp = (float4*)(Cz + off * 4);
+                if (epi == 2) {
+                  const float4 c = *cp;
+                  o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
+                }
+                *cp = o;
+              }
+            }
+        }
+    };
+    if (!part) {
+      finish([&](int qm, int qn, int j, int i, int, int) { return acc[qm][qn][j][i]; });
+    } else {
+      // Split-K, reduced in this launch by the tile's last-arriving slice (the guide's
+      // counter hand-off, cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2, in
+      // its write-through form): every slice stores its raw fp32 partial to workspace slab
+      // ks with sc1 (write-through) stores, each wave drains them, the workgroup syncs and
+      // one lane takes a ticket (relaxed, agent scope); the slice drawing S - 1 reads the S
+      // slabs with sc1 loads (every load of them) and sums them in slice order 0 .. S-1
+      // (deterministic whatever the arrival order), then resets the counter for the next
+      // launch. No agent-scope release / acquire fence: on gfx950 those write back / flush
+      // this XCD's whole L2, which beside the persistent BPTT cost ~20 % of the GEMM.
+      const unsigned slab = (unsigned)((size_t)g.M * g.N * 4);
+      const __amdgpu_buffer_rsrc_t rsw_ = make_rsrc(g.ws, (unsigned)(slab * (size_t)S * g.batch));
+      const unsigned zoff = (unsigned)blockIdx.z * slab, sstride = (unsigned)g.batch * slab;
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g16;
+          if (n >= g.N) continue;
+#pragma unroll
+          for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int m = m0 + qm * 128 + wr * 64 + 16 * i + r16;
+              if (m >= g.M) continue;
+              store_sc1_b128(rsw_, (unsigned)ks * sstride + zoff + (unsigned)((m * g.N + n) * 4),
+                             __builtin_bit_cast(i32x4, acc[qm][qn][j][i]));
+            }
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* flag = (int*)smem;                       // LDS is free: the k-loop has finished
+      unsigned* cnt = g.cnt + (size_t)blockIdx.z * ntm * ntn + tile;
+      if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == (unsigned)(S - 1);
+        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
       }
+      __syncthreads();
+      const bool last = *flag != 0;
+      __syncthreads();                              // flag read before the next prologue's glds
+      if (last)
+        finish([&](int, int, int, int, int m, int n) {
+          const unsigned off = zoff + (unsigned)((m * g.N + n) * 4);
+          f32x4 v = __builtin_bit_cast(f32x4, load_sc1_b128(rsw_, off));
+          for (int s2 = 1; s2 < S; ++s2) v += __builtin_bit_cast(f32x4, load_sc1_b128(rsw_, off + s2 * sstride));
+          return v;
+        });
+    }
     // the next tile's prologue restages buffer 0: every wave's last reads were retired by
     // the final phase's barrier, and the stores above only read registers
-  }
-}
-
-// C = epi(alpha * sum_s ws[s]): float4 per thread over [batch][M][N] (N % 4 == 0)
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S, int batch, int M,
-                                                            int N, void* C, int ldc, long long sC, int epi, float alpha,
-                                                            const float* alpha_dev, const float* alpha_dev2,
-                                                            const bf16_t* __restrict__ bias) {
-  if (alpha_dev) alpha *= *alpha_dev;
-  if (alpha_dev2) alpha *= *alpha_dev2;
-  const long long n4 = (long long)N / 4, per = (long long)M * n4, total = per * batch;
-  const size_t slice = (size_t)batch * M * N;
-  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < total; q += (long long)gridDim.x * 256) {
-    const long long z = q / per, r = q - z * per;
-    const int m = (int)(r / n4), n = (int)(r - (long long)m * n4) * 4;
-    const size_t src = ((size_t)z * M + m) * N + n;
-    float4 acc = *(const float4*)(ws + src);
-    for (int s = 1; s < S; ++s) {
-      const float4 v = *(const float4*)(ws + (size_t)s * slice + src);
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
-    const size_t dst = (size_t)z * sC + (size_t)m * ldc + n;
-    if (epi == 0) {
-      float b[4] = {0.f, 0.f, 0.f, 0.f};
-      if (bias) {
-        const uint2 b2 = *(const uint2*)(bias + n);
-        b[0] = bf2f((bf16_t)(b2.x & 0xffff)); b[1] = bf2f((bf16_t)(b2.x >> 16));
-        b[2] = bf2f((bf16_t)(b2.y & 0xffff)); b[3] = bf2f((bf16_t)(b2.y >> 16));
-      }
-      const unsigned lo = (unsigned)f2bf(alpha * acc.x + b[0]) | ((unsigned)f2bf(alpha * acc.y + b[1]) << 16);
-      const unsigned hi = (unsigned)f2bf(alpha * acc.z + b[2]) | ((unsigned)f2bf(alpha * acc.w + b[3]) << 16);
-      *(uint2*)((bf16_t*)C + dst) = make_uint2(lo, hi);
-    } else {
-      float4 o = make_float4(alpha * acc.x, alpha * acc.y, alpha * acc.z, alpha * acc.w);
-      float4* cp = (float4*)((float*)C + dst);
-      if (epi == 2) {
-        const float4 c = *cp;
-        o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
-      }
-      *cp = o;
-    }
   }
 }
 
@@ -494,7 +507,7 @@ int launch8(const G8Args& a, int cus, hipStream_t st) {
     attr = true;
   }
   const int units = ((a.M + 255) / 256) * ((a.N + 255) / 256) * a.S;
-  int grid = min(cus, (units + 7) & ~7);
+  int grid = min(cus, (units + 7) & ~7);          // cus: the CU budget (device CUs or a cap)
   grid = max(8, grid & ~7);
   hipLaunchKernelGGL(kern, dim3(grid, 1, a.batch), dim3(NTHR), LDS_BYTES, st, a);
   return (int)hipGetLastError();
@@ -507,11 +520,13 @@ extern "C" {
 // fp8: A / B hold e4m3 bytes (K elements per row, K % 128 == 0, row mode only); bf16: row-mode
 // operands need K % 32 == 0, col-mode ones (a_col: A stored [K][M]; b_col: B stored [K][N])
 // M % 8 / N % 8 == 0 and any K. lda / ldb / ldc in elements, batch strides likewise.
-// S > 1: split-K over S k-slices through ws (fp32, >= S * batch * M * N floats).
+// S > 1: split-K over S k-slices through ws (fp32, >= S * batch * M * N floats) and cnt
+// (>= batch * tiles unsigned, all zero; every launch leaves them zero again). Launches that
+// may run concurrently (different streams) need separate cnt buffers.
 int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev,
               const float* alpha_dev2, int M, int N, int K, int lda, int ldb, int ldc, int fp8, int a_col, int b_col,
-              int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws, int cus,
-              hipStream_t st) {
+              int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
+              unsigned* cnt, int cus, hipStream_t st) {
   const int es = fp8 ? 1 : 2;
   if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || N % 4 != 0 || S < 1) return (int)hipErrorInvalidValue;
   if (fp8 && (a_col || b_col || K % 128 != 0)) return (int)hipErrorInvalidValue;
@@ -523,7 +538,7 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
   if ((long long)(a_col ? K : M) * lda * es >= (1LL << 31) || (long long)(b_col ? K : N) * ldb * es >= (1LL << 31))
     return (int)hipErrorInvalidValue;
   if (epi < 0 || epi > 2 || (epi != 0 && bias)) return (int)hipErrorInvalidValue;
-  if (S > 1 && !ws) return (int)hipErrorInvalidValue;
+  if (S > 1 && (!ws || !cnt)) return (int)hipErrorInvalidValue;
   G8Args a;
   a.A = (const unsigned char*)A;
   a.B = (const unsigned char*)B;
@@ -543,18 +558,14 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
   a.kps = (nkt + S - 1) / S;
   a.S = (nkt + a.kps - 1) / a.kps;                // no empty slice
   a.ws = ws;
+  a.cnt = cnt;
   int rc;
   if (fp8) rc = launch8<true, 0, 0>(a, cus, st);
   else if (!a_col && !b_col) rc = launch8<false, 0, 0>(a, cus, st);
   else if (!a_col && b_col) rc = launch8<false, 0, 1>(a, cus, st);
   else if (a_col && b_col) rc = launch8<false, 1, 1>(a, cus, st);
   else rc = launch8<false, 1, 0>(a, cus, st);
-  if (rc || a.S == 1) return rc;
-  const long long quads = (long long)batch * M * (N / 4);
-  const int grid = (int)std::min<long long>((quads + 255) / 256, 4LL * cus);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, (const float*)ws, a.S, batch, M, N, C, ldc,
-                     sC, epi, alpha, alpha_dev, alpha_dev2, (const bf16_t*)bias);
-  return (int)hipGetLastError();
+  return rc;
 }
 
 // k-slices ds2_gemm8 actually uses for a requested S (no empty slice)

@@ -33,27 +33,17 @@ TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
     # projections: persistent 128x256 (cfg 7) 84.2 / 196.3 us vs 87.1 / 200.8 (cfg 1), same box
     (7712, 4800, 800, False, False, 1): 7,     # projection, layers 1-4
     (7712, 4800, 2400, False, False, 1): 7,    # projection, layer 0
-    (7712, 800, 4800, False, True, 1): 2,
-    (7712, 2400, 4800, False, True, 1): 2,
+    # dx = dgx W on the K-contiguous W^T shadow (ops/rnn.py _transpose_async), persistent
+    # 128x256: 66.8 / 196 us (tools/bench_gemm_ours.py); gemm8 reading W column-major
+    # (split 2 / 1) 85 / 253 us
+    (7712, 800, 4800, False, False, 1): 7,
+    (7712, 2400, 4800, False, False, 1): 7,
     (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
 }
-# (N, K, a_col, b_col) of bf16 projections where the library (hipBLASLt) measured faster than
-# every configuration here (tools/bench_gemm_ours.py --only proj, MI355X, M = 7712): GRU-1280
-# (config 5) 153 vs 182 us (K = 1280) and 260 vs 325 us (K = 2400); GRU-1760 305 vs 340 and
-# 390 vs 446 us. In the step: config 5 23.42 vs 24.12-24.19 ms/step; the reference's
-# 7 x bi-ReLU-1760 (N = 3520) 21.70-21.76 vs 22.10-22.22 (same box, alternating).
-# matmul() declines them so the caller's library path runs (DS2_GEMM_CFG forces ours).
-LIBRARY_WINS = {(7680, 1280, False, False), (7680, 2400, False, False),
-                (10560, 1760, False, False), (10560, 2400, False, False),
-                (3520, 1760, False, False), (3520, 2400, False, False)}
 _FORCE = os.environ.get("DS2_GEMM_CFG")
-# DS2_GEMM selects which engine GEMM classes run here: "hip" (all), "torch" (none: library
-# GEMMs, A/B timing only) or a comma list of {proj, dx, wgrad}. Default "proj": measured in
-# the headline step on MI355X (profiles/r2_gemm_family.md) the forward projections win
-# against the TunableOp-tuned hipBLASLt picks (9.32 vs 9.41 ms/step), while the col-mode
-# (transposed-read) dx / weight-gradient kernels still lose (dx +0.42, wgrad +0.8 ms/step).
-# The FC head's GEMMs (FusedHeadCTC) always run here.
-_SPEC = os.environ.get("DS2_GEMM", "proj")
+# DS2_GEMM selects which engine GEMM classes run on the hand-written kernels: "hip" (all, the
+# default), "torch" (none: library GEMMs, A/B timing only) or a comma list of {proj, dx, wgrad}.
+_SPEC = os.environ.get("DS2_GEMM", "hip")
 _CLASSES = ({"proj", "dx", "wgrad"} if _SPEC == "hip" else set() if _SPEC == "torch"
             else {c.strip() for c in _SPEC.split(",") if c.strip()})
 
@@ -143,10 +133,16 @@ def _operand(t: torch.Tensor, row_if_unit_last: bool):
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
-           alpha: float = 1.0, bias: Optional[torch.Tensor] = None) -> bool:
+           alpha: float = 1.0, bias: Optional[torch.Tensor] = None, max_grid: int = 0,
+           splits: Optional[int] = None) -> bool:
     """out (=|+=) alpha * a @ b (+ bias) for 2-D (or batched 3-D) bf16 views of any unit-stride
     orientation: a [M, K], b [K, N]; out fp32 (store / accumulate) or bf16 (store, optional
-    bias). Returns False (nothing launched) when the shape or strides are not covered."""
+    bias). Returns False (nothing launched) when the shape or strides are not covered.
+
+    Routing (tools/bench_gemm8.py, MI355X): the headline's row-row projections keep their
+    measured csrc/gemm.hip persistent tile (TUNED); every other covered shape runs on
+    csrc/gemm8.hip — row-row projections, dx = dgx W with W read as stored (column-mode B),
+    and the column-column weight gradients with split-K sized to the CU count."""
     if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
         return False
     M, K = a.shape[-2], a.shape[-1]
@@ -156,10 +152,6 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
         return False
     A, a_col = oa          # a [M,K] unit-stride K -> row mode (A(m,k) = A[m*lda+k])
     B, b_col = ob          # b [K,N] unit-stride N -> col mode (B(n,k) = B[k*ldb+n])
-    if not supported(M, N, K, a_col, b_col):
-        return False
-    if _FORCE is None and (N, K, a_col, b_col) in LIBRARY_WINS:
-        return False
     for t in (A, B, out):
         if t.data_ptr() % 16 or (t.dim() >= 2 and t.stride(-2) % 8):
             return False
@@ -171,6 +163,13 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
         epi = 2 if accumulate else 1
         if bias is not None:
             return False
+    batch = A.shape[0] if A.dim() == 3 else 1
+    key = (M, N, K, a_col, b_col, batch)
+    if _FORCE is None and key not in TUNED and gemm8_supported(M, N, K, False, a_col, b_col):
+        gemm8(A, B, out, epi, alpha, bias, a_col=a_col, b_col=b_col, max_grid=max_grid, splits=splits)
+        return True
+    if not supported(M, N, K, a_col, b_col):
+        return False
     gemm(A, B, out, M, N, K, a_col, b_col, epi, alpha, bias)
     return True
 
@@ -201,39 +200,69 @@ def gemm8_supported(M: int, N: int, K: int, fp8: bool = False, a_col: bool = Fal
     return (a_col and b_col) or K % 32 == 0
 
 
+_MAX_SPLITS = int(os.environ.get("DS2_GEMM8_MAX_SPLITS", "8"))     # A/B: 1 turns split-K off
+
+
 def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_slice: int = 1024) -> int:
-    """k-slices so that tiles x slices covers the CUs: a 256^2 tile is one workgroup, and the
-    skinny shapes (dx at D = 800: 124 tiles, dW / dU: 76-80) would leave half the chip idle.
-    A slice keeps >= min_slice of K (the prologue / epilogue per unit is ~2 k-tiles)."""
+    """k-slices for a grid of few 256^2 tiles (dx at D = 800: 124 tiles, dW / dU: 76-80),
+    which would leave CUs idle: the split count that minimises the dispatch rounds per unit
+    of work, ceil(tiles * S / cus) / S, with a small per-slice cost for the reduction, each
+    slice >= min_slice of K (measured on the full chip: dW / dU 3 slices 93 / 98 us, 4 slices
+    — a second round — 137 / 141 us). cus: the CUs the launch may use (a capped grid beside
+    the persistent BPTT: 48 -> 5 rounds of 3 slices for 80 tiles)."""
     tiles = _cdiv(M, 256) * _cdiv(N, 256) * batch
-    best = 1
-    for s in range(1, 9):
-        if K // s < min_slice:
+    if cus >= 128 and 2 * tiles > cus:
+        return 1        # full chip, measured: dx D = 2400 (310 tiles) and dW D = 2400 (190) lose with any split
+    best, best_cost = 1, None
+    for s in range(1, _MAX_SPLITS + 1):
+        if s > 1 and K // s < min_slice:
             break
-        best = s
-        if tiles * s >= cus:
-            break
+        cost = _cdiv(tiles * s, cus) / s * (1.0 + 0.05 * (s - 1))
+        if best_cost is None or cost < best_cost - 1e-9:
+            best, best_cost = s, cost
     return best
 
 
 def gemm8(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = 0, alpha: float = 1.0,
           bias: Optional[torch.Tensor] = None, alpha_dev: Optional[torch.Tensor] = None,
           alpha_dev2: Optional[torch.Tensor] = None, a_col: bool = False, b_col: bool = False,
-          splits: Optional[int] = None) -> torch.Tensor:
+          splits: Optional[int] = None, max_grid: int = 0) -> torch.Tensor:
     """out (=, or += for epi 2) alpha * alpha_dev * alpha_dev2 * A @ B^T (+ bias) on the stored
     operands (see the section comment); out bf16 (epi 0) or fp32 (epi 1 / 2). splits=None picks
-    the k-slice count from the shape (gemm8_splits)."""
+    the k-slice count from the shape (gemm8_splits). max_grid > 0 caps the persistent grid
+    (workgroups loop over the units): a launch beside the persistent BPTT."""
     batch = A.shape[0] if A.dim() == 3 else 1
     M = A.shape[-1] if a_col else A.shape[-2]
     K = A.shape[-2] if a_col else A.shape[-1]
     N = B.shape[-1] if b_col else B.shape[-2]
+    cus = _dev_cus(A)
+    if max_grid > 0:
+        cus = min(cus, max_grid)
     if splits is None:
-        splits = gemm8_splits(M, N, K, batch, _dev_cus(A))
+        splits = gemm8_splits(M, N, K, batch, cus)
     C = _ext.ext()
     S = int(C.gemm8_splits(K, A.dtype == torch.float8_e4m3fn, splits)) if splits > 1 else 1
-    ws = torch.empty(S * batch * M * N, device=A.device, dtype=torch.float32) if S > 1 else None
-    C.gemm8(A, B, out, bias, epi, float(alpha), alpha_dev, alpha_dev2, a_col, b_col, S, ws)
+    ws = cnt = None
+    if S > 1:
+        ws = torch.empty(S * batch * M * N, device=A.device, dtype=torch.float32)
+        cnt = _tile_counters(A.device, _cdiv(M, 256) * _cdiv(N, 256) * batch)
+    C.gemm8(A, B, out, bias, epi, float(alpha), alpha_dev, alpha_dev2, a_col, b_col, S, ws, cnt, max_grid)
     return out
+
+
+_counters: Dict[Tuple[int, int], torch.Tensor] = {}
+
+
+def _tile_counters(dev: torch.device, n: int) -> torch.Tensor:
+    """Split-K arrival counters of the current stream (zero between launches: each launch's
+    last-arriving slices reset theirs). One buffer per stream, since launches on different
+    streams may run at the same time; a larger grid gets a fresh zeroed buffer."""
+    key = (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _counters.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.zeros(max(n, 4096), device=dev, dtype=torch.int32)
+        _counters[key] = buf
+    return buf
 
 
 def linear8(x2: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None, alpha: float = 1.0,

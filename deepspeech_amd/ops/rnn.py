@@ -62,6 +62,8 @@ class RnnPlan:
 
 RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))   # diagnostic timing switches only
 _FUSE_DIRSUM = True        # module switch: tests compare the fused direction sum with torch.add
+_DU_GRID = int(os.environ.get("DS2_DU_GRID", "0"))
+_DU_SPLITS = int(os.environ.get("DS2_DU_SPLITS", "2"))       # measured: 2 beside the BPTT (1: 9.21-9.29, 3: 9.09-9.15, 2: 8.98-9.03 ms/step)
 
 
 LDS_BYTES = 160 * 1024
@@ -240,6 +242,25 @@ def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], al
     if b16 is None:
         return torch.mm(x2, W16.t()) * alpha if alpha != 1.0 else torch.mm(x2, W16.t())
     return torch.addmm(b16, x2, W16.t(), alpha=alpha)
+
+
+def _transpose_async(W16: torch.Tensor, side) -> tuple:
+    """(W16^T contiguous bf16, event) for the input-gradient GEMM: written on the
+    weight-gradient side stream during the forward (idle there), so the backward's dx GEMM
+    reads a K-contiguous row-major W^T (csrc/gemm.hip / gemm8 row-row: faster than reading
+    W column-major) at no cost on the critical path."""
+    wT = torch.empty(W16.shape[1], W16.shape[0], device=W16.device, dtype=torch.bfloat16)
+    C = _ext.ext()
+    if side is None:
+        C.transpose_bf16(W16, wT)
+        return wT, None
+    side.wait_stream(torch.cuda.current_stream(W16.device))
+    with torch.cuda.stream(side):
+        wT.record_stream(side)
+        C.transpose_bf16(W16, wT)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    return wT, ev
 
 
 def _mm_bf16(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -507,10 +528,14 @@ class FusedBiLayer(torch.autograd.Function):
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
+        wT = ev = None
+        if x.is_cuda and GM.enabled("dx") and W16.shape[1] % 8 == 0 and W16.shape[0] % 8 == 0:
+            wT, ev = _transpose_async(W16, wgrad_stream(x.device, arena_of(W_f)))
         y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
         dev = x.device
         ctx.save_for_backward(x16, lens, W16, U[0], U[1] if U[1] is not None else torch.empty(0, device=dev),
                               hx, hs, gates)
+        ctx.wT, ctx.wT_ready = wT, ev
         ctx.params = (W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b)
         ctx.plan = plan
         ctx.alpha = alpha
@@ -533,7 +558,15 @@ class FusedBiLayer(torch.autograd.Function):
         dgx, dgh, parts = _run_bwd(dy, lens, [U_f16, U_b16 if d1 else None], hx, hs, gates, plan,
                                    plan.ndir * GH, dgx_scale=ctx.alpha)
         dgx2 = dgx.view(T * N, plan.ndir * GH)
-        dx = _mm_bf16(dgx2, W16).view(T, N, D) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.wT is not None:
+                if ctx.wT_ready is not None:
+                    torch.cuda.current_stream(dgx.device).wait_event(ctx.wT_ready)
+                dx = _mm_bf16(dgx2, ctx.wT.t()).view(T, N, D)
+            else:
+                dx = _mm_bf16(dgx2, W16).view(T, N, D)
+        ctx.wT = ctx.wT_ready = None
         # ---- weight gradients (off the critical path) ----
         # only arena-managed weights (gradients written to main_grad, nothing returned to
         # autograd) may be produced on another stream; the Trainer joins it before Adam
@@ -584,20 +617,35 @@ class FusedBiLayer(torch.autograd.Function):
         ugrp = arena.group_view([U_f, U_b], "grad") if (arena is not None and d1) else None
         if ugrp is not None and arena.first_write(U_f) and arena.first_write(U_b):
             # both directions' dU_d = dgh_d^T h_d as ONE batched GEMM into the packed slots
-            def du(ugrp=ugrp, dgh=dgh, hx=hx):
+            # beside the next layer's persistent BPTT (200 of the 256 CUs) the GEMM gets a
+            # capped grid: fewer, longer-lived workgroups interfere less with the latency-bound
+            # recurrence (DS2_DU_GRID; 0 = the whole chip); the bottom layer's dU (main-stream
+            # tail, nothing beside it) takes the whole chip
+            sch = arena.wgrad
+            on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
+            defer = sch.defer_input and on_side and sch.defer_du and ctx.idx >= sch.min_layer
+            beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
+            grid = _DU_GRID if beside else 0
+            splits = (_DU_SPLITS or None) if beside else None
+
+            def du(ugrp=ugrp, dgh=dgh, hx=hx, grid=grid, splits=splits):
                 steps = dgh.shape[1]
                 g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
                 h3 = hx[:, :steps].reshape(2, steps * plan.NP, plan.H)
                 out = ugrp.view(2, GH, plan.H)
-                if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out)):
+                if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out, max_grid=grid, splits=splits)):
                     try:
                         torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
                     except (RuntimeError, TypeError):
                         out.copy_(torch.bmm(g3, h3))
                 arena.grad_done(U_f, U_b)
-            sch = arena.wgrad
-            on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
-            if sch.defer_input and on_side and ctx.idx == 0 and sch.tail_du:
+            if defer:
+                # every weight gradient after the BPTT chain: a GEMM beside the latency-bound
+                # persistent BPTT slows it by 27-48 % (its L2 / fabric / clock share), more
+                # than the tail gains back (WgradScheduler, DS2_DEFER_DU)
+                sch.deferred.append(du)
+                sch.queue_end_of_backward()
+            elif sch.defer_input and on_side and ctx.idx == 0 and sch.tail_du:
                 # the side stream already carries dW_0 + every deferred dW and ends after the
                 # conv front-end's backward on the main stream: balance by issuing the
                 # bottom layer's dU on the main stream behind the front-end (WgradScheduler.join)
@@ -641,6 +689,7 @@ class WgradScheduler:
         self.defer_input = False
         self.min_layer = int(os.environ.get("DS2_DEFER_MIN_LAYER", "1"))
         self.tail_du = os.environ.get("DS2_TAIL_DU", "1") == "1"
+        self.defer_du = os.environ.get("DS2_DEFER_DU", "0") == "1"
         self.deferred = []
         self.main_tail = []        # GEMMs issued on the main stream once the whole backward is queued
         self._eob_queued = False

@@ -210,3 +210,36 @@ def test_gemm8_split_reproducible():
     o1 = G.gemm8(a, b, torch.empty(4800, 800, device=DEV), 1, 1.0, a_col=True, b_col=True, splits=4)
     o2 = G.gemm8(a, b, torch.empty(4800, 800, device=DEV), 1, 1.0, a_col=True, b_col=True, splits=4)
     assert torch.equal(o1, o2)
+
+
+@pytest.mark.parametrize("R,C", [(4800, 800), (4800, 2400), (72, 136), (8, 8), (1000, 24)])
+def test_transpose_bf16(R, C):
+    """csrc/fill.hip transpose (the dx GEMM's K-contiguous W^T shadow): exact, ragged tiles."""
+    from deepspeech_amd.ops import _ext
+    torch.manual_seed(R + C)
+    w = torch.randn(R, C, device=DEV).to(BF)
+    out = torch.full((C, R), float("nan"), device=DEV, dtype=BF)
+    _ext.ext().transpose_bf16(w, out)
+    assert torch.equal(out, w.t())
+
+
+def test_gemm8_split_counters_reset_and_streams():
+    """Split-K tile counters are left at zero by every launch (a second launch on the same
+    buffer is correct), and launches on two streams use separate counter buffers."""
+    torch.manual_seed(6)
+    a = torch.randn(7712, 2400, device=DEV).to(BF)
+    b = torch.randn(7712, 800, device=DEV).to(BF)
+    ref = a.float().t() @ b.float()
+    s2 = torch.cuda.Stream()
+    outs = []
+    for i in range(3):
+        st = s2 if i == 1 else torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            outs.append(G.gemm8(a, b, torch.empty(2400, 800, device=DEV), 1, 1.0, a_col=True, b_col=True,
+                                splits=3))
+    torch.cuda.synchronize()
+    for o in outs:
+        assert _rel(o, ref) < 2e-5 * 7712 ** 0.5 + 1e-4
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[0], outs[1])
+    for buf in G._counters.values():
+        assert int(buf.abs().sum()) == 0
