@@ -103,6 +103,8 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
               int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
               unsigned* cnt, int cus, hipStream_t st);
 int ds2_gemm8_splits(int K, int fp8, int S);
+int ds2_gemm8_group(int np, const void* const* A, const void* const* B, void* const* C, float* const* ws,
+                    unsigned* const* cnt, const int* dims, int a_col, int b_col, int cus, hipStream_t st);
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
                    void* a8, void* b8, float* part, float* scales, hipStream_t st);
 int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st);
@@ -716,6 +718,64 @@ void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, dou
         "gemm8");
 }
 
+// A group of independent bf16 GEMMs of the same operand modes in one launch (one grid over all
+// their tiles): C[i] (fp32, epi[i] 1 store / 2 accumulate) = A[i] B[i]^T, split-K S[i] through
+// consecutive ranges of one workspace ws (S[i] * M * N floats each) and one zeroed counter
+// buffer cnt (tiles each).
+void gemm8_group(std::vector<at::Tensor> A, std::vector<at::Tensor> B, std::vector<at::Tensor> C,
+                 std::vector<int64_t> epi, std::vector<int64_t> splits, bool a_col, bool b_col, OptT ws, OptT cnt,
+                 int64_t max_grid) {
+  const size_t np = A.size();
+  TORCH_CHECK(np >= 1 && np <= 24 && B.size() == np && C.size() == np && epi.size() == np && splits.size() == np,
+              "gemm8_group: 1..24 members, one A, B, C, epi, splits each");
+  std::vector<const void*> pa(np), pb(np);
+  std::vector<void*> pc(np);
+  std::vector<float*> pw(np, nullptr);
+  std::vector<unsigned*> pn(np, nullptr);
+  std::vector<int> dims(8 * np);
+  int64_t wofs = 0, cofs = 0;
+  for (size_t i = 0; i < np; ++i) {
+    const at::Tensor &a = A[i], &b = B[i], &c = C[i];
+    TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kFloat,
+                "gemm8_group: bf16 operands, fp32 C");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm8_group: 2-D members");
+    for (const at::Tensor* t : {&a, &b, &c}) {
+      TORCH_CHECK(t->is_cuda() && t->stride(-1) == 1, "gemm8_group: unit-stride rows");
+      TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "gemm8_group: 16-B aligned operands");
+    }
+    const int64_t M = a_col ? a.size(1) : a.size(0), K = a_col ? a.size(0) : a.size(1);
+    const int64_t N = b_col ? b.size(1) : b.size(0), Kb = b_col ? b.size(0) : b.size(1);
+    TORCH_CHECK(Kb == K && c.size(0) == M && c.size(1) == N, "gemm8_group: shapes of member ", i);
+    TORCH_CHECK(epi[i] == 1 || epi[i] == 2, "gemm8_group: epi 1 or 2");
+    const int S = ds2_gemm8_splits((int)K, 0, (int)std::max<int64_t>(1, splits[i]));
+    if (S > 1) {
+      const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+      TORCH_CHECK(ws.has_value() && ws->defined() && ws->is_cuda() && ws->scalar_type() == at::kFloat &&
+                      ws->numel() >= wofs + (int64_t)S * M * N,
+                  "gemm8_group: split-K workspace too small");
+      TORCH_CHECK(cnt.has_value() && cnt->defined() && cnt->is_cuda() && cnt->scalar_type() == at::kInt &&
+                      cnt->numel() >= cofs + tiles,
+                  "gemm8_group: split-K counters too small");
+      pw[i] = ws->data_ptr<float>() + wofs;
+      TORCH_CHECK((reinterpret_cast<uintptr_t>(pw[i]) & 15) == 0, "gemm8_group: 16-B aligned workspace");
+      pn[i] = reinterpret_cast<unsigned*>(cnt->data_ptr<int>()) + cofs;
+      wofs += (int64_t)S * M * N;
+      cofs += tiles;
+    }
+    pa[i] = a.data_ptr();
+    pb[i] = b.data_ptr();
+    pc[i] = c.data_ptr();
+    int* d = dims.data() + 8 * i;
+    d[0] = (int)M; d[1] = (int)N; d[2] = (int)K;
+    d[3] = (int)a.stride(0); d[4] = (int)b.stride(0); d[5] = (int)c.stride(0);
+    d[6] = (int)epi[i]; d[7] = S;
+  }
+  check(ds2_gemm8_group((int)np, pa.data(), pb.data(), pc.data(), pw.data(), pn.data(), dims.data(), a_col ? 1 : 0,
+                        b_col ? 1 : 0, max_grid > 0 ? (int)std::min<int64_t>(max_grid, dev_cus()) : dev_cus(),
+                        cur_stream()),
+        "gemm8_group");
+}
+
 // --------------------------------------------------------------------------- GEMM (csrc/gemm.hip)
 // Operands are given as (possibly batched) matrices whose innermost dimension is unit-stride;
 // the leading dimension is the row stride. a_col / b_col select the column-major reading of
@@ -900,6 +960,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("alpha") = 1.0, py::arg("alpha_dev") = py::none(), py::arg("alpha_dev2") = py::none(),
         py::arg("a_col") = false, py::arg("b_col") = false, py::arg("splits") = 1, py::arg("ws") = py::none(),
         py::arg("cnt") = py::none(), py::arg("max_grid") = 0);
+  m.def("gemm8_group", &gemm8_group, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("epi"), py::arg("splits"),
+        py::arg("a_col"), py::arg("b_col"), py::arg("ws"), py::arg("cnt"), py::arg("max_grid"));
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
   m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),

@@ -62,6 +62,7 @@
 // tall-skinny shapes (dx with D = 800: 124 256^2 tiles; dW / dU: 76-80) that would
 // otherwise leave most CUs idle.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -73,22 +74,32 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
-struct G8Args {
+// one GEMM of a launch. A launch holds one problem, the members of a batched GEMM, or a
+// group of unrelated GEMMs of the same operand modes (the deferred weight gradients of every
+// recurrent layer: one grid over all their tiles instead of one launch each)
+struct G8Prob {
   const unsigned char* A;
   const unsigned char* B;
   void* C;
-  const bf16_t* bias;
-  const float* alpha_dev;
-  const float* alpha_dev2;
-  long long sA, sB, sC;   // batch strides: bytes (A, B), elements (C)
+  float* ws;              // S > 1: fp32 partials [S][M][N]
+  unsigned* cnt;          // S > 1: per-tile arrival counters [tiles], zero between launches
   int M, N, Kb;           // Kb: reduction length in BYTES (2K for bf16, K for fp8)
   int lda, ldb, ldc;      // lda / ldb in bytes, ldc in elements
   int epi;
-  float alpha;
   int S, kps;             // split-K: S k-slices of kps k-tiles each (S = 1: no split)
-  float* ws;              // S > 1: fp32 partials [S][batch][M][N]
-  unsigned* cnt;          // S > 1: per-tile arrival counters [batch][tiles], zero between launches
-  int batch;
+  int ustart;             // first work unit of this problem in the launch
+};
+
+constexpr int G8_MAXP = 24;
+
+struct G8Args {
+  G8Prob p[G8_MAXP];
+  const bf16_t* bias;
+  const float* alpha_dev;
+  const float* alpha_dev2;
+  float alpha;
+  int np, total;          // problems, work units of all problems
+  int stagger;            // waves 4-7 run the k-loop half a phase behind waves 0-3
 };
 
 constexpr int NWV = 8;
@@ -160,13 +171,30 @@ __device__ __forceinline__ void col_frag_offsets(unsigned& o0, unsigned& o1, int
   o1 = (unsigned)((k0 + 4) * 256 + ((c ^ csw(k0 + 4)) << 4) + 8 * (p & 1));
 }
 
-__device__ __forceinline__ s16x4 rdtr(const unsigned char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)p);
+// The transposed read as inline asm: hipcc puts an s_waitcnt vmcnt(0) in front of every
+// __builtin_amdgcn_ds_read_tr16_b64 (it cannot tell the read from the in-flight LDS-DMA
+// writes of later k-tiles), which drained the glds pipeline in every phase of a column-mode
+// GEMM (measured: col-col at ~60 % of the row-row kernel's rate). The compiler then also does
+// not wait for these results: the k-loop retires them with an explicit lgkmcnt(0) before the
+// phase's MFMA barrier. addr: LDS byte address (lds_addr), OFF: immediate byte offset.
+template <int OFF>
+__device__ __forceinline__ s16x4 rdtr(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
 }
 
-__device__ __forceinline__ i32x8 col_frag(const unsigned char* half, unsigned o0, unsigned o1) {
-  const s16x4 a = rdtr(half + o0), b = rdtr(half + o1);
-  const s16x4 c = rdtr(half + o0 + 8192), d = rdtr(half + o1 + 8192);
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// fragment of the col half-tile at LDS byte offset HOFF (< 48 KB + 8 KB: immediates) from the
+// lane's two transposed-read addresses a0 / a1 (buffer base included)
+template <int HOFF>
+__device__ __forceinline__ i32x8 col_frag(unsigned a0, unsigned a1) {
+  const s16x4 a = rdtr<HOFF>(a0), b = rdtr<HOFF>(a1);
+  const s16x4 c = rdtr<HOFF + 8192>(a0), d = rdtr<HOFF + 8192>(a1);
   const i32x4 lo = __builtin_bit_cast(i32x4, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
   const i32x4 hi = __builtin_bit_cast(i32x4, __builtin_shufflevector(c, d, 0, 1, 2, 3, 4, 5, 6, 7));
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -233,22 +261,11 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;         // wave's 64-row x 32-col share of a quadrant
-  const int ntm = (g.M + 255) / 256, ntn = (g.N + 255) / 256;
-  const int S = g.S;
-  const int total = ntm * ntn * S, tx = (total + 7) >> 3, xg = blockIdx.x & 7;
+  // work units of all problems, numbered problem by problem; XCD x = blockIdx % 8 walks the
+  // contiguous range [x*Tx, (x+1)*Tx)
+  const int total = g.total, tx = (total + 7) >> 3, xg = blockIdx.x & 7;
   int id = xg * tx + (blockIdx.x >> 3);
   const int id_end = min(total, (xg + 1) * tx), id_step = gridDim.x >> 3;
-  const int nkt_all = (g.Kb + ROWB - 1) / ROWB;
-  // a last k-tile of 32 bf16 with a row-mode operand: its second k-substep holds the next
-  // row's data there (a col-mode operand's k-rows past K load as zeros), so it is skipped
-  const bool ragged = !FP8 && !(AC && BC) && (g.Kb % ROWB) != 0;
-  const int K = g.Kb / (FP8 ? 1 : 2);
-  // bounds of the buffer resources: a row-mode operand holds its rows, a col-mode one K k-rows
-  // (k-rows past K then load as zeros)
-  const __amdgpu_buffer_rsrc_t rsA =
-      make_rsrc(g.A + (size_t)blockIdx.z * g.sA, (unsigned)((size_t)(AC ? K : g.M) * g.lda));
-  const __amdgpu_buffer_rsrc_t rsB =
-      make_rsrc(g.B + (size_t)blockIdx.z * g.sB, (unsigned)((size_t)(BC ? K : g.N) * g.ldb));
   float alpha = g.alpha;
   if (g.alpha_dev) alpha *= *g.alpha_dev;
   if (g.alpha_dev2) alpha *= *g.alpha_dev2;
@@ -260,38 +277,64 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
   // two offsets per fragment (the swizzle depends on the column block).
   const int sw = rsw(r16);
   const int c_lo = (g16 ^ sw) << 4, c_hi = ((4 + g16) ^ sw) << 4;
+  // col mode: LDS byte addresses of the lane's transposed reads in buffer 0
   unsigned ca0[4], ca1[4], cb0[2], cb1[2];
+  const unsigned lds0 = lds_addr(smem);
   if constexpr (AC) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) col_frag_offsets(ca0[i], ca1[i], wr * 4 + i, lane);
+    for (int i = 0; i < 4; ++i) {
+      col_frag_offsets(ca0[i], ca1[i], wr * 4 + i, lane);
+      ca0[i] += lds0;
+      ca1[i] += lds0;
+    }
   }
   if constexpr (BC) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) col_frag_offsets(cb0[j], cb1[j], wc * 2 + j, lane);
+    for (int j = 0; j < 2; ++j) {
+      col_frag_offsets(cb0[j], cb1[j], wc * 2 + j, lane);
+      cb0[j] += lds0 + 2 * HALF;
+      cb1[j] += lds0 + 2 * HALF;
+    }
   }
 
+  int q = 0;                                         // problem of unit id (ids only grow)
   for (; id < id_end; id += id_step) {
-    const int tile = id / S, ks = id - tile * S;
+    while (q + 1 < g.np && id >= g.p[q + 1].ustart) ++q;
+    q = __builtin_amdgcn_readfirstlane(q);
+    const G8Prob& P = g.p[q];
+    const int M = P.M, N = P.N, S = P.S;
+    const int ntm = (M + 255) / 256, ntn = (N + 255) / 256;
+    const int nkt_all = (P.Kb + ROWB - 1) / ROWB;
+    // a last k-tile of 32 bf16 with a row-mode operand: its second k-substep holds the next
+    // row's data there (a col-mode operand's k-rows past K load as zeros), so it is skipped
+    const bool ragged = !FP8 && !(AC && BC) && (P.Kb % ROWB) != 0;
+    const int K = P.Kb / (FP8 ? 1 : 2);
+    // bounds of the buffer resources: a row-mode operand holds its rows, a col-mode one K
+    // k-rows (k-rows past K then load as zeros)
+    const __amdgpu_buffer_rsrc_t rsA = make_rsrc(P.A, (unsigned)((size_t)(AC ? K : M) * P.lda));
+    const __amdgpu_buffer_rsrc_t rsB = make_rsrc(P.B, (unsigned)((size_t)(BC ? K : N) * P.ldb));
+    const int uid = id - P.ustart;
+    const int tile = uid / S, ks = uid - tile * S;
     const int gsz = GROUP_M * ntn, grp = tile / gsz, first_m = grp * GROUP_M;
     const int gm = min(ntm - first_m, GROUP_M), within = tile - grp * gsz;
     const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
-    const int kt0 = ks * g.kps;                      // this unit's k-tiles [kt0, kt0 + nkt)
-    const int nkt = max(0, min(nkt_all - kt0, g.kps));
+    const int kt0 = ks * P.kps;                      // this unit's k-tiles [kt0, kt0 + nkt)
+    const int nkt = max(0, min(nkt_all - kt0, P.kps));
 
     unsigned oA0[2], oA1[2], oB0[2], oB1[2];
     if constexpr (AC) {
-      half_offsets_col(oA0, g.lda, m0, g.M, wave, lane);
-      half_offsets_col(oA1, g.lda, m0 + 128, g.M, wave, lane);
+      half_offsets_col(oA0, P.lda, m0, M, wave, lane);
+      half_offsets_col(oA1, P.lda, m0 + 128, M, wave, lane);
     } else {
-      half_offsets(oA0, g.lda, m0, g.M, wave, lane);
-      half_offsets(oA1, g.lda, m0 + 128, g.M, wave, lane);
+      half_offsets(oA0, P.lda, m0, M, wave, lane);
+      half_offsets(oA1, P.lda, m0 + 128, M, wave, lane);
     }
     if constexpr (BC) {
-      half_offsets_col(oB0, g.ldb, n0, g.N, wave, lane);
-      half_offsets_col(oB1, g.ldb, n0 + 128, g.N, wave, lane);
+      half_offsets_col(oB0, P.ldb, n0, N, wave, lane);
+      half_offsets_col(oB1, P.ldb, n0 + 128, N, wave, lane);
     } else {
-      half_offsets(oB0, g.ldb, n0, g.N, wave, lane);
-      half_offsets(oB1, g.ldb, n0 + 128, g.N, wave, lane);
+      half_offsets(oB0, P.ldb, n0, N, wave, lane);
+      half_offsets(oB1, P.ldb, n0 + 128, N, wave, lane);
     }
     // half-tile h of local k-tile t into buffer t & 1: h 0/1 = A rows 0-127 / 128-255, 2/3 = B.
     // A k-tile advances 128 bytes along a row-mode operand's rows, 64 k-rows of a col one.
@@ -299,18 +342,18 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
       if (t >= nkt) return;
       unsigned char* dst = smem + (t & 1) * BUFB + h * HALF;
       const int kt = kt0 + t;
-      const unsigned ka = AC ? (unsigned)(kt * 64) * (unsigned)g.lda : (unsigned)(kt * ROWB);
-      const unsigned kb = BC ? (unsigned)(kt * 64) * (unsigned)g.ldb : (unsigned)(kt * ROWB);
+      const unsigned ka = AC ? (unsigned)(kt * 64) * (unsigned)P.lda : (unsigned)(kt * ROWB);
+      const unsigned kb = BC ? (unsigned)(kt * 64) * (unsigned)P.ldb : (unsigned)(kt * ROWB);
       if (h == 0) stage_half(dst, rsA, oA0, ka, wave);
       else if (h == 1) stage_half(dst, rsA, oA1, ka, wave);
       else if (h == 2) stage_half(dst, rsB, oB0, kb, wave);
       else stage_half(dst, rsB, oB1, kb, wave);
     };
-    auto read_a = [&](Frag (&a)[4], int buf, int qm) {
+    auto read_a = [&](Frag (&a)[4], auto BUF, auto QM) {
+      constexpr int buf = decltype(BUF)::value, qm = decltype(QM)::value;
       if constexpr (AC) {
-        const unsigned char* h = smem + buf * BUFB + qm * HALF;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[i].v = col_frag(h, ca0[i], ca1[i]);
+        for (int i = 0; i < 4; ++i) a[i].v = col_frag<qm * HALF>(ca0[i] + buf * BUFB, ca1[i] + buf * BUFB);
       } else {
         const unsigned char* h = smem + (wr * 64 + r16) * ROWB + buf * BUFB + qm * HALF;
 #pragma unroll
@@ -318,11 +361,11 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
           a[i].v = cat(*(const i32x4*)(h + i * 16 * ROWB + c_lo), *(const i32x4*)(h + i * 16 * ROWB + c_hi));
       }
     };
-    auto read_b = [&](Frag (&b)[2], int buf, int qn) {
+    auto read_b = [&](Frag (&b)[2], auto BUF, auto QN) {
+      constexpr int buf = decltype(BUF)::value, qn = decltype(QN)::value;
       if constexpr (BC) {
-        const unsigned char* h = smem + buf * BUFB + (2 + qn) * HALF;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[j].v = col_frag(h, cb0[j], cb1[j]);
+        for (int j = 0; j < 2; ++j) b[j].v = col_frag<qn * HALF>(cb0[j] + buf * BUFB, cb1[j] + buf * BUFB);
       } else {
         const unsigned char* h = smem + 2 * HALF + (wc * 32 + r16) * ROWB + buf * BUFB + qn * HALF;
 #pragma unroll
@@ -356,14 +399,18 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
     // half-tiles (wait: 0 none, 1 = vmcnt(4) if half-tile st exists, else vmcnt(0)).
     auto phase = [&](auto BUF, auto QM, auto QN, auto RA, auto RB, int st, int sh, int wait, bool full) {
       constexpr int bf = decltype(BUF)::value, qm = decltype(QM)::value, qn = decltype(QN)::value;
-      if constexpr (decltype(RB)::value) read_b(fb, bf, qn);
+      if constexpr (decltype(RB)::value) read_b(fb, BUF, QN);
       if constexpr (decltype(RA)::value && decltype(RB)::value) __builtin_amdgcn_sched_barrier(0);
-      if constexpr (decltype(RA)::value) read_a(fa, bf, qm);
+      if constexpr (decltype(RA)::value) read_a(fa, BUF, QM);
       stage(st, sh);
       if (wait) {
         if (st < nkt) wait_vm<4>();
         else wait_vm<0>();
       }
+      // staggered: the other wave group still reads this phase's half-tiles after this
+      // barrier, so a wave's reads are retired before it (WAR of the 1-phase restage)
+      // (column mode: the asm transposed reads are waited for here in any case)
+      if (AC || BC || g.stagger) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bar();
       __builtin_amdgcn_sched_barrier(0);
       mfma_tile<FP8, 0>(acc[qm][qn], fa, fb, full);
@@ -374,6 +421,12 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
     using I1 = std::integral_constant<int, 1>;
     using T_ = std::true_type;
     using F_ = std::false_type;
+    // stagger: one extra barrier for waves 4-7 before the k-loop and for waves 0-3 after it,
+    // so every barrier of the loop pairs group 0's phase p "after MFMA" with group 1's phase p
+    // "before MFMA": one group's LDS reads and glds issue run under the other's MFMAs (the SIMD
+    // partners w and w + 4 alternate roles) instead of both bursting together
+    const bool stag = g.stagger != 0;
+    if (stag && wr == 1) bar();
     int t0 = 0;
     for (; t0 + 1 < nkt; t0 += 2) {
       const bool full1 = !(ragged && kt0 + t0 + 1 == nkt_all - 1);
@@ -395,22 +448,22 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
       phase(I0{}, I1{}, I1{}, T_{}, F_{}, nkt, 0, 0, full0);
       phase(I0{}, I1{}, I0{}, F_{}, T_{}, nkt, 0, 0, full0);
     }
+    if (stag && wr == 0) bar();
 
     // epilogue: lane holds C[m][n .. n+3], m = .. + lane % 16, n = .. + 4 (lane / 16). A
     // split unit stores its raw fp32 partial into workspace slice ks (fp32, ld = N).
     const bool part = S > 1;
     // the final epilogue: lane's fragment (qm, qn, j, i) holds C[m][n .. n+3]
     auto finish = [&](auto&& value) {
-      const int epi = g.epi;
-      const size_t esz = epi == 0 ? 2 : 4;
-      char* Cz = (char*)g.C + (size_t)blockIdx.z * g.sC * esz;
+      const int epi = P.epi;
+      char* Cz = (char*)P.C;
       const bool has_bias = epi == 0 && g.bias != nullptr;
 #pragma unroll
       for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g16;
-          if (n >= g.N) continue;
+          if (n >= N) continue;
           float bv[4] = {0.f, 0.f, 0.f, 0.f};
           if (has_bias) {
             const uint2 b2 = *(const uint2*)(g.bias + n);
@@ -422,9 +475,9 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int m = m0 + qm * 128 + wr * 64 + 16 * i + r16;
-              if (m >= g.M) continue;
+              if (m >= M) continue;
               const f32x4 v = value(qm, qn, j, i, m, n);
-              const size_t off = (size_t)m * g.ldc + n;
+              const size_t off = (size_t)m * P.ldc + n;
               if (epi == 0) {
                 const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[0]) | ((unsigned)f2bf(alpha * v[1] + bv[1]) << 16);
                 const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[2]) | ((unsigned)f2bf(alpha * v[3] + bv[3]) << 16);
@@ -453,29 +506,28 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
       // (deterministic whatever the arrival order), then resets the counter for the next
       // launch. No agent-scope release / acquire fence: on gfx950 those write back / flush
       // this XCD's whole L2, which beside the persistent BPTT cost ~20 % of the GEMM.
-      const unsigned slab = (unsigned)((size_t)g.M * g.N * 4);
-      const __amdgpu_buffer_rsrc_t rsw_ = make_rsrc(g.ws, (unsigned)(slab * (size_t)S * g.batch));
-      const unsigned zoff = (unsigned)blockIdx.z * slab, sstride = (unsigned)g.batch * slab;
+      const unsigned slab = (unsigned)((size_t)M * N * 4);
+      const __amdgpu_buffer_rsrc_t rsw_ = make_rsrc(P.ws, (unsigned)(slab * (size_t)S));
 #pragma unroll
       for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g16;
-          if (n >= g.N) continue;
+          if (n >= N) continue;
 #pragma unroll
           for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int m = m0 + qm * 128 + wr * 64 + 16 * i + r16;
-              if (m >= g.M) continue;
-              store_sc1_b128(rsw_, (unsigned)ks * sstride + zoff + (unsigned)((m * g.N + n) * 4),
+              if (m >= M) continue;
+              store_sc1_b128(rsw_, (unsigned)ks * slab + (unsigned)((m * N + n) * 4),
                              __builtin_bit_cast(i32x4, acc[qm][qn][j][i]));
             }
         }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       int* flag = (int*)smem;                       // LDS is free: the k-loop has finished
-      unsigned* cnt = g.cnt + (size_t)blockIdx.z * ntm * ntn + tile;
+      unsigned* cnt = P.cnt + tile;
       if (tid == 0) {
         const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = prev == (unsigned)(S - 1);
@@ -487,9 +539,9 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
       __syncthreads();                              // flag read before the next prologue's glds
       if (last)
         finish([&](int, int, int, int, int m, int n) {
-          const unsigned off = zoff + (unsigned)((m * g.N + n) * 4);
+          const unsigned off = (unsigned)((m * N + n) * 4);
           f32x4 v = __builtin_bit_cast(f32x4, load_sc1_b128(rsw_, off));
-          for (int s2 = 1; s2 < S; ++s2) v += __builtin_bit_cast(f32x4, load_sc1_b128(rsw_, off + s2 * sstride));
+          for (int s2 = 1; s2 < S; ++s2) v += __builtin_bit_cast(f32x4, load_sc1_b128(rsw_, off + s2 * slab));
           return v;
         });
     }
@@ -506,12 +558,61 @@ int launch8(const G8Args& a, int cus, hipStream_t st) {
     DS2_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
     attr = true;
   }
-  const int units = ((a.M + 255) / 256) * ((a.N + 255) / 256) * a.S;
-  int grid = min(cus, (units + 7) & ~7);          // cus: the CU budget (device CUs or a cap)
+  int grid = min(cus, (a.total + 7) & ~7);          // cus: the CU budget (device CUs or a cap)
   grid = max(8, grid & ~7);
-  hipLaunchKernelGGL(kern, dim3(grid, 1, a.batch), dim3(NTHR), LDS_BYTES, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), LDS_BYTES, st, a);
   return (int)hipGetLastError();
 }
+
+// validate one problem and fill its table entry (units from ustart); 0 or a hipError_t
+int fill_prob(G8Prob& p, const void* A, const void* B, void* C, float* ws, unsigned* cnt, int M, int N, int K,
+              int lda, int ldb, int ldc, int fp8, int a_col, int b_col, int epi, int S, int ustart) {
+  const int es = fp8 ? 1 : 2;
+  if (M <= 0 || N <= 0 || K <= 0 || N % 4 != 0 || S < 1) return (int)hipErrorInvalidValue;
+  if (fp8 && (a_col || b_col || K % 128 != 0)) return (int)hipErrorInvalidValue;
+  if (!fp8 && (!a_col || !b_col) && K % 32 != 0) return (int)hipErrorInvalidValue;
+  if ((a_col && M % 8) || (b_col && N % 8)) return (int)hipErrorInvalidValue;
+  if (((lda * es) % 16) || ((ldb * es) % 16) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16))
+    return (int)hipErrorInvalidValue;
+  // 32-bit buffer offsets: each operand under 2 GB, a split's workspace too
+  if ((long long)(a_col ? K : M) * lda * es >= (1LL << 31) || (long long)(b_col ? K : N) * ldb * es >= (1LL << 31))
+    return (int)hipErrorInvalidValue;
+  if (epi < 0 || epi > 2) return (int)hipErrorInvalidValue;
+  const int nkt = (K * es + ROWB - 1) / ROWB;
+  p.kps = (nkt + S - 1) / S;
+  p.S = (nkt + p.kps - 1) / p.kps;                // no empty slice
+  if (p.S > 1 && (!ws || !cnt || (long long)M * N * 4 * p.S >= (1LL << 32))) return (int)hipErrorInvalidValue;
+  p.A = (const unsigned char*)A;
+  p.B = (const unsigned char*)B;
+  p.C = C;
+  p.ws = ws;
+  p.cnt = cnt;
+  p.M = M; p.N = N; p.Kb = K * es;
+  p.lda = lda * es; p.ldb = ldb * es; p.ldc = ldc;
+  p.epi = epi;
+  p.ustart = ustart;
+  return 0;
+}
+
+int stagger_default() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DS2_GEMM8_STAGGER");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
+int dispatch8(G8Args& a, int fp8, int a_col, int b_col, int cus, hipStream_t st) {
+  a.stagger = stagger_default();
+  if (fp8) return launch8<true, 0, 0>(a, cus, st);
+  if (!a_col && !b_col) return launch8<false, 0, 0>(a, cus, st);
+  if (!a_col && b_col) return launch8<false, 0, 1>(a, cus, st);
+  if (a_col && b_col) return launch8<false, 1, 1>(a, cus, st);
+  return launch8<false, 1, 0>(a, cus, st);
+}
+
+int units_of(const G8Prob& p) { return ((p.M + 255) / 256) * ((p.N + 255) / 256) * p.S; }
 
 }  // namespace
 
@@ -519,7 +620,8 @@ extern "C" {
 
 // fp8: A / B hold e4m3 bytes (K elements per row, K % 128 == 0, row mode only); bf16: row-mode
 // operands need K % 32 == 0, col-mode ones (a_col: A stored [K][M]; b_col: B stored [K][N])
-// M % 8 / N % 8 == 0 and any K. lda / ldb / ldc in elements, batch strides likewise.
+// M % 8 / N % 8 == 0 and any K. lda / ldb / ldc in elements, batch strides likewise; the batch
+// members are the launch's problems (batch <= 24).
 // S > 1: split-K over S k-slices through ws (fp32, >= S * batch * M * N floats) and cnt
 // (>= batch * tiles unsigned, all zero; every launch leaves them zero again). Launches that
 // may run concurrently (different streams) need separate cnt buffers.
@@ -528,44 +630,51 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
               int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
               unsigned* cnt, int cus, hipStream_t st) {
   const int es = fp8 ? 1 : 2;
-  if (M <= 0 || N <= 0 || K <= 0 || batch <= 0 || N % 4 != 0 || S < 1) return (int)hipErrorInvalidValue;
-  if (fp8 && (a_col || b_col || K % 128 != 0)) return (int)hipErrorInvalidValue;
-  if (!fp8 && (!a_col || !b_col) && K % 32 != 0) return (int)hipErrorInvalidValue;
-  if ((a_col && M % 8) || (b_col && N % 8)) return (int)hipErrorInvalidValue;
-  if (((lda * es) % 16) || ((ldb * es) % 16) || ((uintptr_t)A % 16) || ((uintptr_t)B % 16))
-    return (int)hipErrorInvalidValue;
-  // 32-bit buffer offsets: each operand (one batch member) under 2 GB
-  if ((long long)(a_col ? K : M) * lda * es >= (1LL << 31) || (long long)(b_col ? K : N) * ldb * es >= (1LL << 31))
-    return (int)hipErrorInvalidValue;
-  if (epi < 0 || epi > 2 || (epi != 0 && bias)) return (int)hipErrorInvalidValue;
-  if (S > 1 && (!ws || !cnt)) return (int)hipErrorInvalidValue;
+  if (batch <= 0 || batch > G8_MAXP || (epi != 0 && bias)) return (int)hipErrorInvalidValue;
   G8Args a;
-  a.A = (const unsigned char*)A;
-  a.B = (const unsigned char*)B;
-  a.C = C;
   a.bias = (const bf16_t*)bias;
   a.alpha_dev = alpha_dev;
   a.alpha_dev2 = alpha_dev2;
-  a.sA = sA * es;
-  a.sB = sB * es;
-  a.sC = sC;
-  a.M = M; a.N = N; a.Kb = K * es;
-  a.lda = lda * es; a.ldb = ldb * es; a.ldc = ldc;
-  a.epi = epi;
   a.alpha = alpha;
-  a.batch = batch;
-  const int nkt = (K * es + ROWB - 1) / ROWB;
-  a.kps = (nkt + S - 1) / S;
-  a.S = (nkt + a.kps - 1) / a.kps;                // no empty slice
-  a.ws = ws;
-  a.cnt = cnt;
-  int rc;
-  if (fp8) rc = launch8<true, 0, 0>(a, cus, st);
-  else if (!a_col && !b_col) rc = launch8<false, 0, 0>(a, cus, st);
-  else if (!a_col && b_col) rc = launch8<false, 0, 1>(a, cus, st);
-  else if (a_col && b_col) rc = launch8<false, 1, 1>(a, cus, st);
-  else rc = launch8<false, 1, 0>(a, cus, st);
-  return rc;
+  a.np = batch;
+  int u = 0;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  for (int b = 0; b < batch; ++b) {
+    G8Prob& p = a.p[b];
+    const int rc = fill_prob(p, (const char*)A + b * sA * es, (const char*)B + b * sB * es,
+                             (char*)C + b * sC * (epi == 0 ? 2 : 4), ws, cnt ? cnt + (size_t)b * tiles : nullptr, M, N,
+                             K, lda, ldb, ldc, fp8, a_col, b_col, epi, S, u);
+    if (rc) return rc;
+    if (ws) p.ws = ws + (size_t)b * p.S * M * N;
+    u += units_of(p);
+  }
+  a.total = u;
+  return dispatch8(a, fp8, a_col, b_col, cus, st);
+}
+
+// A group of independent bf16 GEMMs in one launch (one grid over all their work units): the
+// same operand modes for every member, fp32 C (epi 1 / 2), no bias, alpha = 1. Member i:
+// A[i], B[i], C[i], dims[i] = {M, N, K, lda, ldb, ldc, epi, S}; ws[i] / cnt[i] for S > 1 as in
+// ds2_gemm8 (separate ranges per member).
+int ds2_gemm8_group(int np, const void* const* A, const void* const* B, void* const* C, float* const* ws,
+                    unsigned* const* cnt, const int* dims, int a_col, int b_col, int cus, hipStream_t st) {
+  if (np <= 0 || np > G8_MAXP) return (int)hipErrorInvalidValue;
+  G8Args a;
+  a.bias = nullptr;
+  a.alpha_dev = a.alpha_dev2 = nullptr;
+  a.alpha = 1.f;
+  a.np = np;
+  int u = 0;
+  for (int i = 0; i < np; ++i) {
+    const int* d = dims + 8 * i;
+    if (d[6] == 0) return (int)hipErrorInvalidValue;
+    const int rc = fill_prob(a.p[i], A[i], B[i], C[i], ws[i], cnt[i], d[0], d[1], d[2], d[3], d[4], d[5], 0, a_col,
+                             b_col, d[6], d[7], u);
+    if (rc) return rc;
+    u += units_of(a.p[i]);
+  }
+  a.total = u;
+  return dispatch8(a, 0, a_col, b_col, cus, st);
 }
 
 // k-slices ds2_gemm8 actually uses for a requested S (no empty slice)

@@ -29,13 +29,12 @@ _TILES = {0: (256, 256, 1), 1: (128, 256, 1), 2: (256, 128, 1), 3: (128, 128, 2)
 _PERSISTENT = {6: 0, 7: 1, 8: 2}
 # measured picks: (M, N, K, a_col, b_col, batch) -> cfg
 TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
-    # headline shapes (T2=241, N=32, H=800), tools/bench_gemm_ours.py on MI355X
-    # projections: persistent 128x256 (cfg 7) 84.2 / 196.3 us vs 87.1 / 200.8 (cfg 1), same box
-    (7712, 4800, 800, False, False, 1): 7,     # projection, layers 1-4
-    (7712, 4800, 2400, False, False, 1): 7,    # projection, layer 0
+    # headline shapes (T2=241, N=32, H=800), tools/bench_gemm8.py on MI355X
+    # projection, layers 1-4: persistent 128x256 (cfg 7) 82.5 us, gemm8 82.4 (tie: kept); layer 0
+    # runs on gemm8 (182 vs 196 us)
+    (7712, 4800, 800, False, False, 1): 7,
     # dx = dgx W on the K-contiguous W^T shadow (ops/rnn.py _transpose_async), persistent
-    # 128x256: 66.8 / 196 us (tools/bench_gemm_ours.py); gemm8 reading W column-major
-    # (split 2 / 1) 85 / 253 us
+    # 128x256: 67 / 197 us vs gemm8 82 / 203 (tools/bench_gemm8.py)
     (7712, 800, 4800, False, False, 1): 7,
     (7712, 2400, 4800, False, False, 1): 7,
     (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
@@ -203,14 +202,16 @@ def gemm8_supported(M: int, N: int, K: int, fp8: bool = False, a_col: bool = Fal
 _MAX_SPLITS = int(os.environ.get("DS2_GEMM8_MAX_SPLITS", "8"))     # A/B: 1 turns split-K off
 
 
-def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_slice: int = 1024) -> int:
+def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_slice: int = 1024,
+                 tiles: Optional[int] = None) -> int:
     """k-slices for a grid of few 256^2 tiles (dx at D = 800: 124 tiles, dW / dU: 76-80),
     which would leave CUs idle: the split count that minimises the dispatch rounds per unit
     of work, ceil(tiles * S / cus) / S, with a small per-slice cost for the reduction, each
     slice >= min_slice of K (measured on the full chip: dW / dU 3 slices 93 / 98 us, 4 slices
     — a second round — 137 / 141 us). cus: the CUs the launch may use (a capped grid beside
     the persistent BPTT: 48 -> 5 rounds of 3 slices for 80 tiles)."""
-    tiles = _cdiv(M, 256) * _cdiv(N, 256) * batch
+    if tiles is None:
+        tiles = _cdiv(M, 256) * _cdiv(N, 256) * batch
     if cus >= 128 and 2 * tiles > cus:
         return 1        # full chip, measured: dx D = 2400 (310 tiles) and dW D = 2400 (190) lose with any split
     best, best_cost = 1, None
@@ -248,6 +249,57 @@ def gemm8(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = 0, alp
         cnt = _tile_counters(A.device, _cdiv(M, 256) * _cdiv(N, 256) * batch)
     C.gemm8(A, B, out, bias, epi, float(alpha), alpha_dev, alpha_dev2, a_col, b_col, S, ws, cnt, max_grid)
     return out
+
+
+_GROUP_MAX = 24      # members of one csrc/gemm8.hip group launch (G8_MAXP)
+
+
+def group_operands(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
+    """(A, B) stored column-mode operands of a 2-D weight-gradient product out = a @ b (a [M, K]
+    with unit-stride M, b [K, N] with unit-stride N, out fp32 [M, N]) that gemm8_group takes, or
+    None when the product is not of that form."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype == torch.float32):
+        return None
+    if a.dim() != 2 or b.dim() != 2 or out.dim() != 2 or out.stride(-1) != 1:
+        return None
+    oa, ob = _operand(a, True), _operand(b, False)
+    if oa is None or ob is None or not (oa[1] and ob[1]):
+        return None
+    A, B = oa[0], ob[0]
+    for t in (A, B, out):
+        if t.data_ptr() % 16 or t.stride(-2) % 8:
+            return None
+    M, K, N = a.shape[0], a.shape[1], b.shape[1]
+    if not gemm8_supported(M, N, K, False, True, True):
+        return None
+    return A, B
+
+
+def gemm8_group(members, accumulate: bool = False, max_grid: int = 0) -> None:
+    """out_i (=, or += with ``accumulate``) A_i @ B_i^T for a list of (A, B, out) stored
+    column-mode operands (:func:`group_operands`), as few launches as the group limit allows:
+    one grid over every member's 256^2 tiles, so a set of small weight-gradient GEMMs fills the
+    chip where each alone would leave CUs idle. Split-K only when even the whole group has too
+    few tiles (gemm8_splits on the summed tile count)."""
+    C = _ext.ext()
+    epi = 2 if accumulate else 1
+    for lo in range(0, len(members), _GROUP_MAX):
+        chunk = members[lo:lo + _GROUP_MAX]
+        dev = chunk[0][0].device
+        cus = _dev_cus(chunk[0][0])
+        if max_grid > 0:
+            cus = min(cus, max_grid)
+        tiles = sum(_cdiv(A.shape[1], 256) * _cdiv(B.shape[1], 256) for A, B, _ in chunk)
+        kmin = min(A.shape[0] for A, _, _ in chunk)
+        S = gemm8_splits(0, 0, kmin, cus=cus, tiles=tiles)
+        sp = [int(C.gemm8_splits(A.shape[0], False, S)) if S > 1 else 1 for A, _, _ in chunk]
+        ws = cnt = None
+        if max(sp) > 1:
+            ws = torch.empty(sum(s * A.shape[1] * B.shape[1] for (A, B, _), s in zip(chunk, sp) if s > 1),
+                             device=dev, dtype=torch.float32)
+            cnt = _tile_counters(dev, tiles)
+        C.gemm8_group([m[0] for m in chunk], [m[1] for m in chunk], [m[2] for m in chunk], [epi] * len(chunk), sp,
+                      True, True, ws, cnt, max_grid)
 
 
 _counters: Dict[Tuple[int, int], torch.Tensor] = {}

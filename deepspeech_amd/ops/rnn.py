@@ -595,17 +595,24 @@ class FusedBiLayer(torch.autograd.Function):
         gW = [None, None]
         grp = arena.group_view([W_f, W_b] if d1 else [W_f], "grad") if arena is not None else None
         if grp is not None and arena.first_write(W_f) and (not d1 or arena.first_write(W_b)):
+            def dw_done(W_f=W_f, W_b=W_b if d1 else None):
+                arena.grad_done(W_f, W_b)
+
             def dw(grp=grp, dgx2=dgx2, x2=x2):
                 mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
-                arena.grad_done(W_f, W_b if d1 else None)
+                dw_done()
             sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
-            if sch.defer_input and on_side and ctx.idx >= sch.min_layer:
-                sch.deferred.append(dw)           # run after the last recurrent layer's BPTT
+            grouped = sch.grouped and on_side
+            if sch.defer_input and on_side and (ctx.idx >= sch.min_layer or grouped):
+                # run after the last recurrent layer's BPTT (grouped: every layer's, in one launch)
+                ops = GM.group_operands(dgx2.t(), x2, grp.view(plan.ndir * GH, D)) if grouped else None
+                sch.deferred.append(Deferred(dw, (dgx2, x2), [ops + (grp.view(plan.ndir * GH, D),)] if ops else None,
+                                             dw_done))
                 sch.queue_end_of_backward()
             else:
                 dw()
-            if ctx.idx == 0:
+            if ctx.idx == 0 and not grouped:
                 sch.flush()
         else:
             for d, p in enumerate([W_f, W_b] if d1 else [W_f]):
@@ -623,27 +630,34 @@ class FusedBiLayer(torch.autograd.Function):
             # tail, nothing beside it) takes the whole chip
             sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
-            defer = sch.defer_input and on_side and sch.defer_du and ctx.idx >= sch.min_layer
+            grouped = sch.grouped and on_side
+            defer = sch.defer_input and on_side and sch.defer_du and (ctx.idx >= sch.min_layer or grouped)
             beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
             grid = _DU_GRID if beside else 0
             splits = (_DU_SPLITS or None) if beside else None
 
-            def du(ugrp=ugrp, dgh=dgh, hx=hx, grid=grid, splits=splits):
-                steps = dgh.shape[1]
-                g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
-                h3 = hx[:, :steps].reshape(2, steps * plan.NP, plan.H)
-                out = ugrp.view(2, GH, plan.H)
+            steps = dgh.shape[1]
+            g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
+            h3 = hx[:, :steps].reshape(2, steps * plan.NP, plan.H)
+            out = ugrp.view(2, GH, plan.H)
+
+            def du_done(U_f=U_f, U_b=U_b):
+                arena.grad_done(U_f, U_b)
+
+            def du(g3=g3, h3=h3, out=out, grid=grid, splits=splits):
                 if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out, max_grid=grid, splits=splits)):
                     try:
                         torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
                     except (RuntimeError, TypeError):
                         out.copy_(torch.bmm(g3, h3))
-                arena.grad_done(U_f, U_b)
+                du_done()
             if defer:
                 # every weight gradient after the BPTT chain: a GEMM beside the latency-bound
                 # persistent BPTT slows it by 27-48 % (its L2 / fabric / clock share), more
                 # than the tail gains back (WgradScheduler, DS2_DEFER_DU)
-                sch.deferred.append(du)
+                ops = [GM.group_operands(g3[d], h3[d], out[d]) for d in range(2)] if grouped else None
+                members = [o + (out[d],) for d, o in enumerate(ops)] if ops and all(ops) else None
+                sch.deferred.append(Deferred(du, (dgh, hx), members, du_done))
                 sch.queue_end_of_backward()
             elif sch.defer_input and on_side and ctx.idx == 0 and sch.tail_du:
                 # the side stream already carries dW_0 + every deferred dW and ends after the
@@ -659,9 +673,22 @@ class FusedBiLayer(torch.autograd.Function):
                 if g is None:
                     arena.grad_done(p)
                 gU[d] = g
+        if ctx.idx == 0 and arena is not None and arena.wgrad.grouped and x16.is_cuda and \
+                torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device):
+            arena.wgrad.flush()             # the bottom layer: every deferred GEMM in one group
         gb = _bias_grads([b_f, b_b] if d1 else [b_f], parts[0])
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
+
+
+class Deferred:
+    """A deferred weight-gradient GEMM: ``fn`` runs it (and reports the gradient) on the
+    current stream; ``members`` are its (A, B, out) stored column-mode operands for a grouped
+    launch (None: not groupable), after which ``done`` reports the gradient."""
+    __slots__ = ("fn", "tensors", "members", "done")
+
+    def __init__(self, fn, tensors, members=None, done=None):
+        self.fn, self.tensors, self.members, self.done = fn, tensors, members, done
 
 
 class WgradScheduler:
@@ -686,10 +713,18 @@ class WgradScheduler:
 
     def __init__(self):
         self.streams = {}
+        self.helper_streams = {}   # device -> extra streams the deferred GEMMs spread over
         self.defer_input = False
         self.min_layer = int(os.environ.get("DS2_DEFER_MIN_LAYER", "1"))
         self.tail_du = os.environ.get("DS2_TAIL_DU", "1") == "1"
-        self.defer_du = os.environ.get("DS2_DEFER_DU", "0") == "1"
+        # measured (same box, bench.py headline): dU beside each BPTT 9.35-9.60 ms/step, every
+        # weight gradient after the BPTT chain on 1 / 2 / 3 / 4 streams 9.05-9.10 / 9.01-9.03
+        # / 9.05 / 11.2-11.4 (hipBLASLt routing, for scale: 9.04-9.07)
+        self.defer_du = os.environ.get("DS2_DEFER_DU", "1") == "1"
+        # every deferred weight gradient of the backward (all layers' dW and dU) as ONE grouped
+        # gemm8 launch after the bottom layer's BPTT (GM.gemm8_group): one grid over all their
+        # tiles instead of 10-14 launches of 76-200 tiles each on 1-2 streams
+        self.grouped = GM.enabled("wgrad") and os.environ.get("DS2_WGRAD_GROUP", "1") == "1"
         self.deferred = []
         self.main_tail = []        # GEMMs issued on the main stream once the whole backward is queued
         self._eob_queued = False
@@ -716,9 +751,45 @@ class WgradScheduler:
         self._eob_queued = False
 
     def flush(self) -> None:
-        """Issue every deferred input-weight gradient GEMM (on the current stream)."""
+        """Issue every deferred weight-gradient GEMM, round-robin over the current stream and
+        DS2_WGRAD_STREAMS - 1 helper streams: each GEMM has only 76-80 256^2 tiles, so a few
+        running at once fill the chip where one after another would leave it half idle."""
+        if self.deferred and self.grouped and all(isinstance(d, Deferred) and d.members for d in self.deferred):
+            items, self.deferred = self.deferred, []
+            GM.gemm8_group([m for d in items for m in d.members])
+            for d in items:
+                d.done()
+            return
+        cur = None
+        k = 0
         while self.deferred:
-            self.deferred.pop(0)()
+            item = self.deferred.pop(0)
+            fn, tensors = (item.fn, item.tensors) if isinstance(item, Deferred) else (item, ())
+            if cur is None:
+                cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
+            helpers = self._helpers(cur) if cur is not None else []
+            s = ([cur] + helpers)[k % (1 + len(helpers))] if helpers else None
+            k += 1
+            if s is None or s is cur:
+                fn()
+                continue
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                for t in tensors:
+                    if t is not None:
+                        t.record_stream(s)
+                fn()
+
+    def _helpers(self, cur) -> list:
+        n = int(os.environ.get("DS2_WGRAD_STREAMS", "2")) - 1
+        if n <= 0:
+            return []
+        idx = cur.device.index if cur.device.index is not None else torch.cuda.current_device()
+        hs = self.helper_streams.get(idx)
+        if hs is None or len(hs) < n:
+            hs = [torch.cuda.Stream(device=cur.device) for _ in range(n)]
+            self.helper_streams[idx] = hs
+        return hs[:n]
 
     def drain(self) -> None:
         """Issue every deferred weight-gradient GEMM: leftover input-weight GEMMs (a backward
@@ -759,6 +830,9 @@ class WgradScheduler:
         self.drain()
         for idx, s in self.streams.items():
             torch.cuda.current_stream(idx).wait_stream(s)
+        for idx, hs in self.helper_streams.items():
+            for s in hs:
+                torch.cuda.current_stream(idx).wait_stream(s)
 
 
 _schedulers = weakref.WeakSet()

@@ -243,3 +243,51 @@ def test_gemm8_split_counters_reset_and_streams():
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[0], outs[1])
     for buf in G._counters.values():
         assert int(buf.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm8_group_weight_gradients(accumulate):
+    """A grouped launch of unrelated column-column weight-gradient GEMMs (csrc/gemm8.hip
+    problem table): shapes of the deferred dW / dU of a wide layer, a ragged tiny one and the
+    two directions of a batched dU read through strided views; each member equals its fp32
+    product, stored or accumulated."""
+    torch.manual_seed(7)
+    K = 7712
+    dgh = torch.randn(2, K, 1760, device=DEV).to(BF)
+    h = torch.randn(2, K, 1760, device=DEV).to(BF)
+    dgx = torch.randn(K, 3520, device=DEV).to(BF)
+    x = torch.randn(K, 2400, device=DEV).to(BF)
+    sa = torch.randn(390, 136, device=DEV).to(BF)
+    sb = torch.randn(390, 264, device=DEV).to(BF)
+    ops = [(dgh[0], h[0]), (dgh[1], h[1]), (dgx, x), (sa, sb), (dgx[:, 1760:], h[1])]
+    outs = [torch.randn(a.shape[1], b.shape[1], device=DEV) for a, b in ops]
+    base = [o.clone() for o in outs]
+    members = []
+    for (a, b), o in zip(ops, outs):
+        A, B = G.group_operands(a.t(), b, o)
+        members.append((A, B, o))
+    G.gemm8_group(members, accumulate=accumulate)
+    for (a, b), o, o0 in zip(ops, outs, base):
+        ref = a.float().t() @ b.float() + (o0 if accumulate else 0)
+        assert _rel(o, ref) < 2e-5 * a.shape[0] ** 0.5 + 1e-4
+
+
+def test_gemm8_group_split_and_chunks():
+    """A group with few tiles takes split-K (workspace ranges per member, counters left at
+    zero), and more members than one launch holds run as several launches."""
+    torch.manual_seed(8)
+    ops = [(torch.randn(4000, 256, device=DEV).to(BF), torch.randn(4000, 264, device=DEV).to(BF))
+           for _ in range(3)]
+    outs = [torch.empty(256, 264, device=DEV) for _ in ops]
+    G.gemm8_group([(a, b, o) for (a, b), o in zip(ops, outs)])
+    for (a, b), o in zip(ops, outs):
+        assert _rel(o, a.float().t() @ b.float()) < 2e-5 * 4000 ** 0.5 + 1e-4
+    torch.cuda.synchronize()
+    for buf in G._counters.values():
+        assert int(buf.abs().sum()) == 0
+    many = [(torch.randn(96, 8 * (i % 5 + 1), device=DEV).to(BF), torch.randn(96, 16, device=DEV).to(BF))
+            for i in range(30)]
+    outs = [torch.empty(a.shape[1], 16, device=DEV) for a, _ in many]
+    G.gemm8_group([(a, b, o) for (a, b), o in zip(many, outs)])
+    for (a, b), o in zip(many, outs):
+        assert _rel(o, a.float().t() @ b.float()) < 1e-4

@@ -109,6 +109,71 @@ def main():
         for sp in (1, 2, 3, 4):
             cases[name + " | gemm8 S%d" % sp] = (fl, lambda sp=sp: G.gemm8(dgh, h, o, 1, a_col=True, b_col=True,
                                                                             splits=sp))
+    # wide layers: weight gradients (column-column) of config 5 (H = 1280) and the reference's
+    # clipped-ReLU H = 1760, and config 5's dx
+    for tag, GH, H, D in (("gru1280", 3 * 1280, 1280, 1280), ("relu1760", 1760, 1760, 1760)):
+        name = "dU " + tag
+        if not a.only or a.only in name:
+            dgh = torch.randn(2, M, GH, device=dev, dtype=bf)
+            h = torch.randn(2, M, H, device=dev, dtype=bf)
+            o = torch.empty(2, GH, H, device=dev)
+            fl = 2 * 2.0 * M * GH * H
+            cases[name + " | hipblaslt"] = (fl, lambda dgh=dgh, h=h, o=o: torch.bmm(dgh.transpose(1, 2), h,
+                                                                                   out_dtype=torch.float32, out=o))
+            for sp in (1, 2, 3):
+                cases[name + " | gemm8 S%d" % sp] = (fl, lambda dgh=dgh, h=h, o=o, sp=sp: G.gemm8(
+                    dgh, h, o, 1, a_col=True, b_col=True, splits=sp))
+        name = "dW " + tag
+        if not a.only or a.only in name:
+            dgx = torch.randn(M, 2 * GH, device=dev, dtype=bf)
+            x = torch.randn(M, D, device=dev, dtype=bf)
+            o = torch.empty(2 * GH, D, device=dev)
+            fl = 2.0 * M * 2 * GH * D
+            cases[name + " | hipblaslt"] = (fl, lambda dgx=dgx, x=x, o=o: torch.mm(dgx.t(), x, out_dtype=torch.float32,
+                                                                                   out=o))
+            for sp in (1, 2, 3):
+                cases[name + " | gemm8 S%d" % sp] = (fl, lambda dgx=dgx, x=x, o=o, sp=sp: G.gemm8(
+                    dgx, x, o, 1, a_col=True, b_col=True, splits=sp))
+    name = "dxT gru1280"
+    if not a.only or a.only in name:
+        dgx = torch.randn(M, 7680, device=dev, dtype=bf)
+        Wt = torch.randn(1280, 7680, device=dev, dtype=bf) * 0.05
+        W = Wt.t().contiguous()
+        o = torch.empty(M, 1280, device=dev, dtype=bf)
+        fl = 2.0 * M * 7680 * 1280
+        cases[name + " | hipblaslt"] = (fl, lambda: torch.mm(dgx, W))
+        for sp in (1, 2):
+            cases[name + " | gemm8 rowrow S%d" % sp] = (fl, lambda sp=sp: G.gemm8(dgx, Wt, o, 0, splits=sp))
+            cases[name + " | gemm8 colB S%d" % sp] = (fl, lambda sp=sp: G.gemm8(dgx, W, o, 0, b_col=True, splits=sp))
+    # the whole deferred weight-gradient tail of a model (every layer's dW and both directions'
+    # dU, distinct tensors per layer): one library call each vs one gemm8 call each vs ONE
+    # grouped gemm8 launch (ops/rnn.py WgradScheduler.flush)
+    for tag, GH, H, L in (("gru800", 2400, 800, 5), ("gru1280", 3840, 1280, 7), ("relu1760", 1760, 1760, 7)):
+        name = "tail " + tag
+        if a.only and a.only not in name:
+            continue
+        mem, fl = [], 0.0
+        for li in range(L):
+            D = 2400 if li == 0 else H if tag != "gru800" else 800
+            dgh = torch.randn(2, M, GH, device=dev, dtype=bf)
+            h = torch.randn(2, M, H, device=dev, dtype=bf)
+            dgx = torch.randn(M, 2 * GH, device=dev, dtype=bf)
+            x = torch.randn(M, D, device=dev, dtype=bf)
+            mem += [(dgh[0], h[0], torch.empty(GH, H, device=dev)), (dgh[1], h[1], torch.empty(GH, H, device=dev)),
+                    (dgx, x, torch.empty(2 * GH, D, device=dev))]
+            fl += 2.0 * M * (2 * GH * H + 2 * GH * D)
+
+        def lib(mem=mem):
+            for A, B, o in mem:
+                torch.mm(A.t(), B, out_dtype=torch.float32, out=o)
+
+        def each(mem=mem):
+            for A, B, o in mem:
+                G.gemm8(A, B, o, 1, a_col=True, b_col=True)
+
+        cases[name + " | hipblaslt"] = (fl, lib)
+        cases[name + " | gemm8 each"] = (fl, each)
+        cases[name + " | gemm8 group"] = (fl, lambda mem=mem: G.gemm8_group(mem))
     res = {k: [] for k in cases}
     for _ in range(a.rounds):
         for k, (fl, fn) in cases.items():
