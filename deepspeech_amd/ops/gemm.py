@@ -293,13 +293,19 @@ def gemm8_group(members, accumulate: bool = False, max_grid: int = 0) -> None:
         kmin = min(A.shape[0] for A, _, _ in chunk)
         S = gemm8_splits(0, 0, kmin, cus=cus, tiles=tiles)
         sp = [int(C.gemm8_splits(A.shape[0], False, S)) if S > 1 else 1 for A, _, _ in chunk]
+        # the fewest workgroups that still finish in the same number of rounds: CUs the
+        # quantisation would leave idle in the last round stay free from the start for the
+        # kernels of other streams (the conv front-end's backward beside the tail group)
+        units = tiles * max(sp)
+        rounds = _cdiv(units, cus)
+        grid = min(cus, 8 * _cdiv(_cdiv(units, rounds), 8))
         ws = cnt = None
         if max(sp) > 1:
             ws = torch.empty(sum(s * A.shape[1] * B.shape[1] for (A, B, _), s in zip(chunk, sp) if s > 1),
                              device=dev, dtype=torch.float32)
             cnt = _tile_counters(dev, tiles)
         C.gemm8_group([m[0] for m in chunk], [m[1] for m in chunk], [m[2] for m in chunk], [epi] * len(chunk), sp,
-                      True, True, ws, cnt, max_grid)
+                      True, True, ws, cnt, grid)
 
 
 _counters: Dict[Tuple[int, int], torch.Tensor] = {}

@@ -673,11 +673,14 @@ class FusedBiLayer(torch.autograd.Function):
                 if g is None:
                     arena.grad_done(p)
                 gU[d] = g
-        if ctx.idx == 0 and arena is not None and arena.wgrad.grouped and x16.is_cuda and \
-                torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device):
+        tail = ctx.idx == 0 and arena is not None and arena.wgrad.grouped and x16.is_cuda and \
+            torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
+        if tail:
             arena.wgrad.flush()             # the bottom layer: every deferred GEMM in one group
         gb = _bias_grads([b_f, b_b] if d1 else [b_f], parts[0])
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
+        if tail:
+            arena.wgrad.run_early_update()  # the recurrent stack's optimizer range, beside the front-end
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
 
 
@@ -728,6 +731,8 @@ class WgradScheduler:
         self.deferred = []
         self.main_tail = []        # GEMMs issued on the main stream once the whole backward is queued
         self._eob_queued = False
+        self._early = None         # (fn, params, main stream): set_early_update
+        self.early_done = False
         _schedulers.add(self)
 
     def stream(self, device: torch.device) -> Optional["torch.cuda.Stream"]:
@@ -749,6 +754,31 @@ class WgradScheduler:
         self.deferred.clear()
         self.main_tail.clear()
         self._eob_queued = False
+        self._early = None
+        self.early_done = False
+
+    def set_early_update(self, fn, params) -> None:
+        """For THIS backward: once the bottom recurrent layer has issued its weight gradients
+        (the grouped tail launch and its bias sums, on the side stream), run ``fn()`` — the
+        optimizer update of the parameters whose gradients are then final (FC head and the
+        recurrent stack) — on that side stream, behind the main stream's work issued so far,
+        so it runs beside the conv front-end's backward instead of after it. Skipped (the
+        caller updates everything afterwards; ``early_done`` stays False) if any of ``params``
+        has not been written by then. Call on the stream that runs the backward."""
+        self._early = (fn, params, torch.cuda.current_stream())
+        self.early_done = False
+
+    def run_early_update(self) -> None:
+        if self._early is None:
+            return
+        fn, params, main = self._early
+        self._early = None
+        arena = arena_of(params[0]) if params else None
+        if arena is None or any(arena.first_write(p) for p in params):
+            return
+        torch.cuda.current_stream().wait_stream(main)    # readers of the weights issued so far
+        fn()
+        self.early_done = True
 
     def flush(self) -> None:
         """Issue every deferred weight-gradient GEMM, round-robin over the current stream and

@@ -99,6 +99,15 @@ class Trainer:
         # data parallel: optimizer ranges per gradient bucket behind its all-reduce
         # (GradBucketer.set_optimizer); per_bucket_update=False keeps one update after finish()
         self.per_bucket_update = True
+        # single device: arena elements [0, split) — FC head and recurrent stack, laid out
+        # before the conv front-end in gradient-production order — get their optimizer update
+        # as soon as the recurrent weight gradients are issued (Trainer.step)
+        self._early_split, self._early_params = 0, []
+        names = list(self.arena.names)
+        first_conv = next((i for i, n in enumerate(names) if n.startswith("conv")), None)
+        if self.arena.flat.is_cuda and first_conv:
+            self._early_split = self.arena.offsets[first_conv][0]
+            self._early_params = list(self.arena.params[:first_conv])
         if self.bucketer.enabled and self.arena.flat.is_cuda:
             _check_hw_queues()
 
@@ -128,13 +137,27 @@ class Trainer:
             # bucketer's ordering stream right behind its all-reduce (bitwise the same update)
             lr_t, keep = self.opt.prepare(self.lr, self.global_step)
             self.bucketer.set_optimizer(lambda lo, hi: self.opt.apply_range(lo, hi, lr_t, keep, gscale))
+        early = (not per_bucket and self.nan_policy != "skip" and self._early_split > 0 and lazy and
+                 self.arena.wgrad.grouped and self.arena.wgrad.defer_input)
+        if early:
+            # single device: the FC head's and recurrent stack's Adam + EMA range runs on the
+            # weight-gradient stream right after the grouped tail GEMMs, beside the conv
+            # front-end's backward (WgradScheduler.set_early_update); the front-end's range after
+            lr_t, keep = self.opt.prepare(self.lr, self.global_step)
+            split = self._early_split
+            self.arena.wgrad.set_early_update(lambda: self.opt.apply_range(0, split, lr_t, keep, gscale),
+                                              self._early_params)
         loss.backward(one)
         self.arena.wgrad.join()
         if lazy:
             self.arena.zero_unwritten()
         with TR.phase(TR.ALLREDUCE):
             self.bucketer.finish()
-        if not per_bucket:
+        if early:
+            with TR.phase(TR.EMA):
+                lo = split if self.arena.wgrad.early_done else 0
+                self.opt.apply_range(lo, self.arena.numel, lr_t, keep, gscale)
+        elif not per_bucket:
             skip = None
             if self.nan_policy == "skip":
                 _, skip = self.opt.grad_norm_and_finite(gscale)

@@ -335,6 +335,30 @@ def test_step_is_bitwise_reproducible(cuda):
     assert torch.equal(w0, w1)
 
 
+def test_early_optimizer_range_is_bitwise_whole_update(cuda):
+    """Single device: the FC head's and recurrent stack's Adam + EMA range, issued on the
+    weight-gradient stream beside the conv front-end's backward, gives bitwise the weights,
+    moments and EMA of one whole-arena update after backward (three steps)."""
+    from deepspeech_amd.trainer import Trainer, LRSchedule
+    torch.manual_seed(0)
+    base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
+    batch = to_device(FixedShapeBatches(8, max_frames=300, seed=3, pool=1).next(), cuda)
+    runs = []
+    for early in (True, False):
+        m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+        tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
+        assert tr._early_split > 0
+        if not early:
+            tr._early_split = 0
+        for _ in range(3):
+            tr.step(batch)
+            assert tr.arena.wgrad.early_done == early
+        torch.cuda.synchronize()
+        runs.append((tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b), (a - b).abs().max()
+
+
 @pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
 def test_nhwc_graph_hip_matches_reference(cuda, cell):
     """--nchw False graph on the HIP engine (moments+EMA conv BN in the channels-last
