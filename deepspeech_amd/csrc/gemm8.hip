@@ -21,7 +21,13 @@
 //     ds_read the wave's register subtile (8 A and/or 4 B ds_read_b128)
 //     issue one half-tile of a later k-tile (2 glds per wave)
 //     [phases 3 and 7: s_waitcnt vmcnt(4) — every half-tile but the two just issued landed]
-//     s_barrier ; 16 MFMAs of the wave's 64x32 share of the quadrant ; s_barrier
+//     s_waitcnt lgkmcnt(0) ; s_barrier ; 16 MFMAs of the wave's 64x32 share ; s_barrier
+// Staggered wave groups (MI355X_MICROARCH.md item 9): waves 4-7 execute one extra barrier
+// before the k-loop (waves 0-3 one after it), so every barrier pairs group 0's "after MFMA"
+// with group 1's "before MFMA" of the same phase: the SIMD partners w / w + 4 alternate, one
+// issuing its LDS reads and glds while the other runs its MFMA cluster (measured +11-27 %
+// over both groups bursting together). The lgkmcnt(0) before the first barrier of a phase
+// keeps the 1-phase restage WAR-safe under the half-phase offset.
 // Iteration = 2 k-tiles (even k-tile in buffer 0, odd in buffer 1) = 8 phases; stage plan:
 //     phase 0, 1: odd k-tile t+1's A1, B0 (buffer 1; its A0, B1 were issued a phase 6, 7 earlier)
 //     phase 2..5: k-tile t+2's A0, B1, A1, B0 (buffer 0, each one phase after its last read)
@@ -43,8 +49,12 @@
 // fp8 of a row are the two 16-B chunks the bf16 k-substeps 0 and 1 read; A and B use the
 // same k assignment, so the product is the full sum over the k-tile.
 // Persistent grid: one workgroup per CU (a multiple of 8); XCD x = blockIdx % 8 walks the
-// contiguous tile-id range [x*Tx, (x+1)*Tx) of a grouped order (8 m-tiles x all n-tiles,
+// contiguous work-unit range [x*Tx, (x+1)*Tx) of a grouped order (8 m-tiles x all n-tiles,
 // m fastest), so the tiles an XCD holds at once share A rows and B columns in its L2.
+// Problem table: a launch carries up to 24 independent GEMMs of the same operand modes
+// (batch members, or every recurrent layer's deferred weight gradients); work units are
+// numbered problem by problem and a workgroup looks its problem up from the kernel
+// arguments (scalar loads), so one grid covers all their tiles.
 // Tails: K % 32 == 0 (bf16; a last k-tile of 32 skips its second k-substep) or K % 128 == 0
 // (fp8: the quantiser pads K with zeros); rows past M / N are clamped on load and masked on
 // store.
@@ -54,15 +64,14 @@
 // and dU = dgh^T h read both operands that way. Its half-tile is a [64 k][128 cols] image
 // (256-B k-rows, 16-B chunk c of k-row k at c ^ 2((k & 3) | ((k >> 1) & 4)), 4 k-rows per
 // glds wave-instruction), read as MFMA fragments with ds_read_b64_tr_b16 (8 k of one column
-// per lane from two 4-row transposed reads). k-rows past K come back as zeros from the
-// bounds-checked buffer load, so any K works.
+// per lane from two 4-row transposed reads; inline asm, see rdtr). k-rows past K come back
+// as zeros from the bounds-checked buffer load, so any K works.
 // Split-K (S > 1): work unit = (tile, k-slice); each unit stores its raw fp32 partial tile to
-// a workspace [S][batch][M][N], and the tile's last-arriving slice sums the S partials in
+// a workspace [S][M][N] per problem, and the tile's last-arriving slice sums the S partials in
 // slice order (deterministic) and applies the epilogue, in the same launch. For the
 // tall-skinny shapes (dx with D = 800: 124 256^2 tiles; dW / dU: 76-80) that would
 // otherwise leave most CUs idle.
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -99,7 +108,6 @@ struct G8Args {
   const float* alpha_dev2;
   float alpha;
   int np, total;          // problems, work units of all problems
-  int stagger;            // waves 4-7 run the k-loop half a phase behind waves 0-3
 };
 
 constexpr int NWV = 8;
@@ -408,9 +416,9 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
         else wait_vm<0>();
       }
       // staggered: the other wave group still reads this phase's half-tiles after this
-      // barrier, so a wave's reads are retired before it (WAR of the 1-phase restage)
-      // (column mode: the asm transposed reads are waited for here in any case)
-      if (AC || BC || g.stagger) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // barrier, so a wave's reads are retired before it (WAR of the 1-phase restage; the
+      // asm transposed reads of column mode are waited for only here)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bar();
       __builtin_amdgcn_sched_barrier(0);
       mfma_tile<FP8, 0>(acc[qm][qn], fa, fb, full);
@@ -425,8 +433,7 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
     // so every barrier of the loop pairs group 0's phase p "after MFMA" with group 1's phase p
     // "before MFMA": one group's LDS reads and glds issue run under the other's MFMAs (the SIMD
     // partners w and w + 4 alternate roles) instead of both bursting together
-    const bool stag = g.stagger != 0;
-    if (stag && wr == 1) bar();
+    if (wr == 1) bar();
     int t0 = 0;
     for (; t0 + 1 < nkt; t0 += 2) {
       const bool full1 = !(ragged && kt0 + t0 + 1 == nkt_all - 1);
@@ -448,7 +455,7 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
       phase(I0{}, I1{}, I1{}, T_{}, F_{}, nkt, 0, 0, full0);
       phase(I0{}, I1{}, I0{}, F_{}, T_{}, nkt, 0, 0, full0);
     }
-    if (stag && wr == 0) bar();
+    if (wr == 0) bar();
 
     // epilogue: lane holds C[m][n .. n+3], m = .. + lane % 16, n = .. + 4 (lane / 16). A
     // split unit stores its raw fp32 partial into workspace slice ks (fp32, ld = N).
@@ -594,17 +601,7 @@ int fill_prob(G8Prob& p, const void* A, const void* B, void* C, float* ws, unsig
   return 0;
 }
 
-int stagger_default() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DS2_GEMM8_STAGGER");
-    v = e ? atoi(e) : 1;
-  }
-  return v;
-}
-
-int dispatch8(G8Args& a, int fp8, int a_col, int b_col, int cus, hipStream_t st) {
-  a.stagger = stagger_default();
+int dispatch8(const G8Args& a, int fp8, int a_col, int b_col, int cus, hipStream_t st) {
   if (fp8) return launch8<true, 0, 0>(a, cus, st);
   if (!a_col && !b_col) return launch8<false, 0, 0>(a, cus, st);
   if (!a_col && b_col) return launch8<false, 0, 1>(a, cus, st);

@@ -199,7 +199,7 @@ def gemm8_supported(M: int, N: int, K: int, fp8: bool = False, a_col: bool = Fal
     return (a_col and b_col) or K % 32 == 0
 
 
-_MAX_SPLITS = int(os.environ.get("DS2_GEMM8_MAX_SPLITS", "8"))     # A/B: 1 turns split-K off
+_MAX_SPLITS = 8
 
 
 def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_slice: int = 1024,

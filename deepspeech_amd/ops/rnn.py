@@ -2,18 +2,25 @@
 
 Forward of one recurrent layer on the HIP engine (reference: src/custom_ops.py:36-96):
 
-    gx = x . [W_fw; W_bw]^T * s + [b_fw; b_bw]      one hipBLASLt GEMM, both directions
-    y_fw, y_bw = persistent_recurrence(gx, U, b_h)   csrc/rnn_persistent.hip
-    y = y_fw + y_bw                                   directions summed (quirk Q2)
+    gx = x . [W_fw; W_bw]^T * s + [b_fw; b_bw]      ONE hand-written GEMM for both directions
+                                                     (csrc/gemm8.hip, or gemm.hip where TUNED;
+                                                     fp8 e4m3 operands with --fp8)
+    y  = recurrence_fw(gx) + recurrence_bw(gx)       ONE persistent launch, direction sum fused
+                                                     (csrc/rnn_xcd.hip; rnn_persistent.hip for
+                                                     the widths the XCD kernels do not cover)
 
-Backward:
+Backward (FusedBiLayer):
 
-    dgx, dgh = persistent_bptt(dy, saved gates / states)   csrc/rnn_persistent.hip
-    dU_d = dgh_d^T . h_prev_d     (one GEMM per direction, all steps at once)
-    dW   = dgx^T . x,  dx = dgx . W_cat                (autograd of the projection GEMM)
+    dgx, dgh, bias partials = persistent BPTT         csrc/rnn_xcd.hip (reduce-scatter exchange)
+    dx  = dgx . [W_fw; W_bw]                           gemm on the K-contiguous W^T shadow that the
+                                                       forward transposed on a side stream
+    dW  = dgx^T . x,  dU_d = dgh_d^T . h_prev_d        column-mode gemm8 into the fp32 arena; on one
+                                                       GPU every layer's dW / dU is deferred and run as
+                                                       ONE grouped launch after the bottom layer's BPTT
+                                                       (WgradScheduler), beside the conv front-end
 
-The projection (and its sequence-BN) stays in torch autograd: it is a plain library
-GEMM. Only the serial recurrence is a custom autograd.Function.
+The sequence-BN scale of the projection is folded into its alpha; everything runs without
+torch autograd inside the layer.
 """
 from __future__ import annotations
 
@@ -62,8 +69,9 @@ class RnnPlan:
 
 RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))   # diagnostic timing switches only
 _FUSE_DIRSUM = True        # module switch: tests compare the fused direction sum with torch.add
-_DU_GRID = int(os.environ.get("DS2_DU_GRID", "0"))
-_DU_SPLITS = int(os.environ.get("DS2_DU_SPLITS", "2"))       # measured: 2 beside the BPTT (1: 9.21-9.29, 3: 9.09-9.15, 2: 8.98-9.03 ms/step)
+# split-K of a dU GEMM issued beside the next layer's BPTT (data-parallel runs, where the
+# weight gradients are not deferred): measured 2 (1: 9.21-9.29, 3: 9.09-9.15, 2: 8.98-9.03 ms/step)
+_DU_SPLITS = 2
 
 
 LDS_BYTES = 160 * 1024
@@ -604,7 +612,7 @@ class FusedBiLayer(torch.autograd.Function):
             sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
             grouped = sch.grouped and on_side
-            if sch.defer_input and on_side and (ctx.idx >= sch.min_layer or grouped):
+            if sch.defer_input and on_side and (ctx.idx >= 1 or grouped):
                 # run after the last recurrent layer's BPTT (grouped: every layer's, in one launch)
                 ops = GM.group_operands(dgx2.t(), x2, grp.view(plan.ndir * GH, D)) if grouped else None
                 sch.deferred.append(Deferred(dw, (dgx2, x2), [ops + (grp.view(plan.ndir * GH, D),)] if ops else None,
@@ -624,17 +632,12 @@ class FusedBiLayer(torch.autograd.Function):
         ugrp = arena.group_view([U_f, U_b], "grad") if (arena is not None and d1) else None
         if ugrp is not None and arena.first_write(U_f) and arena.first_write(U_b):
             # both directions' dU_d = dgh_d^T h_d as ONE batched GEMM into the packed slots
-            # beside the next layer's persistent BPTT (200 of the 256 CUs) the GEMM gets a
-            # capped grid: fewer, longer-lived workgroups interfere less with the latency-bound
-            # recurrence (DS2_DU_GRID; 0 = the whole chip); the bottom layer's dU (main-stream
-            # tail, nothing beside it) takes the whole chip
             sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
             grouped = sch.grouped and on_side
-            defer = sch.defer_input and on_side and sch.defer_du and (ctx.idx >= sch.min_layer or grouped)
+            defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped)
             beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
-            grid = _DU_GRID if beside else 0
-            splits = (_DU_SPLITS or None) if beside else None
+            splits = _DU_SPLITS if beside else None
 
             steps = dgh.shape[1]
             g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
@@ -644,8 +647,8 @@ class FusedBiLayer(torch.autograd.Function):
             def du_done(U_f=U_f, U_b=U_b):
                 arena.grad_done(U_f, U_b)
 
-            def du(g3=g3, h3=h3, out=out, grid=grid, splits=splits):
-                if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out, max_grid=grid, splits=splits)):
+            def du(g3=g3, h3=h3, out=out, splits=splits):
+                if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out, splits=splits)):
                     try:
                         torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
                     except (RuntimeError, TypeError):
@@ -654,12 +657,12 @@ class FusedBiLayer(torch.autograd.Function):
             if defer:
                 # every weight gradient after the BPTT chain: a GEMM beside the latency-bound
                 # persistent BPTT slows it by 27-48 % (its L2 / fabric / clock share), more
-                # than the tail gains back (WgradScheduler, DS2_DEFER_DU)
+                # than the tail gains back (WgradScheduler)
                 ops = [GM.group_operands(g3[d], h3[d], out[d]) for d in range(2)] if grouped else None
                 members = [o + (out[d],) for d, o in enumerate(ops)] if ops and all(ops) else None
                 sch.deferred.append(Deferred(du, (dgh, hx), members, du_done))
                 sch.queue_end_of_backward()
-            elif sch.defer_input and on_side and ctx.idx == 0 and sch.tail_du:
+            elif sch.defer_input and on_side and ctx.idx == 0:
                 # the side stream already carries dW_0 + every deferred dW and ends after the
                 # conv front-end's backward on the main stream: balance by issuing the
                 # bottom layer's dU on the main stream behind the front-end (WgradScheduler.join)
@@ -705,29 +708,27 @@ class WgradScheduler:
     * ``stream(device)``: side stream for the recurrent layers' (and head's / front-end's)
       weight-gradient GEMMs (DS2_WGRAD_STREAM=0 keeps them on the current stream). The
       Trainer joins it (:meth:`join`) before the optimizer reads the gradients.
-    * Input-weight gradients (dW = dgx^T x) of layers > 0 may be deferred until the last
-      recurrent layer's BPTT has been issued: the side stream then carries only the
-      recurrent dU GEMMs while the BPTT chain runs, which competes less with it (1 GPU:
-      10.40-10.47 vs 10.60-10.64 ms/step on the same boxes; deferring dU too was slower).
-      With data parallelism it would hold those gradient buckets back to the end of
+    * Single device (``set_deferral``): every recurrent layer's weight gradients (dW = dgx^T x
+      and both directions' dU = dgh^T h) are deferred until the bottom layer's BPTT has been
+      issued, and then run as one grouped gemm8 launch on the side stream, beside the conv
+      front-end's backward. A GEMM beside the latency-bound persistent BPTT slowed it by
+      27-48 % (its L2 / fabric / clock share), more than the overlap gained back. With data
+      parallelism deferral would hold every recurrent gradient bucket back to the end of
       backward, so the Trainer enables it for world_size == 1 only (DS2_DEFER_DW=0/1
-      overrides).
+      overrides); the GEMMs then run per layer on the side stream as each BPTT finishes.
+    * ``set_early_update``: the optimizer range of the parameters that are final once the
+      grouped launch is issued runs on the side stream right behind it.
     """
 
     def __init__(self):
         self.streams = {}
-        self.helper_streams = {}   # device -> extra streams the deferred GEMMs spread over
         self.defer_input = False
-        self.min_layer = int(os.environ.get("DS2_DEFER_MIN_LAYER", "1"))
-        self.tail_du = os.environ.get("DS2_TAIL_DU", "1") == "1"
-        # measured (same box, bench.py headline): dU beside each BPTT 9.35-9.60 ms/step, every
-        # weight gradient after the BPTT chain on 1 / 2 / 3 / 4 streams 9.05-9.10 / 9.01-9.03
-        # / 9.05 / 11.2-11.4 (hipBLASLt routing, for scale: 9.04-9.07)
-        self.defer_du = os.environ.get("DS2_DEFER_DU", "1") == "1"
         # every deferred weight gradient of the backward (all layers' dW and dU) as ONE grouped
         # gemm8 launch after the bottom layer's BPTT (GM.gemm8_group): one grid over all their
-        # tiles instead of 10-14 launches of 76-200 tiles each on 1-2 streams
-        self.grouped = GM.enabled("wgrad") and os.environ.get("DS2_WGRAD_GROUP", "1") == "1"
+        # tiles (measured tail, tools/bench_gemm8.py: 0.84 / 1.96 / 1.32 ms for the headline /
+        # config 5 / 7 x ReLU-1760 vs 1.42 / 2.94 / 2.32 as one hipBLASLt call each); without
+        # it (DS2_GEMM=torch) the GEMMs of layers >= 1 are issued one by one after that BPTT
+        self.grouped = GM.enabled("wgrad")
         self.deferred = []
         self.main_tail = []        # GEMMs issued on the main stream once the whole backward is queued
         self._eob_queued = False
@@ -781,45 +782,17 @@ class WgradScheduler:
         self.early_done = True
 
     def flush(self) -> None:
-        """Issue every deferred weight-gradient GEMM, round-robin over the current stream and
-        DS2_WGRAD_STREAMS - 1 helper streams: each GEMM has only 76-80 256^2 tiles, so a few
-        running at once fill the chip where one after another would leave it half idle."""
+        """Issue every deferred weight-gradient GEMM on the current stream: one grouped launch
+        when every one of them can join it, else one call each."""
         if self.deferred and self.grouped and all(isinstance(d, Deferred) and d.members for d in self.deferred):
             items, self.deferred = self.deferred, []
             GM.gemm8_group([m for d in items for m in d.members])
             for d in items:
                 d.done()
             return
-        cur = None
-        k = 0
         while self.deferred:
             item = self.deferred.pop(0)
-            fn, tensors = (item.fn, item.tensors) if isinstance(item, Deferred) else (item, ())
-            if cur is None:
-                cur = torch.cuda.current_stream() if torch.cuda.is_available() else None
-            helpers = self._helpers(cur) if cur is not None else []
-            s = ([cur] + helpers)[k % (1 + len(helpers))] if helpers else None
-            k += 1
-            if s is None or s is cur:
-                fn()
-                continue
-            s.wait_stream(cur)
-            with torch.cuda.stream(s):
-                for t in tensors:
-                    if t is not None:
-                        t.record_stream(s)
-                fn()
-
-    def _helpers(self, cur) -> list:
-        n = int(os.environ.get("DS2_WGRAD_STREAMS", "2")) - 1
-        if n <= 0:
-            return []
-        idx = cur.device.index if cur.device.index is not None else torch.cuda.current_device()
-        hs = self.helper_streams.get(idx)
-        if hs is None or len(hs) < n:
-            hs = [torch.cuda.Stream(device=cur.device) for _ in range(n)]
-            self.helper_streams[idx] = hs
-        return hs[:n]
+            (item.fn if isinstance(item, Deferred) else item)()
 
     def drain(self) -> None:
         """Issue every deferred weight-gradient GEMM: leftover input-weight GEMMs (a backward
@@ -860,9 +833,6 @@ class WgradScheduler:
         self.drain()
         for idx, s in self.streams.items():
             torch.cuda.current_stream(idx).wait_stream(s)
-        for idx, hs in self.helper_streams.items():
-            for s in hs:
-                torch.cuda.current_stream(idx).wait_stream(s)
 
 
 _schedulers = weakref.WeakSet()

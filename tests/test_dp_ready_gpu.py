@@ -49,8 +49,14 @@ def test_dp_machinery_world1_matches_plain_step(cuda):
                 tr.step(batch)
             torch.cuda.synchronize()
             outs.append((tr.arena.flat.clone(), tr.opt.ema.clone(), tr.arena.p16.clone()))
-        for o in outs[1:]:
-            for x, y in zip(outs[0], o):
-                assert torch.equal(x, y), (x.float() - y.float()).abs().max()
+        # the two bucketed runs share one gradient schedule: bitwise the same update
+        for x, y in zip(outs[1], outs[2]):
+            assert torch.equal(x, y), (x.float() - y.float()).abs().max()
+        # the plain single-device step defers every weight gradient into one grouped GEMM
+        # (full-K tiles) where the bucketed schedule runs them per layer (split-K beside the
+        # BPTT): the same update up to fp32 summation order
+        for x, y in zip(outs[0][:2], outs[1][:2]):
+            assert (x - y).abs().max() <= 1e-6 + 1e-5 * y.abs().max()
+        assert (outs[0][2] != outs[1][2]).float().mean() < 1e-3     # bf16 shadows: rare 1-ulp flips
     finally:
         shutdown(ctx)           # later GPU tests must not run with a live RCCL group
