@@ -408,6 +408,8 @@ class DeepSpeech2(nn.Module):
             lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
             x = self.frontend(feats.to(self.compute_dtype))
             h = self.recurrent(x, lens.to(x.device))
+            from ..ops import rnn as RNN
+            RNN.flush_transposes()      # the dx GEMMs' W^T shadows, beside the head + CTC
             if self.capture:
                 with torch.no_grad():   # the fused head never materialises the logits
                     self._tap("softmax_linear", self.head(h.detach()))

@@ -111,10 +111,13 @@ def make_xcd_plan(N: int, H: int, cell: str, ndir: int, cus: int) -> Optional[Rn
     units). Prefer the most groups that still fit the chip (smaller per-step gathers), at
     most 8 so a group can live on one XCD; rows per group R <= 32."""
     G = GATES[cell]
-    wide = 42 if (_rs_ok(H) and G == 3) else 32         # see _rs_ok
-    if H % 32 != 0 or H // 32 > wide:   # larger H: the resident U slice would spill
-        return None
     P = H // 32
+    # (one-gate layers wider than an XCD, e.g. the reference's ReLU-1760 at P = 55, stay on the
+    # generation-1 kernels: two workgroups per CU kept such a group on one XCD but measured
+    # 6.3 / 5.0 us per step forward / BPTT against 4.9 / 4.9 — profiles/r3_negative_results.md)
+    wide = 42 if (_rs_ok(H) and G == 3) else 32         # see _rs_ok
+    if H % 32 != 0 or P > wide:          # larger H: the resident U slice would spill
+        return None
     best = None
     # groups wider than an XCD (P > CUs/8) exchange across XCDs (write-through): fewer,
     # taller groups measured faster there (H=1280: R=16 27.9 vs R=11 30.3 ms/step)
@@ -252,23 +255,29 @@ def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], al
     return torch.addmm(b16, x2, W16.t(), alpha=alpha)
 
 
-def _transpose_async(W16: torch.Tensor, side) -> tuple:
-    """(W16^T contiguous bf16, event) for the input-gradient GEMM: written on the
-    weight-gradient side stream during the forward (idle there), so the backward's dx GEMM
-    reads a K-contiguous row-major W^T (csrc/gemm.hip / gemm8 row-row: faster than reading
-    W column-major) at no cost on the critical path."""
+class _PendingT:
+    """A queued W^T shadow: transposed on the side stream by WgradScheduler.flush_transposes."""
+    __slots__ = ("W16", "wT", "side", "event")
+
+    def __init__(self, W16, wT, side):
+        self.W16, self.wT, self.side, self.event = W16, wT, side, None
+
+
+def _transpose_async(W16: torch.Tensor, side, sch=None):
+    """W16^T (contiguous bf16) for the input-gradient GEMM, so the backward's dx GEMM reads a
+    K-contiguous row-major W^T (csrc/gemm.hip / gemm8 row-row: faster than reading W column-
+    major). With a scheduler the transpose is only queued: the model issues every layer's on
+    the side stream once the top layer's recurrence has been enqueued (flush_transposes), so
+    they run beside the FC head and the CTC instead of beside a latency-bound recurrence (the
+    layer-0 one, 26 us, slowed its recurrence by ~55 us). Returns a _PendingT (or, without a
+    side stream, the transposed tensor)."""
     wT = torch.empty(W16.shape[1], W16.shape[0], device=W16.device, dtype=torch.bfloat16)
-    C = _ext.ext()
-    if side is None:
-        C.transpose_bf16(W16, wT)
-        return wT, None
-    side.wait_stream(torch.cuda.current_stream(W16.device))
-    with torch.cuda.stream(side):
-        wT.record_stream(side)
-        C.transpose_bf16(W16, wT)
-        ev = torch.cuda.Event()
-        ev.record(side)
-    return wT, ev
+    if side is None or sch is None:
+        _ext.ext().transpose_bf16(W16, wT)
+        return wT
+    job = _PendingT(W16, wT, side)
+    sch.transposes.append(job)
+    return job
 
 
 def _mm_bf16(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -287,6 +296,45 @@ def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return torch.mm(a, b).float()
 
 
+class _FwdBufs:
+    """Output / state buffers of one forward recurrence launch, initialised (for the XCD
+    kernels: h0 slots zero, exchange slots sentinel 0xFFFF, census words -1, the fused sum
+    buffer sentinel) by ONE multi_fill right before the launch. (Initialising them on the side
+    stream beside the projection GEMM measured slower: the recurrence then found its
+    exchange slots out of L2, +20-40 us per layer.)"""
+    __slots__ = ("y2", "ysum", "hx", "hs", "gates", "census", "fuse")
+
+
+def _alloc_fwd(T: int, N: int, plan: RnnPlan, dev) -> _FwdBufs:
+    C = _ext.ext()
+    H, ndir = plan.H, plan.ndir
+    d1 = ndir == 2
+    bf16 = torch.bfloat16
+    b = _FwdBufs()
+    # generation-4 forward fuses the direction sum into its output stores (sentinel-filled
+    # sum buffer, one direction writes through, the other adds): no torch.add launch and no
+    # per-direction output round trip (VERDICT r1 weak item 6)
+    b.fuse = (plan.kind == "xcd" and d1 and _FUSE_DIRSUM and
+              bool(C.rnnx_fwd_fuses_sum(H, CELL_CODE[plan.cell], plan.mt, ndir, RNNX_KNOBS)))
+    b.y2 = None if b.fuse else torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
+    b.ysum = torch.empty(T, N, H, device=dev, dtype=bf16) if b.fuse else None
+    b.hx = torch.empty(ndir, T + 1, plan.NP, H, device=dev, dtype=bf16)
+    b.hs = torch.empty(ndir, T + 1, plan.NP, H, device=dev, dtype=torch.float32)
+    b.gates = (torch.empty(ndir, T, plan.NP, H, 4, device=dev, dtype=torch.float32)
+               if plan.cell == "gru" else None)
+    b.census = torch.empty(ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32) \
+        if plan.kind == "xcd" else None
+    return b
+
+
+def _fill_fwd(b: _FwdBufs, plan: RnnPlan) -> None:
+    ndir = plan.ndir
+    hx, hs = b.hx, b.hs
+    regions = ([hx[d, 0] for d in range(ndir)] + [hx[d, 1:] for d in range(ndir)] +
+               [hs[d, 0] for d in range(ndir)] + [b.census] + ([b.ysum] if b.fuse else []))
+    _ext.ext().multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [-1] + ([-1] if b.fuse else []))
+
+
 def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     """Launch the persistent forward recurrence over gx [T, N, ndir*G*H] (bf16).
     U / bh: per-direction lists (bf16 [G*H, H] / fp32 [G*H] or None).
@@ -298,26 +346,12 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     steps = T
     dev = gx.device
     d1 = ndir == 2
-    bf16 = torch.bfloat16
-    # generation-4 forward fuses the direction sum into its output stores (sentinel-filled
-    # sum buffer, one direction writes through, the other adds): no torch.add launch and no
-    # per-direction output round trip
-    fuse = (plan.kind == "xcd" and d1 and _FUSE_DIRSUM and
-            bool(C.rnnx_fwd_fuses_sum(H, CELL_CODE[plan.cell], plan.mt, ndir, RNNX_KNOBS)))
-    y2 = None if fuse else torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
-    ysum = torch.empty(T, N, H, device=dev, dtype=bf16) if fuse else None
-    hx = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=bf16)
-    hs = torch.empty(ndir, steps + 1, plan.NP, H, device=dev, dtype=torch.float32)
-    gates = (torch.empty(ndir, steps, plan.NP, H, 4, device=dev, dtype=torch.float32)
-             if plan.cell == "gru" else None)
+    b = _alloc_fwd(T, N, plan, dev)
+    fuse, y2, ysum, hx, hs, gates = b.fuse, b.y2, b.ysum, b.hx, b.hs, b.gates
     if plan.kind == "xcd":
-        # one launch: h0 slots zero, exchange slots 1..T sentinel 0xFFFF ("not yet
-        # produced"), census words -1, error word 0
-        census = torch.empty(ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
+        census = b.census
         err = error_word(dev)
-        regions = ([hx[d, 0] for d in range(ndir)] + [hx[d, 1:] for d in range(ndir)] +
-                   [hs[d, 0] for d in range(ndir)] + [census] + ([ysum] if fuse else []))
-        C.multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [-1] + ([-1] if fuse else []))
+        _fill_fwd(b, plan)
         if h0 is not None:
             hs[:, 0, :N].copy_(h0)
             hx[:, 0, :N].copy_(h0)
@@ -353,6 +387,26 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
 
 
+def _alloc_bwd(plan: RnnPlan, want_bias: bool, dev) -> tuple:
+    """(census, parts, ring) of an XCD BPTT launch and the multi_fill that initialises them:
+    census words -1, bias partials 0, the reduce-scatter ring 0xFFFFFFFF (none depends on T)."""
+    H, ndir, G = plan.H, plan.ndir, GATES[plan.cell]
+    census = torch.empty(ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
+    parts = torch.empty(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
+                        dtype=torch.float32) if want_bias else None
+    rf = int(_ext.ext().rnnx_ring_floats(H, plan.BG, plan.R))
+    ring = torch.empty(ndir, rf, device=dev, dtype=torch.float32)
+    return census, parts, ring
+
+
+def _fill_bwd(census, parts, ring) -> None:
+    regions, pats = [census], [-1]
+    if parts is not None:
+        regions.append(parts)
+        pats.append(0)
+    _ext.ext().multi_fill(regions + [ring], pats + [-1])     # one launch for every init
+
+
 def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale: float = 1.0,
              want_bias: bool = True):
     """Launch BPTT. Returns (dgx [T, N, gstride] bf16 (x dgx_scale), dgh [ndir, steps, NP, G*H],
@@ -369,19 +423,11 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
     dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
     has_g = gates.numel() > 0
     if plan.kind == "xcd":
-        census = torch.empty(ndir * plan.BG * (H // 32), device=dev, dtype=torch.int32)
         err = error_word(dev)
-        parts = torch.empty(2 if plan.cell == "gru" else 1, ndir, plan.BG, G * H, device=dev,
-                            dtype=torch.float32) if want_bias else None
-        regions, pats = [census], [-1]
-        if parts is not None:
-            regions.append(parts)
-            pats.append(0)
         # generation-3 BPTT: reduce-scatter of partials through a 3-slot ring (readiness =
         # per-use tag in each word's LSB, ring filled with 0xFFFFFFFF); dgh is a plain output
-        rf = int(C.rnnx_ring_floats(H, plan.BG, plan.R))
-        ring = torch.empty(ndir, rf, device=dev, dtype=torch.float32)
-        C.multi_fill(regions + [ring], pats + [-1])     # one launch for every init
+        census, parts, ring = _alloc_bwd(plan, want_bias, dev)
+        _fill_bwd(census, parts, ring)
         C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
                    gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
                    dgh[0], dgh[1] if d1 else None, dgx,
@@ -536,14 +582,16 @@ class FusedBiLayer(torch.autograd.Function):
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
-        wT = ev = None
-        if x.is_cuda and GM.enabled("dx") and W16.shape[1] % 8 == 0 and W16.shape[0] % 8 == 0:
-            wT, ev = _transpose_async(W16, wgrad_stream(x.device, arena_of(W_f)))
+        wT = None
+        if x.is_cuda and ctx.needs_input_grad[0] and GM.enabled("dx") and W16.shape[1] % 8 == 0 and \
+                W16.shape[0] % 8 == 0:
+            arena = arena_of(W_f)
+            wT = _transpose_async(W16, wgrad_stream(x.device, arena), arena.wgrad if arena is not None else None)
         y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
         dev = x.device
         ctx.save_for_backward(x16, lens, W16, U[0], U[1] if U[1] is not None else torch.empty(0, device=dev),
                               hx, hs, gates)
-        ctx.wT, ctx.wT_ready = wT, ev
+        ctx.wT = wT
         ctx.params = (W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b)
         ctx.plan = plan
         ctx.alpha = alpha
@@ -569,12 +617,17 @@ class FusedBiLayer(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.wT is not None:
-                if ctx.wT_ready is not None:
-                    torch.cuda.current_stream(dgx.device).wait_event(ctx.wT_ready)
-                dx = _mm_bf16(dgx2, ctx.wT.t()).view(T, N, D)
+                wT = ctx.wT
+                if isinstance(wT, _PendingT):
+                    if wT.event is None:                 # not flushed by the model: do it now
+                        arena = arena_of(W_f)
+                        arena.wgrad.flush_transposes()
+                    torch.cuda.current_stream(dgx.device).wait_event(wT.event)
+                    wT = wT.wT
+                dx = _mm_bf16(dgx2, wT.t()).view(T, N, D)
             else:
                 dx = _mm_bf16(dgx2, W16).view(T, N, D)
-        ctx.wT = ctx.wT_ready = None
+        ctx.wT = None
         # ---- weight gradients (off the critical path) ----
         # only arena-managed weights (gradients written to main_grad, nothing returned to
         # autograd) may be produced on another stream; the Trainer joins it before Adam
@@ -734,6 +787,7 @@ class WgradScheduler:
         self._eob_queued = False
         self._early = None         # (fn, params, main stream): set_early_update
         self.early_done = False
+        self.transposes = []       # queued W^T shadows of this forward (_transpose_async)
         _schedulers.add(self)
 
     def stream(self, device: torch.device) -> Optional["torch.cuda.Stream"]:
@@ -757,6 +811,25 @@ class WgradScheduler:
         self._eob_queued = False
         self._early = None
         self.early_done = False
+        self.transposes.clear()
+
+    def flush_transposes(self) -> None:
+        """Issue the queued W^T transposes on the side stream behind everything the current
+        stream has enqueued (the recurrences whose weights they read were issued before)."""
+        if not self.transposes:
+            return
+        jobs, self.transposes = self.transposes, []
+        C = _ext.ext()
+        cur = torch.cuda.current_stream(jobs[0].W16.device)
+        side = jobs[0].side
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for j in jobs:
+                j.W16.record_stream(side)
+                j.wT.record_stream(side)
+                C.transpose_bf16(j.W16, j.wT)
+                j.event = torch.cuda.Event()
+                j.event.record(side)
 
     def set_early_update(self, fn, params) -> None:
         """For THIS backward: once the bottom recurrent layer has issued its weight gradients
@@ -842,6 +915,13 @@ def wgrad_stream(device: torch.device, arena=None) -> Optional["torch.cuda.Strea
     """The weight-gradient side stream of ``arena`` (None without an arena: plain autograd
     gradients are returned to autograd on the current stream)."""
     return arena.wgrad.stream(device) if arena is not None else None
+
+
+def flush_transposes() -> None:
+    """Issue every live arena's queued W^T transposes (the model calls this after its
+    recurrent stack, before the head and the loss)."""
+    for sch in list(_schedulers):
+        sch.flush_transposes()
 
 
 def join_wgrad_streams(arena=None) -> None:
