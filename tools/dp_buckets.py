@@ -17,6 +17,9 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from deepspeech_amd.utils.setenvs import setenvs  # noqa: E402
+
+setenvs([])          # the hardware-queue floor and RCCL settings, before HIP initialises
 
 
 def main():
