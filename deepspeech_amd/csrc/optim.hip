@@ -11,6 +11,8 @@
 // bf16 compute copy of the weights). The gradient is pre-scaled by `gscale` (1/world for
 // the data-parallel mean, or a loss-scale inverse). A separate reduction kernel computes
 // the squared gradient norm and a non-finite flag for the NaN guard.
+#include <algorithm>
+
 #include "common.h"
 
 using namespace ds2;
@@ -114,6 +116,32 @@ __global__ __launch_bounds__(OPT_THREADS) void adam_ema_kernel(
   }
 }
 
+// Same update, block-contiguous: block b streams float4 groups [b*chunk, (b+1)*chunk) of every
+// array (U groups in flight per lane, lanes 16 B apart), so each CU walks its own contiguous
+// pages instead of the whole grid sweeping one stride-spaced front across the arena.
+template <int U>
+__global__ __launch_bounds__(OPT_THREADS) void adam_ema_chunk_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    float* __restrict__ ema, bf16_t* __restrict__ p16, long long n, long long chunk4, float lr_t, float b1,
+    float b2, float eps, float gscale, float ema_keep, const int* __restrict__ skip) {
+  if (skip != nullptr && *skip) return;
+  const long long n4 = n / 4;
+  const long long lo = (long long)blockIdx.x * chunk4, hi = min(n4, lo + chunk4);
+  long long i = lo + threadIdx.x;
+  for (; i + (U - 1) * OPT_THREADS < hi; i += U * OPT_THREADS)
+    adam_groups<U>(p, g, m, v, ema, p16, i, OPT_THREADS, lr_t, b1, b2, eps, gscale, ema_keep);
+  for (; i < hi; i += OPT_THREADS) adam_groups<1>(p, g, m, v, ema, p16, i, OPT_THREADS, lr_t, b1, b2, eps, gscale, ema_keep);
+  if (blockIdx.x == gridDim.x - 1) {                 // tail elements past the last float4
+    for (long long k = n4 * 4 + threadIdx.x; k < n; k += OPT_THREADS) {
+      float pk = p[k], mk = m[k], vk = v[k];
+      adam1(pk, g[k], mk, vk, lr_t, b1, b2, eps, gscale);
+      p[k] = pk; m[k] = mk; v[k] = vk;
+      if (ema != nullptr) ema[k] = ema1(ema[k], pk, ema_keep);
+      if (p16 != nullptr) p16[k] = f2bf(pk);
+    }
+  }
+}
+
 // partial sums of g^2 (fp32 per block), plus a non-finite flag
 __global__ __launch_bounds__(OPT_THREADS) void grad_norm_kernel(const float* __restrict__ g, long long n, float gscale,
                                                                 float* __restrict__ part, int* __restrict__ bad) {
@@ -145,7 +173,7 @@ __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict
 
 int grid_for(long long n) {
   long long g = (n / 4 + OPT_THREADS - 1) / OPT_THREADS;
-  if (g > 2048) g = 2048;
+  if (g > 16384) g = 16384;     // measured (tools/bench_adam.py): 46 M params 270 us at 16384 blocks vs 311 at 2048
   if (g < 1) g = 1;
   return (int)g;
 }
@@ -159,6 +187,18 @@ extern "C" {
 int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
                  float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
                  hipStream_t st) {
+  // arenas past ~120 M parameters (config 5: 146 M) stream faster block-contiguous (1098 vs
+  // 1200 us, interleaved A/B in tools/bench_adam.py); smaller ones (46 M: 278 vs 328 us, 89 M:
+  // 634 vs 748) faster grid-strided
+  if (max_grid == 0 && n >= 120000000LL) max_grid = -2048;
+  if (max_grid < 0) {                                // block-contiguous variant, grid = -max_grid
+    const long long n4 = n / 4;
+    const int grid = (int)std::max<long long>(1, std::min<long long>(-max_grid, (n4 + OPT_THREADS - 1) / OPT_THREADS));
+    const long long chunk4 = (n4 + grid - 1) / grid;
+    hipLaunchKernelGGL(adam_ema_chunk_kernel<2>, dim3(grid), dim3(OPT_THREADS), 0, st, p, g, m, v, ema, (bf16_t*)p16,
+                       n, chunk4, lr_t, b1, b2, eps, gscale, ema_keep, skip);
+    return (int)hipGetLastError();
+  }
   int grid = grid_for(n);
   if (max_grid > 0 && grid > max_grid) grid = max_grid;
   hipLaunchKernelGGL(adam_ema_kernel, dim3(grid), dim3(OPT_THREADS), 0, st, p, g, m, v, ema, (bf16_t*)p16, n,
