@@ -73,6 +73,25 @@ struct DS2RnnX {
   void* ysum;
 };
 int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st);
+struct DS2RnnF8 {
+  int T, N, NP, H, BG, R, steps, gstride, ndir, xcd_map;
+  const int* lens;
+  const void* gx;
+  const void* U8[2];
+  const int* uexp;
+  const float* bh[2];
+  void* y[2];
+  void* hq[2];
+  void* hx[2];
+  float* hsave[2];
+  float* gates[2];
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+};
+int ds2_rnnf8_supported(int H, int N, int ndir);
+int ds2_rnnf8_fwd(const DS2RnnF8* d, hipStream_t st);
+int ds2_fp8_quant_pow2(const void* x, long long n, void* q, int* uexp, unsigned* amax, hipStream_t st);
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs);
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
 long long ds2_rnnx_ring_floats(int H, int BG, int R);
@@ -319,6 +338,73 @@ void rnnx_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U_f, OptT U_b, OptT bh_
   TORCH_CHECK(ndir == 1 || (d.U[1] && d.y[1] && d.ex[1] && d.hsave[1]), "backward-direction buffers missing");
   TORCH_CHECK(cell == 0 || (d.gates[0] && (ndir == 1 || d.gates[1])), "GRU needs gate buffers");
   check(ds2_rnnx_fwd(&d, cur_stream()), "rnnx_fwd");
+}
+
+// csrc/rnn_fp8.hip: GRU forward with e4m3 U (per-tensor power-of-two scale, uexp = E8M0 exponent
+// per direction on the device) and an e4m3 hidden-state exchange hq [ndir][steps+1][NP][H]
+// (slot 0 = e4m3 h0, slots 1.. 0xFF); saves hs / gates / bf16 hx like rnnx_fwd.
+void rnnf8_fwd(at::Tensor gx, at::Tensor lens, at::Tensor U8, at::Tensor uexp, OptT bh_f, OptT bh_b, at::Tensor y,
+               at::Tensor hq, at::Tensor hx, at::Tensor hs, at::Tensor gates, at::Tensor census, at::Tensor err,
+               int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t R, int64_t steps, int64_t gstride,
+               int64_t ndir, int64_t timeout, int64_t xcd_map) {
+  need_gpu(gx, "gx");
+  TORCH_CHECK(gx.scalar_type() == at::kBFloat16 && gx.is_contiguous() && gx.numel() >= T * N * gstride,
+              "gx must be contiguous bf16 [T, N, gstride]");
+  TORCH_CHECK(gstride >= ndir * 3 * H, "gstride");
+  TORCH_CHECK(lens.scalar_type() == at::kInt && lens.numel() == N, "lens must be int32 [N]");
+  TORCH_CHECK(U8.scalar_type() == at::kByte && U8.is_contiguous() && U8.numel() == ndir * 3 * H * H,
+              "U8 must be uint8 [ndir, 3H, H]");
+  TORCH_CHECK(uexp.scalar_type() == at::kInt && uexp.numel() >= ndir, "uexp must be int32 [ndir]");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.is_contiguous() && y.numel() == ndir * T * N * H, "y [ndir,T,N,H]");
+  TORCH_CHECK(hq.scalar_type() == at::kByte && hq.is_contiguous() && hq.numel() == ndir * (steps + 1) * NP * H,
+              "hq must be uint8 [ndir, steps+1, NP, H]");
+  TORCH_CHECK(hx.scalar_type() == at::kBFloat16 && hx.is_contiguous() && hx.numel() == ndir * (steps + 1) * NP * H,
+              "hx must be bf16 [ndir, steps+1, NP, H]");
+  TORCH_CHECK(hs.scalar_type() == at::kFloat && hs.is_contiguous() && hs.numel() == ndir * (steps + 1) * NP * H,
+              "hs must be fp32 [ndir, steps+1, NP, H]");
+  TORCH_CHECK(gates.scalar_type() == at::kFloat && gates.is_contiguous() && gates.numel() == ndir * steps * NP * H * 4,
+              "gates must be fp32 [ndir, steps, NP, H, 4]");
+  TORCH_CHECK(census.scalar_type() == at::kInt && census.numel() >= ndir * BG * (H / 64), "census too small");
+  TORCH_CHECK(ds2_rnnf8_supported((int)H, (int)N, (int)ndir), "rnnf8: unsupported geometry");
+  TORCH_CHECK(steps >= 1 && steps <= T && R >= 1 && R <= 8 && NP == BG * R && BG * ndir <= 8, "rnnf8: plan");
+  for (const at::Tensor* t : {&U8, &y, &hq, &hx, &hs, &gates, &census, &err, &lens, &uexp}) need_gpu(*t, "rnnf8 operand");
+  DS2RnnF8 d;
+  d.T = (int)T; d.N = (int)N; d.NP = (int)NP; d.H = (int)H; d.BG = (int)BG; d.R = (int)R; d.steps = (int)steps;
+  d.gstride = (int)gstride; d.ndir = (int)ndir; d.xcd_map = (int)xcd_map;
+  d.lens = lens.data_ptr<int>();
+  d.gx = gx.data_ptr();
+  const size_t usz = (size_t)3 * H * H, hsz = (size_t)(steps + 1) * NP * H;
+  const size_t ysz = (size_t)T * N * H, gsz = (size_t)steps * NP * H * 4;
+  for (int i = 0; i < 2; ++i) {
+    const bool on = i < ndir;
+    d.U8[i] = on ? (const void*)(U8.data_ptr<uint8_t>() + i * usz) : nullptr;
+    d.y[i] = on ? (void*)(reinterpret_cast<uint16_t*>(y.data_ptr()) + i * ysz) : nullptr;
+    d.hq[i] = on ? (void*)(hq.data_ptr<uint8_t>() + i * hsz) : nullptr;
+    d.hx[i] = on ? (void*)(reinterpret_cast<uint16_t*>(hx.data_ptr()) + i * hsz) : nullptr;
+    d.hsave[i] = on ? hs.data_ptr<float>() + i * hsz : nullptr;
+    d.gates[i] = on ? gates.data_ptr<float>() + i * gsz : nullptr;
+  }
+  d.uexp = uexp.data_ptr<int>();
+  d.bh[0] = ptr_or_null<const float>(bh_f, "bh_f");
+  d.bh[1] = ptr_or_null<const float>(bh_b, "bh_b");
+  d.census = reinterpret_cast<unsigned*>(census.data_ptr<int>());
+  d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  d.timeout = timeout;
+  check(ds2_rnnf8_fwd(&d, cur_stream()), "rnnf8_fwd");
+}
+
+// e4m3 copy of a bf16 tensor scaled by ONE power of two (amax / 2^e <= 448); uexp[0] = 127 + e
+void fp8_quant_pow2(at::Tensor x, at::Tensor q, at::Tensor uexp, at::Tensor amax) {
+  need_gpu(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "x must be contiguous bf16");
+  TORCH_CHECK(q.scalar_type() == at::kByte && q.is_contiguous() && q.numel() == x.numel(), "q must be uint8 like x");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(q.data_ptr()) & 7) == 0,
+              "x 16-B / q 8-B aligned");
+  TORCH_CHECK(uexp.scalar_type() == at::kInt && uexp.numel() >= 1 && amax.scalar_type() == at::kInt && amax.numel() >= 1,
+              "uexp / amax int32 device words");
+  check(ds2_fp8_quant_pow2(x.data_ptr(), x.numel(), q.data_ptr(), uexp.data_ptr<int>(),
+                           reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream()),
+        "fp8_quant_pow2");
 }
 
 void rnnx_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tensor hs_f, OptT hs_b, OptT gates_f,
@@ -924,6 +1010,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stamps") = py::none(), py::arg("dbx_part") = py::none(), py::arg("dbh_part") = py::none(),
         py::arg("dgx_scale") = 1.0);
   m.def("rnn_kpw", &rnn_kpw);
+  m.def("rnnf8_fwd", &rnnf8_fwd);
+  m.def("rnnf8_supported", [](int64_t H, int64_t N, int64_t ndir) { return ds2_rnnf8_supported((int)H, (int)N, (int)ndir); });
+  m.def("fp8_quant_pow2", &fp8_quant_pow2);
   m.def("rnnx_fwd", &rnnx_fwd, py::arg("gx"), py::arg("lens"), py::arg("U_f"), py::arg("U_b"), py::arg("bh_f"),
         py::arg("bh_b"), py::arg("y_f"), py::arg("y_b"), py::arg("hx_f"), py::arg("hx_b"), py::arg("hs_f"),
         py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("census"), py::arg("err"), py::arg("T"),

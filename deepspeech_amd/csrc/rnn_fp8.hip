@@ -1,0 +1,513 @@
+// Persistent bidirectional GRU forward with fp8 recurrent weights and an fp8 hidden-state
+// exchange (gfx950 MX-scaled fp8 MFMA) — the config-5 "fp8 mixed precision" recurrence.
+//
+// Reference behaviour: src/custom_ops.py:36-72 (CustomRNNCell2 GRU, tf.nn.bidirectional_dynamic_rnn:
+// outputs zero past each length, the backward direction reversed within each utterance). Same
+// saved-state buffers as csrc/rnn_xcd.hip (h fp32, gates fp32, h_{t-1} bf16 for the dU GEMM),
+// so the bf16 reduce-scatter BPTT of rnn_xcd.hip runs unchanged on them.
+//
+// Why fp8: a bf16 U slice of 32 units x 3 gates x H = 1280 is 245 KB per workgroup, so a group
+// needs P = H/32 = 40 workgroups — more than the 32 CUs of an XCD — and exchanges write-through
+// across XCDs (5.4 us/step at config 5). In fp8 the slice of 64 units is the same 245 KB, a
+// group is P = H/64 = 20 workgroups on ONE XCD, and its per-step exchange stays in that XCD's
+// L2 (plain stores), like the headline H = 800 layers.
+//
+//  * U: e4m3 with ONE power-of-two scale per tensor (ds2_fp8_quant_pow2: amax, scale 2^e with
+//    amax / 2^e <= 448), applied exactly as the MFMA's E8M0 B-scale. h: e4m3 with unit scale
+//    (|h| < 1 for the GRU), requantised every step when it is published.
+//  * Workgroup = 64 units of one group (direction x batch group of R <= 8 rows), 9 waves:
+//    8 MFMA waves = 4 unit quarters (uq = wave & 3, 16 units, all 3 gates) x 2 K halves
+//    (kh = wave >> 2); wave 8 is the memory wave (gx one step ahead into LDS, outputs two
+//    steps behind out of LDS staging: no MFMA wave ever waits behind a bulk store).
+//  * k-step = 128 of K (one v_mfma_scale_f32_16x16x128_f8f6f4 per gate): a lane's A fragment
+//    (row lane % 16; k in [16g, 16g+16) u [64+16g, 64+16g+16), g = lane / 16) is two 16-B
+//    exchange granules of 16 units each; every granule of the lane's K half is loaded at once
+//    and re-polled in one round (no serial round trips). The last KL of a wave's KB k-steps of
+//    U live in (dynamic) LDS, the rest in VGPRs.
+//  * Exchange: hq[step+1][NP][H] bytes, pre-filled with 0xFF (e4m3 NaN, never published: a NaN
+//    h is canonicalised to 0x7F). A producer packs 16 lanes' bytes into one 16-B granule with
+//    DPP row shifts and stores it (plain when the census finds the group on one XCD, else sc1
+//    write-through); consumers load with sc1 and spin until no byte is the sentinel.
+//  * Transpose-reduce: of a 16x16 accumulator tile, the kh = 0 wave finalises elements j = 0, 1
+//    (rows 4 (lane >> 4) + j) and the kh = 1 wave j = 2, 3: each stores the two it does not own
+//    (lane-contiguous, conflict-free), ONE LDS barrier, then adds the partner's. A lane then
+//    runs the GRU cell for two (row, unit) elements in registers.
+//  * Every spin is bounded (s_memrealtime timeout -> error word, the launch aborts).
+#include <type_traits>
+
+#include "common.h"
+
+using namespace ds2;
+
+namespace {
+
+constexpr int UPW8 = 64;                 // hidden units per workgroup
+constexpr int G8W = 8;                   // MFMA waves
+constexpr int F8TH = (G8W + 1) * 64;     // + the memory wave
+constexpr int MEMW8 = G8W;
+constexpr int ROWS8 = 8;                 // staged rows (R <= 8; the MFMA tile has 16)
+constexpr int G3 = 3;                    // GRU gates
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+struct XF8 {
+  int T, N, NP, H, P, BG, R, steps, gstride, ngroups, xcd_map;
+  const int* lens;
+  const bf16_t* gx;                 // [T][N][gstride] bf16, direction d at columns d*3H
+  const unsigned char* U8[2];       // [3H][H] e4m3 (row = gate*H + unit)
+  const int* uexp;                  // [2] E8M0 exponent of each direction's U scale (127 + e)
+  const float* bh[2];               // [3H] recurrent bias (fp32) or null
+  bf16_t* y[2];                     // [T][N][H] per-direction outputs
+  unsigned char* hq[2];             // [steps+1][NP][H] e4m3 exchange, slots 1.. sentinel 0xFF
+  bf16_t* hx[2];                    // [steps+1][NP][H] bf16 h (slot 0 = h0): the dU GEMM operand
+  float* hsave[2];                  // [steps+1][NP][H] fp32 h
+  float* gates[2];                  // [steps][NP][H][4] fp32 (r, z, n, U_n h + b_hn)
+  unsigned* census;                 // [ngroups * P] pre-filled 0xFFFFFFFF
+  unsigned* err;
+  long long timeout;
+};
+
+__device__ __forceinline__ unsigned xcc_id8() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xf;
+}
+
+// group = blockIdx % 8 (<= 8 groups: one XCD each under round-robin dispatch), member =
+// blockIdx / 8; otherwise contiguous ranges
+__device__ __forceinline__ bool take_role8(int xcd_map, int ngroups, int P, int& grp, int& mem) {
+  if (xcd_map) {
+    const int slot = blockIdx.x & 7;
+    if (slot >= ngroups) return false;
+    grp = slot;
+    mem = blockIdx.x >> 3;
+  } else {
+    grp = blockIdx.x / P;
+    mem = blockIdx.x % P;
+  }
+  return mem < P;
+}
+
+// 1: every member on one XCD, 0: spread, -1: timeout (wave 0)
+__device__ int census8(unsigned* census, int grp, int mem, int P, long long timeout, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  unsigned* c = census + (size_t)grp * P;
+  if (lane == 0) __hip_atomic_store(c + mem, xcc_id8(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (true) {
+    bool ready = true, same = true;
+    unsigned first = 0xffffffffu;
+    for (int q = lane; q < P; q += 64) {
+      const unsigned v = __hip_atomic_load(c + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ready = ready && (v != 0xffffffffu);
+      if (q == lane) first = v;
+      same = same && (v == first);
+    }
+    if (__all(ready)) {
+      const unsigned x0 = __shfl(first, 0, 64);
+      return __all(same && (lane >= P || first == x0)) ? 1 : 0;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+      if (lane == 0) atomicOr(err, 2u);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// no byte of the granule is the sentinel 0xFF: SWAR "has a zero byte" on the complement
+__device__ __forceinline__ bool granule8_ready(i32x4 v) {
+  unsigned any = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned w = ~(unsigned)v[i];
+    any |= (w - 0x01010101u) & ~w & 0x80808080u;
+  }
+  return any == 0;
+}
+
+// f32 -> e4m3 byte (OCP, round to nearest even, saturating); a NaN becomes 0x7F, never the
+// sentinel 0xFF
+__device__ __forceinline__ unsigned f2e4m3(float x) {
+  const unsigned b = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(x, x, 0, false) & 0xffu;
+  return b == 0xffu ? 0x7fu : b;
+}
+
+template <int KB, int KL>
+__global__ __launch_bounds__(F8TH) void rnnf8_fwd_kernel(XF8 a) {
+  constexpr int KR = KB - KL;               // register-resident U k-steps
+  static_assert(KL >= 0 && KR >= 1, "k-steps");
+  constexpr int GP = G3 * UPW8 + 8;         // gx ring row pitch (bf16)
+  constexpr int OP = UPW8 + 4;              // output staging row pitch
+  __shared__ float red_s[2][4][2][2][G3][64];     // [parity][uq][owner kh][element][gate][lane]
+  __shared__ bf16_t gxr_s[2][ROWS8][GP];          // bf16: with KL = 2 the LDS is full
+  __shared__ __attribute__((aligned(16))) float oh_s[2][ROWS8][OP];
+  __shared__ __attribute__((aligned(16))) float oy_s[2][ROWS8][OP];
+  __shared__ float4 og_s[2][ROWS8][OP];
+  __shared__ int len_s[ROWS8];
+  __shared__ int s_mode, s_abort;
+  extern __shared__ __attribute__((aligned(16))) i32x8 ul_dyn[];   // [KL][G8W][G3][64]
+
+  int grp, mem;
+  if (!take_role8(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, N = a.N, NP = a.NP, R = a.R;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW8;
+  const int uq = wave & 3, kh = wave >> 2;
+  const int g16 = lane >> 4;                     // lane group: rows 4 g16 .. 4 g16 + 3 of the tile
+  const int ec = 16 * uq + (lane & 15);          // this lane's unit within the workgroup
+  const int erow0 = 4 * g16 + 2 * kh;            // its two cell elements: rows erow0, erow0 + 1
+  if (tid < ROWS8) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  if (wave == 0) {
+    const int m = census8(a.census, grp, mem, a.P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+  __syncthreads();
+  if (s_abort) return;
+
+  // memory wave: gx granule q -> (row, gate, 8-unit chunk); R x 3 x 8 = 192 granules max
+  constexpr int RGL = (ROWS8 * G3 * (UPW8 / 8) + 63) / 64;     // 3
+  i32x4 gpre[RGL];
+  const int NRG = R * G3 * (UPW8 / 8);
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      const int qq = q < NRG ? q : 0;
+      const int row = qq / (G3 * 8), rem = qq - row * (G3 * 8), g = rem >> 3, c8 = rem & 7;
+      const int b = min(r0 + row, N - 1);
+      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+      gpre[j] = *reinterpret_cast<const i32x4*>(a.gx + ((size_t)t * N + b) * a.gstride + dir * G3 * H + g * H + u0 +
+                                                c8 * 8);
+    }
+  };
+  auto mw_put = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      if (q < NRG) {
+        const int row = q / (G3 * 8), rem = q - row * (G3 * 8), g = rem >> 3, c8 = rem & 7;
+        const bool act = s < len_s[row];
+        const bf16x8 v = __builtin_bit_cast(bf16x8, gpre[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gxr_s[s & 1][row][g * UPW8 + c8 * 8 + k] = act ? (bf16_t)v[k] : (bf16_t)0;
+      }
+    }
+  };
+  // outputs of step s: lane -> (row = lane / 8, 8 units (lane % 8) * 8)
+  auto mw_store = [&](int s) {
+    const int row = lane >> 3, c8 = (lane & 7) * 8;
+    if (row >= R) return;
+    const int b = r0 + row, u = u0 + c8;
+    const int sl = s & 1;
+    f32x4 h0 = *reinterpret_cast<const f32x4*>(&oh_s[sl][row][c8]);
+    f32x4 h1 = *reinterpret_cast<const f32x4*>(&oh_s[sl][row][c8 + 4]);
+    f32x4 y0 = *reinterpret_cast<const f32x4*>(&oy_s[sl][row][c8]);
+    f32x4 y1 = *reinterpret_cast<const f32x4*>(&oy_s[sl][row][c8 + 4]);
+    float4 gv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] = og_s[sl][row][c8 + i];
+    float* hsp = a.hsave[dir] + ((size_t)(s + 1) * NP + b) * H + u;
+    *reinterpret_cast<f32x4*>(hsp) = h0;
+    *reinterpret_cast<f32x4*>(hsp + 4) = h1;
+    bf16x8 hb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hb[i] = (short)f2bf(h0[i]);
+      hb[4 + i] = (short)f2bf(h1[i]);
+    }
+    *reinterpret_cast<bf16x8*>(a.hx[dir] + ((size_t)(s + 1) * NP + b) * H + u) = hb;
+    float4* gp = reinterpret_cast<float4*>(a.gates[dir]) + ((size_t)s * NP + b) * H + u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gp[i] = gv[i];
+    if (b < N) {
+      const int L = len_s[row];
+      const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+      bf16x8 yb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        yb[i] = (short)f2bf(y0[i]);
+        yb[4 + i] = (short)f2bf(y1[i]);
+      }
+      *reinterpret_cast<bf16x8*>(a.y[dir] + ((size_t)t * N + b) * H + u) = yb;
+    }
+  };
+  if (wave == MEMW8) {
+    mw_load(0);
+    mw_put(0);
+    if (a.steps > 1) mw_load(1);
+  }
+  __syncthreads();                                   // gx ring slot 0
+  const bool plain = s_mode == 1;
+  const unsigned hq_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H);
+  const __amdgpu_buffer_rsrc_t rs_hq = make_rsrc(a.hq[dir], hq_bytes);
+
+  if (wave < G8W) {
+    const int KS = H / 128;                          // k-steps of 128 (host: even, 2 KB)
+    // resident U fragments: B[k][n] = U8[g H + u0 + 16 uq + n][128 ks + k] for this lane's n =
+    // lane % 16 and k in [16 g16, +16) u [64 + 16 g16, +16); ks = kh KB + kk
+    i32x8 uf[KR][G3];
+    const unsigned char* Ud = a.U8[dir];
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      const int ks = kh * KB + kk;
+#pragma unroll
+      for (int g = 0; g < G3; ++g) {
+        const unsigned char* p = Ud + (size_t)(g * H + u0 + ec) * H + ks * 128 + 16 * g16;
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(p);
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(p + 64);
+        const i32x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        if (kk < KR) uf[kk < KR ? kk : 0][g] = v;
+        else ul_dyn[(((kk >= KR ? kk - KR : 0) * G8W + wave) * G3 + g) * 64 + lane] = v;   // own slot
+      }
+    }
+    (void)KS;
+    const int sb = __builtin_amdgcn_readfirstlane(a.uexp[dir]);          // E8M0 B scale
+    const int sbw = sb | (sb << 8) | (sb << 16) | (sb << 24);
+    float bhr[G3];
+#pragma unroll
+    for (int g = 0; g < G3; ++g) bhr[g] = a.bh[dir] ? a.bh[dir][g * H + u0 + ec] : 0.f;
+    float hreg[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int row = erow0 + e;
+      hreg[e] = (row < R) ? a.hsave[dir][(size_t)(r0 + row) * H + u0 + ec] : 0.f;   // slot 0 = h0
+    }
+    // padding rows of the 16-row tile re-read row R - 1 (a real, polled row)
+    const int arow = r0 + min(lane & 15, R - 1);
+    for (int s = 0; s < a.steps; ++s) {
+      float gxv[2][G3];
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int g = 0; g < G3; ++g) gxv[e][g] = bf2f(gxr_s[s & 1][min(erow0 + e, ROWS8 - 1)][g * UPW8 + ec]);
+      // every granule of this lane's K half at once; k-step kk's two granules are 64 B apart,
+      // consecutive k-steps 128 B apart (immediate offsets off one base)
+      const unsigned o0 = (unsigned)(((size_t)s * NP + arow) * H + kh * KB * 128 + 16 * g16);
+      i32x4 v[KB][2];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) {
+        v[kk][0] = load_sc1_b128(rs_hq, o0 + 128u * kk);
+        v[kk][1] = load_sc1_b128(rs_hq, o0 + 128u * kk + 64u);
+      }
+      f32x4 acc[G3];
+#pragma unroll
+      for (int g = 0; g < G3; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned done = 0;                             // wave-uniform prefix of consumed k-steps
+      constexpr unsigned FULL = (1u << KB) - 1u;
+      bool ok = true;
+      while (true) {
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk) {
+          if (done == (1u << kk) - 1u && __all(granule8_ready(v[kk][0]) && granule8_ready(v[kk][1]))) {
+            const i32x8 af = __builtin_shufflevector(v[kk][0], v[kk][1], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+            for (int g = 0; g < G3; ++g) {
+              const i32x8 b = kk < KR ? uf[kk < KR ? kk : 0][g]
+                                      : ul_dyn[(((kk >= KR ? kk - KR : 0) * G8W + wave) * G3 + g) * 64 + lane];
+              acc[g] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, b, acc[g], 0, 0, 0, 0x7f7f7f7f, 0, sbw);
+            }
+            done |= 1u << kk;
+          }
+        }
+        if (done == FULL) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { ok = false; break; }
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk)
+          if (!(done & (1u << kk))) {
+            v[kk][0] = load_sc1_b128(rs_hq, o0 + 128u * kk);
+            v[kk][1] = load_sc1_b128(rs_hq, o0 + 128u * kk + 64u);
+          }
+      }
+      if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
+      // transpose-reduce: hand the two elements the partner finalises to it
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int g = 0; g < G3; ++g) red_s[s & 1][uq][kh ^ 1][e][g][lane] = acc[g][2 * (kh ^ 1) + e];
+      lds_barrier();
+      if (s_abort) break;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int row = erow0 + e;
+        float pre[G3];
+#pragma unroll
+        for (int g = 0; g < G3; ++g) pre[g] = acc[g][2 * kh + e] + red_s[s & 1][uq][kh][e][g][lane];
+        const bool real = row < R;
+        const int L = real ? len_s[row] : 0;
+        const bool act = s < L;
+        const float ghn = pre[2] + bhr[2];
+        const float r = sigmoidf_(gxv[e][0] + pre[0] + bhr[0]);
+        const float z = sigmoidf_(gxv[e][1] + pre[1] + bhr[1]);
+        const float n = tanhf_(gxv[e][2] + r * ghn);
+        const float hn = (1.f - z) * n + z * hreg[e];
+        const float hnew = act ? hn : hreg[e];
+        hreg[e] = hnew;
+        // publish: 16 lanes (the tile's 16 units of this row) -> one 16-B e4m3 granule
+        const unsigned b = f2e4m3(hnew);
+        const unsigned w1 = b | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x101, 0xf, 0xf, false) << 8);
+        const unsigned w2 = w1 | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0x102, 0xf, 0xf, false) << 16);
+        const int d1 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x104, 0xf, 0xf, false);
+        const int d2 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x108, 0xf, 0xf, false);
+        const int d3 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x10c, 0xf, 0xf, false);
+        if ((lane & 15) == 0 && real) {
+          const i32x4 gv = {(int)w2, d1, d2, d3};
+          const unsigned off = (unsigned)(((size_t)(s + 1) * NP + r0 + row) * H + u0 + 16 * uq);
+          if (plain) store_b128(rs_hq, off, gv);
+          else store_sc1_b128(rs_hq, off, gv);
+        }
+        if (real) {
+          oh_s[s & 1][row][ec] = hnew;
+          oy_s[s & 1][row][ec] = act ? hn : 0.f;
+          og_s[s & 1][row][ec] = act ? make_float4(r, z, n, ghn) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  } else {
+    for (int s = 0; s < a.steps; ++s) {
+      if (s + 1 < a.steps) mw_put(s + 1);
+      if (s >= 2) mw_store(s - 2);
+      if (s + 2 < a.steps) mw_load(s + 2);
+      lds_barrier();
+      if (s_abort) break;
+    }
+  }
+  __syncthreads();
+  if (wave == MEMW8 && !s_abort) {
+    if (a.steps >= 2) mw_store(a.steps - 2);
+    if (a.steps >= 1) mw_store(a.steps - 1);
+  }
+}
+
+// amax of |x| over a bf16 tensor into *amax (as float bits; zeroed by the caller)
+__global__ __launch_bounds__(256) void amax_bf16_kernel(const bf16_t* __restrict__ x, long long n,
+                                                        unsigned* __restrict__ amax) {
+  float m = 0.f;
+  const long long stride = (long long)gridDim.x * 256 * 8;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += stride) {
+    if (i + 8 <= n) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(bf2f((bf16_t)v[k])));
+    } else {
+      for (long long k = i; k < n; ++k) m = fmaxf(m, fabsf(bf2f(x[k])));
+    }
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));    // non-negative floats order as uints
+}
+
+// e4m3 copy x / 2^e with the smallest e such that amax / 2^e <= 448; uexp = 127 + e (E8M0)
+__global__ __launch_bounds__(256) void quant_pow2_kernel(const bf16_t* __restrict__ x, long long n,
+                                                         const unsigned* __restrict__ amax,
+                                                         unsigned char* __restrict__ q, int* __restrict__ uexp) {
+  const float am = __uint_as_float(*amax);
+  int e = 0;
+  if (am > 0.f) {
+    e = (int)ceilf(log2f(am / 448.f));
+    if (ldexpf(448.f, e) < am) ++e;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *uexp = 127 + e;
+  const float inv = ldexpf(1.f, -e);
+  const long long stride = (long long)gridDim.x * 256 * 8;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += stride) {
+    if (i + 8 <= n) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i);
+      unsigned w[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)v[4 * h]) * inv, bf2f((bf16_t)v[4 * h + 1]) * inv, 0,
+                                                 false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)v[4 * h + 2]) * inv, bf2f((bf16_t)v[4 * h + 3]) * inv, lo,
+                                             true);
+        w[h] = (unsigned)lo;
+      }
+      *reinterpret_cast<uint2*>(q + i) = make_uint2(w[0], w[1]);
+    } else {
+      for (long long k = i; k < n; ++k) q[k] = (unsigned char)f2e4m3(bf2f(x[k]) * inv);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+struct DS2RnnF8 {
+  int T, N, NP, H, BG, R, steps, gstride, ndir, xcd_map;
+  const int* lens;
+  const void* gx;
+  const void* U8[2];
+  const int* uexp;
+  const float* bh[2];
+  void* y[2];
+  void* hq[2];
+  void* hx[2];
+  float* hsave[2];
+  float* gates[2];
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+};
+
+// k-steps of 128 per wave (K half) and how many of them live in LDS, for H
+static int f8_kb(int H) { return H / 256; }
+static int f8_kl(int kb) { return kb > 3 ? kb - 3 : 0; }
+
+int ds2_rnnf8_supported(int H, int N, int ndir) {
+  if (H % 256 != 0 || H / 64 > 32 || H / 256 > 6 || H / 256 < 1) return 0;
+  const int BG = 8 / ndir;
+  const int R = (N + BG - 1) / BG;
+  return R <= ROWS8 ? 1 : 0;
+}
+
+size_t ds2_rnnf8_smem(int H) { return (size_t)f8_kl(f8_kb(H)) * G8W * G3 * 64 * sizeof(i32x8); }
+
+int ds2_rnnf8_fwd(const DS2RnnF8* d, hipStream_t st) {
+  if (d->H % 256 != 0 || d->R < 1 || d->R > ROWS8 || d->NP != d->BG * d->R || d->H / UPW8 > 32) return -40;
+  XF8 a;
+  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = d->H / UPW8; a.BG = d->BG; a.R = d->R;
+  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
+  a.xcd_map = d->xcd_map && a.ngroups <= 8;
+  a.lens = d->lens; a.gx = (const bf16_t*)d->gx; a.uexp = d->uexp;
+  for (int i = 0; i < 2; ++i) {
+    a.U8[i] = (const unsigned char*)d->U8[i]; a.bh[i] = d->bh[i]; a.y[i] = (bf16_t*)d->y[i];
+    a.hq[i] = (unsigned char*)d->hq[i]; a.hx[i] = (bf16_t*)d->hx[i]; a.hsave[i] = d->hsave[i];
+    a.gates[i] = d->gates[i];
+  }
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout;
+  if (d->steps <= 0) return 0;
+  const int grid = a.xcd_map ? 8 * a.P : a.ngroups * a.P;
+  const int kb = f8_kb(d->H);
+  const size_t smem = ds2_rnnf8_smem(d->H);
+  switch (kb) {
+#define DS2_F8(K)                                                                                     \
+  case K: {                                                                                           \
+    auto kern = rnnf8_fwd_kernel<K, (K > 3 ? K - 3 : 0)>;                                             \
+    if (smem > 0)                                                                                     \
+      DS2_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)); \
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(F8TH), smem, st, a);                                    \
+    break;                                                                                            \
+  }
+    DS2_F8(1) DS2_F8(2) DS2_F8(3) DS2_F8(4) DS2_F8(5) DS2_F8(6)
+#undef DS2_F8
+    default: return -41;
+  }
+  return (int)hipGetLastError();
+}
+
+// per-tensor power-of-two e4m3 quantisation of a bf16 tensor (amax scratch: one zeroed uint)
+int ds2_fp8_quant_pow2(const void* x, long long n, void* q, int* uexp, unsigned* amax, hipStream_t st) {
+  if (n <= 0) return 0;
+  long long blocks = (n + 256 * 8 - 1) / (256 * 8);
+  if (blocks > 1024) blocks = 1024;
+  DS2_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(unsigned), st));
+  hipLaunchKernelGGL(amax_bf16_kernel, dim3((int)blocks), dim3(256), 0, st, (const bf16_t*)x, n, amax);
+  hipLaunchKernelGGL(quant_pow2_kernel, dim3((int)blocks), dim3(256), 0, st, (const bf16_t*)x, n, amax,
+                     (unsigned char*)q, uexp);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

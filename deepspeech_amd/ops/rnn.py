@@ -387,6 +387,47 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
 
 
+def fp8_recurrence_ok(plan: RnnPlan, N: int) -> bool:
+    """csrc/rnn_fp8.hip serves this GRU layer (config 5's fp8 mode): H % 256 == 0, H/64 <= 32
+    workgroups per group (one XCD), 8 groups of <= 8 rows, and the same padded batch rows as
+    the layer's bf16 BPTT plan (which runs on the saved state unchanged)."""
+    if plan.cell != "gru" or plan.kind != "xcd" or not _ext.ext().rnnf8_supported(plan.H, N, plan.ndir):
+        return False
+    BG = 8 // plan.ndir
+    return BG * (-(-N // BG)) == plan.NP
+
+
+def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan):
+    """GRU forward with e4m3 recurrent weights (one power-of-two scale per direction, computed
+    on the device) and an e4m3 hidden-state exchange: groups of H/64 workgroups on one XCD
+    (csrc/rnn_fp8.hip). Returns (y, (hx, hs, gates)) in the layout of _run_fwd."""
+    C = _ext.ext()
+    T, N, gstride = gx.shape
+    H, ndir = plan.H, plan.ndir
+    BG = 8 // ndir
+    R = -(-N // BG)
+    NP = BG * R
+    dev = gx.device
+    U8 = torch.empty(ndir, 3 * H, H, device=dev, dtype=torch.uint8)
+    words = torch.empty(4, device=dev, dtype=torch.int32)          # uexp[2], amax scratch
+    for d in range(ndir):
+        C.fp8_quant_pow2(U[d].contiguous(), U8[d], words[d:d + 1], words[3:4])
+    y2 = torch.empty(ndir, T, N, H, device=dev, dtype=torch.bfloat16)
+    hq = torch.empty(ndir, T + 1, NP, H, device=dev, dtype=torch.uint8)
+    hx = torch.empty(ndir, T + 1, NP, H, device=dev, dtype=torch.bfloat16)
+    hs = torch.empty(ndir, T + 1, NP, H, device=dev, dtype=torch.float32)
+    gates = torch.empty(ndir, T, NP, H, 4, device=dev, dtype=torch.float32)
+    census = torch.empty(ndir * BG * (H // 64), device=dev, dtype=torch.int32)
+    # e4m3 h0 = 0x00, exchange slots 0xFF ("not yet produced"), census -1, bf16 / fp32 h0 = 0
+    C.multi_fill([hq[d, 0] for d in range(ndir)] + [hq[d, 1:] for d in range(ndir)] + [census],
+                 [0] * ndir + [-1] * ndir + [-1])
+    C.multi_fill([hx[d, 0] for d in range(ndir)] + [hs[d, 0] for d in range(ndir)], [0] * (2 * ndir))
+    C.rnnf8_fwd(gx.contiguous(), lens, U8, words, bh[0], bh[1] if ndir == 2 else None, y2, hq, hx, hs, gates, census,
+                error_word(dev), T, N, NP, H, BG, R, T, gstride, ndir, TIMEOUT_TICKS, 1)
+    y = torch.add(y2[0], y2[1]) if ndir == 2 else y2[0]
+    return y, (hx, hs, gates)
+
+
 def _alloc_bwd(plan: RnnPlan, want_bias: bool, dev) -> tuple:
     """(census, parts, ring) of an XCD BPTT launch and the multi_fill that initialises them:
     census words -1, bias partials 0, the reduce-scatter ring 0xFFFFFFFF (none depends on T)."""
@@ -587,7 +628,11 @@ class FusedBiLayer(torch.autograd.Function):
                 W16.shape[0] % 8 == 0:
             arena = arena_of(W_f)
             wT = _transpose_async(W16, wgrad_stream(x.device, arena), arena.wgrad if arena is not None else None)
-        y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
+        if fp8 and x.is_cuda and fp8_recurrence_ok(plan, N):
+            # config 5's fp8 mode: the recurrence too (e4m3 U and h exchange); BPTT stays bf16
+            y, (hx, hs, gates) = _run_fwd_fp8(gx, lens, U, bh, plan)
+        else:
+            y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
         dev = x.device
         ctx.save_for_backward(x16, lens, W16, U[0], U[1] if U[1] is not None else torch.empty(0, device=dev),
                               hx, hs, gates)

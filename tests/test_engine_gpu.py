@@ -315,6 +315,31 @@ def test_fp8_projection_close_to_bf16(cuda):
             assert _rel(p.grad, g16[n].grad) < 0.25, n
 
 
+def test_fp8_recurrence_model_close_to_bf16(cuda):
+    """Config 5's fp8 mode at its width (H = 1280, 2 layers): the recurrence runs on
+    csrc/rnn_fp8.hip (e4m3 U and h exchange), the BPTT in bf16 on the saved state. Loss within
+    5 % of the bf16 engine, top-layer / head gradients within 25 %."""
+    from deepspeech_amd.ops import rnn as RNN
+    ref, hip = _pair(cuda, "gru", H=1280, L=2)
+    hip8 = copy.deepcopy(hip)
+    hip8.set_engine("hip", torch.bfloat16, fp8=True)
+    batch = to_device(FixedShapeBatches(8, max_frames=260, seed=4, pool=1).next(), cuda)
+    plan = RNN.plan_for(8, 1280, "gru", 2, cuda)
+    assert RNN.fp8_recurrence_ok(plan, 8)
+    l16 = _loss(hip, batch)
+    l16.backward()
+    l8 = _loss(hip8, batch)
+    l8.backward()
+    RNN.join_wgrad_streams()
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    assert abs(float(l8) - float(l16)) / abs(float(l16)) < 5e-2, (float(l8), float(l16))
+    g16 = dict(hip.named_parameters())
+    for n, p in hip8.named_parameters():
+        if n.startswith("rnn.1") or n.startswith("fc"):
+            assert _rel(p.grad, g16[n].grad) < 0.25, n
+
+
 def test_step_is_bitwise_reproducible(cuda):
     """Two trainers from the same initial state on the same batch produce bitwise-identical
     losses, gradients and updated weights (every fused kernel reduces in a fixed order; the

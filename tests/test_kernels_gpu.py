@@ -261,6 +261,27 @@ def test_adam_ema_matches_torch(cuda):
     assert torch.allclose(outs[0][1], outs[1][1], atol=1e-5)
 
 
+@pytest.mark.parametrize("n", [1000003, 4096 * 37 + 3])
+def test_adam_ema_launch_variants_bitwise(cuda, n):
+    """The grid-strided and the block-contiguous Adam + EMA launches (csrc/optim.hip; the
+    latter serves arenas past 120 M parameters) give bitwise the same p, m, v, ema and bf16
+    copy, ragged tails included."""
+    from deepspeech_amd.ops import _ext
+    C = _ext.ext()
+    torch.manual_seed(9)
+    base = [torch.randn(n, device=cuda) for _ in range(5)]
+    base[3].abs_()
+    outs = []
+    for grid in (0, 333, -7, -2048):
+        p, g, m, v, e = (t.clone() for t in base)
+        p16 = torch.empty(n, device=cuda, dtype=torch.bfloat16)
+        C.adam_ema(p, g, m, v, e, p16, 1e-3, 0.9, 0.999, 1e-8, 0.5, 0.99, None, grid)
+        outs.append((p, m, v, e, p16))
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
+
+
 def test_grad_norm(cuda):
     from deepspeech_amd.ops.optim import ParamArena, FusedAdamEMA
     m = torch.nn.Linear(100, 50).to(cuda)
@@ -359,3 +380,85 @@ def test_fused_direction_sum_bitwise(cuda, cell):
 def _ext_mod():
     from deepspeech_amd.ops import _ext
     return _ext
+
+
+# --------------------------------------------------------------------------- fp8 recurrence
+def test_fp8_quant_pow2(cuda):
+    """csrc/rnn_fp8.hip per-tensor power-of-two e4m3 quantiser: the smallest 2^e with
+    amax / 2^e <= 448, and every element the OCP e4m3 rounding of x / 2^e."""
+    from deepspeech_amd.ops import _ext
+    C = _ext.ext()
+    torch.manual_seed(11)
+    for scale in (0.02, 3.0, 900.0):
+        x = (torch.randn(3 * 256, 256, device=cuda) * scale).to(torch.bfloat16)
+        q = torch.empty(x.shape, device=cuda, dtype=torch.uint8)
+        w = torch.empty(2, device=cuda, dtype=torch.int32)
+        C.fp8_quant_pow2(x, q, w[0:1], w[1:2])
+        e = int(w[0]) - 127
+        amax = float(x.float().abs().max())
+        assert amax / 2.0 ** e <= 448.0 and amax / 2.0 ** (e - 1) > 448.0
+        want = (x.float() / 2.0 ** e).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert float((q != want).float().mean()) == 0.0
+
+
+def _gru_fp8_emulation(gx, lens, U, bh, H):
+    """fp32 model of csrc/rnn_fp8.hip: U quantised to e4m3 with a power-of-two scale, h_{t-1}
+    requantised to e4m3 every step for the recurrent product, the cell in fp32."""
+    T, N, _ = gx.shape
+    ndir = len(U)
+    ys, hss = [], []
+    for d in range(ndir):
+        u = U[d].float()
+        e = math.ceil(math.log2(float(u.abs().max()) / 448.0))
+        if float(u.abs().max()) / 2.0 ** e > 448.0:
+            e += 1
+        uq = (u / 2.0 ** e).to(torch.float8_e4m3fn).float() * 2.0 ** e
+        h = torch.zeros(N, H, device=gx.device)
+        y = torch.zeros(T, N, H, device=gx.device)
+        hs = []
+        for s in range(T):
+            t = torch.tensor([s if d == 0 else max(int(lens[b]) - 1 - s, 0) for b in range(N)], device=gx.device)
+            act = torch.tensor([s < int(lens[b]) for b in range(N)], device=gx.device)
+            g = gx[t, torch.arange(N, device=gx.device), d * 3 * H:(d + 1) * 3 * H].float()
+            gh = h.to(torch.float8_e4m3fn).float() @ uq.t() + bh[d].float()
+            r = torch.sigmoid(g[:, :H] + gh[:, :H])
+            z = torch.sigmoid(g[:, H:2 * H] + gh[:, H:2 * H])
+            n = torch.tanh(g[:, 2 * H:] + r * gh[:, 2 * H:])
+            hn = (1 - z) * n + z * h
+            h = torch.where(act[:, None], hn, h)
+            tt = torch.where(act, t, torch.full_like(t, s))
+            y[tt, torch.arange(N, device=gx.device)] = torch.where(act[:, None], hn, torch.zeros_like(hn))
+            hs.append(h.clone())
+        ys.append(y)
+        hss.append(torch.stack(hs))
+    return sum(ys), hss
+
+
+@pytest.mark.parametrize("N,H,ndir", [(8, 1280, 2), (20, 1024, 2), (8, 1280, 1)])
+def test_fp8_recurrence_matches_emulation(cuda, N, H, ndir):
+    """The fp8 GRU forward (e4m3 U and h exchange, 8 groups of H/64 workgroups) against an
+    fp32 emulation of the same quantisation: outputs and saved states within 2 %, padding
+    positions exactly zero, bf16 h copy = the fp32 state rounded."""
+    from deepspeech_amd.ops import rnn as RNN
+    torch.manual_seed(N + H)
+    T = 19
+    plan = RNN.plan_for(N, H, "gru", ndir, cuda)
+    if not RNN.fp8_recurrence_ok(plan, N):
+        pytest.skip("geometry not served by the fp8 recurrence (plan rows)")
+    gx = (torch.randn(T, N, ndir * 3 * H, device=cuda) * 0.5).to(torch.bfloat16)
+    lens = torch.randint(T // 2, T + 1, (N,), device=cuda, dtype=torch.int32)
+    lens[0] = T
+    U = [(torch.randn(3 * H, H, device=cuda) * (1.5 / H ** 0.5)).to(torch.bfloat16) for _ in range(ndir)]
+    bh = [torch.randn(3 * H, device=cuda) * 0.1 for _ in range(ndir)]
+    y, (hx, hs, gates) = RNN._run_fwd_fp8(gx, lens, U, bh + [None] * (2 - ndir), plan)
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    yr, hsr = _gru_fp8_emulation(gx, lens, U, bh, H)
+    assert _rel(y.float(), yr) < 2e-2, _rel(y.float(), yr)
+    for d in range(ndir):
+        assert _rel(hs[d, 1:, :N], hsr[d]) < 2e-2
+        assert torch.equal(hx[d, 1:, :N], hs[d, 1:, :N].to(torch.bfloat16))
+    for b in range(N):
+        L = int(lens[b])
+        if L < T:
+            assert float(y[L:, b].abs().max()) == 0.0
