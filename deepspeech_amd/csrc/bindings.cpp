@@ -95,7 +95,7 @@ int ds2_fp8_quant_pow2(const void* x, long long n, void* q, int* uexp, unsigned*
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs);
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
 long long ds2_rnnx_ring_floats(int H, int BG, int R);
-int ds2_rnnx_grid(int H, int ngroups, int xcd_map);
+int ds2_rnnx_grid(int H, int cell, int ngroups, int xcd_map);
 int ds2_rnnx_kb(int H, int G, int fwd);
 size_t ds2_rnnx_smem(int H, int G, int mt, int fwd);
 int ds2_ctc_fused(const void* logits, int logits_bf16, const int* lens, const int* labels, const int* label_lens,
@@ -454,7 +454,7 @@ void rnnx_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tens
 
 py::dict rnnx_info(int64_t H, int64_t G, int64_t mt, int64_t ngroups, int64_t xcd_map) {
   py::dict d;
-  d["grid"] = ds2_rnnx_grid((int)H, (int)ngroups, (int)xcd_map);
+  d["grid"] = ds2_rnnx_grid((int)H, G == 3 ? 1 : 0, (int)ngroups, (int)xcd_map);
   d["kb_fwd"] = ds2_rnnx_kb((int)H, (int)G, 1);
   d["kb_bwd"] = ds2_rnnx_kb((int)H, (int)G, 0);
   d["smem_fwd"] = (int64_t)ds2_rnnx_smem((int)H, (int)G, (int)mt, 1);

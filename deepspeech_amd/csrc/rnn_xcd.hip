@@ -1527,6 +1527,573 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Wide one-gate layers (the reference's 7 x bi-RNN(ReLU)-1760, src/train.sh:42): 64 units
+// per workgroup, so a group is P = ceil(H/64) <= 28 workgroups and fits ONE XCD (H/32 = 55
+// did not: two per CU measured slower, profiles/r3_negative_results.md).
+//
+// Forward (rnnw_fwd_kernel): generation-4 structure with two 16-unit n-tiles per MFMA wave:
+// wave w owns units 32 uh + 16 t + c (uh = w & 1, t = 0, 1) over K quarter kq = w >> 1.
+// Every exchange granule of the wave's K quarter is in flight at once (poll_mfma_par: one L2
+// round trip per retry round), the register U slice is capped at 7-8 k-steps (3 waves per
+// SIMD: <= 168 VGPRs) and the rest of the wave's U k-steps lives in LDS (wide_kl). Each lane finalises
+// element j = kq of both tiles (two ReLU cells), publishes two 16-B granules and stages two
+// outputs. The last workgroup of a group may be half empty (H % 64 == 32): its units >= H
+// have zero U rows, load no gx and store nothing.
+// ------------------------------------------------------------------------------------
+constexpr int UWW = 64;           // hidden units per workgroup of the wide kernels
+// k-steps of each wave's U slice kept in LDS: the register slice is capped at 8 k-steps (9
+// spilled at KB >= 11), 7 once KB >= 13 (every exchange granule of the K quarter is in flight,
+// KB x 4 VGPRs)
+constexpr int wide_kl(int kb) { return kb > 12 ? kb - 7 : (kb > 8 ? kb - 8 : 0); }
+
+template <int KB, int KL>
+__global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
+  constexpr int NT = 2;                           // 16-unit n-tiles per MFMA wave
+  constexpr int KR = KB - KL;
+  static_assert(KL >= 0 && KR >= 1, "register k-steps");
+  constexpr int ROWS = 16;
+  constexpr int GP = UWW + 4;                     // gx ring row pitch (floats)
+  constexpr int OP = UWW + 4;                     // output staging row pitch
+  constexpr int RGL = ROWS * (UWW / 8) / 64;      // gx granules per memory-wave lane (2)
+  constexpr int LPR = UWW / 4;                    // output lanes per row (4 units each)
+  constexpr int RPP = 64 / LPR;                   // rows per output pass
+  constexpr int NPS = ROWS / RPP;                 // output passes
+  __shared__ float red_s[2][2][4][3][NT][64];     // [parity][uh][element j][source][tile][lane]
+  __shared__ float gxr_s[2][ROWS][GP];
+  // h only: the output y is h where the step is active and 0 past the length (the memory
+  // wave knows which), so no y staging
+  __shared__ __attribute__((aligned(16))) float oh_s[2][ROWS][OP];
+  __shared__ int len_s[ROWS];
+  __shared__ int s_mode, s_abort;
+  __shared__ bf16x8 ul_s[KL > 0 ? KL : 1][QW][NT][64];   // LDS-resident U k-steps
+
+  int grp, mem;
+  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, KS = H / 32, N = a.N, NP = a.NP, R = a.R;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UWW;
+  const int uh = wave & 1, kq = wave >> 1;
+  const int erow = 4 * (lane >> 4) + (kq & 3);
+  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  if (wave == 0) {
+    const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+  __syncthreads();
+  if (s_abort) return;
+
+  // memory wave: gx granule q -> (row, 8-unit chunk)
+  i32x4 gpre[RGL];
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      const int row = q / (UWW / 8), c8 = q % (UWW / 8);
+      const int b = min(r0 + min(row, R - 1), N - 1);
+      const int t = max(0, min((dir == 0) ? s : (len_s[min(row, R - 1)] - 1 - s), a.T - 1));
+      const int u = min(u0 + c8 * 8, H - 8);
+      gpre[j] = *reinterpret_cast<const i32x4*>(a.gx + ((size_t)t * N + b) * a.gstride + dir * H + u);
+    }
+  };
+  auto mw_put = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      const int row = q / (UWW / 8), c8 = q % (UWW / 8);
+      if (row < R) {
+        const bool act = s < len_s[row] && u0 + c8 * 8 < H;
+        const bf16x8 v = __builtin_bit_cast(bf16x8, gpre[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gxr_s[s & 1][row][c8 * 8 + k] = act ? bf2f((bf16_t)v[k]) : 0.f;
+      }
+    }
+  };
+  unsigned long long yq[NPS];
+#pragma unroll
+  for (int j = 0; j < NPS; ++j) yq[j] = 0ull;
+  auto ysum_ptr = [&](int s, int j) -> unsigned long long* {
+    const int row = min((lane / LPR) + RPP * j, R - 1), c4 = (lane % LPR) * 4;
+    const int b = min(r0 + row, N - 1), L = len_s[row];
+    const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+    return reinterpret_cast<unsigned long long*>(a.ysum + ((size_t)t * N + b) * H + min(u0 + c4, H - 4));
+  };
+  auto mw_ysum_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < NPS; ++j)
+      if (RPP * j < R) yq[j] = __hip_atomic_load(ysum_ptr(s, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // outputs of step s out of staging slot s & 1: lane -> (row, 4 consecutive units) per pass
+  auto mw_store = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < NPS; ++j) {
+      const int row = (lane / LPR) + RPP * j, c4 = (lane % LPR) * 4;
+      const int u = u0 + c4;
+      if (row < R && u < H) {
+        const int b = r0 + row;
+        const f32x4 vh = *reinterpret_cast<const f32x4*>(&oh_s[s & 1][row][c4]);
+        *reinterpret_cast<f32x4*>(a.hsave[dir] + ((size_t)(s + 1) * NP + b) * H + u) = vh;
+        if (b < N) {
+          const int L = len_s[row];
+          const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+          const f32x4 vy = (s < L) ? vh : f32x4{0.f, 0.f, 0.f, 0.f};
+          uint2 o;
+          o.x = (unsigned)f2bf(vy[0]) | ((unsigned)f2bf(vy[1]) << 16);
+          o.y = (unsigned)f2bf(vy[2]) | ((unsigned)f2bf(vy[3]) << 16);
+          if (a.ysum == nullptr) {
+            *reinterpret_cast<uint2*>(a.y[dir] + ((size_t)t * N + b) * H + u) = o;
+          } else {
+            // fused direction sum: same protocol as rnnq_fwd_kernel (the later producer of a
+            // position waits for the other's bf16 value and stores the rounded bf16 sum)
+            unsigned long long* p = ysum_ptr(s, j);
+            const int other = (s < L) ? (L - 1 - s) : s;
+            const bool later = s > other || (s == other && dir == 1);
+            auto canon = [](unsigned h) { return (h & 0xffffu) == 0xffffu ? 0x7fc0u : (h & 0xffffu); };
+            if (!later) {
+              o.x = canon(o.x) | (canon(o.x >> 16) << 16);
+              o.y = canon(o.y) | (canon(o.y >> 16) << 16);
+              __hip_atomic_store(p, ((unsigned long long)o.y << 32) | o.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+              const long long t0 = __builtin_amdgcn_s_memrealtime();
+              unsigned long long q = yq[j];
+              while (true) {
+                const unsigned w0 = (unsigned)q, w1 = (unsigned)(q >> 32);
+                const bool ready = ((~w0 - 0x00010001u) & w0 & 0x80008000u) == 0 &&
+                                   ((~w1 - 0x00010001u) & w1 & 0x80008000u) == 0;
+                if (ready) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { atomicOr(a.err, 4u); break; }
+                __builtin_amdgcn_s_sleep(2);
+                q = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+              const unsigned q0 = (unsigned)q, q1 = (unsigned)(q >> 32);
+              auto add2 = [](unsigned x, unsigned y) {
+                const unsigned lo = f2bf(__uint_as_float(x << 16) + __uint_as_float(y << 16));
+                const unsigned hi = f2bf(__uint_as_float(x & 0xffff0000u) + __uint_as_float(y & 0xffff0000u));
+                return lo | (hi << 16);
+              };
+              *reinterpret_cast<uint2*>(p) = make_uint2(add2(o.x, q0), add2(o.y, q1));
+            }
+          }
+        }
+      }
+    }
+  };
+  if (wave == QW) {
+    mw_load(0);
+    mw_put(0);
+    if (a.steps > 1) mw_load(1);
+  }
+  __syncthreads();   // gx ring slot 0
+  const bool plain = s_mode == 1;
+  const unsigned hx_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H * 2);
+  bf16_t* hxd = a.hx[dir];
+  const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
+
+  if (wave < QW) {
+    int lu[NT];                        // this lane's local unit of each tile
+    bool uok[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      lu[t] = 32 * uh + 16 * t + (lane & 15);
+      uok[t] = u0 + lu[t] < H;
+    }
+    // resident U fragments: B[k][c] = U[u0 + lu[t]][ks*32 + k], ks = kq + 4*kk
+    bf16x8 uf[KR][NT];
+    bool kval[KB];
+    float hreg[NT];
+    {
+      const bf16_t* Ud = a.U[dir];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) {
+        const int ks = kq + 4 * kk;
+        kval[kk] = ks < KS;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          if (kval[kk] && uok[t])
+            v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)(u0 + lu[t]) * H + ks * 32 + 8 * (lane >> 4));
+          if (kk < KR) uf[kk < KR ? kk : 0][t] = v;
+          else ul_s[kk >= KR ? kk - KR : 0][wave][t][lane] = v;   // own slot: no barrier needed
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        hreg[t] = (erow < R && uok[t]) ? a.hsave[dir][(size_t)(r0 + erow) * H + u0 + lu[t]] : 0.f;   // slot 0 = h0
+    }
+    const int arow = r0 + min(lane & 15, R - 1);
+    const bool erow_ok = erow < R;
+    const int L = len_s[erow];
+    for (int s = 0; s < a.steps; ++s) {
+      float gxv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) gxv[t] = gxr_s[s & 1][erow][lu[t]];
+      // every k-step's granule is a constant 256 B past the first (immediate offsets); the
+      // k-step past K of the last quarter (kval false) is never waited on
+      unsigned off[KB];
+      const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + kq * 32 + 8 * (lane >> 4)) * 2);
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) off[kk] = o0 + 256u * kk;
+      f32x4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto mfma_k = [&](int kk, bf16x8 af) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const bf16x8 b = kk < KR ? uf[kk < KR ? kk : 0][t] : ul_s[kk >= KR ? kk - KR : 0][wave][t][lane];
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b, acc[t], 0, 0, 0);
+        }
+      };
+      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, 0, mfma_k);
+      if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
+      // transpose-reduce: hand the three elements this wave does not finalise to their owners
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j == kq) continue;
+        const int src = kq < j ? kq : kq - 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) red_s[s & 1][uh][j][src][t][lane] = acc[t][j];
+      }
+      lds_barrier();
+      if (s_abort) break;
+      const bool act = s < L;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const float own = kq == 0 ? acc[t][0] : kq == 1 ? acc[t][1] : kq == 2 ? acc[t][2] : acc[t][3];
+        const float pre = own + red_s[s & 1][uh][kq][0][t][lane] + red_s[s & 1][uh][kq][1][t][lane] +
+                          red_s[s & 1][uh][kq][2][t][lane];
+        const float hn = fminf(fmaxf(gxv[t] + pre, 0.f), RELU_CAP);
+        const float hnew = act ? hn : hreg[t];
+        hreg[t] = hnew;
+        unsigned hq = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)hnew);
+        hq = hq == 0xffffu ? 0x7fc0u : hq;
+        // 16-B exchange granule = 8 consecutive units of one row = 8 consecutive lanes
+        const unsigned pr = hq | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)hq, 0x101, 0xf, 0xf, false) << 16);
+        const int q1 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x102, 0xf, 0xf, false);
+        const int q2 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x104, 0xf, 0xf, false);
+        const int q3 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x106, 0xf, 0xf, false);
+        if ((lane & 7) == 0 && erow_ok && uok[t]) {
+          const i32x4 v = {(int)pr, q1, q2, q3};
+          const unsigned off2 = (unsigned)((((size_t)(s + 1) * NP + r0 + erow) * H + u0 + lu[t]) * 2);
+          store_granule(plain, rs_hx, hxd, off2, v);
+        }
+        oh_s[s & 1][erow][lu[t]] = hnew;
+      }
+    }
+  } else {
+    for (int s = 0; s < a.steps; ++s) {
+      if (a.ysum != nullptr && s >= 2) mw_ysum_load(s - 2);
+      if (s + 1 < a.steps) mw_put(s + 1);
+      if (s >= 2) mw_store(s - 2);
+      if (s + 2 < a.steps) mw_load(s + 2);
+      lds_barrier();
+      if (s_abort) break;
+    }
+  }
+  __syncthreads();
+  if (wave == QW && !s_abort) {
+    if (a.steps >= 2) {
+      if (a.ysum != nullptr) mw_ysum_load(a.steps - 2);
+      mw_store(a.steps - 2);
+    }
+    if (a.steps >= 1) {
+      if (a.ysum != nullptr) mw_ysum_load(a.steps - 1);
+      mw_store(a.steps - 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Wide one-gate BPTT (rnnw_bwd_kernel): the reduce-scatter protocol of rnnrs_bwd_kernel
+// (tagged-bf16 partials in a 3-slot ring, R <= 8 rows, two producers per gather load) with
+// 64-unit workgroups. A producer's own columns are its 64 units (two 32-column k-steps), so
+// its partial P_j(s) = da_s[:, own] . U[own, :] covers all H units in MTS = H/16 m-tiles,
+// published in unit pairs (32 units per 16-B granule row); a consumer gathers the two pairs
+// of its 64 units from every producer.
+// ------------------------------------------------------------------------------------
+template <int MTU, int GPT>
+__global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
+  constexpr int ROWS = 16;
+  constexpr int KG = UWW / 32;                    // 32-column k-steps of the own columns (2)
+  constexpr int EPT = ROWS * UWW / ETH;           // epilogue elements per thread (4)
+  constexpr int DGP = UWW + 8;                    // da tile pitch (bf16)
+  constexpr int LT = ROWS * (UWW / 4) / 64;       // memory-wave load tasks per lane (4)
+  constexpr int ST = ROWS * (UWW / 8) / 64;       // memory-wave store tasks per lane (2)
+  static_assert(GPT % 2 == 0, "two producers per gather load");
+  __shared__ float red_s[MW][ROWS][UWW + 1];
+  __shared__ __attribute__((aligned(16))) bf16_t dg_s[ROWS][DGP];
+  __shared__ float dyr_s[2][ROWS][UWW];
+  __shared__ float hpr_s[2][ROWS][UWW];
+  __shared__ __attribute__((aligned(16))) float ox_s[2][ROWS][UWW];
+  __shared__ __attribute__((aligned(16))) bf16_t oh_s[2][ROWS][UWW];
+  __shared__ int len_s[ROWS];
+  __shared__ int s_mode, s_abort;
+
+  int grp, mem;
+  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, N = a.N, NP = a.NP, R = a.R, P = a.P, MTS = H / 16, NPR = MTS / 2;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UWW;
+  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  for (int i = tid; i < ROWS * DGP; i += NTH) (&dg_s[0][0])[i] = 0;
+  if (wave == 0) {
+    const int m = group_census(a.census, grp, mem, P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+
+  // resident A fragments: A[m][k] = U[u0 + 32 kg + k][16 mt + m], m-tile mt of unit pair
+  // wave + 7 (i >> 1) (tiles 2p, 2p + 1); own columns >= H (half-empty last workgroup) are 0
+  bf16x8 ua[MTU][KG];
+  {
+    const bf16_t* Ud = a.U[dir];
+#pragma unroll
+    for (int i = 0; i < MTU; ++i) {
+      const int mt = 2 * (wave + MW * (i >> 1)) + (i & 1);
+#pragma unroll
+      for (int kg = 0; kg < KG; ++kg) {
+        bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        const int col0 = u0 + 32 * kg + 8 * (lane >> 4);
+        if (wave < MW && mt < MTS && col0 < H) {
+          const bf16_t* p = Ud + (size_t)col0 * H + 16 * mt + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (short)p[(size_t)j * H];
+        }
+        ua[i][kg] = v;
+      }
+    }
+  }
+  float sbx[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) sbx[i] = 0.f;
+  __syncthreads();   // len_s, dg_s zero rows, census
+
+  // memory wave: load task = (row, 4 units), store task = (row, 8 units)
+  uint2 pdy[LT];
+  float4 php[LT];
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q / (UWW / 4), c4 = (q % (UWW / 4)) * 4;
+      if (row < R && u0 + c4 < H) {
+        const int bp = min(r0 + row, NP - 1), bn = min(r0 + row, N - 1), u = u0 + c4;
+        const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+        pdy[k] = *reinterpret_cast<const uint2*>(a.dy + ((size_t)t * N + bn) * H + u);
+        php[k] = *reinterpret_cast<const float4*>(a.hsave[dir] + ((size_t)(s + 1) * NP + bp) * H + u);   // h_s
+      }
+    }
+  };
+  auto mw_put = [&](int s) {
+    const int slot = s & 1;
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q / (UWW / 4), c4 = (q % (UWW / 4)) * 4;
+      if (row < R) {
+        const bool act = s < len_s[row] && u0 + c4 < H;
+        const float dv[4] = {bf2f((bf16_t)(pdy[k].x & 0xffffu)), bf2f((bf16_t)(pdy[k].x >> 16)),
+                             bf2f((bf16_t)(pdy[k].y & 0xffffu)), bf2f((bf16_t)(pdy[k].y >> 16))};
+        const float hv[4] = {php[k].x, php[k].y, php[k].z, php[k].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dyr_s[slot][row][c4 + i] = act ? dv[i] : 0.f;
+          hpr_s[slot][row][c4 + i] = act ? hv[i] : 0.f;
+        }
+      }
+    }
+  };
+  auto mw_store = [&](int s) {          // da (= dgh = dgx of the one gate) of step s
+#pragma unroll
+    for (int k = 0; k < ST; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q / (UWW / 8), c8 = (q % (UWW / 8)) * 8;
+      const int b = r0 + row, u = u0 + c8;
+      if (row < R && u < H) {
+        *reinterpret_cast<i32x4*>(a.dgh[dir] + ((size_t)s * NP + b) * H + u) =
+            *reinterpret_cast<const i32x4*>(&oh_s[s & 1][row][c8]);
+        if (b < N) {
+          const int L = len_s[row];
+          const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(&ox_s[s & 1][row][c8]);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(&ox_s[s & 1][row][c8 + 4]);
+          bf16x8 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            o[i] = (short)f2bf(x0[i] * a.dgx_scale);
+            o[4 + i] = (short)f2bf(x1[i] * a.dgx_scale);
+          }
+          *reinterpret_cast<bf16x8*>(a.dgx + ((size_t)t * N + b) * a.gstride + dir * H + u) = o;
+        }
+      }
+    }
+  };
+  if (s_abort) return;
+  if (wave == MEMW && a.steps > 0) mw_load(a.steps - 1);
+  const bool plain = s_mode == 1;
+  const size_t slot_floats = (size_t)a.BG * P * R * H;
+  const unsigned ring_bytes = (unsigned)(3 * slot_floats * 4);
+  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(a.ring[dir], ring_bytes);
+  auto tag_of = [&](int s) -> unsigned { return (unsigned)(((a.steps - 1 - s) / 3) & 1); };
+  // [slot][bg][producer][unit pair][row][granule g][8 bf16]: granule (row, g) of pair p holds
+  // units 32 p + {4 g .. 4 g + 3, 16 + 4 g .. 16 + 4 g + 3}
+  auto ring_off16 = [&](int slot, int j, int pr, int row, int g) -> unsigned {
+    return (unsigned)((((((size_t)slot * a.BG + bg) * P + j) * NPR + pr) * R + row) * 4 + g) * 16u;
+  };
+
+  if (wave < MW) {
+    for (int s = a.steps - 1; s >= 0; --s) {
+      const bool has_next = s + 1 < a.steps;
+      // (G) lane -> (producer half h, row, granule g); the two unit pairs of this workgroup
+      {
+        const int h = lane >> 5, grow = (lane >> 2) & 7, gg = lane & 3;
+        constexpr int NI = GPT / 2;
+        float acc8[2][8];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc8[pp][q] = 0.f;
+        if (has_next && grow < R) {
+          const int cs = (s + 1) % 3;
+          const unsigned want = tag_of(s + 1);
+          unsigned off[2][NI];
+          i32x4 v[2][NI];
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+              const int j = min(wave + MW * (2 * i + h), P - 1);
+              off[pp][i] = ring_off16(cs, j, min(2 * mem + pp, NPR - 1), grow, gg);
+              v[pp][i] = load_sc1_b128(rs_ring, off[pp][i]);
+            }
+          const long long t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            if (2 * mem + pp >= NPR) continue;            // half-empty last workgroup
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+              if (wave + MW * (2 * i + h) < P) {
+                while (!granule_tagged16(v[pp][i], want)) {
+                  if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
+                  __builtin_amdgcn_s_sleep(1);
+                  v[pp][i] = load_sc1_b128(rs_ring, off[pp][i]);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  acc8[pp][2 * q] += __uint_as_float((unsigned)v[pp][i][q] << 16);
+                  acc8[pp][2 * q + 1] += __uint_as_float((unsigned)v[pp][i][q] & 0xffff0000u);
+                }
+              }
+            }
+          }
+        }
+        if (grow < R) {
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              red_s[wave][grow + 8 * h][32 * pp + 4 * gg + q] = acc8[pp][q];
+              red_s[wave][grow + 8 * h][32 * pp + 16 + 4 * gg + q] = acc8[pp][4 + q];
+            }
+        }
+      }
+      lds_barrier();                                                        // #1
+      if (s_abort) break;
+      // (E) cell backward (waves 0..3): da tile for the MFMA, dgh / dgx staging
+      if (wave < EW) {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + i * ETH;
+          const int row = e / UWW, c = e % UWW;
+          if (row < R) {
+            float dhrec = 0.f;
+            if (has_next) {
+#pragma unroll
+              for (int w = 0; w < MW; ++w) dhrec += red_s[w][row][c] + red_s[w][row + 8][c];
+            }
+            const bool act = s < len_s[row] && u0 + c < H;
+            const float dh = dyr_s[s & 1][row][c] + dhrec;
+            const float hp = hpr_s[s & 1][row][c];
+            const float da = (act && hp > 0.f && hp < RELU_CAP) ? dh : 0.f;
+            const bf16_t hb = f2bf(da);
+            dg_s[row][c] = hb;
+            oh_s[s & 1][row][c] = hb;
+            ox_s[s & 1][row][c] = da;
+            sbx[i] += da;
+          }
+        }
+      }
+      lds_barrier();                                                        // #2
+      // (M) publish P(s) = da_s[:, own cols] . U[own cols, :] into ring slot s % 3
+      if (s > 0) {
+        const int ws = s % 3;
+        const unsigned tagmask = tag_of(s) ? 0x00010001u : 0u;
+        const bool prow = (lane & 15) < R;
+        bf16x8 bfr[KG];
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg)
+          bfr[kg] = *reinterpret_cast<const bf16x8*>(&dg_s[lane & 15][32 * kg + 8 * (lane >> 4)]);
+        constexpr int NPW = MTU / 2;
+        unsigned offp[NPW];
+#pragma unroll
+        for (int k = 0; k < NPW; ++k) offp[k] = ring_off16(ws, mem, min(wave + MW * k, NPR - 1), lane & 15, lane >> 4);
+        auto publish = [&](auto PLAIN) {
+#pragma unroll
+          for (int k = 0; k < NPW; ++k) {
+            f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k][0], bfr[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k + 1][0], bfr[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+            for (int kg = 1; kg < KG; ++kg) {
+              a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k][kg], bfr[kg], a0, 0, 0, 0);
+              a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[2 * k + 1][kg], bfr[kg], a1, 0, 0, 0);
+            }
+            if (prow && wave + MW * k < NPR) {
+              const i32x4 v = {(int)bf16x2_tagged(a0[0], a0[1], tagmask), (int)bf16x2_tagged(a0[2], a0[3], tagmask),
+                               (int)bf16x2_tagged(a1[0], a1[1], tagmask), (int)bf16x2_tagged(a1[2], a1[3], tagmask)};
+              if constexpr (decltype(PLAIN)::value) store_b128(rs_ring, offp[k], v);
+              else store_sc1_b128(rs_ring, offp[k], v);
+            }
+          }
+        };
+        if (plain) publish(std::true_type{});
+        else publish(std::false_type{});
+      }
+    }
+  } else {
+    for (int s = a.steps - 1; s >= 0; --s) {
+      mw_put(s);
+      if (s + 2 < a.steps) mw_store(s + 2);
+      if (s >= 1) mw_load(s - 1);
+      lds_barrier();                                                        // #1
+      if (s_abort) break;
+      lds_barrier();                                                        // #2
+    }
+  }
+  __syncthreads();
+  if (wave == MEMW && !s_abort) {
+    if (a.steps >= 2) mw_store(1);
+    if (a.steps >= 1) mw_store(0);
+  }
+  // input-bias gradient: reduce the epilogue waves' rows through LDS
+  if (a.dbx_part[dir] != nullptr && !s_abort) {
+    float* bred = &red_s[0][0][0];
+    if (wave < EW) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int e = tid + i * ETH;
+        bred[(e / UWW) * UWW + e % UWW] = sbx[i];
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < UWW; q += NTH) {
+      float sum = 0.f;
+      for (int r = 0; r < ROWS; ++r) sum += bred[r * UWW + q];
+      if (u0 + q < H) a.dbx_part[dir][(size_t)bg * H + u0 + q] += sum;
+    }
+  }
+}
+
 template <int CELL, int MT>
 static int launch_fwd(const XFwd& a, int kb, int grid, size_t smem, hipStream_t st) {
   switch (kb) {
@@ -1577,6 +2144,10 @@ struct DS2RnnX {
 // direction sum into its output stores)
 // generation 4 serves k-steps per wave kbq <= 8 (ReLU) / <= 10 (GRU: beyond 7, the last
 // kbq - 7 of each wave's U k-steps are LDS-resident; knob 65536 keeps H = 1280 on gen 2)
+// wide one-gate layers (rnnw_*): 64 units per workgroup, 32 < H/32 and H <= 1792
+static bool wide_ok(int H, int cell) { return cell == CELL_RELU && H % 32 == 0 && H / 32 > 32 && H <= 1792; }
+static int xcd_p(int H, int cell) { return wide_ok(H, cell) ? (H + UWW - 1) / UWW : H / UPW; }
+
 static bool gen4_ok(int H, int cell, int mt, int knobs) {
   const int kbq = (H / 32 + 3) / 4;
   if ((knobs & 256) || mt != 1) return false;
@@ -1585,12 +2156,12 @@ static bool gen4_ok(int H, int cell, int mt, int knobs) {
 }
 
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs) {
-  return ndir == 2 && gen4_ok(H, cell, mt, knobs) ? 1 : 0;
+  return ndir == 2 && mt == 1 && (wide_ok(H, cell) || gen4_ok(H, cell, mt, knobs)) ? 1 : 0;
 }
 
 // grid size of a launch (blocks with no role exit at once)
-int ds2_rnnx_grid(int H, int ngroups, int xcd_map) {
-  const int P = H / UPW;
+int ds2_rnnx_grid(int H, int cell, int ngroups, int xcd_map) {
+  const int P = xcd_p(H, cell);
   return (xcd_map && ngroups <= 8) ? 8 * P : ngroups * P;
 }
 
@@ -1608,7 +2179,35 @@ size_t ds2_rnnx_smem(int H, int G, int mt, int fwd) {
   return 0;
 }
 
+static int rnnw_fwd(const DS2RnnX* d, hipStream_t st) {
+  if (d->R < 1 || d->R > 8 || d->mt != 1 || d->NP != d->BG * d->R) return -30;
+  XFwd a;
+  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = xcd_p(d->H, d->cell); a.BG = d->BG; a.R = d->R;
+  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
+  a.xcd_map = d->xcd_map && a.ngroups <= 8; a.knobs = d->knobs;
+  a.lens = d->lens; a.gx = (const bf16_t*)d->gx;
+  for (int i = 0; i < 2; ++i) {
+    a.U[i] = (const bf16_t*)d->U[i]; a.bh[i] = d->bh[i]; a.y[i] = (bf16_t*)d->y[i];
+    a.hx[i] = (bf16_t*)d->ex[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
+  }
+  a.ysum = (bf16_t*)d->ysum;
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = nullptr;
+  if (d->ysum != nullptr && d->ndir != 2) return -37;
+  if (d->steps <= 0) return 0;
+  const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
+  const int kbq = (d->H / 32 + 3) / 4;                 // 9..14 for 1024 < H <= 1792
+  switch (kbq) {
+#define DS2_W(K)                                                                                      \
+  case K: hipLaunchKernelGGL((rnnw_fwd_kernel<K, wide_kl(K)>), dim3(grid), dim3(QTH), 0, st, a); break;
+    DS2_W(9) DS2_W(10) DS2_W(11) DS2_W(12) DS2_W(13) DS2_W(14)
+#undef DS2_W
+    default: return -31;
+  }
+  return (int)hipGetLastError();
+}
+
 int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
+  if (wide_ok(d->H, d->cell)) return rnnw_fwd(d, st);
   if (d->H % UPW != 0 || d->R < 1 || d->R > 16 * d->mt || d->NP != d->BG * d->R) return -30;
   const int G = d->cell == CELL_GRU ? 3 : 1;
   const int kb = ds2_rnnx_kb(d->H, G, 1);
@@ -1625,7 +2224,7 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
   a.ysum = (bf16_t*)d->ysum;
   a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->steps <= 0) return 0;
-  const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
+  const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
   // generation 4 (K-quarter split, register epilogue) unless knob 256 asks for generation 2
   const int kbq = (d->H / 32 + 3) / 4;
   // (GRU at kbq = 8 spills under the 3-waves-per-SIMD register budget: kbq 8..10 keep
@@ -1680,7 +2279,38 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
 // floats of the reduce-scatter ring of ONE direction: [3 slots][BG][P][R][H]
 long long ds2_rnnx_ring_floats(int H, int BG, int R) { return 3LL * BG * (H / UPW) * R * H; }
 
+static int rnnw_bwd(const DS2RnnX* d, hipStream_t st) {
+  if (d->R < 1 || d->R > 8 || d->mt != 1 || d->NP != d->BG * d->R) return -30;
+  if (d->ring[0] == nullptr || (d->ndir == 2 && d->ring[1] == nullptr)) return -34;
+  const int P = xcd_p(d->H, d->cell);
+  if (P > 4 * MW) return -35;                         // GPT = 4 producers per gather thread
+  XBwdRS a;
+  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = P; a.BG = d->BG; a.R = d->R;
+  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
+  a.xcd_map = d->xcd_map && a.ngroups <= 8; a.knobs = d->knobs;
+  a.lens = d->lens; a.dy = (const bf16_t*)d->gx;
+  for (int i = 0; i < 2; ++i) {
+    a.U[i] = (const bf16_t*)d->U[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
+    a.dgh[i] = (bf16_t*)d->ex[i]; a.ring[i] = (float*)d->ring[i];
+    a.dbx_part[i] = d->dbx_part[i]; a.dbh_part[i] = d->dbh_part[i];
+  }
+  a.dgx = (bf16_t*)d->dgx; a.dgx_scale = d->dgx_scale;
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = nullptr;
+  if (d->steps <= 0) return 0;
+  const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
+  const int npw = (d->H / 32 + MW - 1) / MW;          // unit pairs per publishing wave
+  switch (2 * npw) {
+    case 10: hipLaunchKernelGGL((rnnw_bwd_kernel<10, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
+    case 12: hipLaunchKernelGGL((rnnw_bwd_kernel<12, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
+    case 14: hipLaunchKernelGGL((rnnw_bwd_kernel<14, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((rnnw_bwd_kernel<16, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
+    default: return -36;
+  }
+  return (int)hipGetLastError();
+}
+
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st) {
+  if (wide_ok(d->H, d->cell)) return rnnw_bwd(d, st);
   if (d->H % UPW != 0 || d->R < 1 || d->R > 16 || d->NP != d->BG * d->R || d->mt != 1) return -30;
   if (d->ring[0] == nullptr || (d->ndir == 2 && d->ring[1] == nullptr)) return -34;
   const int P = d->H / UPW;
@@ -1699,7 +2329,7 @@ int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st) {
   a.dgx = (bf16_t*)d->dgx; a.dgx_scale = d->dgx_scale;
   a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->steps <= 0) return 0;
-  const int grid = ds2_rnnx_grid(d->H, a.ngroups, a.xcd_map);
+  const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
   // bf16 partials (knob 64: fp32): PBF 1 for R <= 8 (two producers per load), 2 for R <= 16
   const int pbf = ((d->H / 16) % 2 != 0 || (d->knobs & 64)) ? 0 : (d->R <= 8 ? 1 : 2);
 #define DS2_RS(C, M, GP)                                                                    \

@@ -106,15 +106,34 @@ def _xcd_lds(H: int, G: int, mt: int) -> int:
         + (2 * 16 * 32 * 16 if G == 3 else 16) + 16 * 4 + G * 32 * 4 + 64
 
 
+def _wide_ok(H: int, cell: str) -> bool:
+    """One-gate layers wider than an XCD at 32 units per workgroup (32 < H/32, H <= 1792, e.g.
+    the reference's ReLU-1760) run the 64-unit wide kernels of csrc/rnn_xcd.hip (rnnw_*):
+    P = ceil(H/64) <= 28 workgroups per group, one XCD. (Two 32-unit workgroups per CU also
+    kept such a group on one XCD but measured slower: profiles/r3_negative_results.md.)"""
+    return cell == "rnn_relu" and H % 32 == 0 and H // 32 > 32 and H <= 1792
+
+
+def _xcd_p(H: int, cell: str) -> int:
+    """Workgroups per group of an XCD-kernel plan."""
+    return -(-H // 64) if _wide_ok(H, cell) else H // 32
+
+
 def make_xcd_plan(N: int, H: int, cell: str, ndir: int, cus: int) -> Optional[RnnPlan]:
     """Generation-2 geometry: groups of R batch rows x all H units (H/32 workgroups of 32
     units). Prefer the most groups that still fit the chip (smaller per-step gathers), at
     most 8 so a group can live on one XCD; rows per group R <= 32."""
     G = GATES[cell]
     P = H // 32
-    # (one-gate layers wider than an XCD, e.g. the reference's ReLU-1760 at P = 55, stay on the
-    # generation-1 kernels: two workgroups per CU kept such a group on one XCD but measured
-    # 6.3 / 5.0 us per step forward / BPTT against 4.9 / 4.9 — profiles/r3_negative_results.md)
+    if _wide_ok(H, cell):
+        # 8 groups (one per XCD) of R <= 8 rows: the wide BPTT's two-producers-per-load gather
+        Pw = _xcd_p(H, cell)
+        BG = 8 // ndir
+        R = -(-N // BG)
+        if R > 8 or ndir * BG * Pw > cus or Pw > cus // 8:
+            return None
+        return RnnPlan(N=N, NP=BG * R, BG=BG, mt=1, nw=8, persistent=True, H=H, S=H // 16, cell=cell,
+                       ndir=ndir, kind="xcd", R=R, xcd_map=1)
     wide = 42 if (_rs_ok(H) and G == 3) else 32         # see _rs_ok
     if H % 32 != 0 or P > wide:          # larger H: the resident U slice would spill
         return None
@@ -710,7 +729,7 @@ class FusedBiLayer(torch.autograd.Function):
             sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
             grouped = sch.grouped and on_side
-            if sch.defer_input and on_side and (ctx.idx >= 1 or grouped):
+            if sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_wgrad(plan, x16.device):
                 # run after the last recurrent layer's BPTT (grouped: every layer's, in one launch)
                 ops = GM.group_operands(dgx2.t(), x2, grp.view(plan.ndir * GH, D)) if grouped else None
                 sch.deferred.append(Deferred(dw, (dgx2, x2), [ops + (grp.view(plan.ndir * GH, D),)] if ops else None,
@@ -733,7 +752,7 @@ class FusedBiLayer(torch.autograd.Function):
             sch = arena.wgrad
             on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
             grouped = sch.grouped and on_side
-            defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped)
+            defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_wgrad(plan, x16.device)
             beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
             splits = _DU_SPLITS if beside else None
 
@@ -783,6 +802,27 @@ class FusedBiLayer(torch.autograd.Function):
         if tail:
             arena.wgrad.run_early_update()  # the recurrent stack's optimizer range, beside the front-end
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
+
+
+# A layer's weight gradients are deferred to the grouped tail launch only when its BPTT leaves
+# fewer than this many CUs idle; with more, they run beside the next layer's BPTT on the side
+# stream. Measured (same box, bench.py): headline (BPTT 200 of 256 CUs) deferral kept;
+# 7 x BiGRU-1280 (160 CUs, 96 idle) 23.10 ms/step beside vs 24.53 deferred; 7 x bi-ReLU-1760
+# (generation-1 kernels) 20.95 deferred vs 21.64 beside.
+_BESIDE_MIN_IDLE_CUS = 96
+
+
+def _bptt_cus(plan: RnnPlan) -> int:
+    """CUs the persistent BPTT of ``plan`` occupies (one workgroup per CU)."""
+    if plan.kind == "xcd":
+        return plan.ndir * plan.BG * _xcd_p(plan.H, plan.cell)
+    return plan.ndir * plan.BG * plan.S if plan.persistent else 1 << 30
+
+
+def _defer_wgrad(plan: RnnPlan, device: torch.device) -> bool:
+    if device.type != "cuda":
+        return True
+    return _ext.num_cus(device.index or 0) - _bptt_cus(plan) < _BESIDE_MIN_IDLE_CUS
 
 
 class Deferred:

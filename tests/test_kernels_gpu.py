@@ -108,6 +108,18 @@ def test_bptt_exchanges(cuda, cell, N, H):
     _rnn_case(cuda, cell, N=N, H=H, T=45, ndir=2, mode="auto", seed=21)
 
 
+@pytest.mark.parametrize("N,H,ndir", [(32, 1760, 2), (20, 1440, 2), (32, 1088, 2), (13, 1760, 1)])
+def test_wide_relu_kernels(cuda, N, H, ndir):
+    # one-gate layers wider than an XCD at 32 units per workgroup run the 64-unit wide kernels
+    # (rnnw_fwd_kernel / rnnw_bwd_kernel): full and half-empty last workgroups (H % 64 == 32),
+    # every LDS/register split of the U slice in use, one direction
+    from deepspeech_amd.ops import rnn as RNN
+    assert RNN._wide_ok(H, "rnn_relu")
+    p = RNN.make_xcd_plan(N, H, "rnn_relu", ndir, 256)
+    assert p is not None and p.kind == "xcd" and p.xcd_map == 1 and p.R <= 8
+    _rnn_case(cuda, "rnn_relu", N=N, H=H, T=37, ndir=ndir, mode="auto", seed=31)
+
+
 def test_unirnn_gru(cuda):
     _rnn_case(cuda, "gru", N=17, H=256, T=40, ndir=1, mode="auto", seed=5)
 
