@@ -1547,8 +1547,9 @@ constexpr int UWW = 64;           // hidden units per workgroup of the wide kern
 // KB x 4 VGPRs)
 constexpr int wide_kl(int kb) { return kb > 12 ? kb - 7 : (kb > 8 ? kb - 8 : 0); }
 
-template <int KB, int KL>
+template <int KB, int KL, int CH, bool STAMPS = false>
 __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
+  using StampT = typename std::conditional<STAMPS, Stamps, NoStamps>::type;
   constexpr int NT = 2;                           // 16-unit n-tiles per MFMA wave
   constexpr int KR = KB - KL;
   static_assert(KL >= 0 && KR >= 1, "register k-steps");
@@ -1690,6 +1691,7 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
   const unsigned hx_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H * 2);
   bf16_t* hxd = a.hx[dir];
   const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
+  StampT st(a.stamps != nullptr && (wave == 0 || wave == QW) && lane == 0);
 
   if (wave < QW) {
     int lu[NT];                        // this lane's local unit of each tile
@@ -1726,6 +1728,7 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
     const bool erow_ok = erow < R;
     const int L = len_s[erow];
     for (int s = 0; s < a.steps; ++s) {
+      st.mark(-1);
       float gxv[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) gxv[t] = gxr_s[s & 1][erow][lu[t]];
@@ -1738,15 +1741,20 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
       f32x4 acc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool nomfma = (a.knobs & 4) != 0;           // knob 4: no MFMA (timing only, wrong results)
       auto mfma_k = [&](int kk, bf16x8 af) {
+        if (nomfma) { acc[0][0] += __builtin_bit_cast(float, (int)af[0]); return; }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const bf16x8 b = kk < KR ? uf[kk < KR ? kk : 0][t] : ul_s[kk >= KR ? kk - KR : 0][wave][t][lane];
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b, acc[t], 0, 0, 0);
         }
       };
-      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, 0, mfma_k);
+      bool ok;
+      if constexpr (CH > 0) ok = poll_mfma<KB, 1, CH>(rs_hx, off, kval, true, a.timeout, mfma_k);
+      else ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, (a.knobs >> 12) & 3, mfma_k);
       if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
+      st.mark(0);
       // transpose-reduce: hand the three elements this wave does not finalise to their owners
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1755,7 +1763,9 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) red_s[s & 1][uh][j][src][t][lane] = acc[t][j];
       }
+      st.mark(1);
       lds_barrier();
+      st.mark(2);
       if (s_abort) break;
       const bool act = s < L;
 #pragma unroll
@@ -1780,14 +1790,18 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
         }
         oh_s[s & 1][erow][lu[t]] = hnew;
       }
+      st.mark(4);
     }
   } else {
     for (int s = 0; s < a.steps; ++s) {
+      st.mark(-1);
       if (a.ysum != nullptr && s >= 2) mw_ysum_load(s - 2);
       if (s + 1 < a.steps) mw_put(s + 1);
-      if (s >= 2) mw_store(s - 2);
+      if (s >= 2 && !(a.knobs & 2)) mw_store(s - 2);     // knob 2: no output stores (timing only)
       if (s + 2 < a.steps) mw_load(s + 2);
+      st.mark(0);
       lds_barrier();
+      st.mark(1);
       if (s_abort) break;
     }
   }
@@ -1802,6 +1816,8 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
       mw_store(a.steps - 1);
     }
   }
+  if (STAMPS && wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
 }
 
 // ------------------------------------------------------------------------------------
@@ -2191,14 +2207,31 @@ static int rnnw_fwd(const DS2RnnX* d, hipStream_t st) {
     a.hx[i] = (bf16_t*)d->ex[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
   }
   a.ysum = (bf16_t*)d->ysum;
-  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = nullptr;
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->ysum != nullptr && d->ndir != 2) return -37;
   if (d->steps <= 0) return 0;
   const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
   const int kbq = (d->H / 32 + 3) / 4;                 // 9..14 for 1024 < H <= 1792
+  const int var = (d->knobs >> 20) & 3;                // A/B variants (timing): 1 = KL 4 CH 7, 2 = KL 2 CH 4
+  if (kbq == 14 && a.stamps != nullptr) {
+    hipLaunchKernelGGL((rnnw_fwd_kernel<14, wide_kl(14), 0, true>), dim3(grid), dim3(QTH), 0, st, a);
+    return (int)hipGetLastError();
+  }
+  if (kbq == 14 && var == 1) {
+    hipLaunchKernelGGL((rnnw_fwd_kernel<14, 4, 7>), dim3(grid), dim3(QTH), 0, st, a);
+    return (int)hipGetLastError();
+  }
+  if (kbq == 14 && var == 3) {
+    hipLaunchKernelGGL((rnnw_fwd_kernel<14, 1, 3>), dim3(grid), dim3(QTH), 0, st, a);
+    return (int)hipGetLastError();
+  }
+  if (kbq == 14 && var == 2) {
+    hipLaunchKernelGGL((rnnw_fwd_kernel<14, 2, 4>), dim3(grid), dim3(QTH), 0, st, a);
+    return (int)hipGetLastError();
+  }
   switch (kbq) {
 #define DS2_W(K)                                                                                      \
-  case K: hipLaunchKernelGGL((rnnw_fwd_kernel<K, wide_kl(K)>), dim3(grid), dim3(QTH), 0, st, a); break;
+  case K: hipLaunchKernelGGL((rnnw_fwd_kernel<K, wide_kl(K), 0>), dim3(grid), dim3(QTH), 0, st, a); break;
     DS2_W(9) DS2_W(10) DS2_W(11) DS2_W(12) DS2_W(13) DS2_W(14)
 #undef DS2_W
     default: return -31;

@@ -60,6 +60,8 @@ def run(cell, N, H, T, ndir, nw, mode, iters, stamps=False):
             w = t[:, :len(names)].double() / T
             active = w.sum(1) > 0
             w = w[active]
+            if w.shape[0] == 0:            # this kernel records no stamps
+                continue
             res[kind + "_cycles_per_step"] = {ph: [round(float(w[:, i].mean()), 0), round(float(w[:, i].min()), 0),
                                                    round(float(w[:, i].max()), 0)] for i, ph in enumerate(names)}
             if p.kind == "xcd":
