@@ -1532,25 +1532,25 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 // per workgroup, so a group is P = ceil(H/64) <= 28 workgroups and fits ONE XCD (H/32 = 55
 // did not: two per CU measured slower, profiles/r3_negative_results.md).
 //
-// Forward (rnnw_fwd_kernel): generation-4 structure with two 16-unit n-tiles per MFMA wave:
-// wave w owns units 32 uh + 16 t + c (uh = w & 1, t = 0, 1) over K quarter kq = w >> 1.
-// Every exchange granule of the wave's K quarter is in flight at once (poll_mfma_par: one L2
-// round trip per retry round), the register U slice is capped at 7-8 k-steps (3 waves per
-// SIMD: <= 168 VGPRs) and the rest of the wave's U k-steps lives in LDS (wide_kl). Each lane finalises
-// element j = kq of both tiles (two ReLU cells), publishes two 16-B granules and stages two
-// outputs. The last workgroup of a group may be half empty (H % 64 == 32): its units >= H
+// Forward (rnnw_fwd_kernel): 8 MFMA waves = 8 K-eighths (k-steps ke + 8 kk), each over all
+// four 16-unit n-tiles of the workgroup, so every exchange granule is polled by ONE wave of
+// the workgroup. (The first version split the waves into 2 unit halves x 4 K-quarters like
+// the generation-4 forward: both halves polled the same granules, and with 14 granules per
+// lane the CU's vector-memory pipe, not the MFMAs, set the step: 5.4 us/step, 5.1 without any
+// MFMA.) Transpose-reduce over the 8 K-eighths: of the 16 (tile, element j) slots of a lane,
+// wave w finalises tile w >> 1, elements j = 2 (w & 1) + {0, 1}; every wave stores its 16
+// slots, ONE barrier, then each owner adds the 8 partials of its two. Every exchange granule
+// of the wave's K-eighth is in flight at once (poll_mfma_par); the last KL of its U k-steps
+// live in LDS. The last workgroup of a group may be half empty (H % 64 == 32): its units >= H
 // have zero U rows, load no gx and store nothing.
 // ------------------------------------------------------------------------------------
 constexpr int UWW = 64;           // hidden units per workgroup of the wide kernels
-// k-steps of each wave's U slice kept in LDS: the register slice is capped at 8 k-steps (9
-// spilled at KB >= 11), 7 once KB >= 13 (every exchange granule of the K quarter is in flight,
-// KB x 4 VGPRs)
-constexpr int wide_kl(int kb) { return kb > 12 ? kb - 7 : (kb > 8 ? kb - 8 : 0); }
+constexpr int wide_kl(int kb) { return kb >= 7 ? 2 : 0; }   // U k-steps per wave in LDS (register budget: 1 spilled at KB = 7)
 
-template <int KB, int KL, int CH, bool STAMPS = false>
+template <int KB, int KL, bool STAMPS = false>
 __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
   using StampT = typename std::conditional<STAMPS, Stamps, NoStamps>::type;
-  constexpr int NT = 2;                           // 16-unit n-tiles per MFMA wave
+  constexpr int NT = 4;                           // 16-unit n-tiles per MFMA wave (all 64 units)
   constexpr int KR = KB - KL;
   static_assert(KL >= 0 && KR >= 1, "register k-steps");
   constexpr int ROWS = 16;
@@ -1560,7 +1560,7 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
   constexpr int LPR = UWW / 4;                    // output lanes per row (4 units each)
   constexpr int RPP = 64 / LPR;                   // rows per output pass
   constexpr int NPS = ROWS / RPP;                 // output passes
-  __shared__ float red_s[2][2][4][3][NT][64];     // [parity][uh][element j][source][tile][lane]
+  __shared__ float red_s[2][QW][16][64];          // [parity][source wave][slot 4 t + j][lane]
   __shared__ float gxr_s[2][ROWS][GP];
   // h only: the output y is h where the step is active and 0 past the length (the memory
   // wave knows which), so no y staging
@@ -1576,8 +1576,8 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
   const int H = a.H, KS = H / 32, N = a.N, NP = a.NP, R = a.R;
   const int bg = grp % a.BG, dir = grp / a.BG;
   const int r0 = bg * R, u0 = mem * UWW;
-  const int uh = wave & 1, kq = wave >> 1;
-  const int erow = 4 * (lane >> 4) + (kq & 3);
+  const int ke = wave;                            // K-eighth (MFMA waves)
+  const int tw = wave >> 1, j0 = 2 * (wave & 1);  // owned tile and first owned element
   if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
   if (wave == 0) {
     const int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
@@ -1694,50 +1694,47 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
   StampT st(a.stamps != nullptr && (wave == 0 || wave == QW) && lane == 0);
 
   if (wave < QW) {
-    int lu[NT];                        // this lane's local unit of each tile
-    bool uok[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      lu[t] = 32 * uh + 16 * t + (lane & 15);
-      uok[t] = u0 + lu[t] < H;
-    }
-    // resident U fragments: B[k][c] = U[u0 + lu[t]][ks*32 + k], ks = kq + 4*kk
+    const int lu = 16 * tw + (lane & 15);          // this lane's local unit (owned tile)
+    const bool uok = u0 + lu < H;
+    // resident U fragments: B[k][c] = U[u0 + 16 t + c][ks*32 + k], ks = ke + 8*kk
     bf16x8 uf[KR][NT];
     bool kval[KB];
-    float hreg[NT];
+    float hreg[2];
+    int erow[2];
     {
       const bf16_t* Ud = a.U[dir];
 #pragma unroll
       for (int kk = 0; kk < KB; ++kk) {
-        const int ks = kq + 4 * kk;
+        const int ks = ke + 8 * kk;
         kval[kk] = ks < KS;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-          if (kval[kk] && uok[t])
-            v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)(u0 + lu[t]) * H + ks * 32 + 8 * (lane >> 4));
+          const int ur = u0 + 16 * t + (lane & 15);
+          if (kval[kk] && ur < H)
+            v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)ur * H + ks * 32 + 8 * (lane >> 4));
           if (kk < KR) uf[kk < KR ? kk : 0][t] = v;
           else ul_s[kk >= KR ? kk - KR : 0][wave][t][lane] = v;   // own slot: no barrier needed
         }
       }
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        hreg[t] = (erow < R && uok[t]) ? a.hsave[dir][(size_t)(r0 + erow) * H + u0 + lu[t]] : 0.f;   // slot 0 = h0
+      for (int e = 0; e < 2; ++e) {
+        erow[e] = 4 * (lane >> 4) + j0 + e;
+        hreg[e] = (erow[e] < R && uok) ? a.hsave[dir][(size_t)(r0 + erow[e]) * H + u0 + lu] : 0.f;   // slot 0 = h0
+      }
     }
     const int arow = r0 + min(lane & 15, R - 1);
-    const bool erow_ok = erow < R;
-    const int L = len_s[erow];
     for (int s = 0; s < a.steps; ++s) {
       st.mark(-1);
-      float gxv[NT];
+      float gxv[2];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) gxv[t] = gxr_s[s & 1][erow][lu[t]];
-      // every k-step's granule is a constant 256 B past the first (immediate offsets); the
-      // k-step past K of the last quarter (kval false) is never waited on
+      for (int e = 0; e < 2; ++e) gxv[e] = gxr_s[s & 1][erow[e]][lu];
+      // every k-step's granule is a constant 512 B past the first (immediate offsets); a
+      // k-step past K (kval false) is never waited on
       unsigned off[KB];
-      const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + kq * 32 + 8 * (lane >> 4)) * 2);
+      const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + ke * 32 + 8 * (lane >> 4)) * 2);
 #pragma unroll
-      for (int kk = 0; kk < KB; ++kk) off[kk] = o0 + 256u * kk;
+      for (int kk = 0; kk < KB; ++kk) off[kk] = o0 + 512u * kk;
       f32x4 acc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1750,32 +1747,30 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b, acc[t], 0, 0, 0);
         }
       };
-      bool ok;
-      if constexpr (CH > 0) ok = poll_mfma<KB, 1, CH>(rs_hx, off, kval, true, a.timeout, mfma_k);
-      else ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, (a.knobs >> 12) & 3, mfma_k);
+      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, (a.knobs >> 12) & 3, mfma_k);
       if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
       st.mark(0);
-      // transpose-reduce: hand the three elements this wave does not finalise to their owners
+      // transpose-reduce: every slot q = 4 t + j to LDS (the owned two as well: a register
+      // array indexed by the wave-dependent tile would live in scratch), one barrier, then
+      // the owner sums the 8 K-eighths of its slots 4 tw + j0 + {0, 1} in wave order
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j == kq) continue;
-        const int src = kq < j ? kq : kq - 1;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) red_s[s & 1][uh][j][src][t][lane] = acc[t][j];
-      }
+      for (int q = 0; q < 16; ++q) red_s[s & 1][wave][q][lane] = acc[q >> 2][q & 3];
       st.mark(1);
       lds_barrier();
       st.mark(2);
       if (s_abort) break;
-      const bool act = s < L;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const float own = kq == 0 ? acc[t][0] : kq == 1 ? acc[t][1] : kq == 2 ? acc[t][2] : acc[t][3];
-        const float pre = own + red_s[s & 1][uh][kq][0][t][lane] + red_s[s & 1][uh][kq][1][t][lane] +
-                          red_s[s & 1][uh][kq][2][t][lane];
-        const float hn = fminf(fmaxf(gxv[t] + pre, 0.f), RELU_CAP);
-        const float hnew = act ? hn : hreg[t];
-        hreg[t] = hnew;
+      for (int e = 0; e < 2; ++e) {
+        const int q = 4 * tw + j0 + e;
+        float pre = 0.f;
+#pragma unroll
+        for (int w = 0; w < QW; ++w) pre += red_s[s & 1][w][q][lane];
+        const int row = erow[e];
+        const int L = len_s[row];
+        const bool act = s < L;
+        const float hn = fminf(fmaxf(gxv[e] + pre, 0.f), RELU_CAP);
+        const float hnew = act ? hn : hreg[e];
+        hreg[e] = hnew;
         unsigned hq = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)hnew);
         hq = hq == 0xffffu ? 0x7fc0u : hq;
         // 16-B exchange granule = 8 consecutive units of one row = 8 consecutive lanes
@@ -1783,12 +1778,12 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
         const int q1 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x102, 0xf, 0xf, false);
         const int q2 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x104, 0xf, 0xf, false);
         const int q3 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x106, 0xf, 0xf, false);
-        if ((lane & 7) == 0 && erow_ok && uok[t]) {
+        if ((lane & 7) == 0 && row < R && uok) {
           const i32x4 v = {(int)pr, q1, q2, q3};
-          const unsigned off2 = (unsigned)((((size_t)(s + 1) * NP + r0 + erow) * H + u0 + lu[t]) * 2);
+          const unsigned off2 = (unsigned)((((size_t)(s + 1) * NP + r0 + row) * H + u0 + lu) * 2);
           store_granule(plain, rs_hx, hxd, off2, v);
         }
-        oh_s[s & 1][erow][lu[t]] = hnew;
+        oh_s[s & 1][row][lu] = hnew;
       }
       st.mark(4);
     }
@@ -2211,28 +2206,14 @@ static int rnnw_fwd(const DS2RnnX* d, hipStream_t st) {
   if (d->ysum != nullptr && d->ndir != 2) return -37;
   if (d->steps <= 0) return 0;
   const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
-  const int kbq = (d->H / 32 + 3) / 4;                 // 9..14 for 1024 < H <= 1792
-  const int var = (d->knobs >> 20) & 3;                // A/B variants (timing): 1 = KL 4 CH 7, 2 = KL 2 CH 4
-  if (kbq == 14 && a.stamps != nullptr) {
-    hipLaunchKernelGGL((rnnw_fwd_kernel<14, wide_kl(14), 0, true>), dim3(grid), dim3(QTH), 0, st, a);
-    return (int)hipGetLastError();
-  }
-  if (kbq == 14 && var == 1) {
-    hipLaunchKernelGGL((rnnw_fwd_kernel<14, 4, 7>), dim3(grid), dim3(QTH), 0, st, a);
-    return (int)hipGetLastError();
-  }
-  if (kbq == 14 && var == 3) {
-    hipLaunchKernelGGL((rnnw_fwd_kernel<14, 1, 3>), dim3(grid), dim3(QTH), 0, st, a);
-    return (int)hipGetLastError();
-  }
-  if (kbq == 14 && var == 2) {
-    hipLaunchKernelGGL((rnnw_fwd_kernel<14, 2, 4>), dim3(grid), dim3(QTH), 0, st, a);
-    return (int)hipGetLastError();
-  }
-  switch (kbq) {
+  const int kb8 = (d->H / 32 + 7) / 8;                 // k-steps per K-eighth: 5..7 for 1024 < H <= 1792
+  switch (kb8) {
 #define DS2_W(K)                                                                                      \
-  case K: hipLaunchKernelGGL((rnnw_fwd_kernel<K, wide_kl(K), 0>), dim3(grid), dim3(QTH), 0, st, a); break;
-    DS2_W(9) DS2_W(10) DS2_W(11) DS2_W(12) DS2_W(13) DS2_W(14)
+  case K:                                                                                             \
+    if (a.stamps) hipLaunchKernelGGL((rnnw_fwd_kernel<K, wide_kl(K), true>), dim3(grid), dim3(QTH), 0, st, a); \
+    else hipLaunchKernelGGL((rnnw_fwd_kernel<K, wide_kl(K), false>), dim3(grid), dim3(QTH), 0, st, a); \
+    break;
+    DS2_W(5) DS2_W(6) DS2_W(7)
 #undef DS2_W
     default: return -31;
   }
