@@ -875,6 +875,318 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
   if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
 }
 
+// ------------------------------------------------------------------------------------
+// GRU forward, generation 5 (rnne_fwd_kernel, H <= 1024): the K-eighth structure of the wide
+// forward for 32-unit GRU workgroups. Generation 4 split its 8 MFMA waves into 2 unit halves x
+// 4 K-quarters, so each exchange granule was polled by both halves; here wave w polls K-eighth
+// w (k-steps w + 8 kk) once and multiplies it into all six 16-unit tiles (2 unit halves x 3
+// gates). Every wave stores its 24 partial slots (tile, element j) to LDS, ONE barrier, and the
+// owner of cell slot (unit half w & 1, element j = w >> 1) sums the 8 K-eighths of its three
+// gates in wave order and runs the GRU cell in registers, as generation 4 does.
+// ------------------------------------------------------------------------------------
+// KL: the last KL of each wave's U k-steps live in LDS; SB: one partial buffer and a second
+// barrier per step instead of two buffers by step parity (the LDS of H = 1280: 48 KB of U)
+template <int KB, int KL, bool SB, bool STAMPS>
+__global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
+  using StampT = typename std::conditional<STAMPS, Stamps, NoStamps>::type;
+  constexpr int CELL = CELL_GRU;
+  constexpr int G = 3;
+  constexpr int NT = 2 * G;                       // tiles t = 3 uh + g
+  constexpr int ROWS = 16;
+  constexpr int GP = G * UPW + 4;                 // gx ring row pitch
+  constexpr int OP = UPW + 4;                     // output staging row pitch
+  constexpr int RG = ROWS * G * (UPW / 8);        // gx granules per step (upper bound)
+  constexpr int RGL = (RG + 63) / 64;
+  constexpr int KR = KB - KL;
+  static_assert(KL >= 0 && KR >= 1, "register k-steps");
+  __shared__ float red_s[SB ? 1 : 2][QW][NT][4][64];   // [parity][source wave][tile][element j][lane]
+  __shared__ bf16x8 ul_s[KL > 0 ? KL : 1][QW][NT][64];  // LDS-resident U k-steps
+  __shared__ float gxr_s[2][ROWS][GP];
+  __shared__ __attribute__((aligned(16))) float oh_s[2][ROWS][OP];
+  __shared__ __attribute__((aligned(16))) float oy_s[2][ROWS][OP];
+  __shared__ float4 og_s[2][ROWS][OP];
+  __shared__ int len_s[ROWS];
+  __shared__ int s_mode, s_abort;
+
+  int grp, mem;
+  if (!take_role(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, KS = H / 32, N = a.N, NP = a.NP, R = a.R;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW;
+  const int uh = wave & 1, jo = (wave >> 1) & 3;  // owned cell slot
+  const int erow = 4 * (lane >> 4) + jo;
+  const int ec = 16 * uh + (lane & 15);
+  if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  if (wave == 0) {
+    int m = group_census(a.census, grp, mem, a.P, a.timeout, a.err);
+    if ((a.knobs & 32768) && m > 0) m = 0;      // knob 32768: force write-through (timing)
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+  __syncthreads();
+  if (s_abort) return;
+
+  // memory wave: gx granule q -> (row, gate, 8-unit chunk)
+  i32x4 gpre[RGL];
+  const int NRG = R * G * (UPW / 8);
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      const int qq = q < NRG ? q : 0;
+      const int row = qq / (G * 4), rem = qq - row * (G * 4), g = rem >> 2, c8 = rem & 3;
+      const int b = min(r0 + row, N - 1);
+      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+      gpre[j] = *reinterpret_cast<const i32x4*>(a.gx + ((size_t)t * N + b) * a.gstride + dir * G * H + g * H + u0 +
+                                                c8 * 8);
+    }
+  };
+  auto mw_put = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      if (q < NRG) {
+        const int row = q / (G * 4), rem = q - row * (G * 4), g = rem >> 2, c8 = rem & 3;
+        const bool act = s < len_s[row];
+        const bf16x8 v = __builtin_bit_cast(bf16x8, gpre[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gxr_s[s & 1][row][g * UPW + c8 * 8 + k] = act ? bf2f((bf16_t)v[k]) : 0.f;
+      }
+    }
+  };
+  // fused direction sum: the other direction's value for this lane's 2 output granules of
+  // step s, loaded ahead (before the gx put) so the round trip hides under the put
+  unsigned long long yq[2] = {0ull, 0ull};
+  auto ysum_ptr = [&](int s, int j) -> unsigned long long* {
+    const int row = min((lane >> 3) + 8 * j, R - 1), c4 = (lane & 7) * 4;
+    const int b = min(r0 + row, N - 1), L = len_s[row];
+    const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+    return reinterpret_cast<unsigned long long*>(a.ysum + ((size_t)t * N + b) * H + u0 + c4);
+  };
+  auto mw_ysum_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) yq[j] = __hip_atomic_load(ysum_ptr(s, j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // outputs of step s out of staging slot s&1: lane -> (row, 4 consecutive units) x 2
+  auto mw_store = [&](int s) {
+    f32x4 vh[2], vy[2];
+    float4 vg[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {         // all LDS reads first, then the stores
+      const int row = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
+      vh[j] = *reinterpret_cast<const f32x4*>(&oh_s[s & 1][row][c4]);
+      vy[j] = *reinterpret_cast<const f32x4*>(&oy_s[s & 1][row][c4]);
+      if (CELL == CELL_GRU)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vg[j][i] = og_s[(CELL == CELL_GRU) ? (s & 1) : 0][row][c4 + i];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
+      if (row < R) {
+        const int b = r0 + row, u = u0 + c4;
+        *reinterpret_cast<f32x4*>(a.hsave[dir] + ((size_t)(s + 1) * NP + b) * H + u) = vh[j];
+        if (CELL == CELL_GRU) {
+          float4* gp = reinterpret_cast<float4*>(a.gates[dir]) + ((size_t)s * NP + b) * H + u;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) gp[i] = vg[j][i];
+        }
+      }
+    }
+    // y (or the fused direction sum) after the state stores: the gate registers are dead
+    // before any wait on the other direction
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
+      if (row < R) {
+        const int b = r0 + row, u = u0 + c4;
+        if (b < N) {
+          const int L = len_s[row];
+          const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+          uint2 o;
+          o.x = (unsigned)f2bf(vy[j][0]) | ((unsigned)f2bf(vy[j][1]) << 16);
+          o.y = (unsigned)f2bf(vy[j][2]) | ((unsigned)f2bf(vy[j][3]) << 16);
+          if (a.ysum == nullptr) {
+            *reinterpret_cast<uint2*>(a.y[dir] + ((size_t)t * N + b) * H + u) = o;
+          } else {
+            // Fused direction sum (reference: the fw + bw outputs summed by the caller,
+            // src/custom_ops.py:36-96). Position t is produced by the forward direction at
+            // step t and by the backward one at step L-1-t (padding positions: both at step
+            // t). The direction that produces it LATER (ties: the backward one) waits for the
+            // other's bf16 value in the sentinel-filled sum buffer and writes the bf16 sum,
+            // rounding exactly like bf16 + bf16 in torch; the earlier one writes its value
+            // through (sc1: the other direction's groups live on other XCDs). No cycle: the
+            // later side of a pair only waits for a step the earlier side reached first.
+            unsigned long long* p = ysum_ptr(s, j);
+            const int other = (s < L) ? (L - 1 - s) : s;
+            const bool later = s > other || (s == other && dir == 1);
+            auto canon = [](unsigned h) { return (h & 0xffffu) == 0xffffu ? 0x7fc0u : (h & 0xffffu); };
+            if (!later) {
+              o.x = canon(o.x) | (canon(o.x >> 16) << 16);
+              o.y = canon(o.y) | (canon(o.y >> 16) << 16);
+              __hip_atomic_store(p, ((unsigned long long)o.y << 32) | o.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+              const long long t0 = __builtin_amdgcn_s_memrealtime();
+              unsigned long long q = yq[j];           // usually already there (loaded ahead)
+              while (true) {
+                const unsigned w0 = (unsigned)q, w1 = (unsigned)(q >> 32);
+                const bool ready = ((~w0 - 0x00010001u) & w0 & 0x80008000u) == 0 &&
+                                   ((~w1 - 0x00010001u) & w1 & 0x80008000u) == 0;
+                if (ready) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { atomicOr(a.err, 4u); break; }
+                __builtin_amdgcn_s_sleep(2);
+                q = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
+              const unsigned q0 = (unsigned)q, q1 = (unsigned)(q >> 32);
+              auto add2 = [](unsigned x, unsigned y) {      // two bf16 pairs -> rounded bf16 sums
+                const unsigned lo = f2bf(__uint_as_float(x << 16) + __uint_as_float(y << 16));
+                const unsigned hi = f2bf(__uint_as_float(x & 0xffff0000u) + __uint_as_float(y & 0xffff0000u));
+                return lo | (hi << 16);
+              };
+              *reinterpret_cast<uint2*>(p) = make_uint2(add2(o.x, q0), add2(o.y, q1));
+            }
+          }
+        }
+      }
+    }
+  };
+  if (wave == QW) {
+    mw_load(0);
+    mw_put(0);
+    if (a.steps > 1) mw_load(1);
+  }
+  __syncthreads();   // gx ring slot 0
+  const bool plain = s_mode == 1;
+  const unsigned hx_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H * 2);
+  bf16_t* hxd = a.hx[dir];
+  const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
+  StampT st(a.stamps != nullptr && (wave == 0 || wave == QW) && lane == 0);
+
+  if (wave < QW) {
+    // resident U fragments: B[k][c] = U[g H + u0 + 16 h + c][ks*32 + k], tile 3 h + g, ks = wave + 8 kk
+    bf16x8 uf[KR][NT];
+    bool kval[KB];
+    float hreg = 0.f, bhr[G];
+    {
+      const bf16_t* Ud = a.U[dir];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) {
+        const int ks = wave + 8 * kk;
+        kval[kk] = ks < KS;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int g = t % G, h = t / G;
+          bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          if (kval[kk])
+            v = *reinterpret_cast<const bf16x8*>(Ud + (size_t)(g * H + u0 + 16 * h + (lane & 15)) * H + ks * 32 +
+                                                 8 * (lane >> 4));
+          if (kk < KR) uf[kk < KR ? kk : 0][t] = v;
+          else ul_s[kk >= KR ? kk - KR : 0][wave][t][lane] = v;   // own slot: no barrier needed
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) bhr[g] = a.bh[dir] ? a.bh[dir][g * H + u0 + ec] : 0.f;
+      if (erow < R) hreg = a.hsave[dir][(size_t)(r0 + erow) * H + u0 + ec];   // slot 0 = h0
+    }
+    const int arow = r0 + min(lane & 15, R - 1);
+    const int nap = (a.knobs >> 12) & 3;
+    const bool erow_ok = erow < R;
+    const int L = len_s[erow];
+    for (int s = 0; s < a.steps; ++s) {
+      st.mark(-1);
+      float gxv[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) gxv[g] = gxr_s[s & 1][erow][g * UPW + ec];
+      unsigned off[KB];
+      const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + wave * 32 + 8 * (lane >> 4)) * 2);
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) off[kk] = o0 + 512u * kk;
+      f32x4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto mfma_k = [&](int kk, bf16x8 af) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const bf16x8 b = kk < KR ? uf[kk < KR ? kk : 0][t] : ul_s[kk >= KR ? kk - KR : 0][wave][t][lane];
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b, acc[t], 0, 0, 0);
+        }
+      };
+      const bool ok = poll_mfma_par<KB>(rs_hx, off, kval, a.timeout, nap, mfma_k);
+      if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
+      st.mark(0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red_s[SB ? 0 : (s & 1)][wave][t][j][lane] = acc[t][j];
+      st.mark(1);
+      lds_barrier();
+      st.mark(2);
+      if (s_abort) break;
+      float pre[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < QW; ++w) v += red_s[SB ? 0 : (s & 1)][w][3 * uh + g][jo][lane];
+        pre[g] = v;
+      }
+      if constexpr (SB) lds_barrier();               // every partial read before the next step's writes
+      const bool act = s < L;
+      float4 gsv = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float ghn = pre[2] + bhr[2];
+      const float r = sigmoidf_(gxv[0] + pre[0] + bhr[0]);
+      const float z = sigmoidf_(gxv[1] + pre[1] + bhr[1]);
+      const float n = tanhf_(gxv[2] + r * ghn);
+      const float hn = (1.f - z) * n + z * hreg;
+      if (act) gsv = make_float4(r, z, n, ghn);
+      const float hnew = act ? hn : hreg;
+      hreg = hnew;
+      unsigned hq = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)hnew);
+      hq = hq == 0xffffu ? 0x7fc0u : hq;
+      const unsigned pr = hq | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)hq, 0x101, 0xf, 0xf, false) << 16);
+      const int q1 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x102, 0xf, 0xf, false);
+      const int q2 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x104, 0xf, 0xf, false);
+      const int q3 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x106, 0xf, 0xf, false);
+      if ((lane & 7) == 0 && erow_ok) {
+        const i32x4 v = {(int)pr, q1, q2, q3};
+        const unsigned off2 = (unsigned)((((size_t)(s + 1) * NP + r0 + erow) * H + u0 + ec) * 2);
+        store_granule(plain, rs_hx, hxd, off2, v);
+      }
+      oh_s[s & 1][erow][ec] = hnew;
+      oy_s[s & 1][erow][ec] = act ? hn : 0.f;
+      og_s[s & 1][erow][ec] = gsv;
+      st.mark(4);
+    }
+  } else {
+    for (int s = 0; s < a.steps; ++s) {
+      st.mark(-1);
+      if (a.ysum != nullptr && s >= 2) mw_ysum_load(s - 2);
+      if (s + 1 < a.steps) mw_put(s + 1);
+      if (s >= 2) mw_store(s - 2);
+      if (s + 2 < a.steps) mw_load(s + 2);
+      st.mark(0);
+      lds_barrier();
+      st.mark(1);
+      if (s_abort) break;
+      if constexpr (SB) lds_barrier();
+    }
+  }
+  __syncthreads();
+  if (wave == QW && !s_abort) {
+    if (a.steps >= 2) {
+      if (a.ysum != nullptr) mw_ysum_load(a.steps - 2);
+      mw_store(a.steps - 2);
+    }
+    if (a.steps >= 1) {
+      if (a.ysum != nullptr) mw_ysum_load(a.steps - 1);
+      mw_store(a.steps - 1);
+    }
+  }
+  if (STAMPS && wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
+}
+
 #ifndef DS2_BWD_CH
 #define DS2_BWD_CH 3              // R > 8 reduce-scatter gather: producers' granules in flight per lane (0 = all; H = 1280 BPTT 6.78 -> 6.63 us/step at 3, 6.65 at 2 and 4)
 #endif
@@ -2245,6 +2557,23 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
   // kbq - 7 k-steps of U in LDS)
   const bool gen4 = gen4_ok(d->H, d->cell, d->mt, d->knobs);
   if (d->ysum != nullptr && (!gen4 || d->ndir != 2)) return -37;   // only gen 4 fuses the sum
+  // generation 5 (K-eighths, each granule polled once) for GRU layers with H <= 1024;
+  // knob 1 << 22 keeps generation 4 (A/B)
+  // (H = 1280 measured slower on generation 5: 7.4 vs 5.75 us/step, its 40-workgroup groups
+  // span XCDs and the U slice needs LDS k-steps and a single partial buffer)
+  if (gen4 && d->cell == CELL_GRU && d->H / 32 <= 32 && !(d->knobs & (1 << 22))) {
+    switch ((d->H / 32 + 7) / 8) {
+#define DS2_E(K, L, B)                                                                                    \
+  case K:                                                                                                 \
+    if (a.stamps) hipLaunchKernelGGL((rnne_fwd_kernel<K, L, B, true>), dim3(grid), dim3(QTH), 0, st, a); \
+    else hipLaunchKernelGGL((rnne_fwd_kernel<K, L, B, false>), dim3(grid), dim3(QTH), 0, st, a);      \
+    break;
+      DS2_E(1, 0, false) DS2_E(2, 0, false) DS2_E(3, 0, false) DS2_E(4, 0, false)
+#undef DS2_E
+      default: return -31;
+    }
+    return (int)hipGetLastError();
+  }
   if (gen4) {
 #define DS2_QL(C, K)                                                                                  \
   if (a.stamps) hipLaunchKernelGGL((rnnq_fwd_kernel<C, K, true>), dim3(grid), dim3(QTH), 0, st, a);    \

@@ -779,7 +779,7 @@ class FusedBiLayer(torch.autograd.Function):
                 members = [o + (out[d],) for d, o in enumerate(ops)] if ops and all(ops) else None
                 sch.deferred.append(Deferred(du, (dgh, hx), members, du_done))
                 sch.queue_end_of_backward()
-            elif sch.defer_input and on_side and ctx.idx == 0:
+            elif sch.defer_input and on_side and ctx.idx == 0 and _defer_wgrad(plan, x16.device):
                 # the side stream already carries dW_0 + every deferred dW and ends after the
                 # conv front-end's backward on the main stream: balance by issuing the
                 # bottom layer's dU on the main stream behind the front-end (WgradScheduler.join)
