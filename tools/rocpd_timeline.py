@@ -50,9 +50,10 @@ def main():
 
 
 _PHASES = [
-    ("recurrence fwd", ("rnnq_fwd", "rnnx_fwd", "rnn_fwd")),
-    ("recurrence BPTT", ("rnnrs_bwd", "rnnx_bwd", "rnn_bwd")),
-    ("projection / FC GEMM (hand-written)", ("gemm_kernel",)),
+    ("recurrence fwd", ("rnne_fwd", "rnnw_fwd", "rnnf8_fwd", "rnnq_fwd", "rnnx_fwd", "rnn_fwd")),
+    ("recurrence BPTT", ("rnnw_bwd", "rnnrs_bwd", "rnnx_bwd", "rnn_bwd")),
+    ("weight-gradient GEMMs (gemm8 column mode)", ("gemm8_kernel<false, 1, 1>", "gemm8_kernel<false, 1, 0>")),
+    ("projection / dx / FC GEMM (hand-written)", ("gemm_kernel", "gemm8_kernel", "transpose_bf16")),
     ("library GEMM (hipBLASLt) BBS = dx", ("_BBS_",)),
     ("library GEMM (hipBLASLt) BSS = weight grads", ("_BSS_",)),
     ("conv front-end fwd", ("conv1_fwd", "conv2_fwd", "bn_cl_apply", "bn_cl_finalize")),
