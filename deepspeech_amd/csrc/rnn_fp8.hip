@@ -381,6 +381,277 @@ __global__ __launch_bounds__(F8TH) void rnnf8_fwd_kernel(XF8 a) {
   }
 }
 
+// Generation 2 of the fp8 forward (rnnf8h_fwd_kernel): 8 MFMA waves = 2 unit halves (uh =
+// wave & 1: 32 units = 2 quarters x 3 gates = 6 tiles) x 4 K-quarters (kq = wave >> 1: k-steps
+// kq + 4 kk). Generation 1 (rnnf8_fwd_kernel: 4 unit quarters x 2 K halves) had each exchange
+// granule polled by 4 waves of the workgroup; here by 2 (the wide bf16 kernels showed the CU's
+// vector-memory pipe, not the MFMAs, setting such a step). K-quarters kq < KS % 4 have one
+// more k-step than the rest: that k-step's U lives in LDS (4 wave slots), the others in VGPRs.
+// Transpose-reduce as in generation 4 of the bf16 forward: a lane finalises element j = kq of
+// its 6 tiles (two GRU cells: units 32 uh + 16 q + lane % 16, q = 0, 1).
+template <int KS>
+__global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
+  constexpr int NT = 2 * G3;                 // tiles t = 3 q + g
+  constexpr int KR = KS / 4;                 // k-steps every K-quarter has (VGPR-resident U)
+  constexpr int NLW = KS % 4;                // K-quarters with one more k-step (LDS-resident U)
+  constexpr int KB = KR + (NLW ? 1 : 0);
+  constexpr int GP = G3 * UPW8 + 8;          // gx ring row pitch (bf16)
+  constexpr int OP = UPW8 + 4;               // output staging row pitch
+  __shared__ float red_s[2][2][4][3][NT][64];     // [parity][uh][element j][source][tile][lane]
+  // three gx slots: the MFMA waves read step s's slot after the step's barrier, while the
+  // memory wave (already past it) fills step s + 2's
+  __shared__ bf16_t gxr_s[3][ROWS8][GP];
+  __shared__ __attribute__((aligned(16))) float oh_s[2][ROWS8][OP];
+  __shared__ __attribute__((aligned(16))) float oy_s[2][ROWS8][OP];
+  __shared__ float4 og_s[2][ROWS8][OP];
+  __shared__ int len_s[ROWS8];
+  __shared__ int s_mode, s_abort;
+  __shared__ float bh_s[G3][UPW8];                // recurrent bias (read after the barrier: VGPR budget)
+  __shared__ i32x8 ul_s[NLW > 0 ? 2 * NLW : 1][NT][64];   // [uh + 2 kq][tile][lane], kq < NLW
+
+  int grp, mem;
+  if (!take_role8(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, N = a.N, NP = a.NP, R = a.R;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW8;
+  const int uh = wave & 1, kq = (wave >> 1) & 3;
+  const int g16 = lane >> 4;
+  const int erow = 4 * g16 + kq;                 // this lane's cell row (element j = kq)
+  const int er = min(erow, ROWS8 - 1);           // for LDS reads (rows >= R are not real)
+  if (tid < ROWS8) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  if (tid < G3 * UPW8) bh_s[tid / UPW8][tid % UPW8] = a.bh[dir] ? a.bh[dir][(tid / UPW8) * H + u0 + tid % UPW8] : 0.f;
+  if (wave == 0) {
+    const int m = census8(a.census, grp, mem, a.P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+  __syncthreads();
+  if (s_abort) return;
+
+  // memory wave: gx granule q -> (row, gate, 8-unit chunk); R x 3 x 8 = 192 granules max
+  constexpr int RGL = (ROWS8 * G3 * (UPW8 / 8) + 63) / 64;     // 3
+  i32x4 gpre[RGL];
+  const int NRG = R * G3 * (UPW8 / 8);
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      const int qq = q < NRG ? q : 0;
+      const int row = qq / (G3 * 8), rem = qq - row * (G3 * 8), g = rem >> 3, c8 = rem & 7;
+      const int b = min(r0 + row, N - 1);
+      const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+      gpre[j] = *reinterpret_cast<const i32x4*>(a.gx + ((size_t)t * N + b) * a.gstride + dir * G3 * H + g * H + u0 +
+                                                c8 * 8);
+    }
+  };
+  auto mw_put = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < RGL; ++j) {
+      const int q = lane + 64 * j;
+      if (q < NRG) {
+        const int row = q / (G3 * 8), rem = q - row * (G3 * 8), g = rem >> 3, c8 = rem & 7;
+        const bool act = s < len_s[row];
+        const bf16x8 v = __builtin_bit_cast(bf16x8, gpre[j]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gxr_s[s % 3][row][g * UPW8 + c8 * 8 + k] = act ? (bf16_t)v[k] : (bf16_t)0;
+      }
+    }
+  };
+  // outputs of step s: lane -> (row = lane / 8, 8 units (lane % 8) * 8)
+  auto mw_store = [&](int s) {
+    const int row = lane >> 3, c8 = (lane & 7) * 8;
+    if (row >= R) return;
+    const int b = r0 + row, u = u0 + c8;
+    const int sl = s & 1;
+    f32x4 h0 = *reinterpret_cast<const f32x4*>(&oh_s[sl][row][c8]);
+    f32x4 h1 = *reinterpret_cast<const f32x4*>(&oh_s[sl][row][c8 + 4]);
+    f32x4 y0 = *reinterpret_cast<const f32x4*>(&oy_s[sl][row][c8]);
+    f32x4 y1 = *reinterpret_cast<const f32x4*>(&oy_s[sl][row][c8 + 4]);
+    float4 gv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gv[i] = og_s[sl][row][c8 + i];
+    float* hsp = a.hsave[dir] + ((size_t)(s + 1) * NP + b) * H + u;
+    *reinterpret_cast<f32x4*>(hsp) = h0;
+    *reinterpret_cast<f32x4*>(hsp + 4) = h1;
+    bf16x8 hb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hb[i] = (short)f2bf(h0[i]);
+      hb[4 + i] = (short)f2bf(h1[i]);
+    }
+    *reinterpret_cast<bf16x8*>(a.hx[dir] + ((size_t)(s + 1) * NP + b) * H + u) = hb;
+    float4* gp = reinterpret_cast<float4*>(a.gates[dir]) + ((size_t)s * NP + b) * H + u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gp[i] = gv[i];
+    if (b < N) {
+      const int L = len_s[row];
+      const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+      bf16x8 yb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        yb[i] = (short)f2bf(y0[i]);
+        yb[4 + i] = (short)f2bf(y1[i]);
+      }
+      *reinterpret_cast<bf16x8*>(a.y[dir] + ((size_t)t * N + b) * H + u) = yb;
+    }
+  };
+  if (wave == MEMW8) {
+    mw_load(0);
+    mw_put(0);
+    if (a.steps > 1) mw_load(1);
+  }
+  __syncthreads();                                   // gx ring slot 0
+  const bool plain = s_mode == 1;
+  const unsigned hq_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H);
+  const __amdgpu_buffer_rsrc_t rs_hq = make_rsrc(a.hq[dir], hq_bytes);
+
+  if (wave < G8W) {
+    const int nk = KR + (kq < NLW ? 1 : 0);          // this wave's k-steps (wave-uniform)
+    // resident U fragments: B[k][n] = U8[g H + u0 + 32 uh + 16 q + n][128 ks + k], n = lane % 16,
+    // k in [16 g16, +16) u [64 + 16 g16, +16); ks = kq + 4 kk
+    i32x8 uf[KR > 0 ? KR : 1][NT];
+    const unsigned char* Ud = a.U8[dir];
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      if (kk >= nk) continue;
+      const int ks = kq + 4 * kk;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int q = t / G3, g = t % G3;
+        const unsigned char* p = Ud + (size_t)(g * H + u0 + 32 * uh + 16 * q + (lane & 15)) * H + ks * 128 + 16 * g16;
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(p);
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(p + 64);
+        const i32x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        if (kk < KR) uf[kk < KR ? kk : 0][t] = v;
+        else ul_s[uh + 2 * kq][t][lane] = v;         // kq < NLW: own slot, no barrier needed
+      }
+    }
+    const int sb = __builtin_amdgcn_readfirstlane(a.uexp[dir]);          // E8M0 B scale
+    const int sbw = sb | (sb << 8) | (sb << 16) | (sb << 24);
+    float hreg[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int u = u0 + 32 * uh + 16 * q + (lane & 15);
+      hreg[q] = (erow < R) ? a.hsave[dir][(size_t)(r0 + erow) * H + u] : 0.f;   // slot 0 = h0
+    }
+    const int arow = r0 + min(lane & 15, R - 1);
+    const int L = len_s[er];
+    for (int s = 0; s < a.steps; ++s) {
+      // every granule of this lane's K-quarter at once: k-step kk's two granules are 64 B
+      // apart, consecutive k-steps of the quarter 512 B
+      const unsigned o0 = (unsigned)(((size_t)s * NP + arow) * H + kq * 128 + 16 * g16);
+      i32x4 v[KB][2];
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) {
+        v[kk][0] = load_sc1_b128(rs_hq, o0 + 512u * kk);
+        v[kk][1] = load_sc1_b128(rs_hq, o0 + 512u * kk + 64u);
+      }
+      f32x4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned done = 0;                             // wave-uniform prefix of consumed k-steps
+      constexpr unsigned FULL = (1u << KB) - 1u;
+      bool ok = true;
+      while (true) {
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk) {
+          if (done != (1u << kk) - 1u) continue;
+          if (kk >= nk) {                            // past this quarter's K: nothing to wait on
+            done |= 1u << kk;
+          } else if (__all(granule8_ready(v[kk][0]) && granule8_ready(v[kk][1]))) {
+            const i32x8 af = __builtin_shufflevector(v[kk][0], v[kk][1], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              const i32x8 b = kk < KR ? uf[kk < KR ? kk : 0][t] : ul_s[uh + 2 * kq][t][lane];
+              acc[t] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, b, acc[t], 0, 0, 0, 0x7f7f7f7f, 0, sbw);
+            }
+            done |= 1u << kk;
+          }
+        }
+        if (done == FULL) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { ok = false; break; }
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk)
+          if (!(done & (1u << kk))) {
+            v[kk][0] = load_sc1_b128(rs_hq, o0 + 512u * kk);
+            v[kk][1] = load_sc1_b128(rs_hq, o0 + 512u * kk + 64u);
+          }
+      }
+      if (!ok) { s_abort = 1; atomicOr(a.err, 1u); }
+      // transpose-reduce: hand the three elements this wave does not finalise to their owners
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j == kq) continue;
+        const int src = kq < j ? kq : kq - 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) red_s[s & 1][uh][j][src][t][lane] = acc[t][j];
+      }
+      lds_barrier();
+      if (s_abort) break;
+      const bool real = erow < R;
+      const bool act = s < L;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        float pre[G3];
+#pragma unroll
+        for (int g = 0; g < G3; ++g) {
+          const int t = G3 * q + g;
+          const float own = kq == 0 ? acc[t][0] : kq == 1 ? acc[t][1] : kq == 2 ? acc[t][2] : acc[t][3];
+          pre[g] = own + red_s[s & 1][uh][kq][0][t][lane] + red_s[s & 1][uh][kq][1][t][lane] +
+                   red_s[s & 1][uh][kq][2][t][lane];
+        }
+        // gx (filled before the previous barrier) and the bias from LDS after the exchange:
+        // held across the poll they pushed the kernel into spilling
+        const int c = 32 * uh + 16 * q + (lane & 15);
+        float gxv[G3];
+#pragma unroll
+        for (int g = 0; g < G3; ++g) gxv[g] = bf2f(gxr_s[s % 3][er][g * UPW8 + c]) + bh_s[g][c];
+        const float ghn = pre[2] + bh_s[2][c];
+        const float r = sigmoidf_(gxv[0] + pre[0]);
+        const float z = sigmoidf_(gxv[1] + pre[1]);
+        const float n = tanhf_(gxv[2] - bh_s[2][c] + r * ghn);
+        const float hn = (1.f - z) * n + z * hreg[q];
+        const float hnew = act ? hn : hreg[q];
+        hreg[q] = hnew;
+        // publish: 16 lanes (the tile's 16 units of this row) -> one 16-B e4m3 granule
+        const unsigned b = f2e4m3(hnew);
+        const unsigned w1 = b | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)b, 0x101, 0xf, 0xf, false) << 8);
+        const unsigned w2 = w1 | ((unsigned)__builtin_amdgcn_update_dpp(0, (int)w1, 0x102, 0xf, 0xf, false) << 16);
+        const int d1 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x104, 0xf, 0xf, false);
+        const int d2 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x108, 0xf, 0xf, false);
+        const int d3 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x10c, 0xf, 0xf, false);
+        const int ec = 32 * uh + 16 * q + (lane & 15);
+        if ((lane & 15) == 0 && real) {
+          const i32x4 gv = {(int)w2, d1, d2, d3};
+          const unsigned off = (unsigned)(((size_t)(s + 1) * NP + r0 + erow) * H + u0 + ec);
+          if (plain) store_b128(rs_hq, off, gv);
+          else store_sc1_b128(rs_hq, off, gv);
+        }
+        if (real) {
+          oh_s[s & 1][erow][ec] = hnew;
+          oy_s[s & 1][erow][ec] = act ? hn : 0.f;
+          og_s[s & 1][erow][ec] = act ? make_float4(r, z, n, ghn) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  } else {
+    for (int s = 0; s < a.steps; ++s) {
+      if (s + 1 < a.steps) mw_put(s + 1);
+      if (s >= 2) mw_store(s - 2);
+      if (s + 2 < a.steps) mw_load(s + 2);
+      lds_barrier();
+      if (s_abort) break;
+    }
+  }
+  __syncthreads();
+  if (wave == MEMW8 && !s_abort) {
+    if (a.steps >= 2) mw_store(a.steps - 2);
+    if (a.steps >= 1) mw_store(a.steps - 1);
+  }
+}
+
 // amax of |x| over a bf16 tensor into *amax (as float bits; zeroed by the caller)
 __global__ __launch_bounds__(256) void amax_bf16_kernel(const bf16_t* __restrict__ x, long long n,
                                                         unsigned* __restrict__ amax) {
@@ -476,7 +747,7 @@ int ds2_rnnf8_fwd(const DS2RnnF8* d, hipStream_t st) {
   XF8 a;
   a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = d->H / UPW8; a.BG = d->BG; a.R = d->R;
   a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
-  a.xcd_map = d->xcd_map && a.ngroups <= 8;
+  a.xcd_map = (d->xcd_map & 1) && a.ngroups <= 8;
   a.lens = d->lens; a.gx = (const bf16_t*)d->gx; a.uexp = d->uexp;
   for (int i = 0; i < 2; ++i) {
     a.U8[i] = (const unsigned char*)d->U8[i]; a.bh[i] = d->bh[i]; a.y[i] = (bf16_t*)d->y[i];
@@ -486,6 +757,15 @@ int ds2_rnnf8_fwd(const DS2RnnF8* d, hipStream_t st) {
   a.census = d->census; a.err = d->err; a.timeout = d->timeout;
   if (d->steps <= 0) return 0;
   const int grid = a.xcd_map ? 8 * a.P : a.ngroups * a.P;
+  if (!(d->xcd_map & 2)) {                          // generation 2 (xcd_map bit 1: generation 1, A/B)
+    switch (d->H / 128) {
+      case 8: hipLaunchKernelGGL((rnnf8h_fwd_kernel<8>), dim3(grid), dim3(F8TH), 0, st, a); break;
+      case 10: hipLaunchKernelGGL((rnnf8h_fwd_kernel<10>), dim3(grid), dim3(F8TH), 0, st, a); break;
+      default: goto gen1;
+    }
+    return (int)hipGetLastError();
+  }
+gen1:
   const int kb = f8_kb(d->H);
   const size_t smem = ds2_rnnf8_smem(d->H);
   switch (kb) {

@@ -442,7 +442,8 @@ def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan):
                  [0] * ndir + [-1] * ndir + [-1])
     C.multi_fill([hx[d, 0] for d in range(ndir)] + [hs[d, 0] for d in range(ndir)], [0] * (2 * ndir))
     C.rnnf8_fwd(gx.contiguous(), lens, U8, words, bh[0], bh[1] if ndir == 2 else None, y2, hq, hx, hs, gates, census,
-                error_word(dev), T, N, NP, H, BG, R, T, gstride, ndir, TIMEOUT_TICKS, 1)
+                error_word(dev), T, N, NP, H, BG, R, T, gstride, ndir, TIMEOUT_TICKS,
+                1 | (2 if RNNX_KNOBS & (1 << 23) else 0))      # knob bit 23: generation-1 fp8 forward (A/B)
     y = torch.add(y2[0], y2[1]) if ndir == 2 else y2[0]
     return y, (hx, hs, gates)
 
