@@ -893,7 +893,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
   constexpr int G = 3;
   constexpr int NT = 2 * G;                       // tiles t = 3 uh + g
   constexpr int ROWS = 16;
-  constexpr int GP = G * UPW + 4;                 // gx ring row pitch
+  constexpr int GP = G * UPW + 8;                 // gx ring row pitch (bf16: one 16-B LDS store per granule)
   constexpr int OP = UPW + 4;                     // output staging row pitch
   constexpr int RG = ROWS * G * (UPW / 8);        // gx granules per step (upper bound)
   constexpr int RGL = (RG + 63) / 64;
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
   static_assert(KL >= 0 && KR >= 1, "register k-steps");
   __shared__ float red_s[SB ? 1 : 2][QW][NT][4][64];   // [parity][source wave][tile][element j][lane]
   __shared__ bf16x8 ul_s[KL > 0 ? KL : 1][QW][NT][64];  // LDS-resident U k-steps
-  __shared__ float gxr_s[2][ROWS][GP];
+  __shared__ __attribute__((aligned(16))) bf16_t gxr_s[2][ROWS][GP];
   __shared__ __attribute__((aligned(16))) float oh_s[2][ROWS][OP];
   __shared__ __attribute__((aligned(16))) float oy_s[2][ROWS][OP];
   __shared__ float4 og_s[2][ROWS][OP];
@@ -949,9 +949,8 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
       if (q < NRG) {
         const int row = q / (G * 4), rem = q - row * (G * 4), g = rem >> 2, c8 = rem & 3;
         const bool act = s < len_s[row];
-        const bf16x8 v = __builtin_bit_cast(bf16x8, gpre[j]);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) gxr_s[s & 1][row][g * UPW + c8 * 8 + k] = act ? bf2f((bf16_t)v[k]) : 0.f;
+        const i32x4 z = {0, 0, 0, 0};
+        *reinterpret_cast<i32x4*>(&gxr_s[s & 1][row][g * UPW + c8 * 8]) = act ? gpre[j] : z;
       }
     }
   };
@@ -1097,7 +1096,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
       st.mark(-1);
       float gxv[G];
 #pragma unroll
-      for (int g = 0; g < G; ++g) gxv[g] = gxr_s[s & 1][erow][g * UPW + ec];
+      for (int g = 0; g < G; ++g) gxv[g] = bf2f(gxr_s[s & 1][erow][g * UPW + ec]);
       unsigned off[KB];
       const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + wave * 32 + 8 * (lane >> 4)) * 2);
 #pragma unroll

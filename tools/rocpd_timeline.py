@@ -50,7 +50,7 @@ def main():
 
 
 _PHASES = [
-    ("recurrence fwd", ("rnne_fwd", "rnnw_fwd", "rnnf8_fwd", "rnnq_fwd", "rnnx_fwd", "rnn_fwd")),
+    ("recurrence fwd", ("rnne_fwd", "rnnw_fwd", "rnnf8", "rnnq_fwd", "rnnx_fwd", "rnn_fwd")),
     ("recurrence BPTT", ("rnnw_bwd", "rnnrs_bwd", "rnnx_bwd", "rnn_bwd")),
     ("weight-gradient GEMMs (gemm8 column mode)", ("gemm8_kernel<false, 1, 1>", "gemm8_kernel<false, 1, 0>")),
     ("projection / dx / FC GEMM (hand-written)", ("gemm_kernel", "gemm8_kernel", "transpose_bf16")),
