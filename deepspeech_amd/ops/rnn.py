@@ -679,24 +679,41 @@ class FusedBiLayer(torch.autograd.Function):
         dgx, dgh, parts = _run_bwd(dy, lens, [U_f16, U_b16 if d1 else None], hx, hs, gates, plan,
                                    plan.ndir * GH, dgx_scale=ctx.alpha)
         dgx2 = dgx.view(T * N, plan.ndir * GH)
-        dx = None
-        if ctx.needs_input_grad[0]:
+
+        def input_grad():
+            if not ctx.needs_input_grad[0]:
+                return None
             if ctx.wT is not None:
                 wT = ctx.wT
                 if isinstance(wT, _PendingT):
                     if wT.event is None:                 # not flushed by the model: do it now
-                        arena = arena_of(W_f)
-                        arena.wgrad.flush_transposes()
+                        arena_of(W_f).wgrad.flush_transposes()
                     torch.cuda.current_stream(dgx.device).wait_event(wT.event)
                     wT = wT.wT
-                dx = _mm_bf16(dgx2, wT.t()).view(T, N, D)
-            else:
-                dx = _mm_bf16(dgx2, W16).view(T, N, D)
-        ctx.wT = None
+                return _mm_bf16(dgx2, wT.t()).view(T, N, D)
+            return _mm_bf16(dgx2, W16).view(T, N, D)
+
         # ---- weight gradients (off the critical path) ----
         # only arena-managed weights (gradients written to main_grad, nothing returned to
         # autograd) may be produced on another stream; the Trainer joins it before Adam
         side = wgrad_stream(x16.device, arena_of(ctx.params[0]))
+        sch = arena_of(ctx.params[0]).wgrad if side is not None else None
+        if (side is not None and ctx.idx == 0 and _GROUP_BEFORE_DX and sch.grouped and sch.defer_input and
+                _defer_wgrad(plan, x16.device)):
+            # bottom layer: the grouped weight-gradient launch (and the optimizer range behind it)
+            # goes out before layer 0's dx GEMM, so it starts as the last BPTT ends (the dx GEMM
+            # reads the transposed W^T copy, which the optimizer does not write)
+            side.wait_stream(torch.cuda.current_stream(x16.device))
+            with torch.cuda.stream(side):
+                for t in (x16, dgx, dgh, hx, parts):
+                    if t is not None:
+                        t.record_stream(side)
+                res = FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, None)
+            dx = input_grad()
+            ctx.wT = None
+            return (dx,) + tuple(res[1:])
+        dx = input_grad()
+        ctx.wT = None
         if side is None:
             return FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx)
         # The layer below only needs dx: its BPTT (200 of the 256 CUs, latency-bound) runs
@@ -811,6 +828,9 @@ class FusedBiLayer(torch.autograd.Function):
 # 7 x BiGRU-1280 (160 CUs, 96 idle) 23.10 ms/step beside vs 24.53 deferred; 7 x bi-ReLU-1760
 # (generation-1 kernels) 20.95 deferred vs 21.64 beside.
 _BESIDE_MIN_IDLE_CUS = 96
+# bottom layer: the grouped launch before layer 0's dx GEMM (same-box A/B, 3 rounds: 8.025 /
+# 8.028 / 8.081 vs 8.091 / 8.024 / 8.101 ms/step after it)
+_GROUP_BEFORE_DX = True
 
 
 def _bptt_cus(plan: RnnPlan) -> int:

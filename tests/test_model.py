@@ -148,3 +148,21 @@ def test_weight_gradient_scheduling_is_per_arena():
     a.wgrad.flush()
     assert ran == ["a"] and RNN.pending_deferred(a) == 0
     assert RNN.wgrad_stream(torch.device("cpu"), a) is None      # no side stream off-GPU
+
+
+def test_xcd_plans_for_wide_and_deferral_rule():
+    """Plan geometry of the XCD recurrence kernels (no GPU needed): one-gate layers wider than
+    an XCD at 32 units per workgroup get 64-unit workgroups (ceil(H/64) per group, 8 groups of
+    <= 8 rows on one XCD each); the weight gradients of a layer are deferred to the grouped tail
+    launch only when its BPTT leaves fewer than 96 CUs idle."""
+    from deepspeech_amd.ops import rnn as RNN
+    p = RNN.make_xcd_plan(32, 1760, "rnn_relu", 2, 256)
+    assert p is not None and p.kind == "xcd" and (p.BG, p.R, p.NP, p.xcd_map) == (4, 8, 32, 1)
+    assert RNN._xcd_p(1760, "rnn_relu") == 28 and RNN._bptt_cus(p) == 224
+    assert RNN.make_xcd_plan(64, 1760, "rnn_relu", 2, 256) is None          # R = 16 > 8
+    assert not RNN._wide_ok(1760, "gru") and not RNN._wide_ok(1024, "rnn_relu")
+    assert RNN._wide_ok(1056, "rnn_relu") and not RNN._wide_ok(1824, "rnn_relu")
+    head = RNN.make_xcd_plan(32, 800, "gru", 2, 256)                        # headline: 200 CUs
+    c5 = RNN.make_xcd_plan(32, 1280, "gru", 2, 256)                         # config 5: 160 CUs
+    assert RNN._bptt_cus(head) == 200 and RNN._bptt_cus(c5) == 160
+    assert 256 - RNN._bptt_cus(head) < RNN._BESIDE_MIN_IDLE_CUS <= 256 - RNN._bptt_cus(c5)
