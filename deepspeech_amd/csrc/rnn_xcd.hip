@@ -1,4 +1,11 @@
-// Persistent bidirectional recurrence, generation 2: XCD-local groups + sentinel hand-off.
+// Persistent bidirectional recurrence on XCD-local workgroup groups with a sentinel hand-off.
+// Kernels in this file (host dispatch at the end):
+//   rnnx_fwd_kernel   generation 2 forward (fallback geometries)
+//   rnnq_fwd_kernel   generation 4 forward: 2 unit halves x 4 K-quarters (GRU H = 1280, ReLU)
+//   rnne_fwd_kernel   generation 5 GRU forward (H <= 1024): 8 K-eighths, one poller per granule
+//   rnnrs_bwd_kernel  generation 3 BPTT: reduce-scatter of tagged-bf16 partials
+//   rnnw_fwd_kernel / rnnw_bwd_kernel   64-unit one-gate layers wider than an XCD (ReLU-1760)
+// The notes below describe the shared exchange protocol (introduced with generation 2).
 //
 // Reference behaviour: src/custom_ops.py:36-96 (CustomRNNCell2 + stacked_brnn through
 // tf.nn.bidirectional_dynamic_rnn: outputs zero past each length, the backward direction

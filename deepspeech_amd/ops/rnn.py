@@ -93,7 +93,8 @@ def _rs_ok(H: int) -> bool:
     Groups wider than one XCD (P > 32) exchange write-through across XCDs; measured on
     MI355X that still beats the generation-1 kernels for the 3-gate GRU (H=1280: fwd 1.52 vs
     1.93, BPTT 2.05 vs 3.68 ms per layer) but not for the one-gate clipped ReLU (H=1760 with
-    8-producer gathers: 1.84 / 2.35 vs 1.26 / 1.41), which make_xcd_plan leaves on gen 1."""
+    8-producer gathers: 1.84 / 2.35 vs 1.26 / 1.41): those layers run the 64-unit wide
+    kernels instead (_wide_ok)."""
     return H // 32 <= 42
 
 
