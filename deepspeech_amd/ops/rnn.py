@@ -820,6 +820,10 @@ class FusedBiLayer(torch.autograd.Function):
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
         if tail:
             arena.wgrad.run_early_update()  # the recurrent stack's optimizer range, beside the front-end
+        elif (ctx.idx == 1 and arena is not None and x16.is_cuda and arena.wgrad.defer_input and
+              not _defer_wgrad(plan, x16.device) and
+              torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)):
+            arena.wgrad.run_early_upper()   # layers >= 1 and the head, beside layer 0's BPTT
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
 
 
@@ -894,6 +898,8 @@ class WgradScheduler:
         self._eob_queued = False
         self._early = None         # (fn, params, main stream): set_early_update
         self.early_done = False
+        self._early_upper = None   # (fn, params, main stream, grid): the stack above layer 0
+        self.early_upper_done = False
         self.transposes = []       # queued W^T shadows of this forward (_transpose_async)
         _schedulers.add(self)
 
@@ -918,6 +924,8 @@ class WgradScheduler:
         self._eob_queued = False
         self._early = None
         self.early_done = False
+        self._early_upper = None
+        self.early_upper_done = False
         self.transposes.clear()
 
     def flush_transposes(self) -> None:
@@ -937,6 +945,27 @@ class WgradScheduler:
                 C.transpose_bf16(j.W16, j.wT)
                 j.event = torch.cuda.Event()
                 j.event.record(side)
+
+    def set_early_upper(self, fn, params, grid: int = 0) -> None:
+        """For THIS backward, when the weight gradients are not deferred: once layer 1 has
+        issued its weight gradients (every parameter above layer 0 is then final), run
+        ``fn(grid)`` — the optimizer range of those parameters — on the side stream, beside
+        layer 0's BPTT on the CUs it leaves idle. The lower range (set_early_update) then
+        covers layer 0 only."""
+        self._early_upper = (fn, params, torch.cuda.current_stream(), grid)
+        self.early_upper_done = False
+
+    def run_early_upper(self) -> None:
+        if self._early_upper is None:
+            return
+        fn, params, main, grid = self._early_upper
+        self._early_upper = None
+        arena = arena_of(params[0]) if params else None
+        if arena is None or any(arena.first_write(p) for p in params):
+            return
+        torch.cuda.current_stream().wait_stream(main)    # readers of the weights issued so far
+        fn(grid)
+        self.early_upper_done = True
 
     def set_early_update(self, fn, params) -> None:
         """For THIS backward: once the bottom recurrent layer has issued its weight gradients
