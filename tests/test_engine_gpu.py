@@ -362,24 +362,34 @@ def test_step_is_bitwise_reproducible(cuda):
     assert torch.equal(w0, w1)
 
 
-def test_early_optimizer_range_is_bitwise_whole_update(cuda):
+@pytest.mark.parametrize("H", [256, 800])
+def test_early_optimizer_range_is_bitwise_whole_update(cuda, H):
     """Single device: the FC head's and recurrent stack's Adam + EMA range, issued on the
     weight-gradient stream beside the conv front-end's backward, gives bitwise the weights,
-    moments and EMA of one whole-arena update after backward (three steps)."""
+    moments and EMA of one whole-arena update after backward (three steps). H = 256: the
+    BPTT leaves >= 96 CUs idle, so the weight gradients run beside each BPTT and the range of
+    the head + layers >= 1 goes out beside layer 0's BPTT (two early ranges); H = 800 (the
+    headline width, 8 rows per group): deferred grouped launch, one early range."""
+    from deepspeech_amd.ops import rnn as RNN
     from deepspeech_amd.trainer import Trainer, LRSchedule
     torch.manual_seed(0)
-    base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
-    batch = to_device(FixedShapeBatches(8, max_frames=300, seed=3, pool=1).next(), cuda)
+    N = 8 if H == 256 else 32
+    base = DeepSpeech2(num_filters=32, num_hidden=H, num_rnn_layers=3, cell="gru").to(cuda)
+    batch = to_device(FixedShapeBatches(N, max_frames=300, seed=3, pool=1).next(), cuda)
+    plan = RNN.plan_for(N, H, "gru", 2, cuda)
+    two_stage = not RNN._defer_wgrad(plan, cuda)
+    assert two_stage == (H == 256)
     runs = []
     for early in (True, False):
         m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
         tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
-        assert tr._early_split > 0
+        assert tr._early_split > 0 and tr._upper_split > 0
         if not early:
             tr._early_split = 0
         for _ in range(3):
             tr.step(batch)
             assert tr.arena.wgrad.early_done == early
+            assert tr.arena.wgrad.early_upper_done == (early and two_stage)
         torch.cuda.synchronize()
         runs.append((tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone()))
     for a, b in zip(*runs):
