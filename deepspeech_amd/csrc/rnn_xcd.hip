@@ -2141,8 +2141,9 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
 // published in unit pairs (32 units per 16-B granule row); a consumer gathers the two pairs
 // of its 64 units from every producer.
 // ------------------------------------------------------------------------------------
-template <int MTU, int GPT>
+template <int MTU, int GPT, bool STAMPS = false>
 __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
+  using StampT = typename std::conditional<STAMPS, Stamps, NoStamps>::type;
   constexpr int ROWS = 16;
   constexpr int KG = UWW / 32;                    // 32-column k-steps of the own columns (2)
   constexpr int EPT = ROWS * UWW / ETH;           // epilogue elements per thread (4)
@@ -2265,6 +2266,7 @@ __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
   const unsigned ring_bytes = (unsigned)(3 * slot_floats * 4);
   const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(a.ring[dir], ring_bytes);
   auto tag_of = [&](int s) -> unsigned { return (unsigned)(((a.steps - 1 - s) / 3) & 1); };
+  StampT st(a.stamps != nullptr && (wave == 0 || wave == MEMW) && lane == 0);
   // [slot][bg][producer][unit pair][row][granule g][8 bf16]: granule (row, g) of pair p holds
   // units 32 p + {4 g .. 4 g + 3, 16 + 4 g .. 16 + 4 g + 3}
   auto ring_off16 = [&](int slot, int j, int pr, int row, int g) -> unsigned {
@@ -2273,6 +2275,7 @@ __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
 
   if (wave < MW) {
     for (int s = a.steps - 1; s >= 0; --s) {
+      st.mark(-1);
       const bool has_next = s + 1 < a.steps;
       // (G) lane -> (producer half h, row, granule g); the two unit pairs of this workgroup
       {
@@ -2327,7 +2330,9 @@ __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
             }
         }
       }
+      st.mark(0);
       lds_barrier();                                                        // #1
+      st.mark(1);
       if (s_abort) break;
       // (E) cell backward (waves 0..3): da tile for the MFMA, dgh / dgx staging
       if (wave < EW) {
@@ -2353,7 +2358,9 @@ __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
           }
         }
       }
+      st.mark(2);
       lds_barrier();                                                        // #2
+      st.mark(3);
       // (M) publish P(s) = da_s[:, own cols] . U[own cols, :] into ring slot s % 3
       if (s > 0) {
         const int ws = s % 3;
@@ -2388,13 +2395,17 @@ __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
         if (plain) publish(std::true_type{});
         else publish(std::false_type{});
       }
+      st.mark(4);
     }
   } else {
     for (int s = a.steps - 1; s >= 0; --s) {
+      st.mark(-1);
       mw_put(s);
       if (s + 2 < a.steps) mw_store(s + 2);
       if (s >= 1) mw_load(s - 1);
+      st.mark(0);
       lds_barrier();                                                        // #1
+      st.mark(1);
       if (s_abort) break;
       lds_barrier();                                                        // #2
     }
@@ -2404,6 +2415,8 @@ __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
     if (a.steps >= 2) mw_store(1);
     if (a.steps >= 1) mw_store(0);
   }
+  if (STAMPS && wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (STAMPS && wave == MEMW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
   // input-bias gradient: reduce the epilogue waves' rows through LDS
   if (a.dbx_part[dir] != nullptr && !s_abort) {
     float* bred = &red_s[0][0][0];
@@ -2644,10 +2657,14 @@ static int rnnw_bwd(const DS2RnnX* d, hipStream_t st) {
     a.dbx_part[i] = d->dbx_part[i]; a.dbh_part[i] = d->dbh_part[i];
   }
   a.dgx = (bf16_t*)d->dgx; a.dgx_scale = d->dgx_scale;
-  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = nullptr;
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout; a.stamps = d->stamps;
   if (d->steps <= 0) return 0;
   const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
   const int npw = (d->H / 32 + MW - 1) / MW;          // unit pairs per publishing wave
+  if (a.stamps != nullptr && npw == 8) {
+    hipLaunchKernelGGL((rnnw_bwd_kernel<16, 4, true>), dim3(grid), dim3(NTH), 0, st, a);
+    return (int)hipGetLastError();
+  }
   switch (2 * npw) {
     case 10: hipLaunchKernelGGL((rnnw_bwd_kernel<10, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
     case 12: hipLaunchKernelGGL((rnnw_bwd_kernel<12, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
