@@ -923,6 +923,10 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
   const int bg = grp % a.BG, dir = grp / a.BG;
   const int r0 = bg * R, u0 = mem * UPW;
   const int uh = wave & 1, jo = (wave >> 1) & 3;  // owned cell slot
+  // K-eighth of this MFMA wave: K-eighth 0 (the one with an extra k-step when H/32 % 8 != 0)
+  // goes to wave 7, away from SIMD 0, which waves 0 and 4 share with the memory wave 8
+  // (same-box A/B 8.030-8.037 vs 8.024-8.055 ms/step: neutral)
+  const int ke = (wave + 1) & 7;
   const int erow = 4 * (lane >> 4) + jo;
   const int ec = 16 * uh + (lane & 15);
   if (tid < ROWS) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
@@ -1078,7 +1082,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
       const bf16_t* Ud = a.U[dir];
 #pragma unroll
       for (int kk = 0; kk < KB; ++kk) {
-        const int ks = wave + 8 * kk;
+        const int ks = ke + 8 * kk;
         kval[kk] = ks < KS;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -1105,7 +1109,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
 #pragma unroll
       for (int g = 0; g < G; ++g) gxv[g] = bf2f(gxr_s[s & 1][erow][g * UPW + ec]);
       unsigned off[KB];
-      const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + wave * 32 + 8 * (lane >> 4)) * 2);
+      const unsigned o0 = (unsigned)((((size_t)s * NP + arow) * H + ke * 32 + 8 * (lane >> 4)) * 2);
 #pragma unroll
       for (int kk = 0; kk < KB; ++kk) off[kk] = o0 + 512u * kk;
       f32x4 acc[NT];
