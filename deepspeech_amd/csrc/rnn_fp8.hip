@@ -536,7 +536,6 @@ __global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
       hreg[q] = (erow < R) ? a.hsave[dir][(size_t)(r0 + erow) * H + u] : 0.f;   // slot 0 = h0
     }
     const int arow = r0 + min(lane & 15, R - 1);
-    const int L = len_s[er];
     for (int s = 0; s < a.steps; ++s) {
       // every granule of this lane's K-quarter at once: k-step kk's two granules are 64 B
       // apart, consecutive k-steps of the quarter 512 B
@@ -590,8 +589,14 @@ __global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
       }
       lds_barrier();
       if (s_abort) break;
-      const bool real = erow < R;
-      const bool act = s < L;
+      // lane-derived LDS / store addresses recomputed from an opaque copy of the lane id each
+      // step: hoisted out of the loop they were held across the poll and spilled (11 scratch
+      // reloads per step)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int er_l = min(4 * (ln >> 4) + kq, ROWS8 - 1);
+      const bool real = 4 * (ln >> 4) + kq < R;
+      const bool act = s < len_s[er_l];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         float pre[G3];
@@ -599,15 +604,15 @@ __global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
         for (int g = 0; g < G3; ++g) {
           const int t = G3 * q + g;
           const float own = kq == 0 ? acc[t][0] : kq == 1 ? acc[t][1] : kq == 2 ? acc[t][2] : acc[t][3];
-          pre[g] = own + red_s[s & 1][uh][kq][0][t][lane] + red_s[s & 1][uh][kq][1][t][lane] +
-                   red_s[s & 1][uh][kq][2][t][lane];
+          pre[g] = own + red_s[s & 1][uh][kq][0][t][ln] + red_s[s & 1][uh][kq][1][t][ln] +
+                   red_s[s & 1][uh][kq][2][t][ln];
         }
         // gx (filled before the previous barrier) and the bias from LDS after the exchange:
         // held across the poll they pushed the kernel into spilling
-        const int c = 32 * uh + 16 * q + (lane & 15);
+        const int c = 32 * uh + 16 * q + (ln & 15);
         float gxv[G3];
 #pragma unroll
-        for (int g = 0; g < G3; ++g) gxv[g] = bf2f(gxr_s[s % 3][er][g * UPW8 + c]) + bh_s[g][c];
+        for (int g = 0; g < G3; ++g) gxv[g] = bf2f(gxr_s[s % 3][er_l][g * UPW8 + c]) + bh_s[g][c];
         const float ghn = pre[2] + bh_s[2][c];
         const float r = sigmoidf_(gxv[0] + pre[0]);
         const float z = sigmoidf_(gxv[1] + pre[1]);
@@ -622,17 +627,17 @@ __global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
         const int d1 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x104, 0xf, 0xf, false);
         const int d2 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x108, 0xf, 0xf, false);
         const int d3 = __builtin_amdgcn_update_dpp(0, (int)w2, 0x10c, 0xf, 0xf, false);
-        const int ec = 32 * uh + 16 * q + (lane & 15);
-        if ((lane & 15) == 0 && real) {
+        const int ec = c;
+        if ((ln & 15) == 0 && real) {
           const i32x4 gv = {(int)w2, d1, d2, d3};
-          const unsigned off = (unsigned)(((size_t)(s + 1) * NP + r0 + erow) * H + u0 + ec);
+          const unsigned off = (unsigned)(((size_t)(s + 1) * NP + r0 + er_l) * H + u0 + ec);
           if (plain) store_b128(rs_hq, off, gv);
           else store_sc1_b128(rs_hq, off, gv);
         }
         if (real) {
-          oh_s[s & 1][erow][ec] = hnew;
-          oy_s[s & 1][erow][ec] = act ? hn : 0.f;
-          og_s[s & 1][erow][ec] = act ? make_float4(r, z, n, ghn) : make_float4(0.f, 0.f, 0.f, 0.f);
+          oh_s[s & 1][er_l][ec] = hnew;
+          oy_s[s & 1][er_l][ec] = act ? hn : 0.f;
+          og_s[s & 1][er_l][ec] = act ? make_float4(r, z, n, ghn) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
     }
