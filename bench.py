@@ -7,7 +7,9 @@ is available offline). Every step is a full training step: forward, CTC loss, ba
 RCCL gradient all-reduce (N > 1), fused Adam + weight EMA.
 
   python bench.py --gpus N --steps K --warmup W
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  (N > 1: either bench.py starts the N ranks itself, or an outer launcher does:
+   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...;
+   a --gpus that disagrees with the launcher's WORLD_SIZE is an error)
 
 Batch: 32 utterances per GPU (the reference's headline batch, src/train.sh:42), each
 padded to 1000 frames (10 s) with per-utterance lengths in (900, 1000] frames (one
@@ -35,7 +37,10 @@ setenvs([])
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU) on this node; without an outer launcher (torchrun) "
+                        "bench.py starts them itself (parallel/launch.py). Default: the launcher's "
+                        "WORLD_SIZE, else 1")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch_size", type=int, default=32, help="utterances per GPU")
@@ -52,12 +57,21 @@ def parse():
                    help="run the data-parallel machinery (process group, gradient buckets, "
                         "collectives on the ordering stream) even on one GPU, to time its overhead")
     p.add_argument("--fp8", action="store_true",
-                   help="fp8 e4m3 input projections (BASELINE config 5; NOT the headline bf16 number)")
+                   help="BASELINE config 5's fp8 mode: MX-fp8 e4m3 input projections and an e4m3 forward "
+                        "recurrence (U and hidden-state exchange); BPTT, weight gradients and the "
+                        "front-end stay bf16. NOT the headline bf16 number")
     return p.parse_args()
 
 
 def main():
     args = parse()
+    from deepspeech_amd.parallel.launch import check_world, maybe_spawn
+    # --gpus N > 1 without torchrun: N child ranks of this same command; this process never
+    # touches the GPU and exits with the job's code
+    code = maybe_spawn(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if code is not None:
+        sys.exit(code)
+    world = check_world(args.gpus)
     import torch
     from deepspeech_amd.parallel.dist import init_distributed, shutdown
     from deepspeech_amd.models import DeepSpeech2
@@ -66,6 +80,7 @@ def main():
     from deepspeech_amd.ops import rnn as RNN
 
     ctx = init_distributed("auto", force_group=args.force_dp)
+    assert ctx.world_size == world, (ctx.world_size, world)
     dev = ctx.device
     if dev.type != "cuda" and args.engine == "hip":
         args.engine = "ref"
@@ -138,7 +153,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": ("fp8(proj)+bf16" if args.fp8 else "bf16") if dtype == torch.bfloat16 else "fp32",
+            "dtype": ("fp8(proj+fwd recurrence)+bf16" if args.fp8 else "bf16") if dtype == torch.bfloat16 else "fp32",
             "data": "synthetic (LibriSpeech-shaped spectrograms, random-init weights)",
             "config": {
                 "model": "DeepSpeech2 2xconv(32) + %dx%s-%d bidirectional + CTC" % (

@@ -699,11 +699,13 @@ class FusedBiLayer(torch.autograd.Function):
         # autograd) may be produced on another stream; the Trainer joins it before Adam
         side = wgrad_stream(x16.device, arena_of(ctx.params[0]))
         sch = arena_of(ctx.params[0]).wgrad if side is not None else None
-        if (side is not None and ctx.idx == 0 and _GROUP_BEFORE_DX and sch.grouped and sch.defer_input and
-                _defer_wgrad(plan, x16.device)):
+        if (side is not None and ctx.idx == 0 and _GROUP_BEFORE_DX and ctx.wT is not None and sch.grouped and
+                sch.defer_input and _defer_wgrad(plan, x16.device)):
             # bottom layer: the grouped weight-gradient launch (and the optimizer range behind it)
             # goes out before layer 0's dx GEMM, so it starts as the last BPTT ends (the dx GEMM
-            # reads the transposed W^T copy, which the optimizer does not write)
+            # reads the transposed W^T copy, which the optimizer does not write; without that copy
+            # dx would read the arena's bf16 shadow that the optimizer range rewrites, so this
+            # ordering is taken only when ctx.wT exists)
             side.wait_stream(torch.cuda.current_stream(x16.device))
             with torch.cuda.stream(side):
                 for t in (x16, dgx, dgh, hx, parts):

@@ -173,7 +173,9 @@ class Trainer:
             self.bucketer.finish()
         if early:
             with TR.phase(TR.EMA):
-                lo = split if self.arena.wgrad.early_done else 0
+                # the upper range [0, usplit) may have been applied beside layer 0's BPTT even
+                # when the lower early range was skipped: never apply it twice
+                lo = split if self.arena.wgrad.early_done else (usplit if self.arena.wgrad.early_upper_done else 0)
                 self.opt.apply_range(lo, self.arena.numel, lr_t, keep, gscale)
         elif not per_bucket:
             skip = None

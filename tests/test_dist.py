@@ -165,6 +165,78 @@ def test_bench_two_ranks_json_contract():
     assert 8.0 < total <= 16.0 * 1.01, total
 
 
+def _run_bench_direct(args, timeout=600):
+    import json
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=timeout)
+    return r, [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+_TINY = ["--steps", "2", "--warmup", "1", "--batch_size", "2", "--frames", "200", "--num_hidden", "32",
+         "--num_rnn_layers", "1", "--num_filters", "4"]
+
+
+def test_bench_gpus_flag_spawns_ranks_without_launcher():
+    """python bench.py --gpus 2 (no torchrun): bench.py starts the two ranks itself
+    (parallel/launch.py) and rank 0 prints one JSON line for the 2-rank job."""
+    r, rows = _run_bench_direct(["--gpus", "2"] + _TINY)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert len(rows) == 1, r.stdout
+    out = rows[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 4 and out["value"] > 0
+
+
+def test_bench_gpus_mismatch_with_launcher_fails():
+    """--gpus 3 under a 2-rank torchrun is an error, not a silent 2-rank run."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "3"] + _TINY
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "does not match the launcher's WORLD_SIZE=2" in r.stdout + r.stderr
+
+
+def test_launcher_failing_rank_stops_job(tmp_path):
+    """A rank that fails ends the job with its exit code and the other ranks are stopped."""
+    sys.path.insert(0, ROOT)
+    from deepspeech_amd.parallel.launch import spawn_local
+    script = tmp_path / "w.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "assert os.environ['WORLD_SIZE'] == '3' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "open(os.environ['OUT'] + str(r), 'w').write(os.environ['LOCAL_RANK'])\n"
+                      "sys.exit(7) if r == 1 else time.sleep(600)\n")
+    import time
+    t0 = time.time()
+    code = spawn_local(3, [sys.executable, str(script)], {"OUT": str(tmp_path / "r")})
+    assert code == 7 and time.time() - t0 < 60
+    assert sorted(p.name for p in tmp_path.glob("r*")) == ["r0", "r1", "r2"]
+
+
+def test_scale_harness_cpu_table(tmp_path):
+    """tools/scale.py over gloo: the 1- and 2-rank benches plus the bucket-size all-reduce,
+    one table with weak-scaling efficiency and busbw."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    out = tmp_path / "scale"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale.py"), "--cpu", "--worlds", "1,2",
+                        "--bucket_mb", "0.5", "--out", str(out), "--"] + _TINY,
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+    res = json.loads((out / "scale.json").read_text())
+    assert [row["n_gpus"] for row in res["runs"]] == [1, 2]
+    assert set(res["allreduce"]) == {"fp32", "bf16"} and res["allreduce"]["fp32"][0]["world"] == 2
+    md = (out / "scale.md").read_text()
+    assert "| 1 |" in md and "| 2 |" in md and "busbw" in md
+
+
 def test_allreduce_bandwidth_tool_two_ranks():
     """tools/bench_allreduce.py (nccl-tests conventions) under torch.distributed.run, 2 CPU
     ranks over gloo: one JSON line per size on rank 0 with busbw = algbw * 2(n-1)/n."""

@@ -50,3 +50,21 @@ def test_dp2_gradients_equal_sum_of_local(cuda, tmp_path):
     # gradient is ~eps-sized (float summation order)
     assert ((g[0]["w_step"] - w_ref).abs() > 1e-5).float().mean() < 1e-3
     assert (g[0]["w_step"] - w_ref).abs().max() < 2.5e-3
+
+
+def test_bench_gpus2_self_launch_on_one_gpu():
+    """bench.py --gpus 2 without torchrun on the GPU path: two HIP-engine ranks started by
+    bench.py itself (parallel/launch.py), sharing cuda:0 over gloo (RCCL refuses two ranks
+    on one device), full DP step (bucketed all-reduce + per-bucket Adam); rank 0 prints the
+    2-rank job's JSON line."""
+    import json
+    env = dict(os.environ, PYTHONPATH=ROOT, DS2_DIST_BACKEND="gloo", DS2_DEVICE_INDEX="0", OMP_NUM_THREADS="2")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+           "--batch_size", "8", "--frames", "300", "--num_hidden", "256", "--num_rnn_layers", "2"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    rows = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(rows) == 1 and rows[0]["n_gpus"] == 2 and rows[0]["config"]["parallelism"] == "dp2"
+    assert rows[0]["config"]["engine"] == "hip" and rows[0]["final_loss"] == rows[0]["final_loss"]

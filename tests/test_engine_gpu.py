@@ -380,20 +380,27 @@ def test_early_optimizer_range_is_bitwise_whole_update(cuda, H):
     two_stage = not RNN._defer_wgrad(plan, cuda)
     assert two_stage == (H == 256)
     runs = []
-    for early in (True, False):
+    # "upper_only": the lower early range is skipped after the upper one ran (the
+    # fallback update must not apply [0, usplit) a second time)
+    for mode in ("early", "none") + (("upper_only",) if two_stage else ()):
+        early = mode != "none"
         m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
         tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9))
         assert tr._early_split > 0 and tr._upper_split > 0
         if not early:
             tr._early_split = 0
+        sch = tr.arena.wgrad
+        if mode == "upper_only":
+            sch.run_early_update = lambda sch=sch: setattr(sch, "_early", None)
         for _ in range(3):
             tr.step(batch)
-            assert tr.arena.wgrad.early_done == early
-            assert tr.arena.wgrad.early_upper_done == (early and two_stage)
+            assert sch.early_done == (mode == "early")
+            assert sch.early_upper_done == (early and two_stage)
         torch.cuda.synchronize()
         runs.append((tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone()))
-    for a, b in zip(*runs):
-        assert torch.equal(a, b), (a - b).abs().max()
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert torch.equal(a, b), (a - b).abs().max()
 
 
 @pytest.mark.parametrize("cell", ["gru", "rnn_relu"])

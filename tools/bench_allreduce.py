@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 from deepspeech_amd.utils.setenvs import setenvs  # noqa: E402
 
 setenvs([])
-import torch  # noqa: E402
+import torch  # noqa: E402,F401  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
 
@@ -35,7 +35,14 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks on this node when no launcher is active (parallel/launch.py)")
     a = ap.parse_args()
+    from deepspeech_amd.parallel.launch import check_world, maybe_spawn
+    code = maybe_spawn(a.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if code is not None:
+        sys.exit(code)
+    check_world(a.gpus)
     from deepspeech_amd.parallel.dist import init_distributed
     ctx = init_distributed("auto" if a.device == "auto" else a.device, force_group=True)
     n = ctx.world_size
