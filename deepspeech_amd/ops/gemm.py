@@ -36,7 +36,10 @@ TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
     # dx = dgx W on the K-contiguous W^T shadow (ops/rnn.py _transpose_async), persistent
     # 128x256: 67 / 197 us vs gemm8 82 / 203 (tools/bench_gemm8.py)
     (7712, 800, 4800, False, False, 1): 7,
-    (7712, 2400, 4800, False, False, 1): 7,
+    # layer 0's dx (7712, 2400, 4800) runs on gemm8 (non-persistent): it shares the chip with
+    # the grouped weight-gradient launch, and a persistent grid's statically assigned tiles
+    # then finish with its most-delayed workgroup (858-1042 us beside the group vs 234 us as
+    # gemm8; 197 us alone; round 4 timeline, profiles/r4_headline.md)
     (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
 }
 _FORCE = os.environ.get("DS2_GEMM_CFG")

@@ -748,9 +748,9 @@ class FusedBiLayer(torch.autograd.Function):
                 mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
                 dw_done()
             sch = arena.wgrad
-            on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
+            on_side = x16.is_cuda and sch.on_side(x16.device)
             grouped = sch.grouped and on_side
-            if sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_wgrad(plan, x16.device):
+            if sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device, ctx.idx):
                 # run after the last recurrent layer's BPTT (grouped: every layer's, in one launch)
                 ops = GM.group_operands(dgx2.t(), x2, grp.view(plan.ndir * GH, D)) if grouped else None
                 sch.deferred.append(Deferred(dw, (dgx2, x2), [ops + (grp.view(plan.ndir * GH, D),)] if ops else None,
@@ -771,9 +771,9 @@ class FusedBiLayer(torch.autograd.Function):
         if ugrp is not None and arena.first_write(U_f) and arena.first_write(U_b):
             # both directions' dU_d = dgh_d^T h_d as ONE batched GEMM into the packed slots
             sch = arena.wgrad
-            on_side = x16.is_cuda and torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
+            on_side = x16.is_cuda and sch.on_side(x16.device)
             grouped = sch.grouped and on_side
-            defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_wgrad(plan, x16.device)
+            defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device, ctx.idx)
             beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
             splits = _DU_SPLITS if beside else None
 
@@ -815,17 +815,16 @@ class FusedBiLayer(torch.autograd.Function):
                     arena.grad_done(p)
                 gU[d] = g
         tail = ctx.idx == 0 and arena is not None and arena.wgrad.grouped and x16.is_cuda and \
-            torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)
+            arena.wgrad.on_side(x16.device)
         if tail:
             arena.wgrad.flush()             # the bottom layer: every deferred GEMM in one group
         gb = _bias_grads([b_f, b_b] if d1 else [b_f], parts[0])
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
         if tail:
             arena.wgrad.run_early_update()  # the recurrent stack's optimizer range, beside the front-end
-        elif (ctx.idx == 1 and arena is not None and x16.is_cuda and arena.wgrad.defer_input and
-              not _defer_wgrad(plan, x16.device) and
-              torch.cuda.current_stream(x16.device) != torch.cuda.default_stream(x16.device)):
-            arena.wgrad.run_early_upper()   # layers >= 1 and the head, beside layer 0's BPTT
+        elif (ctx.idx >= 1 and ctx.idx == _upper_trigger(plan, x16.device) and arena is not None and x16.is_cuda and
+              arena.wgrad.defer_input and arena.wgrad.on_side(x16.device)):
+            arena.wgrad.run_early_upper(ctx.idx)   # layers >= idx and the head, beside the next BPTT
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
 
 
@@ -851,6 +850,24 @@ def _defer_wgrad(plan: RnnPlan, device: torch.device) -> bool:
     if device.type != "cuda":
         return True
     return _ext.num_cus(device.index or 0) - _bptt_cus(plan) < _BESIDE_MIN_IDLE_CUS
+
+
+# with deferral, only the bottom _DEFER_LAYERS layers' weight gradients join the grouped tail
+# launch; the layers above run theirs beside the next BPTT (and their optimizer range goes out
+# once the lowest of them has issued its gradients). Headline, same box, round 4: all deferred
+# 8.101 / 8.076 ms/step, bottom 3 8.077 / 8.089, bottom 2 8.129 / 8.122, bottom 1 8.125 / 8.115:
+# the tail shrinks (1.69 -> 1.24 ms at 2) but the BPTT chain grows as much (2.50 -> 2.93 ms of
+# kernel time: shared L2 / fabric), profiles/r4_negative_results.md. Kept: all deferred.
+_DEFER_LAYERS = 1 << 30
+
+
+def _defer_layer(plan: RnnPlan, device: torch.device, idx: int) -> bool:
+    return _defer_wgrad(plan, device) and idx < _DEFER_LAYERS
+
+
+def _upper_trigger(plan: RnnPlan, device: torch.device) -> int:
+    """Layer whose issued weight gradients complete the head + every layer above it."""
+    return _DEFER_LAYERS if _defer_wgrad(plan, device) else 1
 
 
 class Deferred:
@@ -900,8 +917,9 @@ class WgradScheduler:
         self._eob_queued = False
         self._early = None         # (fn, params, main stream): set_early_update
         self.early_done = False
-        self._early_upper = None   # (fn, params, main stream, grid): the stack above layer 0
+        self._early_upper = None   # (ranger, fn, main stream, grid): the layers run beside the BPTT
         self.early_upper_done = False
+        self.early_upper_hi = 0
         self.transposes = []       # queued W^T shadows of this forward (_transpose_async)
         _schedulers.add(self)
 
@@ -914,6 +932,13 @@ class WgradScheduler:
             s = torch.cuda.Stream(device=torch.device("cuda", idx))
             self.streams[idx] = s
         return s
+
+    def on_side(self, device: torch.device) -> bool:
+        """True when the current stream is this arena's weight-gradient side stream (the step
+        itself may run on a non-default, high-priority main stream)."""
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        s = self.streams.get(idx)
+        return s is not None and torch.cuda.current_stream(idx) == s
 
     def set_deferral(self, on: bool) -> None:
         env = os.environ.get("DS2_DEFER_DW")
@@ -928,6 +953,7 @@ class WgradScheduler:
         self.early_done = False
         self._early_upper = None
         self.early_upper_done = False
+        self.early_upper_hi = 0
         self.transposes.clear()
 
     def flush_transposes(self) -> None:
@@ -948,25 +974,31 @@ class WgradScheduler:
                 j.event = torch.cuda.Event()
                 j.event.record(side)
 
-    def set_early_upper(self, fn, params, grid: int = 0) -> None:
-        """For THIS backward, when the weight gradients are not deferred: once layer 1 has
-        issued its weight gradients (every parameter above layer 0 is then final), run
-        ``fn(grid)`` — the optimizer range of those parameters — on the side stream, beside
-        layer 0's BPTT on the CUs it leaves idle. The lower range (set_early_update) then
-        covers layer 0 only."""
-        self._early_upper = (fn, params, torch.cuda.current_stream(), grid)
+    def set_early_upper(self, ranger, fn, grid: int = 0) -> None:
+        """For THIS backward: once the lowest layer b whose weight gradients run beside the
+        BPTT (not deferred to the grouped tail launch) has issued them, every parameter of the
+        head and of layers >= b is final: ``ranger(b)`` gives that arena range as (end, params)
+        and ``fn(end, grid)`` runs its optimizer update on the side stream, beside layer b-1's
+        BPTT on the CUs it leaves idle. The lower range (set_early_update) then starts at
+        ``early_upper_hi``."""
+        self._early_upper = (ranger, fn, torch.cuda.current_stream(), grid)
         self.early_upper_done = False
 
-    def run_early_upper(self) -> None:
+    def run_early_upper(self, b: int) -> None:
         if self._early_upper is None:
             return
-        fn, params, main, grid = self._early_upper
+        ranger, fn, main, grid = self._early_upper
+        r = ranger(b)
+        if r is None:
+            return
         self._early_upper = None
+        hi, params = r
         arena = arena_of(params[0]) if params else None
         if arena is None or any(arena.first_write(p) for p in params):
             return
         torch.cuda.current_stream().wait_stream(main)    # readers of the weights issued so far
-        fn(grid)
+        fn(hi, grid)
+        self.early_upper_hi = hi
         self.early_upper_done = True
 
     def set_early_update(self, fn, params) -> None:

@@ -18,6 +18,7 @@ No host synchronisation happens inside the step; the loss is returned as a devic
 from __future__ import annotations
 
 from dataclasses import dataclass
+import os
 from typing import Dict, Optional
 
 import torch
@@ -110,19 +111,26 @@ class Trainer:
         # before the conv front-end in gradient-production order — get their optimizer update
         # as soon as the recurrent weight gradients are issued (Trainer.step)
         self._early_split, self._early_params = 0, []
-        self._upper_split, self._upper_params = 0, []
+        self._layer_first = {}     # recurrent layer k -> arena index of its first parameter
         names = list(self.arena.names)
         first_conv = next((i for i, n in enumerate(names) if n.startswith("conv")), None)
         if self.arena.flat.is_cuda and first_conv:
             self._early_split = self.arena.offsets[first_conv][0]
             self._early_params = list(self.arena.params[:first_conv])
-            # the head and the recurrent layers above layer 0 (laid out before it)
-            first_l0 = next((i for i, n in enumerate(names) if n.startswith("rnn.0.")), None)
-            if first_l0:
-                self._upper_split = self.arena.offsets[first_l0][0]
-                self._upper_params = list(self.arena.params[:first_l0])
+            for i, n in enumerate(names[:first_conv]):
+                if n.startswith("rnn."):
+                    self._layer_first.setdefault(int(n.split(".")[1]), i)
         if self.bucketer.enabled and self.arena.flat.is_cuda:
             _check_hw_queues()
+
+    def upper_range(self, b: int):
+        """(end, params) of the arena range holding the FC head and the recurrent layers >= b:
+        everything laid out before layer b-1 (the arena is in gradient-production order). None
+        when there is no such split (b < 1 or no layer b-1 in the arena)."""
+        i = self._layer_first.get(b - 1) if b >= 1 else None
+        if not i:
+            return None
+        return self.arena.offsets[i][0], list(self.arena.params[:i])
 
     @property
     def lr(self) -> float:
@@ -157,14 +165,17 @@ class Trainer:
             # weight-gradient stream right after the grouped tail GEMMs, beside the conv
             # front-end's backward (WgradScheduler.set_early_update); the front-end's range after
             lr_t, keep = self.opt.prepare(self.lr, self.global_step)
-            split, usplit, sch = self._early_split, self._upper_split, self.arena.wgrad
+            split, sch = self._early_split, self.arena.wgrad
             self.arena.wgrad.set_early_update(
-                lambda: self.opt.apply_range(usplit if sch.early_upper_done else 0, split, lr_t, keep, gscale),
+                lambda: self.opt.apply_range(sch.early_upper_hi if sch.early_upper_done else 0, split, lr_t, keep,
+                                             gscale),
                 self._early_params)
-            if usplit > 0 and _EARLY_UPPER:
-                # (used when the weight gradients run beside each BPTT: config 5 geometry)
-                sch.set_early_upper(lambda grid: self.opt.apply_range(0, usplit, lr_t, keep, gscale, max_grid=grid),
-                                    self._upper_params, _UPPER_GRID)
+            if self._layer_first and _EARLY_UPPER:
+                # the head and the layers whose weight gradients ran beside the BPTT (not in the
+                # grouped tail launch): their range goes out beside the next BPTT, on a capped grid
+                sch.set_early_upper(self.upper_range,
+                                    lambda hi, grid: self.opt.apply_range(0, hi, lr_t, keep, gscale, max_grid=grid),
+                                    _UPPER_GRID)
         loss.backward(one)
         self.arena.wgrad.join()
         if lazy:
@@ -175,7 +186,8 @@ class Trainer:
             with TR.phase(TR.EMA):
                 # the upper range [0, usplit) may have been applied beside layer 0's BPTT even
                 # when the lower early range was skipped: never apply it twice
-                lo = split if self.arena.wgrad.early_done else (usplit if self.arena.wgrad.early_upper_done else 0)
+                sch = self.arena.wgrad
+                lo = split if sch.early_done else (sch.early_upper_hi if sch.early_upper_done else 0)
                 self.opt.apply_range(lo, self.arena.numel, lr_t, keep, gscale)
         elif not per_bucket:
             skip = None

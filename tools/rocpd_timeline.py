@@ -3,7 +3,14 @@
 start offset, duration, overlap with the previous kernel and a short name per dispatch.
 Useful to see stream overlap (e.g. weight-gradient GEMMs running beside the BPTT kernel).
 
-  python tools/rocpd_timeline.py gpurun_out/prof/run_results.db --anchor adam_ema --index -2
+  python tools/rocpd_timeline.py gpurun_out/prof/run_results.db [--index -2] [--phases]
+
+A step is windowed on a kernel that runs ONCE per step at its START (``--anchor``, default the
+conv1 forward): from one occurrence up to (not including) the next. Round 3 ended a step at an
+``adam_ema`` launch, but a step issues two or three optimizer ranges, so that window dropped the
+end of the step. The summary line reports the step period (anchor to
+anchor), the span of the step's own kernels, and the TAIL: from the end of the last recurrence
+kernel (BPTT) to the end of the step's last kernel.
 """
 from __future__ import annotations
 
@@ -14,39 +21,52 @@ import sqlite3
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--anchor", default="adam_ema", help="kernel-name substring that ends a step")
-    ap.add_argument("--index", type=int, default=-2, help="which anchor occurrence ends the step shown")
+    ap.add_argument("--anchor", default="conv1_fwd", help="kernel-name substring that STARTS a step (once per step)")
+    ap.add_argument("--index", type=int, default=-2,
+                    help="which anchor occurrence starts the step shown (needs a following anchor)")
     ap.add_argument("--width", type=int, default=70)
     ap.add_argument("--phases", action="store_true", help="also print a per-phase table")
+    ap.add_argument("--quiet", action="store_true", help="summary only (no per-kernel lines)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = sorted(c.execute("select name, start, end from kernels"), key=lambda r: r[1])
-    ends = [i for i, r in enumerate(rows) if a.anchor in r[0]]
-    if len(ends) < 2:
+    starts = [i for i, r in enumerate(rows) if a.anchor in r[0]]
+    if len(starts) < 2:
         raise SystemExit("need two anchors")
-    hi = ends[a.index]
-    lo = ends[a.index - 1] + 1
+    idx = a.index if a.index >= 0 else len(starts) + a.index
+    if idx + 1 >= len(starts):
+        idx = len(starts) - 2
+    lo, nxt = starts[idx], starts[idx + 1]
+    step = rows[lo:nxt]
     t0 = rows[lo][1]
+    period = (rows[nxt][1] - t0) / 1e3
     busy_end = t0
     total_busy = 0.0
-    for name, s, e in rows[lo:hi + 1]:
+    last_bptt_end = None
+    for name, s, e in step:
         short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         ov = max(0, min(busy_end, e) - s)
-        print("%9.1f us  %8.1f us  ovl %7.1f  %s" % ((s - t0) / 1e3, (e - s) / 1e3, ov / 1e3, short[:a.width]))
+        if not a.quiet:
+            print("%9.1f us  %8.1f us  ovl %7.1f  %s" % ((s - t0) / 1e3, (e - s) / 1e3, ov / 1e3, short[:a.width]))
         total_busy += (e - max(s, busy_end)) / 1e3 if e > busy_end else 0.0
         busy_end = max(busy_end, e)
-    print("step span %.1f us, union of kernel time %.1f us" % ((busy_end - t0) / 1e3, total_busy))
+        if phase_of(name) == "recurrence BPTT":
+            last_bptt_end = e if last_bptt_end is None else max(last_bptt_end, e)
+    span = (busy_end - t0) / 1e3
+    line = "step period %.1f us, span of its kernels %.1f us, union of kernel time %.1f us" % (period, span, total_busy)
+    if last_bptt_end is not None:
+        line += "; last BPTT ends at %.1f us, tail %.1f us" % ((last_bptt_end - t0) / 1e3, (busy_end - last_bptt_end) / 1e3)
+    print(line)
     if a.phases:
         # per-phase busy time (kernel time, overlapping kernels counted in each) and the
-        # phase's share of the step span
+        # phase's share of the step period
         acc = {}
-        for name, s, e in rows[lo:hi + 1]:
+        for name, s, e in step:
             ph = phase_of(name)
             acc[ph] = acc.get(ph, 0.0) + (e - s) / 1e3
-        span = (busy_end - t0) / 1e3
-        print("\n| phase | kernel us | % of step span |\n|---|---|---|")
+        print("\n| phase | kernel us | % of step period |\n|---|---|---|")
         for ph, us in sorted(acc.items(), key=lambda kv: -kv[1]):
-            print("| %s | %.0f | %.1f |" % (ph, us, 100 * us / span))
+            print("| %s | %.0f | %.1f |" % (ph, us, 100 * us / period))
 
 
 _PHASES = [
