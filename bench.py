@@ -56,6 +56,10 @@ def parse():
     p.add_argument("--force_dp", action="store_true",
                    help="run the data-parallel machinery (process group, gradient buckets, "
                         "collectives on the ordering stream) even on one GPU, to time its overhead")
+    p.add_argument("--no_infer", action="store_true",
+                   help="skip the streaming-inference RTF measured after the training timing "
+                        "(BASELINE metric's inference half; rank 0, outside the timed region)")
+    p.add_argument("--infer_seconds", type=float, default=10.0, help="audio per stream of the RTF runs")
     p.add_argument("--fp8", action="store_true",
                    help="BASELINE config 5's fp8 mode: MX-fp8 e4m3 input projections and an e4m3 forward "
                         "recurrence (U and hidden-state exchange); BPTT, weight gradients and the "
@@ -141,6 +145,10 @@ def main():
     value = total_audio / elapsed
     flops = ctx.all_reduce_sum(flops)
     lossv = float(loss.float().item()) if loss is not None else float("nan")
+    shutdown(ctx)
+    infer = None
+    if ctx.is_main and not args.no_infer:
+        infer = streaming_rtf(dev, args.engine, args.infer_seconds)
     if ctx.is_main:
         out = {
             "metric": "audio-sec/sec training throughput (whole node), DS2 BiGRU",
@@ -168,8 +176,37 @@ def main():
             "achieved_tflops": round(flops / elapsed / 1e12, 2),
             "final_loss": round(lossv, 4),
         }
+        if infer is not None:
+            out["inference"] = infer
         print(json.dumps(out), flush=True)
-    shutdown(ctx)
+
+
+def streaming_rtf(dev, engine: str, seconds: float):
+    """Streaming-inference real-time factor (BASELINE metric's second half; north-star config
+    4: 2 x conv + 5 x uni-GRU-800 + CTC, greedy and prefix-beam-16 decoding), measured AFTER
+    and outside the training timing. RTF = compute seconds / audio seconds per stream, 0.5 s
+    chunks, 1 and 32 concurrent streams (a chunk of all streams is one launch sequence, HIP
+    graph replay), synthetic features and random-init weights (infer.py). Reference eval path:
+    src/deepSpeech_test.py:112-136 (whole-utterance greedy decode)."""
+    import torch
+    from deepspeech_amd.infer import rtf
+    from deepspeech_amd.models import DeepSpeech2
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=32, num_hidden=800, num_rnn_layers=5, cell="gru", bidirectional=False).to(dev)
+    m.set_engine(engine, torch.bfloat16 if engine == "hip" else torch.float32)
+    if dev.type != "cuda":
+        seconds = min(seconds, 2.0)
+    rtf(m, seconds=1.0, chunk_s=0.5, batch=1)          # warm-up: plans, kernels, graph capture
+    res = {"model": "DS2 2xconv(32) + 5x uni-GRU-800 + CTC", "chunk_s": 0.5, "audio_s_per_stream": seconds,
+           "unit": "RTF = compute s / audio s per stream (lower is better)"}
+    for B in (1, 32):
+        for dec in ("greedy", "beam"):
+            r, _ = rtf(m, seconds=seconds, chunk_s=0.5, batch=B, decoder=dec, beam_width=16)
+            key = "rtf_%s%s_streams%d" % (dec, "16" if dec == "beam" else "", B)
+            res[key] = round(r, 6)
+            res["x_realtime_total_%s%s_streams%d" % (dec, "16" if dec == "beam" else "", B)] = \
+                round(B / r, 1) if r > 0 else None
+    return res
 
 
 if __name__ == "__main__":

@@ -14,16 +14,7 @@ __device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((unsig
 
 // round-to-nearest-even f32 -> bf16 in hardware (gfx950 v_cvt_pk_bf16_f32; NaN stays a quiet
 // NaN). The integer emulation it replaces cost ~6 VALU ops + a NaN branch per value.
-#ifndef DS2_SW_F2BF
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
-#else   // the integer emulation (A/B variant: build.py --variant swf2bf -D DS2_SW_F2BF)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
-#endif
 
 // v_exp_f32 + v_rcp_f32 (1 ulp): the IEEE-correct division would add a 10-instruction
 // div_scale/div_fmas/div_fixup sequence per call on the recurrence's critical path

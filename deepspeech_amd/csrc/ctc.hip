@@ -448,11 +448,8 @@ extern "C" {
 // unused state slot costs time: 10-s utterances (~150 labels, 301 states) run SPL 5, not 8.
 static int ctc_spl(int SPmax) {
   const int need = (SPmax + 63) / 64;
-#ifdef DS2_CTC_SPL_POW2   // A/B build: power-of-two tile widths only (the round-1 set)
-  for (int k : {4, 8, 16, 32}) if (k >= need) return k;
-#else
+  // (the round-1 power-of-two set {4, 8, 16, 32} measured slower: profiles/r2_s4_ctc_spl.md)
   for (int k : {4, 5, 6, 8, 12, 16, 32}) if (k >= need) return k;
-#endif
   return -1;
 }
 

@@ -134,14 +134,9 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* img, int rb, int ks,
     const int k0 = ks * 32 + 8 * g + q;
     const unsigned char* b0 = img + k0 * (ROWS * 2) + ((c ^ (int)csw(k0)) << 4) + 8 * (p & 1);
     const unsigned char* b1 = img + (k0 + 4) * (ROWS * 2) + ((c ^ (int)csw(k0 + 4)) << 4) + 8 * (p & 1);
-#ifdef DS2_GEMM_TR_TIMING
-    (void)b1;   // timing-only build: one plain 16-B read in place of the two transposed reads
-    return *(const bf16x8*)((uintptr_t)b0 & ~(uintptr_t)15);
-#else
     const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)b0);
     const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)b1);
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#endif
   }
 }
 

@@ -24,17 +24,10 @@ constexpr int OPT_THREADS = 256;
 // One float4 group: loads issued for U groups before any math (U x 5 loads in flight per
 // lane), non-temporal: every byte is touched exactly once per step, so nothing is worth
 // keeping in L2 / MALL for the next kernel.
-#ifndef DS2_ADAM_NT
-#define DS2_ADAM_NT 1
-#endif
 template <typename T>
-__device__ __forceinline__ T ld_s(const T* p) {
-  if constexpr (DS2_ADAM_NT) return __builtin_nontemporal_load(p); else return *p;
-}
+__device__ __forceinline__ T ld_s(const T* p) { return __builtin_nontemporal_load(p); }
 template <typename T>
-__device__ __forceinline__ void st_s(T v, T* p) {
-  if constexpr (DS2_ADAM_NT) __builtin_nontemporal_store(v, p); else *p = v;
-}
+__device__ __forceinline__ void st_s(T v, T* p) { __builtin_nontemporal_store(v, p); }
 // One element's update with every rounding spelled out (explicit fma / _rn products, nothing
 // left to the compiler's contraction choice), so the vector-group paths and the scalar tail
 // round identically: the result of an element does not depend on how the arena is split
@@ -96,15 +89,9 @@ __global__ __launch_bounds__(OPT_THREADS) void adam_ema_kernel(
   const long long n4 = n / 4;
   const long long stride = (long long)gridDim.x * OPT_THREADS;
   long long i = (long long)blockIdx.x * OPT_THREADS + threadIdx.x;
-#ifndef DS2_ADAM_U
-#define DS2_ADAM_U 2      // float4 groups in flight per lane (A/B: build.py --variant ... -D DS2_ADAM_U=4)
-#endif
-  if (DS2_ADAM_U >= 4)
-    for (; i + 3 * stride < n4; i += 4 * stride)
-      adam_groups<4>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
-  if (DS2_ADAM_U >= 2)
-    for (; i + stride < n4; i += 2 * stride)
-      adam_groups<2>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
+  // two float4 groups in flight per lane (four measured no faster)
+  for (; i + stride < n4; i += 2 * stride)
+    adam_groups<2>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
   for (; i < n4; i += stride) adam_groups<1>(p, g, m, v, ema, p16, i, stride, lr_t, b1, b2, eps, gscale, ema_keep);
   // tail
   for (long long k = n4 * 4 + (long long)blockIdx.x * OPT_THREADS + threadIdx.x; k < n; k += stride) {

@@ -762,15 +762,12 @@ int ds2_rnnf8_fwd(const DS2RnnF8* d, hipStream_t st) {
   a.census = d->census; a.err = d->err; a.timeout = d->timeout;
   if (d->steps <= 0) return 0;
   const int grid = a.xcd_map ? 8 * a.P : a.ngroups * a.P;
-  if (!(d->xcd_map & 2)) {                          // generation 2 (xcd_map bit 1: generation 1, A/B)
-    switch (d->H / 128) {
-      case 8: hipLaunchKernelGGL((rnnf8h_fwd_kernel<8>), dim3(grid), dim3(F8TH), 0, st, a); break;
-      case 10: hipLaunchKernelGGL((rnnf8h_fwd_kernel<10>), dim3(grid), dim3(F8TH), 0, st, a); break;
-      default: goto gen1;
-    }
-    return (int)hipGetLastError();
+  // generation 2 where it is instantiated (H = 1024, 1280); generation 1 for the other widths
+  switch (d->H / 128) {
+    case 8: hipLaunchKernelGGL((rnnf8h_fwd_kernel<8>), dim3(grid), dim3(F8TH), 0, st, a); return (int)hipGetLastError();
+    case 10: hipLaunchKernelGGL((rnnf8h_fwd_kernel<10>), dim3(grid), dim3(F8TH), 0, st, a); return (int)hipGetLastError();
+    default: break;
   }
-gen1:
   const int kb = f8_kb(d->H);
   const size_t smem = ds2_rnnf8_smem(d->H);
   switch (kb) {

@@ -541,12 +541,8 @@ __global__ __launch_bounds__(NTH) void rnnx_fwd_kernel(XFwd a) {
 // plain/write-through stores), so the host-side plan is shared.
 // ------------------------------------------------------------------------------------
 constexpr int QW = 8;             // MFMA waves of the generation-4 forward
-#ifndef DS2_NARROW_CH
-#define DS2_NARROW_CH 0           // KL == 0: 0 = all granules in flight with wave-wide re-poll (poll_mfma_par)
-#endif
-#ifndef DS2_WIDE_CH
-#define DS2_WIDE_CH 2             // wide layers (KL > 0): granules in flight per lane, 0 = all (CH 2/3/4/6/8 measured 5.67/5.75/5.77/6.16/7.49 us/step at H = 1280)
-#endif
+constexpr int DS2_NARROW_CH = 0;  // KL == 0: 0 = all granules in flight with wave-wide re-poll (poll_mfma_par)
+constexpr int DS2_WIDE_CH = 2;    // wide layers (KL > 0): granules in flight per lane, 0 = all (CH 2/3/4/6/8 measured 5.67/5.75/5.77/6.16/7.49 us/step at H = 1280)
 constexpr int QTH = (QW + 1) * 64;
 
 // KL > 0 (wide layers, H = 1280 GRU: 10 k-steps per wave): the LAST KL k-steps of each
@@ -1197,9 +1193,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
   if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
 }
 
-#ifndef DS2_BWD_CH
-#define DS2_BWD_CH 3              // R > 8 reduce-scatter gather: producers' granules in flight per lane (0 = all; H = 1280 BPTT 6.78 -> 6.63 us/step at 3, 6.65 at 2 and 4)
-#endif
+constexpr int DS2_BWD_CH = 3;     // R > 8 reduce-scatter gather: producers' granules in flight per lane (0 = all; H = 1280 BPTT 6.78 -> 6.63 us/step at 3, 6.65 at 2 and 4)
 
 
 // ------------------------------------------------------------------------------------
@@ -1265,33 +1259,19 @@ struct XBwdRS {
 // (the per-value version with NaN selects made the publish phase ~1.6k cycles longer). The
 // +1 can carry out of the low half only from 0xFFFF (a negative NaN with a full payload),
 // which is first replaced by the canonical NaN 0x7FC0.
-#ifndef DS2_TAG_TRUNC
-// Hardware RNE pair conversion (one v_cvt_pk_bf16_f32), then the LSB set to the tag by an
-// XOR flip: |error| <= 1.5 bf16 ulp, 3 VALU ops per pair on the publish critical path
-// (the truncate-and-step variant below is < 1 ulp but 5-6 ops). No carry, so the 0xFFFF
-// special case is not needed.
+// Hardware RNE pair conversion (one v_cvt_pk_bf16_f32), then the LSB set to the tag: |error|
+// <= 1.5 bf16 ulp, 3 VALU ops per pair on the publish critical path (a truncate-and-step
+// variant is < 1 ulp but 5-6 ops, measured slower). No carry, so no 0xFFFF special case.
 __device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
   typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
   const bf2_t p = {(__bf16)lo, (__bf16)hi};
   const unsigned d = __builtin_bit_cast(unsigned, p);
-#ifdef DS2_TAG_ANDOR
-  return d ^ ((d & 0x00010001u) ^ tagmask);
-#else
   // one bitfield insert instead of and + or (gfx9 VOP3 takes no literal, so the compiler
   // cannot fuse them into v_and_or_b32): r = (mask & tagmask) | (~mask & d)
   unsigned r;
   asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(0x00010001u), "s"(tagmask), "v"(d));
   return r;
-#endif
 }
-#else
-__device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
-  unsigned d = __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
-  if ((d & 0xffffu) == 0xffffu) d = (d & 0xffff0000u) | 0x7fc0u;
-  const unsigned x = (d & 0x00010001u) ^ tagmask;
-  return d + x;
-}
-#endif
 
 __device__ __forceinline__ bool granule_tagged16(i32x4 v, unsigned tag) {
   const unsigned want = tag ? 0x00010001u : 0u;
@@ -1716,17 +1696,6 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
                 else store_sc1_b128(rs_ring, offp[k], v);
               }
             };
-#ifdef DS2_PUB_PIPE
-            f32x4 acc[MTU];
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-              for (int i = 0; i < MTU; ++i)
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], g ? acc[i] : f32x4{0.f, 0.f, 0.f, 0.f},
-                                                                 0, 0, 0);
-#pragma unroll
-            for (int k = 0; k < NP; ++k) store_pair(k, acc[2 * k], acc[2 * k + 1]);
-#else
             // a pair past MTS multiplies the zero fragments loaded for it and is not stored
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
@@ -1739,7 +1708,6 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
               }
               store_pair(k, a0, a1);
             }
-#endif
             };
             if (plain) publish(std::true_type{});
             else publish(std::false_type{});
@@ -2584,7 +2552,7 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
   // knob 1 << 22 keeps generation 4 (A/B)
   // (H = 1280 measured slower on generation 5: 7.4 vs 5.75 us/step, its 40-workgroup groups
   // span XCDs and the U slice needs LDS k-steps and a single partial buffer)
-  if (gen4 && d->cell == CELL_GRU && d->H / 32 <= 32 && !(d->knobs & (1 << 22))) {
+  if (gen4 && d->cell == CELL_GRU && d->H / 32 <= 32) {
     switch ((d->H / 32 + 7) / 8) {
 #define DS2_E(K, L, B)                                                                                    \
   case K:                                                                                                 \

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import torch
 
-_FC_SPLIT_MAX = int(__import__('os').environ.get('DS2_FC_SPLITK', '16'))   # 1: one unsplit GEMM (A/B)
+_FC_SPLIT_MAX = 16         # split-K ceiling of the FC head's weight-gradient GEMM
 
 from .. import BLANK
 from . import _ext

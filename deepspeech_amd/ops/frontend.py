@@ -20,7 +20,7 @@ from . import _ext
 from .optim import arena_of, emit_grad
 from ..utils import trace as TR
 
-_HEAD_SIDE = os.environ.get("DS2_HEAD_SIDE", "1") == "1"
+_HEAD_SIDE = True         # FC-head weight gradient on the side stream
 
 BN_EPS = 1e-3
 BN_MOMENTUM = 0.01

@@ -91,3 +91,43 @@ def test_fp8_projection_training_tracks_bf16(cuda):
     print("fp8 windowed bf16/fp8 loss: %s; max rel %.4f" % (table, float(rel.max())))
     assert wf[-1] < 0.5 * wf[0], table
     assert float(rel.max()) < 0.10, table
+
+
+def test_fp8_recurrence_training_tracks_bf16(cuda):
+    """Config 5's full fp8 mode — MX-fp8 projections AND the e4m3 forward recurrence of
+    csrc/rnn_fp8.hip (H % 256 == 0, so this geometry really routes through it: asserted) —
+    trains along the bf16 trajectory: 300 steps, same weights and batches. The BPTT runs in
+    bf16 on the fp8 forward's saved states (straight-through), which is what this pins; the
+    reference has no fp8 mode (parity unpinned). Measured on MI355X (round 4): windows
+    175.0/184.8 48.9/54.5 9.3/11.6 2.6/3.0 1.3/1.5 0.9/0.9 0.6/0.7 0.5/0.5 0.4/0.4 0.3/0.3 —
+    the fp8 run lags the bf16 one by a few steps on the steep part of the descent (max window
+    difference 24 %, where the projection-only fp8 mode above stays within 2 %: 3-bit-mantissa
+    U and exchanged h), then reaches the same loss. Pinned: every window within 35 %, the last
+    three within 15 %, both runs learn > 100x."""
+    from deepspeech_amd.ops import rnn as RNN
+    torch.manual_seed(11)
+    N, H = 8, 256
+    base = DeepSpeech2(num_filters=32, num_hidden=H, num_rnn_layers=2, cell="gru").to(cuda)
+    f8 = copy.deepcopy(base)
+    base.set_engine("hip", torch.bfloat16)
+    f8.set_engine("hip", torch.bfloat16, fp8=True)
+    assert RNN.fp8_recurrence_ok(RNN.plan_for(N, H, "gru", 2, cuda), N)
+    batches = [to_device(FixedShapeBatches(N, max_frames=300, seed=40 + s, pool=1).next(), cuda) for s in range(4)]
+    sched = LRSchedule(3e-4, 10 ** 9, 1.0)
+    tb, tf = Trainer(base, sched), Trainer(f8, sched)
+    lb, lf = [], []
+    for i in range(300):
+        b = batches[i % 4]
+        lb.append(tb.step(b).detach().float())
+        lf.append(tf.step(b).detach().float())
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    lb, lf = torch.stack(lb).cpu(), torch.stack(lf).cpu()
+    assert torch.isfinite(lf).all()
+    wb, wf = lb.view(-1, 30).mean(1), lf.view(-1, 30).mean(1)
+    rel = ((wf - wb).abs() / wb)
+    table = " ".join("%.1f/%.1f" % (a, c) for a, c in zip(wb.tolist(), wf.tolist()))
+    print("fp8-recurrence windowed bf16/fp8 loss: %s; max rel %.4f" % (table, float(rel.max())))
+    assert wf[-1] < 0.01 * wf[0] and wb[-1] < 0.01 * wb[0], table
+    assert float(rel.max()) < 0.35, table
+    assert float(rel[-3:].max()) < 0.15, table

@@ -153,7 +153,7 @@ def test_bench_two_ranks_json_contract():
     aggregate value (summed audio / max elapsed), n_gpus and dp degree reported."""
     out = _run_bench(2, {"CUDA_VISIBLE_DEVICES": ""},
                      ["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch_size", "2", "--frames", "200",
-                      "--num_hidden", "32", "--num_rnn_layers", "1", "--num_filters", "4"])
+                      "--num_hidden", "32", "--num_rnn_layers", "1", "--num_filters", "4", "--no_infer"])
     assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
     assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
     assert out["value"] > 0 and out["ms_per_step"] > 0
@@ -177,17 +177,22 @@ def _run_bench_direct(args, timeout=600):
 
 _TINY = ["--steps", "2", "--warmup", "1", "--batch_size", "2", "--frames", "200", "--num_hidden", "32",
          "--num_rnn_layers", "1", "--num_filters", "4"]
+_TINY_NOINF = _TINY + ["--no_infer"]
 
 
 def test_bench_gpus_flag_spawns_ranks_without_launcher():
     """python bench.py --gpus 2 (no torchrun): bench.py starts the two ranks itself
     (parallel/launch.py) and rank 0 prints one JSON line for the 2-rank job."""
-    r, rows = _run_bench_direct(["--gpus", "2"] + _TINY)
+    r, rows = _run_bench_direct(["--gpus", "2", "--infer_seconds", "1"] + _TINY)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert len(rows) == 1, r.stdout
     out = rows[0]
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 4 and out["value"] > 0
+    # the inference half of the BASELINE metric: streaming RTF, greedy and beam-16, 1 / 32 streams
+    inf = out["inference"]
+    for k in ("rtf_greedy_streams1", "rtf_beam16_streams1", "rtf_greedy_streams32", "rtf_beam16_streams32"):
+        assert inf[k] > 0, k
 
 
 def test_bench_gpus_mismatch_with_launcher_fails():
@@ -195,7 +200,7 @@ def test_bench_gpus_mismatch_with_launcher_fails():
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "3"] + _TINY
+           os.path.join(ROOT, "bench.py"), "--gpus", "3"] + _TINY_NOINF
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "does not match the launcher's WORLD_SIZE=2" in r.stdout + r.stderr
@@ -226,7 +231,7 @@ def test_scale_harness_cpu_table(tmp_path):
         env.pop(k, None)
     out = tmp_path / "scale"
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale.py"), "--cpu", "--worlds", "1,2",
-                        "--bucket_mb", "0.5", "--out", str(out), "--"] + _TINY,
+                        "--bucket_mb", "0.5", "--out", str(out), "--"] + _TINY_NOINF,
                        env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     import json

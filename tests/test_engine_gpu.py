@@ -316,16 +316,20 @@ def test_fp8_projection_close_to_bf16(cuda):
 
 
 def test_fp8_recurrence_model_close_to_bf16(cuda):
-    """Config 5's fp8 mode at its width (H = 1280, 2 layers): the recurrence runs on
-    csrc/rnn_fp8.hip (e4m3 U and h exchange), the BPTT in bf16 on the saved state. Loss within
-    5 % of the bf16 engine, top-layer / head gradients within 25 %."""
+    """Config 5's fp8 mode at its width AND production batch (H = 1280, N = 32: 8 rows per
+    group, 2 layers): the recurrence runs on csrc/rnn_fp8.hip (e4m3 U and h exchange), the BPTT
+    in bf16 on the saved state (a straight-through gradient of the quantised forward). First
+    step: loss within 5 % of the bf16 engine, top-layer / head gradients within 25 %; then 3
+    full training steps each (Trainer: fused Adam + EMA), losses within 5 % step by step."""
     from deepspeech_amd.ops import rnn as RNN
+    from deepspeech_amd.trainer import LRSchedule, Trainer
     ref, hip = _pair(cuda, "gru", H=1280, L=2)
     hip8 = copy.deepcopy(hip)
     hip8.set_engine("hip", torch.bfloat16, fp8=True)
-    batch = to_device(FixedShapeBatches(8, max_frames=260, seed=4, pool=1).next(), cuda)
-    plan = RNN.plan_for(8, 1280, "gru", 2, cuda)
-    assert RNN.fp8_recurrence_ok(plan, 8)
+    batch = to_device(FixedShapeBatches(32, max_frames=260, seed=4, pool=1).next(), cuda)
+    plan = RNN.plan_for(32, 1280, "gru", 2, cuda)
+    assert RNN.fp8_recurrence_ok(plan, 32)
+    t16, t8 = copy.deepcopy(hip), copy.deepcopy(hip8)
     l16 = _loss(hip, batch)
     l16.backward()
     l8 = _loss(hip8, batch)
@@ -338,6 +342,11 @@ def test_fp8_recurrence_model_close_to_bf16(cuda):
     for n, p in hip8.named_parameters():
         if n.startswith("rnn.1") or n.startswith("fc"):
             assert _rel(p.grad, g16[n].grad) < 0.25, n
+    tr16, tr8 = Trainer(t16, LRSchedule(1e-4, 1000, 0.9)), Trainer(t8, LRSchedule(1e-4, 1000, 0.9))
+    for _ in range(3):
+        a, b = float(tr16.step(batch)), float(tr8.step(batch))
+        assert abs(a - b) / abs(a) < 5e-2, (a, b)
+    RNN.check_errors()
 
 
 def test_step_is_bitwise_reproducible(cuda):

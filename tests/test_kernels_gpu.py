@@ -446,7 +446,7 @@ def _gru_fp8_emulation(gx, lens, U, bh, H):
     return sum(ys), hss
 
 
-@pytest.mark.parametrize("N,H,ndir", [(8, 1280, 2), (20, 1024, 2), (8, 1280, 1)])
+@pytest.mark.parametrize("N,H,ndir", [(8, 1280, 2), (20, 1024, 2), (8, 1280, 1), (32, 1280, 2)])
 def test_fp8_recurrence_matches_emulation(cuda, N, H, ndir):
     """The fp8 GRU forward (e4m3 U and h exchange, 8 groups of H/64 workgroups) against an
     fp32 emulation of the same quantisation: outputs and saved states within 2 %, padding
@@ -456,6 +456,8 @@ def test_fp8_recurrence_matches_emulation(cuda, N, H, ndir):
     T = 19
     plan = RNN.plan_for(N, H, "gru", ndir, cuda)
     if not RNN.fp8_recurrence_ok(plan, N):
+        # (32, 1280, 2) is config 5's production geometry (8 rows per group): it must run
+        assert (N, H) != (32, 1280), "config 5 geometry not served by the fp8 recurrence"
         pytest.skip("geometry not served by the fp8 recurrence (plan rows)")
     gx = (torch.randn(T, N, ndir * 3 * H, device=cuda) * 0.5).to(torch.bfloat16)
     lens = torch.randint(T // 2, T + 1, (N,), device=cuda, dtype=torch.int32)

@@ -88,7 +88,7 @@ def main(argv=None) -> int:
     rows = []
     for w in worlds:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(w), "--steps", str(a.steps),
-               "--warmup", str(a.warmup), "--bucket_mb", str(a.bucket_mb)] + extra
+               "--warmup", str(a.warmup), "--bucket_mb", str(a.bucket_mb), "--no_infer"] + extra
         r, wall = _run(cmd, a.timeout, os.path.join(a.out, "bench_n%d.log" % w) if a.out else None)
         got = _json_lines(r.stdout)
         if r.returncode != 0 or len(got) != 1:
