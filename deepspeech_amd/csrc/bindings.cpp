@@ -92,6 +92,28 @@ struct DS2RnnF8 {
 int ds2_rnnf8_supported(int H, int N, int ndir);
 int ds2_rnnf8_fwd(const DS2RnnF8* d, hipStream_t st);
 int ds2_fp8_quant_pow2(const void* x, long long n, void* q, int* uexp, unsigned* amax, hipStream_t st);
+struct DS2RnnF8B {
+  int T, N, NP, H, BG, R, steps, gstride, ndir, xcd_map;
+  const int* lens;
+  const void* dy;
+  const void* U8T[2];
+  const int* uexp;
+  const float* hsave[2];
+  const float* gates[2];
+  void* dgh[2];
+  void* dgx;
+  void* ring[2];
+  float* dbx_part[2];
+  float* dbh_part[2];
+  float dgx_scale;
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+};
+int ds2_rnnf8_bwd_supported(int H, int N, int ndir);
+long long ds2_rnnf8_ring_words(int H, int BG, int R);
+int ds2_rnnf8_bwd(const DS2RnnF8B* d, hipStream_t st);
+int ds2_fp8_quant_pow2_t(const void* x, int rows, int cols, void* q, int* uexp, unsigned* amax, hipStream_t st);
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs);
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
 long long ds2_rnnx_ring_floats(int H, int BG, int R);
@@ -122,8 +144,22 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
               int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
               unsigned* cnt, int cus, hipStream_t st);
 int ds2_gemm8_splits(int K, int fp8, int S);
+struct DS2G8Opt {      // csrc/gemm8.hip: Adam + EMA in the grouped GEMM's epilogue
+  float* p;
+  float* m;
+  float* v;
+  float* ema;
+  unsigned short* p16;
+  const float* gbase;
+  float lr_t, b1, b2, eps, gscale, keep;
+  int on, store_g;
+};
 int ds2_gemm8_group(int np, const void* const* A, const void* const* B, void* const* C, float* const* ws,
-                    unsigned* const* cnt, const int* dims, int a_col, int b_col, int cus, hipStream_t st);
+                    unsigned* const* cnt, const int* dims, int a_col, int b_col, int cus, const DS2G8Opt* opt,
+                    hipStream_t st);
+int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema, void* p16, const long long* lohi,
+                        int nr, float lr_t, float b1, float b2, float eps, float gscale, float ema_keep,
+                        hipStream_t st);
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
                    void* a8, void* b8, float* part, float* scales, hipStream_t st);
 int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st);
@@ -407,6 +443,77 @@ void fp8_quant_pow2(at::Tensor x, at::Tensor q, at::Tensor uexp, at::Tensor amax
         "fp8_quant_pow2");
 }
 
+// csrc/rnn_fp8.hip: transposed e4m3 copy q [cols][rows] of a bf16 [rows][cols] tensor scaled by
+// one power of two (the fp8 BPTT's U^T); uexp[0] = 127 + e
+void fp8_quant_pow2_t(at::Tensor x, at::Tensor q, at::Tensor uexp, at::Tensor amax) {
+  need_gpu(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() == 2, "x must be contiguous bf16 2-D");
+  TORCH_CHECK(q.scalar_type() == at::kByte && q.is_contiguous() && q.numel() == x.numel(), "q must be uint8 like x");
+  TORCH_CHECK(uexp.scalar_type() == at::kInt && uexp.numel() >= 1 && amax.scalar_type() == at::kInt && amax.numel() >= 1,
+              "uexp / amax int32 device words");
+  check(ds2_fp8_quant_pow2_t(x.data_ptr(), (int)x.size(0), (int)x.size(1), q.data_ptr(), uexp.data_ptr<int>(),
+                             reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream()),
+        "fp8_quant_pow2_t");
+}
+
+// csrc/rnn_fp8.hip fp8 GRU BPTT: U8T [ndir, H, 3H] e4m3 U^T (uexp per direction), saved fp32
+// h / gates of the forward, tagged-bf16 reduce-scatter ring [ndir, ring_words] filled 0xFF..
+void rnnf8_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U8T, at::Tensor uexp, at::Tensor hs, at::Tensor gates,
+               at::Tensor dgh, at::Tensor dgx, OptT dbx_part, OptT dbh_part, double dgx_scale, at::Tensor census,
+               at::Tensor err, at::Tensor ring, int64_t T, int64_t N, int64_t NP, int64_t H, int64_t BG, int64_t R,
+               int64_t steps, int64_t gstride, int64_t ndir, int64_t timeout, int64_t xcd_map) {
+  need_gpu(dy, "dy");
+  TORCH_CHECK(ds2_rnnf8_bwd_supported((int)H, (int)N, (int)ndir), "rnnf8_bwd: unsupported geometry");
+  TORCH_CHECK(steps >= 1 && steps <= T && R >= 1 && R <= 8 && NP == BG * R && BG * ndir <= 8, "rnnf8_bwd: plan");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && dy.numel() == T * N * H, "dy bf16 [T,N,H]");
+  TORCH_CHECK(lens.scalar_type() == at::kInt && lens.numel() == N, "lens must be int32 [N]");
+  TORCH_CHECK(U8T.scalar_type() == at::kByte && U8T.is_contiguous() && U8T.numel() == ndir * 3 * H * H,
+              "U8T must be uint8 [ndir, H, 3H]");
+  TORCH_CHECK(uexp.scalar_type() == at::kInt && uexp.numel() >= ndir, "uexp must be int32 [ndir]");
+  TORCH_CHECK(hs.scalar_type() == at::kFloat && hs.is_contiguous() && hs.numel() >= ndir * (steps + 1) * NP * H &&
+                  hs.numel() % ndir == 0, "hs fp32 [ndir, >= steps+1, NP, H]");
+  TORCH_CHECK(gates.scalar_type() == at::kFloat && gates.is_contiguous() && gates.numel() >= ndir * steps * NP * H * 4 &&
+                  gates.numel() % ndir == 0, "gates fp32 [ndir, >= steps, NP, H, 4]");
+  TORCH_CHECK(dgh.scalar_type() == at::kBFloat16 && dgh.is_contiguous() && dgh.numel() == ndir * steps * NP * 3 * H,
+              "dgh bf16 [ndir, steps, NP, 3H]");
+  TORCH_CHECK(dgx.scalar_type() == at::kBFloat16 && dgx.is_contiguous() && dgx.numel() == T * N * gstride &&
+                  gstride >= ndir * 3 * H, "dgx bf16 [T, N, gstride]");
+  const long long rw = ds2_rnnf8_ring_words((int)H, (int)BG, (int)R);
+  TORCH_CHECK(ring.scalar_type() == at::kInt && ring.is_contiguous() && ring.numel() >= ndir * rw, "ring too small");
+  TORCH_CHECK(census.scalar_type() == at::kInt && census.numel() >= ndir * BG * (H / 64), "census too small");
+  for (const OptT* o : {&dbx_part, &dbh_part})
+    if (o->has_value() && (*o)->defined())
+      TORCH_CHECK((*o)->scalar_type() == at::kFloat && (*o)->is_contiguous() && (*o)->numel() == ndir * BG * 3 * H,
+                  "bias partials fp32 [ndir, BG, 3H]");
+  for (const at::Tensor* t : {&U8T, &hs, &gates, &dgh, &dgx, &census, &err, &lens, &uexp, &ring}) need_gpu(*t, "rnnf8_bwd operand");
+  DS2RnnF8B d;
+  d.T = (int)T; d.N = (int)N; d.NP = (int)NP; d.H = (int)H; d.BG = (int)BG; d.R = (int)R; d.steps = (int)steps;
+  d.gstride = (int)gstride; d.ndir = (int)ndir; d.xcd_map = (int)xcd_map;
+  d.lens = lens.data_ptr<int>();
+  d.dy = dy.data_ptr();
+  const size_t usz = (size_t)3 * H * H, hsz = hs.numel() / ndir, gsz = gates.numel() / ndir;
+  const size_t dsz = (size_t)steps * NP * 3 * H, bsz = (size_t)BG * 3 * H;
+  float* bx = ptr_or_null<float>(dbx_part, "dbx_part");
+  float* bh = ptr_or_null<float>(dbh_part, "dbh_part");
+  for (int i = 0; i < 2; ++i) {
+    const bool on = i < ndir;
+    d.U8T[i] = on ? (const void*)(U8T.data_ptr<uint8_t>() + i * usz) : nullptr;
+    d.hsave[i] = on ? hs.data_ptr<float>() + i * hsz : nullptr;
+    d.gates[i] = on ? gates.data_ptr<float>() + i * gsz : nullptr;
+    d.dgh[i] = on ? (void*)(reinterpret_cast<uint16_t*>(dgh.data_ptr()) + i * dsz) : nullptr;
+    d.ring[i] = on ? (void*)(ring.data_ptr<int>() + i * rw) : nullptr;
+    d.dbx_part[i] = (on && bx) ? bx + i * bsz : nullptr;
+    d.dbh_part[i] = (on && bh) ? bh + i * bsz : nullptr;
+  }
+  d.dgx = dgx.data_ptr();
+  d.uexp = uexp.data_ptr<int>();
+  d.dgx_scale = (float)dgx_scale;
+  d.census = reinterpret_cast<unsigned*>(census.data_ptr<int>());
+  d.err = reinterpret_cast<unsigned*>(err.data_ptr<int>());
+  d.timeout = timeout;
+  check(ds2_rnnf8_bwd(&d, cur_stream()), "rnnf8_bwd");
+}
+
 void rnnx_bwd(at::Tensor dy, at::Tensor lens, at::Tensor U_f, OptT U_b, at::Tensor hs_f, OptT hs_b, OptT gates_f,
               OptT gates_b, at::Tensor dgh_f, OptT dgh_b, at::Tensor dgx, OptT dbx_part, OptT dbh_part,
               double dgx_scale, at::Tensor census, at::Tensor err, int64_t T, int64_t N, int64_t NP, int64_t H,
@@ -537,6 +644,25 @@ void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, 
                      (float)b2, (float)eps, (float)gscale, (float)ema_keep, ptr_or_null<const int>(skip, "skip"),
                      (int)max_grid, cur_stream()),
         "adam_ema");
+}
+
+// Adam + EMA over several (lo, hi) element ranges of whole-arena buffers in one launch
+void adam_ema_ranges(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, OptT p16,
+                     std::vector<int64_t> lohi, double lr_t, double b1, double b2, double eps, double gscale,
+                     double ema_keep) {
+  need_gpu(p, "p");
+  need_gpu(g, "g");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 arena expected");
+  const long long n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "arena size mismatch");
+  TORCH_CHECK(lohi.size() % 2 == 0, "adam_ema_ranges: (lo, hi) pairs");
+  for (size_t i = 0; i < lohi.size(); ++i) TORCH_CHECK(lohi[i] >= 0 && lohi[i] <= n, "adam_ema_ranges: range");
+  std::vector<long long> r(lohi.begin(), lohi.end());
+  check(ds2_adam_ema_ranges(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                            ptr_or_null<float>(ema, "ema"), ptr_or_null<void>(p16, "p16"), r.data(),
+                            (int)(r.size() / 2), (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale,
+                            (float)ema_keep, cur_stream()),
+        "adam_ema_ranges");
 }
 
 int64_t grad_norm_blocks(int64_t n) { return ds2_grad_norm_blocks(n); }
@@ -808,9 +934,13 @@ void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, dou
 // their tiles): C[i] (fp32, epi[i] 1 store / 2 accumulate) = A[i] B[i]^T, split-K S[i] through
 // consecutive ranges of one workspace ws (S[i] * M * N floats each) and one zeroed counter
 // buffer cnt (tiles each).
+// opt: [p, m, v, ema or None, p16 or None, grad arena] fp32 arena buffers and optf = [lr_t, b1,
+// b2, eps, gscale, keep]: Adam + EMA of the members' elements in the epilogue (members: epi 1
+// views of the gradient arena); store_g also writes the gradient.
 void gemm8_group(std::vector<at::Tensor> A, std::vector<at::Tensor> B, std::vector<at::Tensor> C,
                  std::vector<int64_t> epi, std::vector<int64_t> splits, bool a_col, bool b_col, OptT ws, OptT cnt,
-                 int64_t max_grid) {
+                 int64_t max_grid, std::vector<c10::optional<at::Tensor>> opt, std::vector<double> optf,
+                 bool store_g) {
   const size_t np = A.size();
   TORCH_CHECK(np >= 1 && np <= 24 && B.size() == np && C.size() == np && epi.size() == np && splits.size() == np,
               "gemm8_group: 1..24 members, one A, B, C, epi, splits each");
@@ -856,9 +986,43 @@ void gemm8_group(std::vector<at::Tensor> A, std::vector<at::Tensor> B, std::vect
     d[3] = (int)a.stride(0); d[4] = (int)b.stride(0); d[5] = (int)c.stride(0);
     d[6] = (int)epi[i]; d[7] = S;
   }
+  DS2G8Opt o{};
+  if (!opt.empty()) {
+    TORCH_CHECK(opt.size() == 6 && optf.size() == 6, "gemm8_group: opt = [p, m, v, ema, p16, grad], 6 constants");
+    auto f32 = [&](int i, bool need) -> float* {
+      const auto& t = opt[i];
+      if (!t.has_value() || !t->defined()) {
+        TORCH_CHECK(!need, "gemm8_group: optimizer buffer ", i, " required");
+        return nullptr;
+      }
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "gemm8_group: fp32 arena ", i);
+      return t->data_ptr<float>();
+    };
+    o.p = f32(0, true); o.m = f32(1, true); o.v = f32(2, true); o.ema = f32(3, false);
+    const float* g = f32(5, true);
+    const int64_t n = opt[5]->numel();
+    for (int i : {0, 1, 2, 3})
+      TORCH_CHECK(!opt[i].has_value() || !opt[i]->defined() || opt[i]->numel() == n, "gemm8_group: arena sizes");
+    if (opt[4].has_value() && opt[4]->defined()) {
+      TORCH_CHECK(opt[4]->scalar_type() == at::kBFloat16 && opt[4]->numel() == n && opt[4]->is_contiguous(),
+                  "gemm8_group: bf16 shadow");
+      o.p16 = reinterpret_cast<unsigned short*>(opt[4]->data_ptr());
+    }
+    for (size_t i = 0; i < np; ++i) {
+      const int64_t e0 = C[i].data_ptr<float>() - g;
+      TORCH_CHECK(e0 >= 0 && e0 % 4 == 0 && C[i].stride(0) % 4 == 0 && epi[i] == 1 &&
+                      e0 + (C[i].size(0) - 1) * C[i].stride(0) + C[i].size(1) <= n,
+                  "gemm8_group: fused-optimizer member ", i, " must be an aligned first-write view of the arena");
+    }
+    o.gbase = g;
+    o.lr_t = (float)optf[0]; o.b1 = (float)optf[1]; o.b2 = (float)optf[2]; o.eps = (float)optf[3];
+    o.gscale = (float)optf[4]; o.keep = (float)optf[5];
+    o.on = 1;
+    o.store_g = store_g ? 1 : 0;
+  }
   check(ds2_gemm8_group((int)np, pa.data(), pb.data(), pc.data(), pw.data(), pn.data(), dims.data(), a_col ? 1 : 0,
                         b_col ? 1 : 0, max_grid > 0 ? (int)std::min<int64_t>(max_grid, dev_cus()) : dev_cus(),
-                        cur_stream()),
+                        o.on ? &o : nullptr, cur_stream()),
         "gemm8_group");
 }
 
@@ -1013,6 +1177,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("rnnf8_fwd", &rnnf8_fwd);
   m.def("rnnf8_supported", [](int64_t H, int64_t N, int64_t ndir) { return ds2_rnnf8_supported((int)H, (int)N, (int)ndir); });
   m.def("fp8_quant_pow2", &fp8_quant_pow2);
+  m.def("fp8_quant_pow2_t", &fp8_quant_pow2_t);
+  m.def("rnnf8_bwd", &rnnf8_bwd);
+  m.def("rnnf8_bwd_supported", [](int64_t H, int64_t N, int64_t ndir) {
+    return ds2_rnnf8_bwd_supported((int)H, (int)N, (int)ndir);
+  });
+  m.def("rnnf8_ring_words", [](int64_t H, int64_t BG, int64_t R) { return ds2_rnnf8_ring_words((int)H, (int)BG, (int)R); });
   m.def("rnnx_fwd", &rnnx_fwd, py::arg("gx"), py::arg("lens"), py::arg("U_f"), py::arg("U_b"), py::arg("bh_f"),
         py::arg("bh_b"), py::arg("y_f"), py::arg("y_b"), py::arg("hx_f"), py::arg("hx_b"), py::arg("hs_f"),
         py::arg("hs_b"), py::arg("gates_f"), py::arg("gates_b"), py::arg("census"), py::arg("err"), py::arg("T"),
@@ -1038,6 +1208,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
   m.def("adam_ema", &adam_ema);
+  m.def("adam_ema_ranges", &adam_ema_ranges);
   m.def("grad_norm_blocks", &grad_norm_blocks);
   m.def("grad_norm", &grad_norm);
   m.def("cast_bf16", &cast_bf16);
@@ -1050,7 +1221,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("a_col") = false, py::arg("b_col") = false, py::arg("splits") = 1, py::arg("ws") = py::none(),
         py::arg("cnt") = py::none(), py::arg("max_grid") = 0);
   m.def("gemm8_group", &gemm8_group, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("epi"), py::arg("splits"),
-        py::arg("a_col"), py::arg("b_col"), py::arg("ws"), py::arg("cnt"), py::arg("max_grid"));
+        py::arg("a_col"), py::arg("b_col"), py::arg("ws"), py::arg("cnt"), py::arg("max_grid"),
+        py::arg("opt") = std::vector<c10::optional<at::Tensor>>{}, py::arg("optf") = std::vector<double>{},
+        py::arg("store_g") = false);
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
   m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),

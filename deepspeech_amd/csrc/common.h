@@ -67,10 +67,47 @@ __device__ __forceinline__ void st_flag(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Two bf16 partials in one dword, each carrying the use tag of a reduce-scatter ring slot in
+// its mantissa LSB (the BPTT kernels of rnn_xcd.hip and rnn_fp8.hip); this conversion sits on
+// the critical path of every BPTT step.
+// Hardware RNE pair conversion (one v_cvt_pk_bf16_f32), then the LSB set to the tag: |error|
+// <= 1.5 bf16 ulp, 3 VALU ops per pair on the publish critical path (a truncate-and-step
+// variant is < 1 ulp but 5-6 ops, measured slower). No carry, so no 0xFFFF special case.
+__device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  const bf2_t p = {(__bf16)lo, (__bf16)hi};
+  const unsigned d = __builtin_bit_cast(unsigned, p);
+  // one bitfield insert instead of and + or (gfx9 VOP3 takes no literal, so the compiler
+  // cannot fuse them into v_and_or_b32): r = (mask & tagmask) | (~mask & d)
+  unsigned r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(0x00010001u), "s"(tagmask), "v"(d));
+  return r;
+}
+
+__device__ __forceinline__ bool granule_tagged16(i32x4 v, unsigned tag) {
+  const unsigned want = tag ? 0x00010001u : 0u;
+  return (((unsigned)v[0] & 0x00010001u) == want) && (((unsigned)v[1] & 0x00010001u) == want) &&
+         (((unsigned)v[2] & 0x00010001u) == want) && (((unsigned)v[3] & 0x00010001u) == want);
+}
+
 // Workgroup barrier that orders LDS only. __syncthreads() also emits s_waitcnt vmcnt(0),
 // which makes every wave wait for ALL its outstanding global loads and stores at the
 // barrier — fatal for a wave that keeps prefetches in flight across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One element of TF's Adam (epsilon-hat form) and of the weight EMA, every rounding spelled out
+// (explicit fma / _rn products, nothing left to the compiler's contraction choice), so every
+// kernel that applies the update — the streaming optimizer (optim.hip) and the fused epilogue
+// of the grouped weight-gradient GEMM (gemm8.hip) — rounds identically: the result of an
+// element does not depend on which kernel or which launch split updated it.
+__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float lr_t, float b1, float b2,
+                                      float eps, float gscale) {
+  const float gj = __fmul_rn(g, gscale);
+  m = __fmaf_rn(b1, m, __fmul_rn(1.f - b1, gj));
+  v = __fmaf_rn(b2, v, __fmul_rn(__fmul_rn(1.f - b2, gj), gj));
+  p = __fmaf_rn(-lr_t, __fdiv_rn(m, __fadd_rn(__fsqrt_rn(v), eps)), p);
+}
+__device__ __forceinline__ float ema1(float e, float p, float keep) { return __fmaf_rn(keep, __fsub_rn(e, p), p); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -66,6 +66,13 @@
 // glds wave-instruction), read as MFMA fragments with ds_read_b64_tr_b16 (8 k of one column
 // per lane from two 4-row transposed reads; inline asm, see rdtr). k-rows past K come back
 // as zeros from the bounds-checked buffer load, so any K works.
+// Fused optimizer epilogue (G8Opt.on, group launches of fp32 first-write members): the launch
+// is the tail of a single-device backward that produces every recurrent weight gradient, so
+// instead of storing a gradient tile for a separate Adam pass to read back, the epilogue
+// applies Adam + weight EMA to the same arena elements at once (adam1 / ema1 of common.h,
+// bitwise the streaming optimizer's update): per element it reads p, m, v, ema and writes p, m,
+// v, ema and the bf16 compute shadow (the gradient itself only with store_g). The members' C
+// are views of the gradient arena; p / m / v / ema / p16 are indexed at the same element.
 // Split-K (S > 1): work unit = (tile, k-slice); each unit stores its raw fp32 partial tile to
 // a workspace [S][M][N] per problem, and the tile's last-arriving slice sums the S partials in
 // slice order (deterministic) and applies the epilogue, in the same launch. For the
@@ -77,6 +84,19 @@
 #include "common.h"
 
 using namespace ds2;
+
+// Adam + EMA applied in the epilogue (see the header): arena bases and this step's constants
+// (the same layout is declared in bindings.cpp)
+struct DS2G8Opt {
+  float* p;
+  float* m;
+  float* v;
+  float* ema;             // may be null (no EMA)
+  unsigned short* p16;    // bf16 shadow, may be null
+  const float* gbase;     // gradient arena base: element index of C(m, n) = C - gbase + m*ldc + n
+  float lr_t, b1, b2, eps, gscale, keep;
+  int on, store_g;
+};
 
 namespace {
 
@@ -101,8 +121,11 @@ struct G8Prob {
 
 constexpr int G8_MAXP = 24;
 
+using G8Opt = DS2G8Opt;
+
 struct G8Args {
   G8Prob p[G8_MAXP];
+  G8Opt opt;
   const bf16_t* bias;
   const float* alpha_dev;
   const float* alpha_dev2;
@@ -262,9 +285,37 @@ __device__ __forceinline__ void mfma_tile(f32x4 (&acc)[2][4], const Frag (&a)[4]
     for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(acc[j][i]));
 }
 
+// Adam + EMA of the 4 consecutive arena elements [e, e + 4) with gradient gv and their loaded
+// state p, m, v, em (e % 4 == 0: the host checks the members' offsets and row strides).
+// Non-temporal: the optimizer state is touched once per step and must not evict the GEMM's
+// operands from L2.
+__device__ __forceinline__ void opt_update4(const G8Opt& o, long long e, f32x4 gv, f32x4 p, f32x4 m, f32x4 v,
+                                            f32x4 em) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float pj = p[j], mj = m[j], vj = v[j];
+    adam1(pj, gv[j], mj, vj, o.lr_t, o.b1, o.b2, o.eps, o.gscale);
+    p[j] = pj; m[j] = mj; v[j] = vj;
+    em[j] = ema1(em[j], pj, o.keep);
+  }
+  __builtin_nontemporal_store(p, (f32x4*)(o.p + e));
+  __builtin_nontemporal_store(m, (f32x4*)(o.m + e));
+  __builtin_nontemporal_store(v, (f32x4*)(o.v + e));
+  if (o.ema) __builtin_nontemporal_store(em, (f32x4*)(o.ema + e));
+  if (o.p16) {
+    bf16_t* p16 = o.p16;
+    const unsigned lo = (unsigned)f2bf(p[0]) | ((unsigned)f2bf(p[1]) << 16);
+    const unsigned hi = (unsigned)f2bf(p[2]) | ((unsigned)f2bf(p[3]) << 16);
+    *(uint2*)(p16 + e) = make_uint2(lo, hi);
+  }
+  if (o.store_g) __builtin_nontemporal_store(gv, (f32x4*)(const_cast<float*>(o.gbase) + e));
+}
+
 template <bool FP8, int AC, int BC>
 __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
   static_assert(!FP8 || (!AC && !BC), "fp8 operands are K-contiguous");
+  // the fused optimizer epilogue exists only in the weight-gradient (column-column) variant
+  constexpr bool OPTEPI = !FP8 && AC && BC;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -463,6 +514,52 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
     // the final epilogue: lane's fragment (qm, qn, j, i) holds C[m][n .. n+3]
     auto finish = [&](auto&& value) {
       const int epi = P.epi;
+      if constexpr (OPTEPI) {
+        if (epi == 1 && g.opt.on) {
+          // fused optimizer: OB row fragments of one (qm, qn, j) column block at a time, all
+          // their state loads issued before any update (OB x the loads in flight of a
+          // fragment-by-fragment chain, which left the epilogue latency-bound)
+          constexpr int OB = 2;
+          const long long cb = (long long)((const float*)P.C - g.opt.gbase);
+#pragma unroll
+          for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int n = n0 + qn * 128 + wc * 32 + 16 * j + 4 * g16;
+#pragma unroll
+              for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+                for (int i0 = 0; i0 < 4; i0 += OB) {
+                  long long e[OB];
+                  bool ok[OB];
+                  f32x4 sp[OB], sm[OB], sv[OB], se[OB];
+#pragma unroll
+                  for (int b = 0; b < OB; ++b) {
+                    const int m = m0 + qm * 128 + wr * 64 + 16 * (i0 + b) + r16;
+                    ok[b] = m < M && n < N;
+                    e[b] = cb + (long long)(ok[b] ? m : 0) * P.ldc + (ok[b] ? n : 0);
+                    sp[b] = __builtin_nontemporal_load((const f32x4*)(g.opt.p + e[b]));
+                    sm[b] = __builtin_nontemporal_load((const f32x4*)(g.opt.m + e[b]));
+                    sv[b] = __builtin_nontemporal_load((const f32x4*)(g.opt.v + e[b]));
+                    se[b] = g.opt.ema ? __builtin_nontemporal_load((const f32x4*)(g.opt.ema + e[b]))
+                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+                  }
+#pragma unroll
+                  for (int b = 0; b < OB; ++b) {
+                    if (!ok[b]) continue;
+                    const int m = m0 + qm * 128 + wr * 64 + 16 * (i0 + b) + r16;
+                    const f32x4 v = value(qm, qn, j, i0 + b, m, n);
+                    opt_update4(g.opt, e[b], f32x4{alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3]}, sp[b],
+                                sm[b], sv[b], se[b]);
+                  }
+                  // one batch's loads in flight at a time (hoisting the next batch's loads above
+                  // these updates needs more VGPRs than the kernel has: spills)
+                  __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+          return;
+        }
+      }
       char* Cz = (char*)P.C;
       const bool has_bias = epi == 0 && g.bias != nullptr;
 #pragma unroll
@@ -629,6 +726,7 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
   const int es = fp8 ? 1 : 2;
   if (batch <= 0 || batch > G8_MAXP || (epi != 0 && bias)) return (int)hipErrorInvalidValue;
   G8Args a;
+  a.opt = G8Opt{};
   a.bias = (const bf16_t*)bias;
   a.alpha_dev = alpha_dev;
   a.alpha_dev2 = alpha_dev2;
@@ -653,10 +751,24 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
 // same operand modes for every member, fp32 C (epi 1 / 2), no bias, alpha = 1. Member i:
 // A[i], B[i], C[i], dims[i] = {M, N, K, lda, ldb, ldc, epi, S}; ws[i] / cnt[i] for S > 1 as in
 // ds2_gemm8 (separate ranges per member).
+// opt (may be null): Adam + EMA applied in the epilogue instead of storing the gradient (every
+// member epi 1, C a view of the gradient arena opt->gbase with element offset and ldc % 4 == 0)
 int ds2_gemm8_group(int np, const void* const* A, const void* const* B, void* const* C, float* const* ws,
-                    unsigned* const* cnt, const int* dims, int a_col, int b_col, int cus, hipStream_t st) {
+                    unsigned* const* cnt, const int* dims, int a_col, int b_col, int cus, const DS2G8Opt* opt,
+                    hipStream_t st) {
   if (np <= 0 || np > G8_MAXP) return (int)hipErrorInvalidValue;
   G8Args a;
+  a.opt = G8Opt{};
+  if (opt != nullptr && opt->on) {
+    if (!a_col || !b_col) return (int)hipErrorInvalidValue;   // only that variant has the epilogue
+    if (!opt->p || !opt->m || !opt->v || !opt->gbase) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < np; ++i) {
+      const int* d = dims + 8 * i;
+      const long long e0 = (const float*)C[i] - opt->gbase;
+      if (d[6] != 1 || d[5] % 4 != 0 || e0 < 0 || e0 % 4 != 0) return (int)hipErrorInvalidValue;
+    }
+    a.opt = *opt;
+  }
   a.bias = nullptr;
   a.alpha_dev = a.alpha_dev2 = nullptr;
   a.alpha = 1.f;

@@ -28,18 +28,10 @@ template <typename T>
 __device__ __forceinline__ T ld_s(const T* p) { return __builtin_nontemporal_load(p); }
 template <typename T>
 __device__ __forceinline__ void st_s(T v, T* p) { __builtin_nontemporal_store(v, p); }
-// One element's update with every rounding spelled out (explicit fma / _rn products, nothing
-// left to the compiler's contraction choice), so the vector-group paths and the scalar tail
-// round identically: the result of an element does not depend on how the arena is split
-// into launches (Trainer's per-layer optimizer ranges are bitwise the single launch).
-__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float lr_t, float b1, float b2,
-                                      float eps, float gscale) {
-  const float gj = __fmul_rn(g, gscale);
-  m = __fmaf_rn(b1, m, __fmul_rn(1.f - b1, gj));
-  v = __fmaf_rn(b2, v, __fmul_rn(__fmul_rn(1.f - b2, gj), gj));
-  p = __fmaf_rn(-lr_t, __fdiv_rn(m, __fadd_rn(__fsqrt_rn(v), eps)), p);
-}
-__device__ __forceinline__ float ema1(float e, float p, float keep) { return __fmaf_rn(keep, __fsub_rn(e, p), p); }
+// adam1 / ema1 (common.h): one element's update with every rounding spelled out, so the
+// vector-group paths, the scalar tail and the fused GEMM epilogue round identically: the
+// result of an element does not depend on how the arena is split into launches (Trainer's
+// per-layer optimizer ranges are bitwise the single launch).
 
 template <int U>
 __device__ __forceinline__ void adam_groups(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
@@ -129,6 +121,30 @@ __global__ __launch_bounds__(OPT_THREADS) void adam_ema_chunk_kernel(
   }
 }
 
+// The same update over a list of arena ranges in ONE launch (the elements of a step that the
+// grouped weight-gradient GEMM's fused epilogue did not update: FC head, biases, padding):
+// thread i takes float4 group i of the ranges' concatenation. Ranges start and end on
+// float4 boundaries (host-checked).
+constexpr int ADAM_MAXR = 64;
+struct AdamRanges {
+  long long lo4[ADAM_MAXR];     // first float4 group of range r
+  long long pre4[ADAM_MAXR + 1];  // float4 groups before range r (pre4[nr] = total)
+  int nr;
+};
+
+__global__ __launch_bounds__(OPT_THREADS) void adam_ema_ranges_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+    float* __restrict__ ema, bf16_t* __restrict__ p16, AdamRanges rg, float lr_t, float b1, float b2, float eps,
+    float gscale, float ema_keep) {
+  const long long total = rg.pre4[rg.nr];
+  const long long stride = (long long)gridDim.x * OPT_THREADS;
+  int r = 0;
+  for (long long i = (long long)blockIdx.x * OPT_THREADS + threadIdx.x; i < total; i += stride) {
+    while (i >= rg.pre4[r + 1]) ++r;          // i only grows: the range index only advances
+    adam_groups<1>(p, g, m, v, ema, p16, rg.lo4[r] + (i - rg.pre4[r]), 0, lr_t, b1, b2, eps, gscale, ema_keep);
+  }
+}
+
 // partial sums of g^2 (fp32 per block), plus a non-finite flag
 __global__ __launch_bounds__(OPT_THREADS) void grad_norm_kernel(const float* __restrict__ g, long long n, float gscale,
                                                                 float* __restrict__ part, int* __restrict__ bad) {
@@ -190,6 +206,26 @@ int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void*
   if (max_grid > 0 && grid > max_grid) grid = max_grid;
   hipLaunchKernelGGL(adam_ema_kernel, dim3(grid), dim3(OPT_THREADS), 0, st, p, g, m, v, ema, (bf16_t*)p16, n,
                      lr_t, b1, b2, eps, gscale, ema_keep, skip);
+  return (int)hipGetLastError();
+}
+
+// lohi: nr (lo, hi) element ranges of the arena, each a multiple of 4 at both ends
+int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema, void* p16, const long long* lohi,
+                        int nr, float lr_t, float b1, float b2, float eps, float gscale, float ema_keep,
+                        hipStream_t st) {
+  if (nr < 0 || nr > ADAM_MAXR) return (int)hipErrorInvalidValue;
+  AdamRanges rg;
+  rg.nr = nr;
+  rg.pre4[0] = 0;
+  for (int r = 0; r < nr; ++r) {
+    const long long lo = lohi[2 * r], hi = lohi[2 * r + 1];
+    if (lo < 0 || hi < lo || lo % 4 || hi % 4) return (int)hipErrorInvalidValue;
+    rg.lo4[r] = lo / 4;
+    rg.pre4[r + 1] = rg.pre4[r] + (hi - lo) / 4;
+  }
+  if (rg.pre4[nr] == 0) return 0;
+  hipLaunchKernelGGL(adam_ema_ranges_kernel, dim3(grid_for(rg.pre4[nr] * 4)), dim3(OPT_THREADS), 0, st, p, g, m, v,
+                     ema, (bf16_t*)p16, rg, lr_t, b1, b2, eps, gscale, ema_keep);
   return (int)hipGetLastError();
 }
 

@@ -657,6 +657,406 @@ __global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// fp8 BPTT (rnnf8_bwd_kernel): config 5's backward on the forward's geometry — groups of
+// P = H/64 workgroups of 64 units, one XCD per group (8 groups: 2 directions x 4 batch groups
+// of R <= 8 rows), so the per-step exchange stays in the XCD's L2 (plain stores). The bf16
+// reduce-scatter BPTT of rnn_xcd.hip needs 32-unit workgroups at H = 1280 (a 64-unit bf16
+// U^T slice, 491 KB, does not fit a CU), i.e. P = 40 > 32 CUs: groups straddle XCDs and
+// exchange write-through (5.2 us/step).
+//  * Same protocol as rnnw_bwd_kernel: P_j(s) = dg_s[:, own cols] . U[own cols, :] for all H
+//    units, published as tagged bf16 unit pairs into a 3-slot ring; a consumer gathers its
+//    two pairs from every producer (two producers per 16-B load).
+//  * Own columns: 3 gates x 64 units = 192 = k-step 0 (gates 0 and 1, 128 deep) + k-step 1
+//    (gate 2, the second 64 of its 128 zero), one v_mfma_scale_f32_16x16x128_f8f6f4 each. U^T
+//    is e4m3 with the forward's per-tensor power-of-two scale (E8M0 A scale); k-step 0's
+//    fragments live in VGPRs, k-step 1's real half (16 B per lane) in LDS.
+//  * dg (the gate-gradient operand) is requantised to e4m3 every step with ONE power-of-two
+//    scale per batch row (E8M0 B scale, the same in all four lanes that hold a row, so the
+//    product does not depend on how the hardware pairs lanes with K blocks); the dU GEMM and
+//    dgx outputs stay bf16 and exact.
+// ------------------------------------------------------------------------------------
+constexpr int BMW8 = 7;                  // worker waves (gather + MFMA); 0..3 also run the cell
+constexpr int BEW8 = 4;
+constexpr int BMEM8 = 7;                 // memory wave
+constexpr int BTH8 = 8 * 64;
+
+struct XF8B {
+  int T, N, NP, H, P, BG, R, steps, gstride, ngroups, xcd_map;
+  const int* lens;
+  const bf16_t* dy;                 // [T][N][H]
+  const unsigned char* U8T[2];      // [H][3H] e4m3 U^T: U8T[m][g H + u] = U[g H + u][m] / 2^e
+  const int* uexp;                  // [2] E8M0 exponent of each direction's U scale
+  const float* hsave[2];            // [steps+1][NP][H] fp32 h (slot s = h before step s)
+  const float* gates[2];            // [steps][NP][H][4] (r, z, n, U_n h + b_hn)
+  bf16_t* dgh[2];                   // [steps][NP][3H] bf16 output (dU GEMM operand)
+  bf16_t* dgx;                      // [T][N][gstride] bf16 (x dgx_scale)
+  unsigned* ring[2];                // [3][BG][P][H/32][R][4] 16-B granules, filled 0xFFFFFFFF
+  float* dbx_part[2];               // [BG][3H] (+=)
+  float* dbh_part[2];
+  float dgx_scale;
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+};
+
+// E8M0 exponent byte e + 127 of the smallest power of two 2^e with amax / 2^e <= 448
+__device__ __forceinline__ int e8m0_for(float amax) {
+  if (!(amax > 0.f)) return 127;
+  int e = (int)ceilf(__log2f(amax / 448.f));
+  if (ldexpf(448.f, e) < amax) ++e;
+  if (ldexpf(448.f, e - 1) >= amax) --e;
+  return min(254, max(1, e + 127));
+}
+
+template <int MTU, int GPT>
+__global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
+  constexpr int ROWS = 16;                        // MFMA tile rows (R <= 8 real)
+  constexpr int EPT = 2;                          // epilogue elements per thread (rows wave + 4 i, i < 2)
+  constexpr int LT = ROWS8 * (UPW8 / 4) / 64;     // memory-wave load tasks per lane (2)
+  constexpr int ST = ROWS8 * G3 * (UPW8 / 8) / 64;  // store tasks per lane (3)
+  static_assert(GPT % 2 == 0, "two producers per gather load");
+  __shared__ float red_s[BMW8][ROWS][UPW8 + 1];
+  __shared__ __attribute__((aligned(16))) unsigned char dq_s[2][ROWS][128];   // e4m3 dg by k-step
+  __shared__ int dsc_s[ROWS];                                               // E8M0 per row (4 copies)
+  __shared__ float dyr_s[2][ROWS8][UPW8];
+  __shared__ float hpr_s[2][ROWS8][UPW8];
+  __shared__ float4 gr_s[2][ROWS8][UPW8];
+  __shared__ __attribute__((aligned(16))) bf16_t ox_s[2][ROWS8][G3][UPW8];  // dgx (scaled)
+  __shared__ __attribute__((aligned(16))) bf16_t oh_s[2][ROWS8][G3][UPW8];  // dgh
+  __shared__ i32x4 ul_s[MTU][BMW8][64];                                     // k-step 1 A halves
+  __shared__ int len_s[ROWS8];
+  __shared__ int s_mode, s_abort;
+
+  int grp, mem;
+  if (!take_role8(a.xcd_map, a.ngroups, a.P, grp, mem)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, GH = G3 * H, N = a.N, NP = a.NP, R = a.R, P = a.P, MTS = H / 16, NPR = MTS / 2;
+  const int bg = grp % a.BG, dir = grp / a.BG;
+  const int r0 = bg * R, u0 = mem * UPW8;
+  if (tid < ROWS8) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
+  if (tid < ROWS) dsc_s[tid] = 0x7f7f7f7f;
+  for (int i = tid; i < 2 * ROWS * 128 / 4; i += BTH8) reinterpret_cast<int*>(&dq_s[0][0][0])[i] = 0;
+  if (wave == 0) {
+    const int m = census8(a.census, grp, mem, P, a.timeout, a.err);
+    if (lane == 0) { s_mode = m; s_abort = (m < 0); }
+  }
+  // resident A fragments of m-tile mt = 2 (wave + 7 (i >> 1)) + (i & 1): A[m][k] = U^T, unit m =
+  // 16 mt + lane % 16, k-step 0: k in [16 g, +16) = gate 0 units u0 + 16 g.., [64 + 16 g, +16) =
+  // gate 1; k-step 1: [16 g, +16) = gate 2 (the rest zero), g = lane / 16
+  i32x8 ua[MTU];
+  {
+    const unsigned char* Ut = a.U8T[dir];
+#pragma unroll
+    for (int i = 0; i < MTU; ++i) {
+      const int mt = 2 * (wave + BMW8 * (i >> 1)) + (i & 1);
+      i32x4 lo = {0, 0, 0, 0}, hi = lo, l2 = lo;
+      if (wave < BMW8 && mt < MTS) {
+        const unsigned char* p = Ut + (size_t)(16 * mt + (lane & 15)) * GH + u0 + 16 * (lane >> 4);
+        lo = *reinterpret_cast<const i32x4*>(p);
+        hi = *reinterpret_cast<const i32x4*>(p + H);
+        l2 = *reinterpret_cast<const i32x4*>(p + 2 * H);
+      }
+      ua[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      if (wave < BMW8) ul_s[i][wave][lane] = l2;
+    }
+  }
+  float carry[EPT], sbx[EPT][G3], sbh[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    carry[i] = 0.f;
+    sbh[i] = 0.f;
+#pragma unroll
+    for (int g = 0; g < G3; ++g) sbx[i][g] = 0.f;
+  }
+  __syncthreads();   // len_s, dq_s zeros, ul_s, census
+
+  // memory wave: load task = (row, 4 units), store task = (row, gate, 8 units)
+  uint2 pdy[LT];
+  float4 php[LT];
+  float4 pgt[LT][4];
+  auto mw_load = [&](int s) {
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q / (UPW8 / 4), c4 = (q % (UPW8 / 4)) * 4;
+      if (row < R) {
+        const int bp = min(r0 + row, NP - 1), bn = min(r0 + row, N - 1), u = u0 + c4;
+        const int t = max(0, min((dir == 0) ? s : (len_s[row] - 1 - s), a.T - 1));
+        pdy[k] = *reinterpret_cast<const uint2*>(a.dy + ((size_t)t * N + bn) * H + u);
+        const float4* gp = reinterpret_cast<const float4*>(a.gates[dir]) + ((size_t)s * NP + bp) * H + u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pgt[k][i] = gp[i];
+        php[k] = *reinterpret_cast<const float4*>(a.hsave[dir] + ((size_t)s * NP + bp) * H + u);
+      }
+    }
+  };
+  auto mw_put = [&](int s) {
+    const int slot = s & 1;
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q / (UPW8 / 4), c4 = (q % (UPW8 / 4)) * 4;
+      if (row < R) {
+        const bool act = s < len_s[row];
+        const float dv[4] = {bf2f((bf16_t)(pdy[k].x & 0xffffu)), bf2f((bf16_t)(pdy[k].x >> 16)),
+                             bf2f((bf16_t)(pdy[k].y & 0xffffu)), bf2f((bf16_t)(pdy[k].y >> 16))};
+        const float hv[4] = {php[k].x, php[k].y, php[k].z, php[k].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dyr_s[slot][row][c4 + i] = act ? dv[i] : 0.f;
+          hpr_s[slot][row][c4 + i] = act ? hv[i] : 0.f;
+          gr_s[slot][row][c4 + i] = act ? pgt[k][i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  };
+  auto mw_store = [&](int s) {          // dgx and dgh of step s from the staging area
+#pragma unroll
+    for (int k = 0; k < ST; ++k) {
+      const int q = lane + 64 * k;
+      const int row = q / (G3 * 8), rem = q - row * (G3 * 8), g = rem >> 3, c8 = (rem & 7) * 8;
+      if (row < R) {
+        const int b = r0 + row, u = u0 + c8;
+        *reinterpret_cast<i32x4*>(a.dgh[dir] + ((size_t)s * NP + b) * GH + g * H + u) =
+            *reinterpret_cast<const i32x4*>(&oh_s[s & 1][row][g][c8]);
+        if (b < N) {
+          const int L = len_s[row];
+          const int t = (s < L) ? ((dir == 0) ? s : (L - 1 - s)) : s;
+          *reinterpret_cast<i32x4*>(a.dgx + ((size_t)t * N + b) * a.gstride + dir * GH + g * H + u) =
+              *reinterpret_cast<const i32x4*>(&ox_s[s & 1][row][g][c8]);
+        }
+      }
+    }
+  };
+  if (s_abort) return;
+  if (wave == BMEM8 && a.steps > 0) mw_load(a.steps - 1);
+  const bool plain = s_mode == 1;
+  const unsigned ring_bytes = (unsigned)((size_t)3 * a.BG * P * NPR * R * 64);
+  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(a.ring[dir], ring_bytes);
+  auto tag_of = [&](int s) -> unsigned { return (unsigned)(((a.steps - 1 - s) / 3) & 1); };
+  // [slot][bg][producer][unit pair][row][granule g][8 bf16]: granule (row, g) of pair p holds
+  // units 32 p + {4 g .. 4 g + 3, 16 + 4 g .. 16 + 4 g + 3}
+  auto ring_off16 = [&](int slot, int j, int pr, int row, int g) -> unsigned {
+    return (unsigned)((((((size_t)slot * a.BG + bg) * P + j) * NPR + pr) * R + row) * 4 + g) * 16u;
+  };
+
+  if (wave < BMW8) {
+    const int sa = __builtin_amdgcn_readfirstlane(a.uexp[dir]);
+    const int saw = sa | (sa << 8) | (sa << 16) | (sa << 24);       // U^T: one E8M0 for all blocks
+    for (int s = a.steps - 1; s >= 0; --s) {
+      const bool has_next = s + 1 < a.steps;
+      // (G) lane -> (producer half h, row, granule g); the two unit pairs of this workgroup
+      {
+        const int h = lane >> 5, grow = (lane >> 2) & 7, gg = lane & 3;
+        constexpr int NI = GPT / 2;
+        float acc8[2][8];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc8[pp][q] = 0.f;
+        if (has_next && grow < R) {
+          const int cs = (s + 1) % 3;
+          const unsigned want = tag_of(s + 1);
+          unsigned off[2][NI];
+          i32x4 v[2][NI];
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+              const int j = min(wave + BMW8 * (2 * i + h), P - 1);
+              off[pp][i] = ring_off16(cs, j, 2 * mem + pp, grow, gg);
+              v[pp][i] = load_sc1_b128(rs_ring, off[pp][i]);
+            }
+          const long long t0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+              if (wave + BMW8 * (2 * i + h) < P) {
+                while (!granule_tagged16(v[pp][i], want)) {
+                  if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
+                  __builtin_amdgcn_s_sleep(1);
+                  v[pp][i] = load_sc1_b128(rs_ring, off[pp][i]);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  acc8[pp][2 * q] += __uint_as_float((unsigned)v[pp][i][q] << 16);
+                  acc8[pp][2 * q + 1] += __uint_as_float((unsigned)v[pp][i][q] & 0xffff0000u);
+                }
+              }
+            }
+          }
+        }
+        if (grow < R) {
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              red_s[wave][grow + 8 * h][32 * pp + 4 * gg + q] = acc8[pp][q];
+              red_s[wave][grow + 8 * h][32 * pp + 16 + 4 * gg + q] = acc8[pp][4 + q];
+            }
+        }
+      }
+      lds_barrier();                                                        // #1
+      if (s_abort) break;
+      // (E) cell backward (waves 0..3, row wave + 4 i, unit = lane): dgh / dgx staging and the
+      // e4m3 dg operand with one power-of-two scale per row (wave-wide amax of the row)
+      if (wave < BEW8) {
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int row = wave + BEW8 * i, c = lane;
+          if (row < R) {                                  // wave-uniform
+            float dhrec = 0.f;
+            if (has_next) {
+#pragma unroll
+              for (int w = 0; w < BMW8; ++w) dhrec += red_s[w][row][c] + red_s[w][row + 8][c];
+            }
+            const bool act = s < len_s[row];
+            const float dh = dyr_s[s & 1][row][c] + carry[i] + dhrec;
+            const float hp = hpr_s[s & 1][row][c];
+            const float4 gv = gr_s[s & 1][row][c];
+            const float r = gv.x, z = gv.y, n = gv.z, ghn = gv.w;
+            const float dn = dh * (1.f - z);
+            const float dz = dh * (hp - n);
+            const float dan = dn * (1.f - n * n);
+            const float dr = dan * ghn;
+            float ghv[G3] = {dr * r * (1.f - r), dz * z * (1.f - z), dan * r};
+            float gxs[G3] = {ghv[0], ghv[1], dan};
+            carry[i] = act ? dh * z : 0.f;
+            if (!act) {
+#pragma unroll
+              for (int g = 0; g < G3; ++g) { ghv[g] = 0.f; gxs[g] = 0.f; }
+            }
+            const float am = wave_max(fmaxf(fmaxf(fabsf(ghv[0]), fabsf(ghv[1])), fabsf(ghv[2])));
+            const int eb = e8m0_for(am);
+            const float inv = __uint_as_float((unsigned)(254 - eb) << 23);   // 2^-(eb - 127)
+            dq_s[0][row][c] = (unsigned char)f2e4m3(ghv[0] * inv);
+            dq_s[0][row][64 + c] = (unsigned char)f2e4m3(ghv[1] * inv);
+            dq_s[1][row][c] = (unsigned char)f2e4m3(ghv[2] * inv);
+            if (lane == 0) dsc_s[row] = eb | (eb << 8) | (eb << 16) | (eb << 24);
+#pragma unroll
+            for (int g = 0; g < G3; ++g) {
+              oh_s[s & 1][row][g][c] = f2bf(ghv[g]);
+              ox_s[s & 1][row][g][c] = f2bf(gxs[g] * a.dgx_scale);
+              sbx[i][g] += gxs[g];
+            }
+            sbh[i] += ghv[G3 - 1];
+          }
+        }
+      }
+      lds_barrier();                                                        // #2
+      // (M) publish P(s) = dg_s[:, own cols] . U[own cols, :] into ring slot s % 3
+      if (s > 0) {
+        const int ws = s % 3;
+        const unsigned tagmask = tag_of(s) ? 0x00010001u : 0u;
+        const bool prow = (lane & 15) < R;
+        const unsigned char* dr = &dq_s[0][lane & 15][16 * (lane >> 4)];
+        const i32x8 b0 = __builtin_shufflevector(*reinterpret_cast<const i32x4*>(dr),
+                                                 *reinterpret_cast<const i32x4*>(dr + 64), 0, 1, 2, 3, 4, 5, 6, 7);
+        const i32x4 z4 = {0, 0, 0, 0};
+        const i32x8 b1 = __builtin_shufflevector(*reinterpret_cast<const i32x4*>(dr + ROWS * 128), z4, 0, 1, 2, 3, 4,
+                                                 5, 6, 7);
+        const int sbw = dsc_s[lane & 15];
+        constexpr int NPW = MTU / 2;
+        unsigned offp[NPW];
+#pragma unroll
+        for (int k = 0; k < NPW; ++k) offp[k] = ring_off16(ws, mem, min(wave + BMW8 * k, NPR - 1), lane & 15, lane >> 4);
+        auto publish = [&](auto PLAIN) {
+#pragma unroll
+          for (int k = 0; k < NPW; ++k) {
+            const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+            f32x4 a0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ua[2 * k], b0, zero, 0, 0, 0, saw, 0, sbw);
+            f32x4 a1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ua[2 * k + 1], b0, zero, 0, 0, 0, saw, 0, sbw);
+            const i32x8 u2a = __builtin_shufflevector(ul_s[2 * k][wave][lane], z4, 0, 1, 2, 3, 4, 5, 6, 7);
+            const i32x8 u2b = __builtin_shufflevector(ul_s[2 * k + 1][wave][lane], z4, 0, 1, 2, 3, 4, 5, 6, 7);
+            a0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2a, b1, a0, 0, 0, 0, saw, 0, sbw);
+            a1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2b, b1, a1, 0, 0, 0, saw, 0, sbw);
+            if (prow && wave + BMW8 * k < NPR) {
+              const i32x4 v = {(int)bf16x2_tagged(a0[0], a0[1], tagmask), (int)bf16x2_tagged(a0[2], a0[3], tagmask),
+                               (int)bf16x2_tagged(a1[0], a1[1], tagmask), (int)bf16x2_tagged(a1[2], a1[3], tagmask)};
+              if constexpr (decltype(PLAIN)::value) store_b128(rs_ring, offp[k], v);
+              else store_sc1_b128(rs_ring, offp[k], v);
+            }
+          }
+        };
+        if (plain) publish(std::true_type{});
+        else publish(std::false_type{});
+      }
+    }
+  } else {
+    for (int s = a.steps - 1; s >= 0; --s) {
+      mw_put(s);
+      if (s + 2 < a.steps) mw_store(s + 2);
+      if (s >= 1) mw_load(s - 1);
+      lds_barrier();                                                        // #1
+      if (s_abort) break;
+      lds_barrier();                                                        // #2
+    }
+  }
+  __syncthreads();
+  if (wave == BMEM8 && !s_abort) {
+    if (a.steps >= 2) mw_store(1);
+    if (a.steps >= 1) mw_store(0);
+  }
+  // bias gradients: the epilogue waves' rows reduced through LDS, one read-modify-write per
+  // (gate, unit) of the workgroup's own [bg] partial row (layout of rnnrs_bwd_kernel)
+  if (a.dbx_part[dir] != nullptr && !s_abort) {
+    constexpr int BW = (G3 + 1) * UPW8;
+    static_assert(BMW8 * ROWS * (UPW8 + 1) >= ROWS8 * BW, "bias reduction does not fit the LDS scratch");
+    float* bred = &red_s[0][0][0];
+    if (wave < BEW8) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        const int row = wave + BEW8 * i;
+#pragma unroll
+        for (int g = 0; g < G3; ++g) bred[row * BW + g * UPW8 + lane] = sbx[i][g];
+        bred[row * BW + G3 * UPW8 + lane] = sbh[i];
+      }
+    }
+    __syncthreads();
+    for (int q = tid; q < BW; q += BTH8) {
+      float sum = 0.f;
+      for (int r = 0; r < ROWS8; ++r) sum += bred[r * BW + q];
+      const int g = q / UPW8, c = q % UPW8;
+      const size_t base = (size_t)bg * GH + u0 + c;
+      if (g < G3) {
+        a.dbx_part[dir][base + (size_t)g * H] += sum;
+        if (a.dbh_part[dir] != nullptr && g < G3 - 1) a.dbh_part[dir][base + (size_t)g * H] += sum;
+      } else if (a.dbh_part[dir] != nullptr) {
+        a.dbh_part[dir][base + (size_t)(G3 - 1) * H] += sum;
+      }
+    }
+  }
+}
+
+// e4m3 TRANSPOSED copy q[c][r] = x[r][c] / 2^e of a bf16 [rows][cols] tensor (the BPTT's U^T),
+// with e from *amax as quant_pow2_kernel (uexp written as 127 + e). 64 x 64 tiles through LDS.
+__global__ __launch_bounds__(256) void quant_pow2_t_kernel(const bf16_t* __restrict__ x, int rows, int cols,
+                                                           const unsigned* __restrict__ amax,
+                                                           unsigned char* __restrict__ q, int* __restrict__ uexp) {
+  __shared__ float t_s[64][65];
+  const float am = __uint_as_float(*amax);
+  int e = 0;
+  if (am > 0.f) {
+    e = (int)ceilf(log2f(am / 448.f));
+    if (ldexpf(448.f, e) < am) ++e;
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *uexp = 127 + e;
+  const float inv = ldexpf(1.f, -e);
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    t_s[r][c] = (r0 + r < rows && c0 + c < cols) ? bf2f(x[(size_t)(r0 + r) * cols + c0 + c]) : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int c = i >> 6, r = i & 63;
+    if (c0 + c < cols && r0 + r < rows) q[(size_t)(c0 + c) * rows + r0 + r] = (unsigned char)f2e4m3(t_s[r][c] * inv);
+  }
+}
+
 // amax of |x| over a bf16 tensor into *amax (as float bits; zeroed by the caller)
 __global__ __launch_bounds__(256) void amax_bf16_kernel(const bf16_t* __restrict__ x, long long n,
                                                         unsigned* __restrict__ amax) {
@@ -783,6 +1183,77 @@ int ds2_rnnf8_fwd(const DS2RnnF8* d, hipStream_t st) {
 #undef DS2_F8
     default: return -41;
   }
+  return (int)hipGetLastError();
+}
+
+struct DS2RnnF8B {
+  int T, N, NP, H, BG, R, steps, gstride, ndir, xcd_map;
+  const int* lens;
+  const void* dy;
+  const void* U8T[2];
+  const int* uexp;
+  const float* hsave[2];
+  const float* gates[2];
+  void* dgh[2];
+  void* dgx;
+  void* ring[2];
+  float* dbx_part[2];
+  float* dbh_part[2];
+  float dgx_scale;
+  unsigned* census;
+  unsigned* err;
+  long long timeout;
+};
+
+// fp8 BPTT geometry: H = 256 k, k = 1..5 (P = H/64 <= 20 workgroups per group), R <= 8
+int ds2_rnnf8_bwd_supported(int H, int N, int ndir) {
+  if (H % 256 != 0 || H / 256 < 1 || H / 256 > 5) return 0;
+  const int BG = 8 / ndir;
+  return (N + BG - 1) / BG <= ROWS8 ? 1 : 0;
+}
+
+// ring words (uint32) of one direction: [3][BG][P][H/32][R][4] granules of 4 words
+long long ds2_rnnf8_ring_words(int H, int BG, int R) { return 3LL * BG * (H / 64) * (H / 32) * R * 16; }
+
+int ds2_rnnf8_bwd(const DS2RnnF8B* d, hipStream_t st) {
+  if (!ds2_rnnf8_bwd_supported(d->H, d->N, d->ndir) || d->R < 1 || d->R > ROWS8 || d->NP != d->BG * d->R ||
+      d->BG * d->ndir > 8)
+    return -40;
+  XF8B a;
+  a.T = d->T; a.N = d->N; a.NP = d->NP; a.H = d->H; a.P = d->H / UPW8; a.BG = d->BG; a.R = d->R;
+  a.steps = d->steps; a.gstride = d->gstride; a.ngroups = d->ndir * d->BG;
+  a.xcd_map = (d->xcd_map & 1) && a.ngroups <= 8;
+  a.lens = d->lens; a.dy = (const bf16_t*)d->dy; a.uexp = d->uexp;
+  for (int i = 0; i < 2; ++i) {
+    a.U8T[i] = (const unsigned char*)d->U8T[i]; a.hsave[i] = d->hsave[i]; a.gates[i] = d->gates[i];
+    a.dgh[i] = (bf16_t*)d->dgh[i]; a.ring[i] = (unsigned*)d->ring[i];
+    a.dbx_part[i] = d->dbx_part[i]; a.dbh_part[i] = d->dbh_part[i];
+  }
+  a.dgx = (bf16_t*)d->dgx; a.dgx_scale = d->dgx_scale;
+  a.census = d->census; a.err = d->err; a.timeout = d->timeout;
+  if (d->steps <= 0) return 0;
+  const int grid = a.xcd_map ? 8 * a.P : a.ngroups * a.P;
+  switch (d->H / 256) {
+    case 1: hipLaunchKernelGGL((rnnf8_bwd_kernel<4, 2>), dim3(grid), dim3(BTH8), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((rnnf8_bwd_kernel<6, 2>), dim3(grid), dim3(BTH8), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((rnnf8_bwd_kernel<8, 2>), dim3(grid), dim3(BTH8), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((rnnf8_bwd_kernel<10, 4>), dim3(grid), dim3(BTH8), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((rnnf8_bwd_kernel<12, 4>), dim3(grid), dim3(BTH8), 0, st, a); break;
+    default: return -41;
+  }
+  return (int)hipGetLastError();
+}
+
+// transposed per-tensor power-of-two e4m3 quantisation (the BPTT's U^T): q [cols][rows]
+int ds2_fp8_quant_pow2_t(const void* x, int rows, int cols, void* q, int* uexp, unsigned* amax, hipStream_t st) {
+  const long long n = (long long)rows * cols;
+  if (n <= 0) return 0;
+  long long blocks = (n + 256 * 8 - 1) / (256 * 8);
+  if (blocks > 512) blocks = 512;
+  DS2_HIP_CHECK(hipMemsetAsync(amax, 0, sizeof(unsigned), st));
+  hipLaunchKernelGGL(amax_bf16_kernel, dim3((int)blocks), dim3(256), 0, st, (const bf16_t*)x, n, amax);
+  hipLaunchKernelGGL(quant_pow2_t_kernel, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, st,
+                     (const bf16_t*)x, rows, cols, amax, (unsigned char*)q, uexp);
   return (int)hipGetLastError();
 }
 

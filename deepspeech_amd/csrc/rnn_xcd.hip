@@ -1252,32 +1252,7 @@ struct XBwdRS {
   unsigned long long* stamps;
 };
 
-// Two bf16 partials in one dword, each carrying the use tag in its mantissa LSB: the fp32
-// value's truncation, moved up one ulp where its LSB disagrees with the tag (the nearest
-// bf16 with the right LSB: error < 1 ulp). Packed integer ops (perm, and, xor, add): this
-// conversion sits on the critical path of every BPTT step and wave64 VALU ops cost 4 cycles
-// (the per-value version with NaN selects made the publish phase ~1.6k cycles longer). The
-// +1 can carry out of the low half only from 0xFFFF (a negative NaN with a full payload),
-// which is first replaced by the canonical NaN 0x7FC0.
-// Hardware RNE pair conversion (one v_cvt_pk_bf16_f32), then the LSB set to the tag: |error|
-// <= 1.5 bf16 ulp, 3 VALU ops per pair on the publish critical path (a truncate-and-step
-// variant is < 1 ulp but 5-6 ops, measured slower). No carry, so no 0xFFFF special case.
-__device__ __forceinline__ unsigned bf16x2_tagged(float lo, float hi, unsigned tagmask) {
-  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
-  const bf2_t p = {(__bf16)lo, (__bf16)hi};
-  const unsigned d = __builtin_bit_cast(unsigned, p);
-  // one bitfield insert instead of and + or (gfx9 VOP3 takes no literal, so the compiler
-  // cannot fuse them into v_and_or_b32): r = (mask & tagmask) | (~mask & d)
-  unsigned r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(0x00010001u), "s"(tagmask), "v"(d));
-  return r;
-}
-
-__device__ __forceinline__ bool granule_tagged16(i32x4 v, unsigned tag) {
-  const unsigned want = tag ? 0x00010001u : 0u;
-  return (((unsigned)v[0] & 0x00010001u) == want) && (((unsigned)v[1] & 0x00010001u) == want) &&
-         (((unsigned)v[2] & 0x00010001u) == want) && (((unsigned)v[3] & 0x00010001u) == want);
-}
+// bf16x2_tagged / granule_tagged16 (tagged bf16 partials of the reduce-scatter ring): common.h
 
 // A ring word carries its use tag in the mantissa LSB (see rnnrs_bwd_kernel): the granule is
 // ready when all four words carry the expected tag.

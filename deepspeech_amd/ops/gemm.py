@@ -278,12 +278,19 @@ def group_operands(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
     return A, B
 
 
-def gemm8_group(members, accumulate: bool = False, max_grid: int = 0) -> None:
+def gemm8_group(members, accumulate: bool = False, max_grid: int = 0, opt=None) -> None:
     """out_i (=, or += with ``accumulate``) A_i @ B_i^T for a list of (A, B, out) stored
     column-mode operands (:func:`group_operands`), as few launches as the group limit allows:
     one grid over every member's 256^2 tiles, so a set of small weight-gradient GEMMs fills the
     chip where each alone would leave CUs idle. Split-K only when even the whole group has too
-    few tiles (gemm8_splits on the summed tile count)."""
+    few tiles (gemm8_splits on the summed tile count).
+
+    ``opt`` = (tensors, constants, store_g): instead of storing each out_i, the epilogue applies
+    Adam + weight EMA to the same arena elements (csrc/gemm8.hip "Fused optimizer epilogue");
+    tensors = [p, m, v, ema | None, p16 | None, grad arena], constants = [lr_t, b1, b2, eps,
+    gscale, keep]; the outs must be aligned views of the grad arena (first writes)."""
+    if opt is not None and accumulate:
+        raise ValueError("the fused optimizer epilogue needs first-write members")
     C = _ext.ext()
     epi = 2 if accumulate else 1
     for lo in range(0, len(members), _GROUP_MAX):
@@ -307,8 +314,12 @@ def gemm8_group(members, accumulate: bool = False, max_grid: int = 0) -> None:
             ws = torch.empty(sum(s * A.shape[1] * B.shape[1] for (A, B, _), s in zip(chunk, sp) if s > 1),
                              device=dev, dtype=torch.float32)
             cnt = _tile_counters(dev, tiles)
-        C.gemm8_group([m[0] for m in chunk], [m[1] for m in chunk], [m[2] for m in chunk], [epi] * len(chunk), sp,
-                      True, True, ws, cnt, grid)
+        if opt is None:
+            C.gemm8_group([m[0] for m in chunk], [m[1] for m in chunk], [m[2] for m in chunk], [epi] * len(chunk),
+                          sp, True, True, ws, cnt, grid)
+        else:
+            C.gemm8_group([m[0] for m in chunk], [m[1] for m in chunk], [m[2] for m in chunk], [epi] * len(chunk),
+                          sp, True, True, ws, cnt, grid, list(opt[0]), [float(x) for x in opt[1]], bool(opt[2]))
 
 
 _counters: Dict[Tuple[int, int], torch.Tensor] = {}

@@ -341,6 +341,36 @@ class FusedAdamEMA:
                             lr_t, self.b1, self.b2, self.eps, gscale, keep, skip_flag, int(max_grid))
 
     @torch.no_grad()
+    def apply_excluding(self, lo: int, hi: int, exclude, lr_t: float, keep: float, gscale: float = 1.0) -> None:
+        """Adam + EMA of arena elements [lo, hi) except the ``exclude`` ranges (already updated
+        this step, e.g. by the grouped weight-gradient GEMM's fused epilogue): the remaining
+        intervals in one launch (csrc/optim.hip adam_ema_ranges) when they fit its table."""
+        todo, pos = [], lo
+        for a, b in sorted(exclude):
+            a, b = max(a, lo), min(b, hi)
+            if b <= a:
+                continue
+            if a > pos:
+                todo.append((pos, a))
+            pos = max(pos, b)
+        if pos < hi:
+            todo.append((pos, hi))
+        if not todo:
+            return
+        if self.use_hip and len(todo) > 1 and len(todo) <= 64 and all(a % 4 == 0 and b % 4 == 0 for a, b in todo):
+            ar = self.arena
+            _ext.ext().adam_ema_ranges(ar.flat, ar.grad, self.m, self.v, self.ema, self.p16,
+                                       [x for r in todo for x in r], lr_t, self.b1, self.b2, self.eps, gscale, keep)
+            return
+        for a, b in todo:
+            self.apply_range(a, b, lr_t, keep, gscale)
+
+    def fused_constants(self, lr_t: float, keep: float, gscale: float = 1.0):
+        """(tensors, constants) of a fused-epilogue update (gemm.gemm8_group ``opt``)."""
+        return ([self.arena.flat, self.m, self.v, self.ema, self.p16, self.arena.grad],
+                [lr_t, self.b1, self.b2, self.eps, gscale, keep if self.ema is not None else 0.0])
+
+    @torch.no_grad()
     def step(self, lr: float, global_step: int, gscale: float = 1.0,
              skip_flag: Optional[torch.Tensor] = None) -> None:
         """One Adam + EMA update of the whole arena."""

@@ -448,6 +448,48 @@ def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan):
     return y, (hx, hs, gates)
 
 
+# config 5's fp8 mode: the BPTT too runs on the fp8 geometry (csrc/rnn_fp8.hip rnnf8_bwd_kernel:
+# e4m3 U^T and dg operands, one XCD per group) where the fp8 forward ran; False keeps the bf16
+# reduce-scatter BPTT on the saved states (tests compare the two)
+_FP8_BPTT = os.environ.get("DS2_FP8_BPTT", "1") == "1"
+
+
+def fp8_bptt_ok(plan: RnnPlan, N: int) -> bool:
+    return _FP8_BPTT and fp8_recurrence_ok(plan, N) and bool(_ext.ext().rnnf8_bwd_supported(plan.H, N, plan.ndir))
+
+
+def _run_bwd_fp8(dy, lens, U, hs, gates, plan: RnnPlan, gstride: int, dgx_scale: float = 1.0,
+                 want_bias: bool = True):
+    """fp8 GRU BPTT (csrc/rnn_fp8.hip): groups of H/64 workgroups on one XCD, U^T in e4m3 with
+    a per-tensor power-of-two scale (computed here on the device), the gate gradients requantised
+    to e4m3 per batch row each step. Same outputs as _run_bwd: (dgx [T, N, gstride] bf16 x
+    dgx_scale, dgh [ndir, steps, NP, 3H] bf16, bias partials [2, ndir, BG, 3H] or None)."""
+    C = _ext.ext()
+    T, N, H = dy.shape
+    ndir = plan.ndir
+    BG = 8 // ndir
+    R = -(-N // BG)
+    NP = BG * R
+    assert NP == plan.NP, (NP, plan.NP)
+    dev = dy.device
+    steps = T
+    dy = dy.to(torch.bfloat16).contiguous()
+    U8T = torch.empty(ndir, H, 3 * H, device=dev, dtype=torch.uint8)
+    words = torch.empty(4, device=dev, dtype=torch.int32)          # uexp[2], amax scratch
+    for d in range(ndir):
+        C.fp8_quant_pow2_t(U[d].contiguous(), U8T[d], words[d:d + 1], words[3:4])
+    dgh = torch.empty(ndir, steps, NP, 3 * H, device=dev, dtype=torch.bfloat16)
+    dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
+    census = torch.empty(ndir * BG * (H // 64), device=dev, dtype=torch.int32)
+    parts = torch.empty(2, ndir, BG, 3 * H, device=dev, dtype=torch.float32) if want_bias else None
+    ring = torch.empty(ndir, int(C.rnnf8_ring_words(H, BG, R)), device=dev, dtype=torch.int32)
+    _fill_bwd(census, parts, ring)
+    C.rnnf8_bwd(dy, lens, U8T, words, hs, gates, dgh, dgx, parts[0] if parts is not None else None,
+                parts[1] if parts is not None else None, float(dgx_scale), census, error_word(dev), ring,
+                T, N, NP, H, BG, R, steps, gstride, ndir, TIMEOUT_TICKS, 1)
+    return dgx, dgh, parts
+
+
 def _alloc_bwd(plan: RnnPlan, want_bias: bool, dev) -> tuple:
     """(census, parts, ring) of an XCD BPTT launch and the multi_fill that initialises them:
     census words -1, bias partials 0, the reduce-scatter ring 0xFFFFFFFF (none depends on T)."""
@@ -648,13 +690,15 @@ class FusedBiLayer(torch.autograd.Function):
                 W16.shape[0] % 8 == 0:
             arena = arena_of(W_f)
             wT = _transpose_async(W16, wgrad_stream(x.device, arena), arena.wgrad if arena is not None else None)
+        ctx.fp8_bwd = False
         if fp8 and x.is_cuda and fp8_recurrence_ok(plan, N):
-            # config 5's fp8 mode: the recurrence too (e4m3 U and h exchange); BPTT stays bf16.
-            # The BPTT differentiates the bf16-U recurrence at the fp8 forward's saved states, so
-            # the gradient is straight-through with respect to the quantisation of U and of the
-            # exchanged h (no quantisation gradient); tests/test_convergence_gpu.py pins the
-            # resulting 300-step loss curve against the bf16 recurrence
+            # config 5's fp8 mode: the recurrence too (e4m3 U and h exchange), and its BPTT on the
+            # same geometry with the same e4m3 U (rnnf8_bwd_kernel; dg requantised per row). The
+            # gradient is straight-through with respect to the quantisation of the exchanged h and
+            # of dg (no quantisation gradient); tests/test_convergence_gpu.py pins the resulting
+            # 300-step loss curve against the bf16 recurrence
             y, (hx, hs, gates) = _run_fwd_fp8(gx, lens, U, bh, plan)
+            ctx.fp8_bwd = fp8_bptt_ok(plan, N)
         else:
             y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
         dev = x.device
@@ -680,8 +724,12 @@ class FusedBiLayer(torch.autograd.Function):
         d1 = plan.ndir == 2
         T, N, D = x16.shape
         GH = GATES[plan.cell] * plan.H
-        dgx, dgh, parts = _run_bwd(dy, lens, [U_f16, U_b16 if d1 else None], hx, hs, gates, plan,
-                                   plan.ndir * GH, dgx_scale=ctx.alpha)
+        if getattr(ctx, "fp8_bwd", False):
+            dgx, dgh, parts = _run_bwd_fp8(dy, lens, [U_f16, U_b16 if d1 else None], hs, gates, plan,
+                                           plan.ndir * GH, dgx_scale=ctx.alpha)
+        else:
+            dgx, dgh, parts = _run_bwd(dy, lens, [U_f16, U_b16 if d1 else None], hx, hs, gates, plan,
+                                       plan.ndir * GH, dgx_scale=ctx.alpha)
         dgx2 = dgx.view(T * N, plan.ndir * GH)
 
         def input_grad():
@@ -904,6 +952,10 @@ class WgradScheduler:
       overrides); the GEMMs then run per layer on the side stream as each BPTT finishes.
     * ``set_early_update``: the optimizer range of the parameters that are final once the
       grouped launch is issued runs on the side stream right behind it.
+    * ``set_fused_update``: the grouped launch applies Adam + EMA to its members' elements in
+      its epilogue (csrc/gemm8.hip) instead of storing their gradients; ``fused_ranges`` then
+      lists the arena element ranges already updated this step, which every later optimizer
+      range of the step skips.
     """
 
     def __init__(self):
@@ -924,6 +976,8 @@ class WgradScheduler:
         self.early_upper_done = False
         self.early_upper_hi = 0
         self.transposes = []       # queued W^T shadows of this forward (_transpose_async)
+        self._fused = None         # (arena, tensors, constants, store_g): set_fused_update
+        self.fused_ranges = []     # arena element ranges the grouped epilogue updated this step
         _schedulers.add(self)
 
     def stream(self, device: torch.device) -> Optional["torch.cuda.Stream"]:
@@ -958,6 +1012,8 @@ class WgradScheduler:
         self.early_upper_done = False
         self.early_upper_hi = 0
         self.transposes.clear()
+        self._fused = None
+        self.fused_ranges = []
 
     def flush_transposes(self) -> None:
         """Issue the queued W^T transposes on the side stream behind everything the current
@@ -1027,12 +1083,41 @@ class WgradScheduler:
         fn()
         self.early_done = True
 
+    def set_fused_update(self, arena, tensors, constants, store_g: bool = False) -> None:
+        """For THIS backward: the grouped tail launch applies the optimizer to its members'
+        elements in its epilogue (tensors / constants as gemm.gemm8_group's ``opt``)."""
+        self._fused = (arena, list(tensors), list(constants), bool(store_g))
+        self.fused_ranges = []
+
+    def _fused_opt(self, members):
+        """gemm8_group ``opt`` for these members, or None when the epilogue cannot take them
+        (not all contiguous, 16-B aligned first-write views of this arena's gradient buffer)."""
+        if self._fused is None:
+            return None
+        arena, tensors, constants, store_g = self._fused
+        g = arena.grad
+        base, n = g.data_ptr(), g.numel()
+        ranges = []
+        for _, _, out in members:
+            e0 = (out.data_ptr() - base) // 4
+            if (out.dtype != torch.float32 or not out.is_contiguous() or (out.data_ptr() - base) % 16 or
+                    e0 < 0 or e0 + out.numel() > n or out.shape[-1] % 4):
+                return None
+            ranges.append((e0, e0 + out.numel()))
+        return (tensors, constants, store_g), ranges
+
     def flush(self) -> None:
         """Issue every deferred weight-gradient GEMM on the current stream: one grouped launch
         when every one of them can join it, else one call each."""
         if self.deferred and self.grouped and all(isinstance(d, Deferred) and d.members for d in self.deferred):
             items, self.deferred = self.deferred, []
-            GM.gemm8_group([m for d in items for m in d.members])
+            members = [m for d in items for m in d.members]
+            fused = self._fused_opt(members)
+            if fused is not None:
+                GM.gemm8_group(members, opt=fused[0])
+                self.fused_ranges.extend(fused[1])
+            else:
+                GM.gemm8_group(members)
             for d in items:
                 d.done()
             return

@@ -203,6 +203,7 @@ def main(argv=None) -> int:
     ev_prev = None
     first_attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) == 0
     sum_on = ctx.is_main and (not args.dummy or args.summaries_on_dummy) and args.summary_every > 0
+    trainer.keep_grads = sum_on          # gradient histograms read arena.grad after the step
 
     def check_divergence():
         bad = trainer.first_nonfinite_step()

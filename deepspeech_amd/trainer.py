@@ -53,6 +53,14 @@ def lr_schedule_from_args(args, steps_per_epoch: int) -> LRSchedule:
 # full grid 21.16 / 21.08, 192 blocks 21.04 / 20.99, 512 blocks 21.04 / 20.98)
 _EARLY_UPPER = True
 _UPPER_GRID = 512
+# single device, weight gradients deferred to the grouped tail launch: that launch can apply Adam +
+# EMA to the recurrent weights in its epilogue (csrc/gemm8.hip "Fused optimizer epilogue")
+# instead of storing their gradients for a separate optimizer pass to read back. Bitwise the
+# same update (tests/test_gemm_gpu.py), but measured slower at the headline (same box, round 4:
+# 8.21 vs 8.04 ms/step): the grid's workgroups finish their tiles in lockstep, so every
+# epilogue streams its 2.2 MB of optimizer state at the same moment (HBM-bound, +450 us on the
+# group) instead of overlapping the MFMA work; off until that is staggered
+_FUSED_OPT = False
 
 
 def _check_hw_queues() -> None:
@@ -107,6 +115,9 @@ class Trainer:
         # data parallel: optimizer ranges per gradient bucket behind its all-reduce
         # (GradBucketer.set_optimizer); per_bucket_update=False keeps one update after finish()
         self.per_bucket_update = True
+        # keep_grads: the fused optimizer epilogue also stores the gradients it consumed (set
+        # when something reads arena.grad after a step: gradient summaries)
+        self.keep_grads = False
         # single device: arena elements [0, split) — FC head and recurrent stack, laid out
         # before the conv front-end in gradient-production order — get their optimizer update
         # as soon as the recurrent weight gradients are issued (Trainer.step)
@@ -166,9 +177,12 @@ class Trainer:
             # front-end's backward (WgradScheduler.set_early_update); the front-end's range after
             lr_t, keep = self.opt.prepare(self.lr, self.global_step)
             split, sch = self._early_split, self.arena.wgrad
+            if _FUSED_OPT:
+                tensors, consts = self.opt.fused_constants(lr_t, keep, gscale)
+                sch.set_fused_update(self.arena, tensors, consts, store_g=self.keep_grads)
             self.arena.wgrad.set_early_update(
-                lambda: self.opt.apply_range(sch.early_upper_hi if sch.early_upper_done else 0, split, lr_t, keep,
-                                             gscale),
+                lambda: self.opt.apply_excluding(sch.early_upper_hi if sch.early_upper_done else 0, split,
+                                                 sch.fused_ranges, lr_t, keep, gscale),
                 self._early_params)
             if self._layer_first and _EARLY_UPPER:
                 # the head and the layers whose weight gradients ran beside the BPTT (not in the
@@ -188,7 +202,7 @@ class Trainer:
                 # when the lower early range was skipped: never apply it twice
                 sch = self.arena.wgrad
                 lo = split if sch.early_done else (sch.early_upper_hi if sch.early_upper_done else 0)
-                self.opt.apply_range(lo, self.arena.numel, lr_t, keep, gscale)
+                self.opt.apply_excluding(lo, self.arena.numel, sch.fused_ranges, lr_t, keep, gscale)
         elif not per_bucket:
             skip = None
             if self.nan_policy == "skip":

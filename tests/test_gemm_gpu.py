@@ -291,3 +291,85 @@ def test_gemm8_group_split_and_chunks():
     G.gemm8_group([(a, b, o) for (a, b), o in zip(many, outs)])
     for (a, b), o in zip(many, outs):
         assert _rel(o, a.float().t() @ b.float()) < 1e-4
+
+
+@pytest.mark.parametrize("split_case", [False, True])
+def test_gemm8_group_fused_adam_epilogue_bitwise(split_case):
+    """The grouped weight-gradient launch with the fused optimizer epilogue (csrc/gemm8.hip):
+    Adam + EMA + bf16 shadow of every member's arena elements equal BITWISE the plain launch
+    (gradients stored) followed by the streaming optimizer (csrc/optim.hip), members at
+    offsets inside one arena with untouched gaps between them; store_g also leaves the
+    gradients bitwise as the plain launch stores them. split_case: few tiles -> split-K, the
+    last-arriving slice applies the update."""
+    from deepspeech_amd.ops import _ext
+    torch.manual_seed(21)
+    C = _ext.ext()
+    if split_case:
+        shapes = [(4000, 256, 264), (4000, 128, 96)]
+    else:
+        shapes = [(7712, 4800, 800), (7712, 2400, 800), (7712, 800, 800), (7712, 96, 264)]   # 134 tiles: no split
+    ops = [(torch.randn(K, M, device=DEV).to(BF), torch.randn(K, N, device=DEV).to(BF)) for K, M, N in shapes]
+    offs, pos = [], 128
+    for K, M, N in shapes:
+        offs.append(pos)
+        pos += M * N + 64                     # a 64-element gap no member owns
+    n = pos + 256
+    p0 = torch.randn(n, device=DEV)
+    m0 = torch.randn(n, device=DEV) * 1e-3
+    v0 = torch.rand(n, device=DEV) * 1e-4
+    e0 = torch.randn(n, device=DEV)
+    lr_t, b1, b2, eps, gscale, keep = 3e-4, 0.9, 0.999, 1e-8, 0.5, 0.99
+
+    def arena():
+        return dict(p=p0.clone(), m=m0.clone(), v=v0.clone(), e=e0.clone(), g=torch.zeros(n, device=DEV),
+                    p16=torch.zeros(n, device=DEV, dtype=BF))
+
+    def members(a):
+        out = []
+        for (A, B), o, (K, M, N) in zip(ops, offs, shapes):
+            view = a["g"][o:o + M * N].view(M, N)
+            oa, ob = G.group_operands(A.t(), B, view)
+            out.append((oa, ob, view))
+        return out
+    ref = arena()
+    G.gemm8_group(members(ref))
+    ranges = [(o, o + M * N) for o, (K, M, N) in zip(offs, shapes)]
+    for lo, hi in ranges:
+        C.adam_ema(ref["p"][lo:hi], ref["g"][lo:hi], ref["m"][lo:hi], ref["v"][lo:hi], ref["e"][lo:hi],
+                   ref["p16"][lo:hi], lr_t, b1, b2, eps, gscale, keep, None, 0)
+    for store_g in (False, True):
+        got = arena()
+        G.gemm8_group(members(got), opt=([got["p"], got["m"], got["v"], got["e"], got["p16"], got["g"]],
+                                         [lr_t, b1, b2, eps, gscale, keep], store_g))
+        torch.cuda.synchronize()
+        for k in ("p", "m", "v", "e", "p16"):
+            assert torch.equal(got[k], ref[k]), (k, store_g)
+        if store_g:
+            assert torch.equal(got["g"], ref["g"])
+        else:
+            assert int((got["g"] != 0).sum()) == 0          # no gradient written
+    for buf in G._counters.values():
+        assert int(buf.abs().sum()) == 0
+
+
+def test_adam_ema_ranges_bitwise():
+    """One launch over several arena ranges (csrc/optim.hip adam_ema_ranges) equals one
+    adam_ema launch per range, bitwise, and leaves the elements between ranges untouched."""
+    from deepspeech_amd.ops import _ext
+    torch.manual_seed(22)
+    C = _ext.ext()
+    n = 50000
+    bufs = [torch.randn(n, device=DEV), torch.randn(n, device=DEV), torch.randn(n, device=DEV) * 1e-3,
+            torch.rand(n, device=DEV) * 1e-4, torch.randn(n, device=DEV)]
+    ranges = [(0, 1000), (1024, 1028), (4096, 40000), (40064, 49996)]
+    a = [t.clone() for t in bufs] + [torch.zeros(n, device=DEV, dtype=BF)]
+    b = [t.clone() for t in bufs] + [torch.zeros(n, device=DEV, dtype=BF)]
+    for lo, hi in ranges:
+        C.adam_ema(a[0][lo:hi], a[1][lo:hi], a[2][lo:hi], a[3][lo:hi], a[4][lo:hi], a[5][lo:hi], 1e-3, 0.9, 0.999,
+                   1e-8, 1.0, 0.9, None, 0)
+    C.adam_ema_ranges(b[0], b[1], b[2], b[3], b[4], b[5], [x for r in ranges for x in r], 1e-3, 0.9, 0.999, 1e-8,
+                      1.0, 0.9)
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(b[0][1000:1024], bufs[0][1000:1024])

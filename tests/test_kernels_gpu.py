@@ -476,3 +476,99 @@ def test_fp8_recurrence_matches_emulation(cuda, N, H, ndir):
         L = int(lens[b])
         if L < T:
             assert float(y[L:, b].abs().max()) == 0.0
+
+
+def _e4m3_pow2(x, amax):
+    """x / 2^e rounded to e4m3, times 2^e, with the smallest e such that amax / 2^e <= 448
+    (per-element amax tensor broadcast against x; amax 0 -> e = 0)."""
+    am = amax.clamp_min(1e-30)
+    e = torch.ceil(torch.log2(am / 448.0))
+    e = torch.where(am / torch.exp2(e) > 448.0, e + 1, e)
+    e = torch.where(am / torch.exp2(e - 1) <= 448.0, e - 1, e)
+    e = torch.where(amax > 0, e, torch.zeros_like(e))
+    return (x / torch.exp2(e)).to(torch.float8_e4m3fn).float() * torch.exp2(e)
+
+
+def _gru_bptt_fp8_emulation(dy, lens, U, hs, gates, H, ndir):
+    """fp32 model of csrc/rnn_fp8.hip rnnf8_bwd_kernel on the forward's saved states: U^T in
+    e4m3 with the per-tensor power-of-two scale, the gate gradients of each (row, 64-unit
+    workgroup) requantised to e4m3 with one power-of-two scale every step; dgh / dgx exact."""
+    T, N, _ = dy.shape
+    P = H // 64
+    dgx = torch.zeros(T, N, ndir * 3 * H, device=dy.device)
+    dghs = []
+    ar = torch.arange(N, device=dy.device)
+    for d in range(ndir):
+        u = U[d].float()
+        uq = _e4m3_pow2(u, u.abs().max())
+        carry = torch.zeros(N, H, device=dy.device)
+        dhrec = torch.zeros(N, H, device=dy.device)
+        dgh = torch.zeros(T, N, 3 * H, device=dy.device)
+        for s in range(T - 1, -1, -1):
+            act = torch.tensor([s < int(lens[b]) for b in range(N)], device=dy.device)
+            t = torch.tensor([s if d == 0 else max(int(lens[b]) - 1 - s, 0) for b in range(N)], device=dy.device)
+            dh = torch.where(act[:, None], dy[t, ar].float(), 0.0) + carry + dhrec
+            g = gates[d, s, :N].float()
+            r, z, n, ghn = g[..., 0], g[..., 1], g[..., 2], g[..., 3]
+            hp = hs[d, s, :N].float()
+            dn = dh * (1 - z)
+            dz = dh * (hp - n)
+            dan = dn * (1 - n * n)
+            dr = dan * ghn
+            ghv = torch.cat([dr * r * (1 - r), dz * z * (1 - z), dan * r], 1) * act[:, None]
+            gxs = torch.cat([ghv[:, :2 * H], dan * act[:, None]], 1)
+            carry = torch.where(act[:, None], dh * z, 0.0)
+            dgh[s] = ghv
+            tt = torch.where(act, t, torch.full_like(t, s))
+            dgx[tt, ar, d * 3 * H:(d + 1) * 3 * H] = gxs
+            blk = ghv.view(N, 3, P, 64).abs().amax(dim=(1, 3))             # [N, P]
+            am = blk[:, None, :, None].expand(N, 3, P, 64).reshape(N, 3 * H)
+            dhrec = _e4m3_pow2(ghv, am) @ uq
+        dghs.append(dgh)
+    return dgx, dghs
+
+
+@pytest.mark.parametrize("N,H,ndir", [(8, 256, 2), (32, 1280, 2), (20, 1024, 2), (8, 1280, 1)])
+def test_fp8_bptt_matches_emulation(cuda, N, H, ndir):
+    """The fp8 GRU BPTT (csrc/rnn_fp8.hip rnnf8_bwd_kernel: groups of H/64 workgroups on one XCD,
+    e4m3 U^T, per-(row, workgroup) e4m3 gate gradients, tagged-bf16 reduce-scatter) on the saved
+    states of the fp8 forward, against an fp32 emulation of the same quantisation: dgx, dgh and
+    the bias partials within 3 %, padding exactly zero. (32, 1280, 2) is config 5's production
+    geometry."""
+    from deepspeech_amd.ops import rnn as RNN
+    torch.manual_seed(7 * N + H)
+    T = 19
+    plan = RNN.plan_for(N, H, "gru", ndir, cuda)
+    ok = RNN.fp8_bptt_ok(plan, N)
+    if (N, H, ndir) == (32, 1280, 2):
+        assert ok, "config 5 geometry not served by the fp8 BPTT"
+    if not ok:
+        pytest.skip("geometry not served by the fp8 BPTT")
+    gx = (torch.randn(T, N, ndir * 3 * H, device=cuda) * 0.5).to(torch.bfloat16)
+    lens = torch.randint(T // 2, T + 1, (N,), device=cuda, dtype=torch.int32)
+    lens[0] = T
+    U = [(torch.randn(3 * H, H, device=cuda) * (1.5 / H ** 0.5)).to(torch.bfloat16) for _ in range(ndir)]
+    bh = [torch.randn(3 * H, device=cuda) * 0.1 for _ in range(ndir)]
+    y, (hx, hs, gates) = RNN._run_fwd_fp8(gx, lens, U, bh + [None] * (2 - ndir), plan)
+    dy = torch.randn(T, N, H, device=cuda).to(torch.bfloat16)
+    for b in range(N):
+        dy[int(lens[b]):, b] = 0
+    dgx, dgh, parts = RNN._run_bwd_fp8(dy, lens, U + [None] * (2 - ndir), hs, gates, plan, ndir * 3 * H)
+    torch.cuda.synchronize()
+    RNN.check_errors()
+    dgx_r, dgh_r = _gru_bptt_fp8_emulation(dy, lens, U, hs, gates, H, ndir)
+    assert _rel(dgx.float(), dgx_r) < 3e-2, _rel(dgx.float(), dgx_r)
+    for d in range(ndir):
+        assert _rel(dgh[d, :, :N].float(), dgh_r[d]) < 3e-2, (d, _rel(dgh[d, :, :N].float(), dgh_r[d]))
+        assert float(dgh[d, :, N:].float().abs().max() if dgh.shape[2] > N else 0) == 0.0
+        db = parts[0, d].sum(0)
+        assert _rel(db, dgx_r[..., d * 3 * H:(d + 1) * 3 * H].sum((0, 1))) < 3e-2
+    for b in range(N):
+        L = int(lens[b])
+        if L < T:
+            assert float(dgx[L:, b].abs().max()) == 0.0
+    # and close to the bf16 reduce-scatter BPTT on the same states (quantisation only)
+    if plan.kind == "xcd":
+        dgx16, _, _ = RNN._run_bwd(dy, lens, U + [None] * (2 - ndir), hx, hs, gates, plan, ndir * 3 * H)
+        torch.cuda.synchronize()
+        assert _rel(dgx.float(), dgx16.float()) < 8e-2, _rel(dgx.float(), dgx16.float())

@@ -18,6 +18,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from deepspeech_amd.ops import gemm as G  # noqa: E402
+from deepspeech_amd.ops import _ext  # noqa: E402
 
 
 def timeit(fn, iters=10):
@@ -174,6 +175,27 @@ def main():
         cases[name + " | hipblaslt"] = (fl, lib)
         cases[name + " | gemm8 each"] = (fl, each)
         cases[name + " | gemm8 group"] = (fl, lambda mem=mem: G.gemm8_group(mem))
+        # the same group writing views of ONE gradient arena, then the optimizer over those
+        # elements (separate streaming Adam + EMA launch) vs the fused optimizer epilogue
+        n = sum(o.numel() for _, _, o in mem)
+        ar = dict(g=torch.zeros(n, device=dev), p=torch.randn(n, device=dev), m=torch.zeros(n, device=dev),
+                  v=torch.zeros(n, device=dev), e=torch.randn(n, device=dev),
+                  p16=torch.zeros(n, device=dev, dtype=bf))
+        amem, pos = [], 0
+        for A, B, o in mem:
+            amem.append((A, B, ar["g"][pos:pos + o.numel()].view_as(o)))
+            pos += o.numel()
+        Cx = _ext.ext()
+
+        def sep(amem=amem, ar=ar):
+            G.gemm8_group(amem)
+            Cx.adam_ema(ar["p"], ar["g"], ar["m"], ar["v"], ar["e"], ar["p16"], 1e-4, 0.9, 0.999, 1e-8, 1.0, 0.999,
+                        None, 0)
+        opt = ([ar["p"], ar["m"], ar["v"], ar["e"], ar["p16"], ar["g"]], [1e-4, 0.9, 0.999, 1e-8, 1.0, 0.999], False)
+        cases[name + " | gemm8 group + adam"] = (fl, sep)
+        cases[name + " | gemm8 group fused adam"] = (fl, lambda amem=amem, opt=opt: G.gemm8_group(amem, opt=opt))
+        cases[name + " | adam alone"] = (fl, lambda ar=ar: Cx.adam_ema(
+            ar["p"], ar["g"], ar["m"], ar["v"], ar["e"], ar["p16"], 1e-4, 0.9, 0.999, 1e-8, 1.0, 0.999, None, 0))
     res = {k: [] for k in cases}
     for _ in range(a.rounds):
         for k, (fl, fn) in cases.items():
