@@ -26,10 +26,14 @@ issued on the ordering stream right behind its all-reduce, so the update of the 
 buckets (FC head, top layers) streams while the lower layers' BPTT and the remaining
 collectives run, and only the last bucket's range is left after backward. Every arena
 element's update is independent and rounded the same way whatever the launch split, so
-the result is bitwise the whole-arena update. A bucket's range is issued only once the
-main stream has passed the point where the NEXT bucket became ready (or finish()): by then
-the backward op that produced the bucket's last gradient has enqueued everything that
-reads those weights (dgrad / dx GEMMs), so an update never races a pending read.
+the result is bitwise the whole-arena update. A bucket's range is issued right behind its
+own collective, ordered after everything the main stream has enqueued when the bucket
+becomes ready. That is safe because every fused op enqueues its weight-reading work (the
+recurrence, dx / dgrad GEMMs, the W^T shadow copies) on the main stream BEFORE it reports a
+gradient of those weights, so when the last member of a bucket reports, every reader of the
+bucket's weights is already ahead of the recorded point (ops/rnn.py FusedBiLayer._backward,
+ops/frontend.py FusedHead._backward). (Round 3 issued a range only when the NEXT bucket
+became ready, which held each update ~1 ms behind its all-reduce: profiles/r3_dp_buckets.md.)
 """
 from __future__ import annotations
 
@@ -139,7 +143,9 @@ class GradBucketer:
 
     def _flush_updates(self) -> None:
         """Issue the pending buckets' optimizer ranges behind their collectives (ordering
-        stream), after the main stream's work enqueued so far (see module docstring)."""
+        stream), after the main stream's work enqueued so far (see module docstring). The
+        wait is an event the main stream records now: waiting on the stream object itself is
+        the same marker, taken at this point of the main stream's queue."""
         if not self._opt_pending:
             return
         os_ = self._order_stream
@@ -165,8 +171,6 @@ class GradBucketer:
         if self._launched[b]:
             return
         self._launched[b] = True
-        if self._opt is not None:
-            self._flush_updates()                # earlier buckets: their readers are enqueued
         s, e, idx = self.buckets[b]
         g = self.arena.grad[s:e]
         os_ = self._order_stream
@@ -174,6 +178,7 @@ class GradBucketer:
             self._works.append((b, self._collective(b, g)))
             if self._opt is not None:
                 self._opt_pending.append(b)
+                self._flush_updates()
             return
         # the collective (ProcessGroupNCCL waits on the CURRENT stream at issue time) is
         # issued from the ordering stream, which waits on each member's producer event:
@@ -188,6 +193,7 @@ class GradBucketer:
             self._works.append((b, self._collective(b, g)))
         if self._opt is not None:
             self._opt_pending.append(b)
+            self._flush_updates()                # this bucket's readers are enqueued already
 
     def _collective(self, b: int, g: torch.Tensor):
         if self.compress:
