@@ -973,6 +973,11 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
             const i32x8 u2b = __builtin_shufflevector(ul_s[2 * k + 1][wave][lane], z4, 0, 1, 2, 3, 4, 5, 6, 7);
             a0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2a, b1, a0, 0, 0, 0, saw, 0, sbw);
             a1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2b, b1, a1, 0, 0, 0, saw, 0, sbw);
+            // the VALU conversion below reads the scaled MFMA's accumulators: hipcc (ROCm 7.2)
+            // pads only 12 wait states after v_mfma_scale_f32_16x16x128_f8f6f4, too few here (the
+            // publish then stored partly-updated sums: tools/probe_mfma_layout.hip and the
+            // emulation test). The operand-tied s_nop keeps 8 more between them.
+            asm volatile("s_nop 7" : "+v"(a0), "+v"(a1));
             if (prow && wave + BMW8 * k < NPR) {
               const i32x4 v = {(int)bf16x2_tagged(a0[0], a0[1], tagmask), (int)bf16x2_tagged(a0[2], a0[3], tagmask),
                                (int)bf16x2_tagged(a1[0], a1[1], tagmask), (int)bf16x2_tagged(a1[2], a1[3], tagmask)};
