@@ -451,7 +451,9 @@ def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan):
 # config 5's fp8 mode: the BPTT too runs on the fp8 geometry (csrc/rnn_fp8.hip rnnf8_bwd_kernel:
 # e4m3 U^T and dg operands, one XCD per group) where the fp8 forward ran; False keeps the bf16
 # reduce-scatter BPTT on the saved states (tests compare the two)
-_FP8_BPTT = os.environ.get("DS2_FP8_BPTT", "1") == "1"
+# (tools/bench_rnn_fp8.py, H = 1280, N = 32: 4.72 vs 5.32 us/step; config 5 fp8 19.58 vs 19.69-19.79
+# ms/step, same box)
+_FP8_BPTT = True
 
 
 def fp8_bptt_ok(plan: RnnPlan, N: int) -> bool:
