@@ -174,9 +174,14 @@ long long ds2_conv2_wgrad_part_floats(int grid);
 long long ds2_conv1_wgrad_part_floats(int grid);
 int ds2_conv1_fwd_grid(int N, int T1);
 int ds2_conv2_fwd(const void* x, const void* w, const float* bias, void* y, float* part, int grid, int N, int T1,
-                  int F1, int T2, int F2, hipStream_t st);
+                  int F1, int T2, int F2, long long* trace, hipStream_t st);
+struct DS2Conv2DgradBn {  // csrc/conv_frontend.hip: conv1's BN-backward sums in the dgrad epilogue
+  const void* y1;
+  const float *mean, *invstd, *gamma, *beta;
+  float* part;
+};
 int ds2_conv2_dgrad(const void* dy, const void* w, void* dx, int grid, int N, int T1, int F1, int T2, int F2,
-                    hipStream_t st);
+                    const DS2Conv2DgradBn* bn, long long* trace, hipStream_t st);
 int ds2_conv2_wgrad(const void* dy, const void* x, float* part, int grid, float* dw, int N, int T1, int F1, int T2,
                     int F2, hipStream_t st);
 int ds2_conv1_fwd(const void* x, const void* w, const float* bias, void* y, float* part, int N, int T, int F0,
@@ -189,7 +194,7 @@ int ds2_bn_cl_apply(const void* y, const float* mean, const float* invstd, const
                     void* out, int N, int T, int F, int tmaj, hipStream_t st);
 int ds2_bn_cl_bwd(const void* dz, const void* y, const float* mean, const float* invstd, const float* gamma,
                   const float* beta, float* part, int nb, float* dgamma, float* dbeta, void* dy, int N, int T, int F,
-                  int tmaj, hipStream_t st);
+                  int tmaj, int part_ready, hipStream_t st);
 int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev, int M, int N, int K,
              int lda, int ldb, int ldc, int Ml, int Nl, int Kl, int a_col, int b_col, int epi, float alpha, int batch,
              long long sA, long long sB, long long sC, int cfg, hipStream_t st);
@@ -704,8 +709,16 @@ void conv1_fwd(at::Tensor x, at::Tensor w, OptT bias, at::Tensor y, at::Tensor p
 }
 int64_t conv1_fwd_grid(int64_t N, int64_t T1) { return ds2_conv1_fwd_grid((int)N, (int)T1); }
 
+// per-tile phase stamps of workgroups 0..7 (optional int64 [8 * 16 * 5], tools/conv_timeline.py)
+long long* trace_ptr(const OptT& trace) {
+  if (!trace) return nullptr;
+  TORCH_CHECK(trace->is_cuda() && trace->scalar_type() == at::kLong && trace->numel() >= 8 * 16 * 5 &&
+                  trace->is_contiguous(), "trace must be a contiguous cuda int64 tensor of >= 640 elements");
+  return reinterpret_cast<long long*>(trace->data_ptr<int64_t>());
+}
+
 // x [N,T1,F1,32], w [32,32,10,5] -> y [N,T2,F2,32], part [grid, 64]
-void conv2_fwd(at::Tensor x, at::Tensor w, OptT bias, at::Tensor y, at::Tensor part, int64_t grid) {
+void conv2_fwd(at::Tensor x, at::Tensor w, OptT bias, at::Tensor y, at::Tensor part, int64_t grid, OptT trace) {
   need_bf16(x, "x"); need_bf16(w, "w"); need_bf16(y, "y");
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(3) == 32 && y.size(3) == 32 && w.numel() == 32 * 32 * 50,
               "conv2_fwd shapes");
@@ -713,17 +726,33 @@ void conv2_fwd(at::Tensor x, at::Tensor w, OptT bias, at::Tensor y, at::Tensor p
   need_f32(part, "part", grid * 64);
   check(ds2_conv2_fwd(x.data_ptr(), w.data_ptr(), ptr_or_null<float>(bias, "bias"), y.data_ptr(),
                       part.data_ptr<float>(), (int)grid, (int)x.size(0), (int)x.size(1), (int)x.size(2),
-                      (int)y.size(1), (int)y.size(2), cur_stream()), "conv2_fwd");
+                      (int)y.size(1), (int)y.size(2), trace_ptr(trace), cur_stream()), "conv2_fwd");
 }
 
 // dy [N,T2,F2,32], w [32,32,10,5] -> dx [N,T1,F1,32]
-void conv2_dgrad(at::Tensor dy, at::Tensor w, at::Tensor dx, int64_t grid) {
+// bn (optional, all or none): y1 = conv1's output (dx's shape), conv1's BN mean / invstd / gamma
+// / beta, and part [grid * 64] fp32 that receives per-workgroup BN-backward sums over dx
+void conv2_dgrad(at::Tensor dy, at::Tensor w, at::Tensor dx, int64_t grid, OptT y1, OptT mean, OptT invstd,
+                 OptT gamma, OptT beta, OptT part, OptT trace) {
   need_bf16(dy, "dy"); need_bf16(w, "w"); need_bf16(dx, "dx");
   TORCH_CHECK(dy.dim() == 4 && dx.dim() == 4 && dy.size(3) == 32 && dx.size(3) == 32 && w.numel() == 32 * 32 * 50,
               "conv2_dgrad shapes");
   TORCH_CHECK(grid > 0, "grid");
+  DS2Conv2DgradBn bn{};
+  const bool with_bn = y1.has_value();
+  if (with_bn) {
+    TORCH_CHECK(mean && invstd && gamma && beta && part, "conv2_dgrad: the BN arguments come all or none");
+    need_bf16(*y1, "y1");
+    TORCH_CHECK(y1->sizes() == dx.sizes(), "y1 must have dx's shape");
+    need_f32(*mean, "mean", 32); need_f32(*invstd, "invstd", 32); need_f32(*gamma, "gamma", 32);
+    need_f32(*beta, "beta", 32); need_f32(*part, "part", grid * 64);
+    bn = DS2Conv2DgradBn{y1->data_ptr(), mean->data_ptr<float>(), invstd->data_ptr<float>(),
+                         gamma->data_ptr<float>(), beta->data_ptr<float>(), part->data_ptr<float>()};
+  }
   check(ds2_conv2_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), (int)grid, (int)dx.size(0), (int)dx.size(1),
-                        (int)dx.size(2), (int)dy.size(1), (int)dy.size(2), cur_stream()), "conv2_dgrad");
+                        (int)dx.size(2), (int)dy.size(1), (int)dy.size(2), with_bn ? &bn : nullptr,
+                        trace_ptr(trace), cur_stream()),
+        "conv2_dgrad");
 }
 
 // dy [N,T2,F2,32], x [N,T1,F1,32] -> dw (fp32, 32*32*10*5), part scratch
@@ -770,8 +799,10 @@ void bn_cl_apply(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor ga
                         tmaj ? 1 : 0, cur_stream()), "bn_cl_apply");
 }
 
+// part_ready: part already holds nb partial sums (conv2_dgrad's bn epilogue), skip the reduce pass
 void bn_cl_bwd(at::Tensor dz, at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor beta,
-               at::Tensor part, int64_t nb, at::Tensor dgamma, at::Tensor dbeta, at::Tensor dy, bool tmaj) {
+               at::Tensor part, int64_t nb, at::Tensor dgamma, at::Tensor dbeta, at::Tensor dy, bool tmaj,
+               bool part_ready) {
   need_bf16(dz, "dz"); need_bf16(y, "y"); need_bf16(dy, "dy");
   TORCH_CHECK(y.dim() == 4 && y.size(3) == 32 && dz.numel() == y.numel() && dy.numel() == y.numel(),
               "bn_cl_bwd shapes");
@@ -781,7 +812,7 @@ void bn_cl_bwd(at::Tensor dz, at::Tensor y, at::Tensor mean, at::Tensor invstd, 
   check(ds2_bn_cl_bwd(dz.data_ptr(), y.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                       gamma.data_ptr<float>(), beta.data_ptr<float>(), part.data_ptr<float>(), (int)nb,
                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dy.data_ptr(), (int)y.size(0),
-                      (int)y.size(1), (int)y.size(2), tmaj ? 1 : 0, cur_stream()), "bn_cl_bwd");
+                      (int)y.size(1), (int)y.size(2), tmaj ? 1 : 0, part_ready ? 1 : 0, cur_stream()), "bn_cl_bwd");
 }
 
 // --------------------------------------------------------------------------- greedy CTC decode
@@ -1230,15 +1261,21 @@ PYBIND11_MODULE(_C, m) {
         py::arg("blank"), py::arg("score") = py::none());
   m.def("conv1_fwd", &conv1_fwd);
   m.def("conv1_fwd_grid", &conv1_fwd_grid);
-  m.def("conv2_fwd", &conv2_fwd);
-  m.def("conv2_dgrad", &conv2_dgrad);
+  m.def("conv2_fwd", &conv2_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("part"),
+        py::arg("grid"), py::arg("trace") = py::none());
+  m.def("conv2_dgrad", &conv2_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("grid"),
+        py::arg("y1") = py::none(), py::arg("mean") = py::none(), py::arg("invstd") = py::none(),
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("part") = py::none(),
+        py::arg("trace") = py::none());
   m.def("conv2_wgrad", &conv2_wgrad);
   m.def("conv1_wgrad", &conv1_wgrad);
   m.def("conv2_wgrad_part_floats", &conv2_wgrad_part_floats);
   m.def("conv1_wgrad_part_floats", &conv1_wgrad_part_floats);
   m.def("bn_cl_finalize", &bn_cl_finalize);
   m.def("bn_cl_apply", &bn_cl_apply);
-  m.def("bn_cl_bwd", &bn_cl_bwd);
+  m.def("bn_cl_bwd", &bn_cl_bwd, py::arg("dz"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"),
+        py::arg("beta"), py::arg("part"), py::arg("nb"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dy"),
+        py::arg("tmaj"), py::arg("part_ready") = false);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
         py::arg("K"), py::arg("a_col"), py::arg("b_col"), py::arg("epi"), py::arg("alpha"), py::arg("cfg"),
         py::arg("alpha_dev") = py::none(), py::arg("Ml") = 0, py::arg("Nl") = 0, py::arg("Kl") = 0);

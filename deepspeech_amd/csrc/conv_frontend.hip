@@ -41,6 +41,13 @@
 
 using namespace ds2;
 
+// optional BatchNorm-backward sums fused into the conv2 data-gradient epilogue (bindings.cpp)
+struct DS2Conv2DgradBn {
+  const void* y1;                                  // conv1 output [N][T1][F1][32] bf16
+  const float *mean, *invstd, *gamma, *beta;       // conv1 BN batch statistics and affine
+  float* part;                                     // [grid][32][2]
+};
+
 namespace {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -101,6 +108,17 @@ __device__ __forceinline__ void write_stats(float s, float q, float* sh /* [wave
 // =====================================================================================
 // conv2 forward
 // =====================================================================================
+// A tile is one output row t2 (all f2, all 32 co); it reads input rows 2 t2 .. 2 t2 + 9. Wave w
+// multiplies k-steps [25 w, 25 w + 25) of the 100 (kt, kf, ci-half), its 25 weight fragments in
+// VGPRs for the whole launch; the 4 partial sums meet in wave 0 through a 2-level LDS tree and
+// wave 0 adds the bias, stores bf16 and accumulates the BN batch statistics of the stored
+// values. The input rows land by global_load_lds in channel-chunk planes: plane (row j, 16-B
+// channel chunk c) holds C2F_PL positions at a 16-B stride, so the 16 lanes of a ds_read_b128
+// lane group read 16 consecutive 16-B slots (conflict-free) and a fragment address is a lane
+// base + a compile-time offset. Positions past F1 read the next plane (or the tail pad): they
+// only reach outputs f2 >= F2, which are not stored. Two ~74-KB workgroups per CU, so one's
+// reduction and staging overlap the other's MFMA loop; tiles go to XCDs in contiguous ranges
+// so the 8 input rows neighbouring tiles share are L2 hits.
 struct Conv2Fwd {
   const bf16_t* x;    // z1 [N][T1][F1][32]
   const bf16_t* w;    // [32][32][10][5]
@@ -108,255 +126,381 @@ struct Conv2Fwd {
   bf16_t* y;          // [N][T2][F2][32]
   float* part;        // [grid][32][2]
   int N, T1, F1, T2, F2;
+  long long* trace;   // optional [8 workgroups][16 tiles][C2_TRACE] s_memrealtime stamps (diagnostics)
 };
 constexpr int C2_KT = 10, C2_KF = 5;
-constexpr int C2_WAVES = 8;                     // 2 waves per SIMD: one's LDS reads hide under the other's MFMAs
-constexpr int C2_KPW = 13;                      // k-steps per wave (100 = 4 x 13 + 4 x 12 for fwd)
-constexpr int PR = 80;                          // LDS bytes per position row: 64 data + 16 pad
-// With 80-B rows the 16 lanes of every ds_read_b128 lane group (consecutive positions, one
-// 16-B chunk) hit 16 distinct 16-B bank slots: conflict-free with affine addresses, so each
-// A-fragment read is one lane-base VGPR + a wave-uniform offset.
-constexpr int C2_STG = 7;                       // 16-B staging loads per thread (512 threads)
+// per-tile phase stamps of workgroups 0..7 (wave 0, lane 0): tile start, rows landed, MFMA loop
+// done, partial sums reduced, outputs stored (tools/conv_timeline.py)
+constexpr int C2_TRACE = 5;
+__device__ __forceinline__ void c2_stamp(long long* tr, int it, int k) {
+  if (tr != nullptr && blockIdx.x < 8 && threadIdx.x == 0 && it < 16)
+    tr[((int)blockIdx.x * 16 + it) * C2_TRACE + k] = __builtin_amdgcn_s_memrealtime();
+}
+constexpr int PR = 80;                           // LDS bytes per position row (64 data + 16 pad; dgrad)
+constexpr int C2F_KPW = 25;                      // k-steps per wave
+constexpr int C2F_PL = 80;                       // positions per plane (F1 <= 80)
+constexpr int C2F_BUF = (C2_KT * 4 * C2F_PL + 20) * 16;   // 40 planes + the last plane's overrun
+constexpr int C2F_RED = 2 * 12 * 64 * 16;        // two waves' partial sums (f32x4 per lane)
+constexpr int C2F_SMEM = C2F_BUF + C2F_RED;
+static_assert(C2F_SMEM >= 32 * 16 * C2_KT * C2_KF * 2, "one ci half of the weights is staged through LDS");
 
-// copy `nch` 16-B chunks of a contiguous run of 64-B position rows into 80-B LDS rows
-struct Stager {
-  i32x4 v[C2_STG];
-  __device__ __forceinline__ void load(const unsigned char* src, int nch) {
-#pragma unroll
-    for (int k = 0; k < C2_STG; ++k) {
-      const int p = min((int)threadIdx.x + 512 * k, nch - 1);     // clamp, never predicate a load
-      v[k] = *(const i32x4*)(src + (size_t)p * 16);
-    }
-  }
-  __device__ __forceinline__ void store(unsigned char* dst, int nch) const {
-#pragma unroll
-    for (int k = 0; k < C2_STG; ++k) {
-      const int p = (int)threadIdx.x + 512 * k;
-      if (p < nch) *(i32x4*)(dst + (p >> 2) * PR + (p & 3) * 16) = v[k];
-    }
-  }
-};
+template <int S0>
+__device__ __forceinline__ void conv2_fwd_body(const Conv2Fwd& a);
 
-// wave w's k-step range within a K of `total` steps split over `nw` waves (first waves +1)
-__device__ __forceinline__ void kspan(int w, int nw, int total, int& s0, int& n) {
-  const int q = total / nw, r = total % nw;
-  n = q + (w < r ? 1 : 0);
-  s0 = w * q + min(w, r);
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv2_fwd_kernel(Conv2Fwd a) {
+  DS2_DCHECK(a.T2 == (a.T1 - C2_KT) / 2 + 1 && a.F2 == a.F1 - 4 && a.F1 <= C2F_PL && a.F2 <= 32 * MT);
+  switch (uni(threadIdx.x >> 6)) {                   // k-step s = kt * 10 + kf * 2 + ci-half
+    case 0: conv2_fwd_body<0>(a); break;
+    case 1: conv2_fwd_body<C2F_KPW>(a); break;
+    case 2: conv2_fwd_body<2 * C2F_KPW>(a); break;
+    default: conv2_fwd_body<3 * C2F_KPW>(a); break;
+  }
 }
 
-__global__ __launch_bounds__(512) void conv2_fwd_kernel(Conv2Fwd a) {
+// S0: the wave's first k-step (compile-time, so every LDS offset of the loop is an immediate)
+template <int S0>
+__device__ __forceinline__ void conv2_fwd_body(const Conv2Fwd& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  DS2_DCHECK(a.T2 == (a.T1 - C2_KT) / 2 + 1 && a.F2 == a.F1 - 4 && a.F1 <= 80);
-  const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
+  const int tid = threadIdx.x, lane = tid & 63, w = S0 / C2F_KPW;
   const int hi = lane >> 5, col = lane & 31;
-  unsigned char* const buf = smem;                                   // [10*F1][80 B]
-  f32x4* red = (f32x4*)(smem + C2_KT * a.F1 * PR);                   // [8 waves][12][64] f32x4
-  int s0, nks;
-  kspan(w, C2_WAVES, C2_KT * C2_KF * 2, s0, nks);
+  unsigned char* const buf = smem;
+  f32x4* red = (f32x4*)(smem + C2F_BUF);                             // [2 slots][12][64]
 
-  bf16x8 bfr[C2_KPW];
+  // weights -> VGPR fragments through LDS, one ci half at a time, as the image [16 ci][32 co][50]
+  // (dword copies; consecutive co 100 B apart, so the 16-bit gathers are conflict-free)
+  bf16x8 bfr[C2F_KPW];
+  {
+    const unsigned short* wl = (const unsigned short*)smem;
+    const unsigned* wsrc = (const unsigned*)a.w;                     // [32 co][32 ci][25 dwords]
+    for (int hh = 0; hh < 2; ++hh) {
+      for (int d = tid; d < 32 * 16 * 25; d += 256) {
+        const int co = d / 400, rem = d - co * 400, ci = rem / 25, e = rem - ci * 25;
+        ((unsigned*)smem)[(ci * 32 + co) * 25 + e] = wsrc[(co * 32 + 16 * hh + ci) * 25 + e];
+      }
+      __syncthreads();
 #pragma unroll
-  for (int i = 0; i < C2_KPW; ++i) {
-    const int s = s0 + min(i, nks - 1);
-    const int kt = s / 10, kf = (s % 10) >> 1, hh = s & 1;
-    bf16x8 v;
+      for (int i = 0; i < C2F_KPW; ++i) {
+        const int s = S0 + i;
+        if ((s & 1) != hh) continue;
+        const int kt = s / 10, kf = (s % 10) >> 1;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ci = 16 * hh + 8 * hi + j;
-      v[j] = (short)a.w[((col * CC + ci) * C2_KT + kt) * C2_KF + kf];
+        for (int j = 0; j < 8; ++j) bfr[i][j] = (short)wl[((8 * hi + j) * 32 + col) * 50 + kt * C2_KF + kf];
+      }
+      __syncthreads();
     }
-    bfr[i] = v;
   }
-  unsigned lb[MT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m) lb[m] = (unsigned)(min(32 * m + col, a.F2 - 1) * PR + hi * 16);
-  const float bco = a.bias ? a.bias[col] : 0.f;
-
+  const float bco = (w == 0 && a.bias) ? a.bias[col] : 0.f;
   const int ntiles = a.N * a.T2;
-  const int nch = C2_KT * a.F1 * 4;
-  auto src_of = [&](int t) {
+  const int F1 = a.F1, nr = (F1 + 63) >> 6;               // wave rounds per plane
+  const int X = (gridDim.x % 8 == 0) ? 8 : 1;
+  const int per = (int)gridDim.x / X, xi = (int)blockIdx.x % X, wi = (int)blockIdx.x / X;
+  const int t_lo = (int)((long long)ntiles * xi / X), t_hi = (int)((long long)ntiles * (xi + 1) / X);
+
+  // stage input rows 2 t2 .. 2 t2 + 9: plane p = (row j = p >> 2, chunk c = p & 3), positions
+  // 64 r + lane of round r (a wave round never crosses a plane, so its LDS run is lane-linear)
+  auto issue = [&](int t) {
     const int n = t / a.T2, t2 = t - n * a.T2;
-    return (const unsigned char*)(a.x + ((size_t)n * a.T1 + 2 * t2) * a.F1 * CC);
+    const bf16_t* base = a.x + ((size_t)n * a.T1 + 2 * t2) * F1 * CC;
+    for (int k = w; k < C2_KT * 4 * nr; k += 4) {
+      const int p = k / nr, pos = 64 * (k - p * nr) + lane;
+      if (pos < F1) glds16(base + ((size_t)(p >> 2) * F1 + pos) * CC + (p & 3) * 8, buf + (p * C2F_PL + pos - lane) * 16);
+    }
   };
-  Stager stg;
+  const unsigned char* const lbase = buf + col * 16 + hi * C2F_PL * 16;
+  auto ldA = [&](int i, bf16x8 (&dst)[MT]) {
+    const int s = S0 + i;
+    const int kt = s / 10, kf = (s % 10) >> 1;
+    const int off = ((kt * 4 + 2 * (s & 1)) * C2F_PL + kf) * 16;       // constant
+#pragma unroll
+    for (int m = 0; m < MT; ++m) dst[m] = *(const bf16x8*)(lbase + off + m * 32 * 16);
+  };
+
   float ssum = 0.f, ssq = 0.f;
-  if ((int)blockIdx.x < ntiles) {
-    stg.load(src_of(blockIdx.x), nch);
-    stg.store(buf, nch);
-    if ((int)(blockIdx.x + gridDim.x) < ntiles) stg.load(src_of(blockIdx.x + gridDim.x), nch);
-  }
-  lds_barrier();
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  int it = 0;
+  if (t_lo + wi < t_hi) issue(t_lo + wi);
+  for (int tile = t_lo + wi; tile < t_hi; tile += per, ++it) {
+    const int n = tile / a.T2, t2 = tile - n * a.T2;
+    c2_stamp(a.trace, it, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                   // this tile's rows are in buf
+    c2_stamp(a.trace, it, 1);
     f32x16 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x16){};
     bf16x8 af[2][MT];
-    auto ldA = [&](int i, bf16x8 (&dst)[MT]) {
-      const int s = s0 + i;
-      const unsigned off = (unsigned)(((s / 10) * a.F1 + ((s % 10) >> 1)) * PR + (s & 1) * 32);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) dst[m] = *(const bf16x8*)(buf + lb[m] + off);
-    };
     ldA(0, af[0]);
 #pragma unroll
-    for (int i = 0; i < C2_KPW; ++i) {
-      if (i < nks) {                               // wave-uniform (only the last step varies)
-        if (i + 1 < nks) ldA(i + 1, af[(i + 1) & 1]);
+    for (int i = 0; i < C2F_KPW; ++i) {
+      if (i + 1 < C2F_KPW) ldA(i + 1, af[(i + 1) & 1]);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m] = mfma32(af[i & 1][m], bfr[i], acc[m]);
-      }
+      for (int m = 0; m < MT; ++m) acc[m] = mfma32(af[i & 1][m], bfr[i], acc[m]);
     }
-    lds_barrier();                                   // every wave is done reading buf
+    auto put = [&](int slot) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4)
-        red[(w * 12 + m * 4 + r4) * 64 + lane] =
-            (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
-    const int next = tile + gridDim.x;
-    if (next < ntiles) stg.store(buf, nch);
-    lds_barrier();
-    if (next + (int)gridDim.x < ntiles) stg.load(src_of(next + gridDim.x), nch);
-    const int n = tile / a.T2, t2 = tile - n * a.T2;
-    bf16_t* yrow = a.y + ((size_t)n * a.T2 + t2) * a.F2 * CC;
-    for (int item = tid; item < 12 * 64; item += 512) {   // (e = m*4 + r4, lane) items; channel = tid & 31
-      const int e = item >> 6, l2 = item & 63, m = e >> 2, r4 = e & 3;
-      f32x4 v = red[e * 64 + l2];
+        for (int r4 = 0; r4 < 4; ++r4)
+          red[(slot * 12 + m * 4 + r4) * 64 + lane] =
+              (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
+    };
+    auto add = [&](int slot) {
 #pragma unroll
-      for (int wv = 1; wv < C2_WAVES; ++wv) v += red[(wv * 12 + e) * 64 + l2];
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f2 = 32 * m + j + 8 * r4 + 4 * (l2 >> 5);
-        if (f2 < a.F2) {
-          const bf16_t b = f2bf(v[j] + bco);
-          yrow[f2 * CC + col] = b;
-          const float vb = bf2f(b);
-          ssum += vb;
-          ssq += vb * vb;
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const f32x4 v = red[(slot * 12 + m * 4 + r4) * 64 + lane];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[m][4 * r4 + e] += v[e];
         }
-      }
+    };
+    // tree: w2 -> slot 0, w3 -> slot 1; w0 += 0, w1 += 1; then w1 -> slot 0; w0 += 0
+    c2_stamp(a.trace, it, 2);
+    lds_barrier();                                     // buf free; the previous tile's red reads done
+    if (w >= 2) put(w - 2);
+    lds_barrier();
+    if (w < 2) add(w);
+    lds_barrier();
+    if (w == 1) put(0);
+    lds_barrier();
+    if (w == 0) add(0);
+    c2_stamp(a.trace, it, 3);
+    if (tile + per < t_hi) issue(tile + per);          // after every LDS read of this tile
+    if (w == 0) {
+      // the row goes through reduction slot 0 (wave 0 read it last) as bf16 [F2][32], then out
+      // in 16-B chunks (48 two-byte stores per lane otherwise)
+      unsigned short* stg = (unsigned short*)red;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int f2 = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (m < 2 || f2 < a.F2) {
+            const bf16_t b = f2bf(acc[m][r] + bco);
+            stg[f2 * CC + col] = b;
+            const float vb = bf2f(b);
+            ssum += vb;
+            ssq += vb * vb;
+          }
+        }
+      i32x4* dst = (i32x4*)(a.y + ((size_t)n * a.T2 + t2) * a.F2 * CC);
+      for (int q = lane; q < a.F2 * 4; q += 64) dst[q] = ((const i32x4*)stg)[q];
     }
-    // red is rewritten only after the next tile's MFMA loop and its barrier
+    c2_stamp(a.trace, it, 4);
   }
-  lds_barrier();
-  write_stats(ssum, ssq, (float*)red, C2_WAVES, a.part);
+  __syncthreads();
+  write_stats(ssum, ssq, (float*)red, 4, a.part);
 }
 
 // =====================================================================================
 // conv2 data gradient: dx[n][t1][f1][ci] = sum dy[n][(t1-kt)/2][f1-kf][co] w[co][ci][kt][kf]
 // =====================================================================================
+// A tile is the output row pair (2u, 2u+1); parity p = t1 & 1 reads dy rows u-ai (ai = 0..4)
+// with kt = 2 ai + p. Wave w computes parity w & 1 over half (w >> 1) of that parity's 50
+// (ai, kf, co-half) k-steps, its 25 weight fragments in VGPRs for the whole launch; waves 2, 3
+// hand their partial sums to waves 0, 1 through LDS (one round), which store. Two ~64-KB
+// workgroups per CU, so one's reduction and staging overlap the other's MFMA loop. Each dy row
+// lands by global_load_lds in an LDS slot of C2D_PR zero-padded 80-B position rows (positions
+// -4 .. 95; the pads are zeroed once and never written), so an A fragment address is one lane
+// base + a wave-uniform offset and out-of-range positions read zeros. Tiles go to XCDs in
+// contiguous ranges, so the 4 rows neighbouring tiles share are L2 hits. With bn set, waves 0 / 1
+// also read conv1's output at the positions they store and accumulate conv1's BatchNorm-backward
+// sums (each lane owns one channel), so that reduction pass never re-reads dx.
 struct Conv2Dgrad {
   const bf16_t* dy;   // [N][T2][F2][32]
   const bf16_t* w;    // [32][32][10][5]
   bf16_t* dx;         // [N][T1][F1][32]
   int N, T1, F1, T2, F2;
+  // optional: conv1's BatchNorm-backward sums over the stored dx (see bn_cl_bwd_reduce_kernel):
+  // y1 = conv1's output [N][T1][F1][32], part [grid][32][2] = (sum dz*m, sum dz*m*xhat)
+  const bf16_t* y1;
+  const float *mean, *invstd, *gamma, *beta;
+  float* part;
+  long long* trace;   // optional phase stamps, as Conv2Fwd::trace
 };
-constexpr int C2D_STG = 3;                       // 16-B staging loads per thread (5 rows x F2 <= 76)
+constexpr int C2D_KPW = 25;                      // k-steps per wave (one parity's 50 in halves)
+constexpr int C2D_PR = 4 + 32 * MT;              // LDS position rows per dy row (positions -4 .. 95)
+constexpr int C2D_BUF = 5 * C2D_PR * PR;         // 40000 B
+constexpr int C2D_HALF = 12 * 64 * 16;           // one wave's partial sums (f32x4 per lane)
+constexpr int C2D_SMEM = C2D_BUF + 2 * C2D_HALF;
+static_assert(C2D_SMEM >= 16 * CC * C2_KT * C2_KF * 2, "one co half of the weights is staged through LDS");
 
-__global__ __launch_bounds__(512) void conv2_dgrad_kernel(Conv2Dgrad a) {
+template <int S0>
+__device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a, int par);
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv2_dgrad_kernel(Conv2Dgrad a) {
+  DS2_DCHECK(a.F2 <= 32 * MT - 4 && a.F1 == a.F2 + 4 && a.F1 > 64);
+  const int w = uni(threadIdx.x >> 6), par = w & 1;
+  if (w >> 1) conv2_dgrad_body<C2D_KPW>(a, par);     // k-step s = ai * 10 + kf * 2 + co-half
+  else conv2_dgrad_body<0>(a, par);
+}
+
+// S0: the wave's first k-step (compile-time, so every LDS offset of the loop is an immediate)
+template <int S0>
+__device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a, const int par) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
   const int hi = lane >> 5, col = lane & 31;
-  const int par = w >> 2, wq = w & 3;            // waves 0-3: even output row, 4-7: odd
-  unsigned char* const buf = smem;                                   // [5*F2][80 B]
-  f32x4* red = (f32x4*)(smem + 5 * a.F2 * PR);                       // [8 waves][12][64]
-  int s0, nks;
-  kspan(wq, 4, C2_KT * C2_KF, s0, nks);          // 50 k-steps per parity
+  unsigned char* const buf = smem;
+  f32x4* red = (f32x4*)(smem + C2D_BUF);                             // [2 slots][12][64]
 
-  bf16x8 bfr[C2_KPW];
+  // weights -> VGPR fragments through LDS, one co half (51.2 KB of OIHW) at a time: coalesced
+  // 16-B global loads, then 16-bit LDS gathers
+  bf16x8 bfr[C2D_KPW];
+  {
+    const unsigned short* wl = (const unsigned short*)smem;
+    for (int hh = 0; hh < 2; ++hh) {
+      const i32x4* src = (const i32x4*)(a.w + (size_t)hh * 16 * CC * C2_KT * C2_KF);
+      for (int o = tid; o < 16 * CC * C2_KT * C2_KF / 8; o += 256) ((i32x4*)smem)[o] = src[o];
+      __syncthreads();
 #pragma unroll
-  for (int i = 0; i < C2_KPW; ++i) {
-    const int s = s0 + min(i, nks - 1);
-    const int ai = s / 10, kf = (s % 10) >> 1, hh = s & 1;
-    const int kt = 2 * ai + par;
-    bf16x8 v;
+      for (int i = 0; i < C2D_KPW; ++i) {
+        const int s = S0 + i;
+        if ((s & 1) != hh) continue;
+        const int ai = s / 10, kf = (s % 10) >> 1;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int co = 16 * hh + 8 * hi + j;
-      v[j] = (short)a.w[((co * CC + col) * C2_KT + kt) * C2_KF + kf];
+        for (int j = 0; j < 8; ++j)
+          bfr[i][j] = (short)wl[(((8 * hi + j) * CC + col) * C2_KT + 2 * ai + par) * C2_KF + kf];
+      }
+      __syncthreads();
     }
-    bfr[i] = v;
   }
+  for (int o = tid * 16; o < C2D_BUF; o += 256 * 16) *(i32x4*)(buf + o) = (i32x4){0, 0, 0, 0};
+
   const int U = (a.T1 + 1) >> 1;
   const int ntiles = a.N * U;
-  const int nch = 5 * a.F2 * 4;
-  const size_t rowEl = (size_t)a.F2 * CC;
-  // rows u-4 .. u of dy (row slot j = row - (u-4)); rows outside [0, T2) are never read
-  i32x4 stg[C2D_STG];
-  auto load = [&](int t) {
+  const int F2 = a.F2, nq = 5 * F2, nr = (nq + 63) >> 6;   // 16-B chunks per dy row, wave rounds
+  // tiles: X contiguous ranges (one per XCD when the grid is a multiple of 8; workgroup b runs
+  // on XCD b % 8), dealt round-robin to that XCD's workgroups
+  const int X = (gridDim.x % 8 == 0) ? 8 : 1;
+  const int per = (int)gridDim.x / X, xi = (int)blockIdx.x % X, wi = (int)blockIdx.x / X;
+  const int t_lo = (int)((long long)ntiles * xi / X), t_hi = (int)((long long)ntiles * (xi + 1) / X);
+
+  // stage dy rows u-4..u of tile t into the 5 slots (rows outside [0, T2) are clamped: their
+  // k-steps are skipped); a lane's 16-B chunk q of a slot is position q / 5, chunk q % 5, and
+  // chunk 4 (the row's pad column, never read) repeats chunk 3
+  auto issue = [&](int t) {
     const int n = t / U, u = t - n * U;
-    const bf16_t* base = a.dy + (size_t)n * a.T2 * rowEl;
-#pragma unroll
-    for (int k = 0; k < C2D_STG; ++k) {
-      const int p = min(tid + 512 * k, nch - 1);
-      const int row = min(max(u - 4 + (p >> 2) / a.F2, 0), a.T2 - 1);
-      const int pos = (p >> 2) % a.F2;
-      stg[k] = *(const i32x4*)(base + row * rowEl + pos * CC + (p & 3) * 8);
+    const bf16_t* base = a.dy + (size_t)n * a.T2 * F2 * CC;
+    for (int k = w; k < 5 * nr; k += 4) {
+      const int j = k / nr, r = k - j * nr;
+      const int q = 64 * r + lane;
+      if (q < nq) {
+        const int pos = (q * 52429) >> 18, c = min(q - 5 * pos, 3);    // q / 5 for q < 2^14
+        const int row = min(max(u - 4 + j, 0), a.T2 - 1);
+        glds16(base + ((size_t)row * F2 + pos) * CC + c * 8, buf + (j * C2D_PR + 4) * PR + 1024 * r);
+      }
     }
   };
-  auto store = [&]() {
+  const unsigned char* const lbase = buf + col * PR + hi * 16;
+  const bool bn = a.mean != nullptr;
+  const float bmu = bn ? a.mean[col] : 0.f, bis = bn ? a.invstd[col] : 0.f;
+  const float bg = bn ? a.gamma[col] : 0.f, bbt = bn ? a.beta[col] : 0.f;
+  float bs = 0.f, bq = 0.f;
+  auto ldA = [&](int i, bf16x8 (&dst)[MT]) {
+    const int s = S0 + i;
+    const int ai = s / 10, kf = (s % 10) >> 1;
+    const int off = ((4 - ai) * C2D_PR + 4 - kf) * PR + (s & 1) * 32;     // >= 0, constant
 #pragma unroll
-    for (int k = 0; k < C2D_STG; ++k) {
-      const int p = tid + 512 * k;
-      if (p < nch) *(i32x4*)(buf + (p >> 2) * PR + (p & 3) * 16) = stg[k];
-    }
+    for (int m = 0; m < MT; ++m) dst[m] = *(const bf16x8*)(lbase + off + m * 32 * PR);
   };
-  if ((int)blockIdx.x < ntiles) {
-    load(blockIdx.x);
-    store();
-    if ((int)(blockIdx.x + gridDim.x) < ntiles) load(blockIdx.x + gridDim.x);
-  }
-  lds_barrier();
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+
+  __syncthreads();                                     // pads zeroed before any staging lands
+  int it = 0;
+  if (t_lo + wi < t_hi) issue(t_lo + wi);
+  for (int tile = t_lo + wi; tile < t_hi; tile += per, ++it) {
     const int n = tile / U, u = tile - n * U;
+    c2_stamp(a.trace, it, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                   // this tile's rows are in buf
+    c2_stamp(a.trace, it, 1);
     f32x16 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = (f32x16){};
+    bf16x8 af[2][MT];
+    ldA(0, af[0]);
 #pragma unroll
-    for (int i = 0; i < C2_KPW; ++i) {
-      const int s = s0 + i;
-      const int ai = s / 10, kf = (s % 10) >> 1;
-      const int t2 = u - ai;
-      if (i < nks && t2 >= 0 && t2 < a.T2) {     // wave-uniform
-        const int slotb = (4 - ai) * a.F2;
-        bf16x8 av[MT];
+    for (int i = 0; i < C2D_KPW; ++i) {
+      if (i + 1 < C2D_KPW) ldA(i + 1, af[(i + 1) & 1]);
+      const int t2 = u - (S0 + i) / 10;
+      if (t2 >= 0 && t2 < a.T2) {                      // wave-uniform
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const int f2 = 32 * m + col - kf;
-          const unsigned R = (unsigned)(slotb + min(max(f2, 0), a.F2 - 1));
-          av[m] = *(const bf16x8*)(buf + R * PR + (s & 1) * 32 + hi * 16);
-          if (!(f2 >= 0 && f2 < a.F2)) av[m] = (bf16x8){};
-        }
-#pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m] = mfma32(av[m], bfr[i], acc[m]);
+        for (int m = 0; m < MT; ++m) acc[m] = mfma32(af[i & 1][m], bfr[i], acc[m]);
       }
     }
+    c2_stamp(a.trace, it, 2);
+    lds_barrier();                                     // buf free; the previous tile's red reads done
+    if (w >= 2) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+          red[(par * 12 + m * 4 + r4) * 64 + lane] =
+              (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
+    }
     lds_barrier();
+    if (w < 2) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4)
-        red[(w * 12 + m * 4 + r4) * 64 + lane] =
-            (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
-    const int next = tile + gridDim.x;
-    if (next < ntiles) store();
-    lds_barrier();
-    if (next + (int)gridDim.x < ntiles) load(next + gridDim.x);
-    for (int item = tid; item < 2 * 12 * 64; item += 512) {
-      const int opar = item / 768, e = (item >> 6) % 12, l2 = item & 63, m = e >> 2, r4 = e & 3;
-      const int t1 = 2 * u + opar;
-      f32x4 v = red[((4 * opar) * 12 + e) * 64 + l2];
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const f32x4 x = red[(par * 12 + m * 4 + r4) * 64 + lane];
 #pragma unroll
-      for (int wv = 1; wv < 4; ++wv) v += red[((4 * opar + wv) * 12 + e) * 64 + l2];
-      if (t1 < a.T1) {
-        bf16_t* xrow = a.dx + ((size_t)n * a.T1 + t1) * a.F1 * CC;
+          for (int e = 0; e < 4; ++e) acc[m][4 * r4 + e] += x[e];
+        }
+    }
+    c2_stamp(a.trace, it, 3);
+    const int t1 = 2 * u + par;
+    if (w < 2 && t1 < a.T1) {                          // wave-uniform
+      // the row goes through this wave's own reduction slot (read above) as bf16 [F1][32], then
+      // out in 16-B chunks: the epilogue issues no global store before its conv1 loads (a load
+      // behind a store to a possibly aliasing pointer would wait for the store)
+      const size_t rowoff = ((size_t)n * a.T1 + t1) * a.F1 * CC;
+      unsigned short* stg = (unsigned short*)(red + par * 12 * 64);
+      // one per-lane base; rows 0..63 at compile-time offsets (global-load immediates), the last
+      // m-tile's rows clamped to the row (they are neither stored nor counted past F1)
+      const unsigned short* yb = (const unsigned short*)a.y1 + rowoff + 4 * hi * CC + col;
+      const int lastoff = (a.F1 - 1 - 4 * hi) * CC;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int f1 = 32 * m + j + 8 * r4 + 4 * (l2 >> 5);
-          if (f1 < a.F1) xrow[f1 * CC + (l2 & 31)] = f2bf(v[j]);
+      for (int m = 0; m < MT; ++m) {
+        unsigned short yv[16];
+        if (bn) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int fo = (32 * m + (r & 3) + 8 * (r >> 2)) * CC;
+            yv[r] = m < 2 ? yb[fo] : yb[min(fo, lastoff)];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int f1 = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (m < 2 || f1 < a.F1) {
+            const bf16_t d = f2bf(acc[m][r]);
+            stg[f1 * CC + col] = d;
+            if (bn) {
+              const float xh = (bf2f(yv[r]) - bmu) * bis;
+              const float zz = xh * bg + bbt;
+              const float dd = (zz > 0.f && zz < CLIP) ? bf2f(d) : 0.f;
+              bs += dd;
+              bq += dd * xh;
+            }
+          }
         }
       }
+      i32x4* dst = (i32x4*)(a.dx + rowoff);
+      for (int q = lane; q < a.F1 * 4; q += 64) dst[q] = ((const i32x4*)stg)[q];
     }
+    if (tile + per < t_hi) issue(tile + per);          // after every LDS read of this tile
+    c2_stamp(a.trace, it, 4);
+  }
+  if (bn) {
+    // per-workgroup sums: lanes l, l ^ 32 and waves 0, 1 share a channel
+    bs += __shfl_xor(bs, 32, 64);
+    bq += __shfl_xor(bq, 32, 64);
+    float* sh = (float*)red;
+    __syncthreads();
+    if (w < 2 && lane < 32) { sh[(w * 32 + lane) * 2] = bs; sh[(w * 32 + lane) * 2 + 1] = bq; }
+    __syncthreads();
+    if (tid < 64) a.part[(size_t)blockIdx.x * 64 + tid] = sh[tid] + sh[64 + tid];
   }
 }
 
@@ -774,11 +918,36 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_reduce_kernel(const bf16_t* __r
     mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; g[j] = gamma[c0 + j]; bt[j] = beta[c0 + j];
     s[j] = 0.f; q[j] = 0.f;
   }
-  const int stride = F + 1;
-  for (int row = blockIdx.x; row < N * T; row += gridDim.x) {
-    const int n = row / T, t = row - n * T;
-    const bf16_t* yr = y + (size_t)row * F * CC;
-    if (tmaj) {
+  auto acc8 = [&](const bf16x8 v, const bf16x8 d) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (bf2f((bf16_t)v[j]) - mu[j]) * is[j];
+      const float zz = xh * g[j] + bt[j];
+      const float dd = (zz > 0.f && zz < CLIP) ? bf2f((bf16_t)d[j]) : 0.f;
+      s[j] += dd;
+      q[j] += dd * xh;
+    }
+  };
+  if (!tmaj) {
+    // channels-last: one flat stream of 16-B chunks whose channel octet is (chunk & 3) = (tid & 3)
+    // (the grid stride is a multiple of 4), 4 chunks of each operand in flight per thread
+    const long long total = (long long)N * T * F * 4, step = (long long)gridDim.x * 256;
+    const bf16x8* y8 = (const bf16x8*)y;
+    const bf16x8* d8 = (const bf16x8*)dz;
+    long long e = (long long)blockIdx.x * 256 + tid;
+    for (; e + 3 * step < total; e += 4 * step) {
+      bf16x8 v[4], d[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[k] = y8[e + k * step]; d[k] = d8[e + k * step]; }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc8(v[k], d[k]);
+    }
+    for (; e < total; e += step) acc8(y8[e], d8[e]);
+  } else {
+    const int stride = F + 1;
+    for (int row = blockIdx.x; row < N * T; row += gridDim.x) {
+      const int n = row / T, t = row - n * T;
+      const bf16_t* yr = y + (size_t)row * F * CC;
       __syncthreads();
       const bf16_t* dr = dz + ((size_t)t * N + n) * CC * F;
       for (int e = tid; e < CC * F; e += 256) {
@@ -786,26 +955,14 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_reduce_kernel(const bf16_t* __r
         tr[c * stride + f] = dr[e];
       }
       __syncthreads();
-    }
-    for (int ch = tid; ch < F * 4; ch += 256) {
-      const int f = ch >> 2;
-      const bf16x8 v = *(const bf16x8*)(yr + ch * 8);
-      bf16x8 d;
-      if (tmaj) {
+      for (int ch = tid; ch < F * 4; ch += 256) {
+        const int f = ch >> 2;
+        bf16x8 d;
 #pragma unroll
         for (int j = 0; j < 8; ++j) d[j] = (short)tr[(c0 + j) * stride + f];
         // the transposed (channels-last) copy, so the apply pass reads it coalesced
         if (dz_cl != nullptr) *(bf16x8*)(dz_cl + (size_t)row * F * CC + ch * 8) = d;
-      } else {
-        d = *(const bf16x8*)(dz + (size_t)row * F * CC + ch * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (bf2f((bf16_t)v[j]) - mu[j]) * is[j];
-        const float zz = xh * g[j] + bt[j];
-        const float dd = (zz > 0.f && zz < CLIP) ? bf2f((bf16_t)d[j]) : 0.f;
-        s[j] += dd;
-        q[j] += dd * xh;
+        acc8(*(const bf16x8*)(yr + ch * 8), d);
       }
     }
   }
@@ -873,8 +1030,7 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_apply_kernel(const bf16_t* dz,
                                                               const float* __restrict__ beta,
                                                               const float* __restrict__ dbeta,
                                                               const float* __restrict__ dgamma,
-                                                              bf16_t* dy, int N, int T, int F, int tmaj) {
-  __shared__ bf16_t tr[32 * 97];
+                                                              bf16_t* dy, int N, int T, int F) {
   const int tid = threadIdx.x, c0 = (tid & 3) * 8;
   const float M = (float)N * T * F;
   float mu[8], is[8], g[8], bt[8], mdb[8], mdg[8];
@@ -883,40 +1039,31 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_apply_kernel(const bf16_t* dz,
     mu[j] = mean[c0 + j]; is[j] = invstd[c0 + j]; g[j] = gamma[c0 + j]; bt[j] = beta[c0 + j];
     mdb[j] = dbeta[c0 + j] / M; mdg[j] = dgamma[c0 + j] / M;
   }
-  const int stride = F + 1;
-  for (int row = blockIdx.x; row < N * T; row += gridDim.x) {
-    const int n = row / T, t = row - n * T;
-    const bf16_t* yr = y + (size_t)row * F * CC;
-    if (tmaj) {
-      __syncthreads();
-      const bf16_t* dr = dz + ((size_t)t * N + n) * CC * F;
-      for (int e = tid; e < CC * F; e += 256) {
-        const int c = e / F, f = e - c * F;
-        tr[c * stride + f] = dr[e];
-      }
-      __syncthreads();
-    }
-    for (int ch = tid; ch < F * 4; ch += 256) {
-      const int f = ch >> 2;
-      const bf16x8 v = *(const bf16x8*)(yr + ch * 8);
-      bf16x8 d;
-      if (tmaj) {
+  auto one = [&](const bf16x8 v, const bf16x8 d) {
+    bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = (short)tr[(c0 + j) * stride + f];
-      } else {
-        d = *(const bf16x8*)(dz + (size_t)row * F * CC + ch * 8);
-      }
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (bf2f((bf16_t)v[j]) - mu[j]) * is[j];
-        const float zz = xh * g[j] + bt[j];
-        const float dd = (zz > 0.f && zz < CLIP) ? bf2f((bf16_t)d[j]) : 0.f;
-        o[j] = (short)f2bf(g[j] * is[j] * (dd - mdb[j] - xh * mdg[j]));
-      }
-      *(bf16x8*)(dy + (size_t)row * F * CC + ch * 8) = o;
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (bf2f((bf16_t)v[j]) - mu[j]) * is[j];
+      const float zz = xh * g[j] + bt[j];
+      const float dd = (zz > 0.f && zz < CLIP) ? bf2f((bf16_t)d[j]) : 0.f;
+      o[j] = (short)f2bf(g[j] * is[j] * (dd - mdb[j] - xh * mdg[j]));
     }
+    return o;
+  };
+  // one flat stream of 16-B chunks, channel octet (chunk & 3) = (tid & 3); 4 in flight
+  const long long total = (long long)N * T * F * 4, step = (long long)gridDim.x * 256;
+  const bf16x8* y8 = (const bf16x8*)y;
+  const bf16x8* d8 = (const bf16x8*)dz;
+  bf16x8* o8 = (bf16x8*)dy;
+  long long e = (long long)blockIdx.x * 256 + tid;
+  for (; e + 3 * step < total; e += 4 * step) {
+    bf16x8 v[4], d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = y8[e + k * step]; d[k] = d8[e + k * step]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o8[e + k * step] = one(v[k], d[k]);
   }
+  for (; e < total; e += step) o8[e] = one(y8[e], d8[e]);
 }
 
 template <typename K>
@@ -935,30 +1082,33 @@ int shape_ok(int T1, int F1, int T2, int F2) {
 
 extern "C" {
 
-size_t ds2_conv2_fwd_smem(int F1) { return (size_t)C2_KT * F1 * PR + C2_WAVES * 12 * 64 * 16; }
-size_t ds2_conv2_dgrad_smem(int F2) { return (size_t)5 * F2 * PR + C2_WAVES * 12 * 64 * 16; }
+size_t ds2_conv2_fwd_smem(int) { return (size_t)C2F_SMEM; }
+size_t ds2_conv2_dgrad_smem(int) { return (size_t)C2D_SMEM; }
 size_t ds2_conv2_wgrad_smem(int F1) { return (size_t)2 * (80 * 64 + (9 * F1 + 84) * 64); }
 long long ds2_conv2_wgrad_part_floats(int grid) { return (long long)grid * C2W_PAIRS * 1024; }
 long long ds2_conv1_wgrad_part_floats(int grid) { return (long long)grid * 5 * 1024; }
 int ds2_conv1_fwd_grid(int N, int T1) { return N * ((T1 + C1_ROWS - 1) / C1_ROWS); }
 
 int ds2_conv2_fwd(const void* x, const void* w, const float* bias, void* y, float* part, int grid, int N, int T1,
-                  int F1, int T2, int F2, hipStream_t st) {
+                  int F1, int T2, int F2, long long* trace, hipStream_t st) {
   if (int e = shape_ok(T1, F1, T2, F2)) return e;
   const size_t smem = ds2_conv2_fwd_smem(F1);
   DS2_HIP_CHECK((hipError_t)set_smem(conv2_fwd_kernel, smem));
-  Conv2Fwd a{(const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y, part, N, T1, F1, T2, F2};
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(grid), dim3(512), smem, st, a);
+  Conv2Fwd a{(const bf16_t*)x, (const bf16_t*)w, bias, (bf16_t*)y, part, N, T1, F1, T2, F2, trace};
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(grid), dim3(256), smem, st, a);
   return (int)hipGetLastError();
 }
 
 int ds2_conv2_dgrad(const void* dy, const void* w, void* dx, int grid, int N, int T1, int F1, int T2, int F2,
-                    hipStream_t st) {
+                    const DS2Conv2DgradBn* bn, long long* trace, hipStream_t st) {
   if (int e = shape_ok(T1, F1, T2, F2)) return e;
+  if (F1 <= 64) return -42;                              // rows 0..63 are stored unchecked
   const size_t smem = ds2_conv2_dgrad_smem(F2);
   DS2_HIP_CHECK((hipError_t)set_smem(conv2_dgrad_kernel, smem));
-  Conv2Dgrad a{(const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, N, T1, F1, T2, F2};
-  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(grid), dim3(512), smem, st, a);
+  Conv2Dgrad a{(const bf16_t*)dy, (const bf16_t*)w, (bf16_t*)dx, N, T1, F1, T2, F2,
+               bn ? (const bf16_t*)bn->y1 : nullptr, bn ? bn->mean : nullptr, bn ? bn->invstd : nullptr,
+               bn ? bn->gamma : nullptr, bn ? bn->beta : nullptr, bn ? bn->part : nullptr, trace};
+  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(grid), dim3(256), smem, st, a);
   return (int)hipGetLastError();
 }
 
@@ -1018,18 +1168,20 @@ int ds2_bn_cl_apply(const void* y, const float* mean, const float* invstd, const
 
 int ds2_bn_cl_bwd(const void* dz, const void* y, const float* mean, const float* invstd, const float* gamma,
                   const float* beta, float* part, int nb, float* dgamma, float* dbeta, void* dy, int N, int T, int F,
-                  int tmaj, hipStream_t st) {
+                  int tmaj, int part_ready, hipStream_t st) {
   if (F > 96) return -45;
+  if (part_ready && tmaj) return -46;                    // the time-major path transposes in the reduce
   // time-major dz: the reduce pass (which transposes it through LDS anyway) leaves a
   // channels-last copy in dy, and the apply pass then works in place on dy, coalesced
   // (the apply's own per-row LDS transpose ran at ~1/9 of the bandwidth roofline)
-  hipLaunchKernelGGL(bn_cl_bwd_reduce_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)dz, (const bf16_t*)y, mean,
-                     invstd, gamma, beta, part, N, T, F, tmaj, tmaj ? (bf16_t*)dy : (bf16_t*)nullptr);
+  if (!part_ready)   // else part holds nb partial sums already (conv2_dgrad_kernel's bn epilogue)
+    hipLaunchKernelGGL(bn_cl_bwd_reduce_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)dz, (const bf16_t*)y,
+                       mean, invstd, gamma, beta, part, N, T, F, tmaj, tmaj ? (bf16_t*)dy : (bf16_t*)nullptr);
   hipLaunchKernelGGL(bn_cl_bwd_finalize_kernel, dim3(CC), dim3(256), 0, st, part, nb, dbeta, dgamma);
   const int rows = N * T;
   hipLaunchKernelGGL(bn_cl_bwd_apply_kernel, dim3(rows < 4096 ? rows : 4096), dim3(256), 0, st,
                      tmaj ? (const bf16_t*)dy : (const bf16_t*)dz, (const bf16_t*)y, mean, invstd, gamma, beta,
-                     dbeta, dgamma, (bf16_t*)dy, N, T, F, 0);
+                     dbeta, dgamma, (bf16_t*)dy, N, T, F);
   return (int)hipGetLastError();
 }
 

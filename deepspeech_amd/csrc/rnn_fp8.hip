@@ -671,10 +671,11 @@ __global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
 //    (gate 2, the second 64 of its 128 zero), one v_mfma_scale_f32_16x16x128_f8f6f4 each. U^T
 //    is e4m3 with the forward's per-tensor power-of-two scale (E8M0 A scale); k-step 0's
 //    fragments live in VGPRs, k-step 1's real half (16 B per lane) in LDS.
-//  * dg (the gate-gradient operand) is requantised to e4m3 every step with ONE power-of-two
-//    scale per batch row (E8M0 B scale, the same in all four lanes that hold a row, so the
-//    product does not depend on how the hardware pairs lanes with K blocks); the dU GEMM and
-//    dgx outputs stay bf16 and exact.
+//  * dg (the gate-gradient operand) is requantised to e4m3 every step with one power-of-two
+//    scale per (batch row, 32-unit group) over the three gates: the scale byte of B lane (n, b)
+//    covers the contiguous K block [32b, 32b + 32) (not the 32 bytes lane group b holds), which
+//    in the k-step layout is one gate's 32 units, so block b of both k-steps takes group b & 1's
+//    scale; the dU GEMM and dgx outputs stay bf16.
 // ------------------------------------------------------------------------------------
 constexpr int BMW8 = 7;                  // worker waves (gather + MFMA); 0..3 also run the cell
 constexpr int BEW8 = 4;
@@ -700,13 +701,22 @@ struct XF8B {
   long long timeout;
 };
 
-// E8M0 exponent byte e + 127 of the smallest power of two 2^e with amax / 2^e <= 448
-__device__ __forceinline__ int e8m0_for(float amax) {
-  if (!(amax > 0.f)) return 127;
-  int e = (int)ceilf(__log2f(amax / 448.f));
-  if (ldexpf(448.f, e) < amax) ++e;
-  if (ldexpf(448.f, e - 1) >= amax) --e;
-  return min(254, max(1, e + 127));
+// max over the 16 lanes of a DPP row (row_ror 8, 4, 2, 1): every lane ends with the row's max
+__device__ __forceinline__ float row16_max(float v) {
+#define DS2_ROR(N) v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + (N), 0xf, 0xf, false)))
+  DS2_ROR(8); DS2_ROR(4); DS2_ROR(2); DS2_ROR(1);
+#undef DS2_ROR
+  return v;
+}
+
+// E8M0 exponent byte of the smallest power of two 2^e with amax / 2^e <= 448 (e4m3 max), from the
+// bits of a non-negative finite amax: 448 = 1.75 * 2^8, so amax = (1 + f) 2^(E-127)
+// needs e = E - 135, or E - 134 when its mantissa exceeds 0.75 (integer ops only: scalar when
+// amax is wave-uniform)
+__device__ __forceinline__ int e8m0_bits(unsigned amax_bits) {
+  if (amax_bits == 0u) return 127;
+  const int eb = (int)(amax_bits >> 23) - 8 + ((amax_bits & 0x7fffffu) > 0x600000u ? 1 : 0);
+  return min(254, max(1, eb));
 }
 
 template <int MTU, int GPT>
@@ -718,7 +728,7 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
   static_assert(GPT % 2 == 0, "two producers per gather load");
   __shared__ float red_s[BMW8][ROWS][UPW8 + 1];
   __shared__ __attribute__((aligned(16))) unsigned char dq_s[2][ROWS][128];   // e4m3 dg by k-step
-  __shared__ int dsc_s[ROWS];                                               // E8M0 per row (4 copies)
+  __shared__ int dsc_s[ROWS][4];                 // E8M0 (4 copies) per (row, K block of either k-step)
   __shared__ float dyr_s[2][ROWS8][UPW8];
   __shared__ float hpr_s[2][ROWS8][UPW8];
   __shared__ float4 gr_s[2][ROWS8][UPW8];
@@ -736,7 +746,7 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
   const int bg = grp % a.BG, dir = grp / a.BG;
   const int r0 = bg * R, u0 = mem * UPW8;
   if (tid < ROWS8) len_s[tid] = (tid < R && r0 + tid < N) ? a.lens[r0 + tid] : 0;
-  if (tid < ROWS) dsc_s[tid] = 0x7f7f7f7f;
+  if (tid < ROWS * 4) (&dsc_s[0][0])[tid] = 0x7f7f7f7f;
   for (int i = tid; i < 2 * ROWS * 128 / 4; i += BTH8) reinterpret_cast<int*>(&dq_s[0][0][0])[i] = 0;
   if (wave == 0) {
     const int m = census8(a.census, grp, mem, P, a.timeout, a.err);
@@ -902,7 +912,7 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
       lds_barrier();                                                        // #1
       if (s_abort) break;
       // (E) cell backward (waves 0..3, row wave + 4 i, unit = lane): dgh / dgx staging and the
-      // e4m3 dg operand with one power-of-two scale per row (wave-wide amax of the row)
+      // e4m3 dg operand with one power-of-two scale per (row, gate, 32-unit K block)
       if (wave < BEW8) {
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
@@ -929,13 +939,23 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
 #pragma unroll
               for (int g = 0; g < G3; ++g) { ghv[g] = 0.f; gxs[g] = 0.f; }
             }
-            const float am = wave_max(fmaxf(fmaxf(fabsf(ghv[0]), fabsf(ghv[1])), fabsf(ghv[2])));
-            const int eb = e8m0_for(am);
-            const float inv = __uint_as_float((unsigned)(254 - eb) << 23);   // 2^-(eb - 127)
-            dq_s[0][row][c] = (unsigned char)f2e4m3(ghv[0] * inv);
-            dq_s[0][row][64 + c] = (unsigned char)f2e4m3(ghv[1] * inv);
-            dq_s[1][row][c] = (unsigned char)f2e4m3(ghv[2] * inv);
-            if (lane == 0) dsc_s[row] = eb | (eb << 8) | (eb << 16) | (eb << 24);
+            // K block b of k-step 0 is gate b >> 1's units 32 (b & 1) + [0, 32), of k-step 1 gate
+            // 2's (b < 2; blocks 2, 3 are zero): one scale per (row, 32-unit group) over the three
+            // gates serves block b of both k-steps as the group b & 1's. Its amax: DPP max inside
+            // each 16-lane row, then the 4 row maxima through SGPRs (non-negative floats order
+            // as unsigned ints).
+            const unsigned m = __float_as_uint(row16_max(fmaxf(fmaxf(fabsf(ghv[0]), fabsf(ghv[1])), fabsf(ghv[2]))));
+            const int e01 = e8m0_bits(max(__builtin_amdgcn_readlane(m, 0), __builtin_amdgcn_readlane(m, 16)));
+            const int e23 = e8m0_bits(max(__builtin_amdgcn_readlane(m, 32), __builtin_amdgcn_readlane(m, 48)));
+            const int ebl = c < 32 ? e01 : e23;
+            const float invl = __uint_as_float((unsigned)(254 - ebl) << 23);    // 2^-(eb - 127)
+            dq_s[0][row][c] = (unsigned char)f2e4m3(ghv[0] * invl);
+            dq_s[0][row][64 + c] = (unsigned char)f2e4m3(ghv[1] * invl);
+            dq_s[1][row][c] = (unsigned char)f2e4m3(ghv[2] * invl);
+            if (c == 0) {
+              const int w01 = e01 * 0x01010101, w23 = e23 * 0x01010101;
+              dsc_s[row][0] = w01; dsc_s[row][1] = w23; dsc_s[row][2] = w01; dsc_s[row][3] = w23;
+            }
 #pragma unroll
             for (int g = 0; g < G3; ++g) {
               oh_s[s & 1][row][g][c] = f2bf(ghv[g]);
@@ -958,7 +978,7 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
         const i32x4 z4 = {0, 0, 0, 0};
         const i32x8 b1 = __builtin_shufflevector(*reinterpret_cast<const i32x4*>(dr + ROWS * 128), z4, 0, 1, 2, 3, 4,
                                                  5, 6, 7);
-        const int sbw = dsc_s[lane & 15];
+        const int sbw0 = dsc_s[lane & 15][lane >> 4], sbw1 = sbw0;
         constexpr int NPW = MTU / 2;
         unsigned offp[NPW];
 #pragma unroll
@@ -967,12 +987,12 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
 #pragma unroll
           for (int k = 0; k < NPW; ++k) {
             const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-            f32x4 a0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ua[2 * k], b0, zero, 0, 0, 0, saw, 0, sbw);
-            f32x4 a1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ua[2 * k + 1], b0, zero, 0, 0, 0, saw, 0, sbw);
+            f32x4 a0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ua[2 * k], b0, zero, 0, 0, 0, saw, 0, sbw0);
+            f32x4 a1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ua[2 * k + 1], b0, zero, 0, 0, 0, saw, 0, sbw0);
             const i32x8 u2a = __builtin_shufflevector(ul_s[2 * k][wave][lane], z4, 0, 1, 2, 3, 4, 5, 6, 7);
             const i32x8 u2b = __builtin_shufflevector(ul_s[2 * k + 1][wave][lane], z4, 0, 1, 2, 3, 4, 5, 6, 7);
-            a0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2a, b1, a0, 0, 0, 0, saw, 0, sbw);
-            a1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2b, b1, a1, 0, 0, 0, saw, 0, sbw);
+            a0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2a, b1, a0, 0, 0, 0, saw, 0, sbw1);
+            a1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(u2b, b1, a1, 0, 0, 0, saw, 0, sbw1);
             // the VALU conversion below reads the scaled MFMA's accumulators: hipcc (ROCm 7.2)
             // pads only 12 wait states after v_mfma_scale_f32_16x16x128_f8f6f4, too few here (the
             // publish then stored partly-updated sums: tools/probe_mfma_layout.hip and the

@@ -145,8 +145,7 @@ class StreamingRecognizer:
         x = m.frontend(feats)
         lens = torch.full((self.B,), x.shape[0], dtype=torch.int32, device=self.dev)
         for i, layer in enumerate(m.rnn):
-            x, h = self._layer(layer, x, lens, self._h[i])
-            self._h[i].copy_(h)                                # state carried in place
+            x, _ = self._layer(layer, x, lens, self._h[i], out=self._h[i])   # state carried in place
         lp = torch.log_softmax(m.head(x).float(), -1)
         return lp, lp.argmax(-1)
 
@@ -174,15 +173,21 @@ class StreamingRecognizer:
         graph.replay()
         return out[0].clone(), out[1].clone()
 
-    def _layer(self, layer, x, lens, h0):
+    def _layer(self, layer, x, lens, h0, out=None):
+        """One uni-directional layer from state h0 [B, H]; returns (y, h_last [B, H]), h_last
+        written into `out` when given (it may be h0 itself: the kernel has read h0 by then)."""
         m = self.model
         if m.engine == "hip":
             from .ops import rnn as RNN
-            y, h = RNN.recurrent_layer_infer(layer, x, lens, None if h0 is None else h0.unsqueeze(0))
+            y, h = RNN.recurrent_layer_infer(layer, x, lens, None if h0 is None else h0.unsqueeze(0),
+                                             h_out=None if out is None else out.unsqueeze(0))
             return y, h[0]
         gx = layer.input_projection_ref(x, layer.fw, lens)
         bh = layer.fw.b_h.to(x.dtype) if layer.fw.b_h is not None else None
         y, h = R.recurrent_scan(layer.cell, gx, layer.fw.U.to(x.dtype), bh, lens, h0)
+        if out is not None:
+            out.copy_(h)
+            h = out
         return y, h
 
     @torch.no_grad()

@@ -245,7 +245,7 @@ class FrontendCL(torch.autograd.Function):
         w2_16 = _bf16_of(w2)
         with TR.phase(TR.conv(2)):
             y2 = torch.empty(N, T2, F2, 32, **bf)
-            grid = max(1, min(N * T2, ncu))
+            grid = max(1, min(N * T2, 2 * ncu))                 # two workgroups per CU
             part2 = torch.empty(grid * 64, **f32)
             C_.conv2_fwd(z1, w2_16, b2.detach().float().contiguous(), y2, part2, grid)
         with TR.phase(TR.bn(2)):
@@ -275,8 +275,7 @@ class FrontendCL(torch.autograd.Function):
         T1 = y1.shape[1]
         grid = max(1, min(N * T2, ctx.ncu))
         nb2 = max(1, min(N * T2, 1024))
-        nb1 = max(1, min(N * T1, 1024))
-        part = torch.empty(max(nb1, nb2) * 64, **f32)
+        part = torch.empty(max(2 * ctx.ncu, nb2) * 64, **f32)
         with TR.phase(TR.bn(2, True)):
             (dg2, ipg2), (db2, ipb2) = _grad_buffer(g2), _grad_buffer(be2)
             dy2 = torch.empty_like(y2)
@@ -287,12 +286,14 @@ class FrontendCL(torch.autograd.Function):
             C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
             gw2 = _deliver(w2, dw2, ip2)
             dz1 = torch.empty_like(y1)
-            C_.conv2_dgrad(dy2, w2_16, dz1, max(1, min(N * ((T1 + 1) // 2), ctx.ncu)))
+            # two workgroups per CU; the epilogue also leaves conv1's BN-backward sums in part
+            dgrid = max(1, min(N * ((T1 + 1) // 2), 2 * ctx.ncu))
+            C_.conv2_dgrad(dy2, w2_16, dz1, dgrid, y1, mean1, inv1, g1f, be1f, part)
         gg2, gb2, gbias2 = _deliver(g2, dg2, ipg2), _deliver(be2, db2, ipb2), _zero_grad_of(b2)
         with TR.phase(TR.bn(1, True)):
             (dg1, ipg1), (db1, ipb1) = _grad_buffer(g1), _grad_buffer(be1)
             dy1 = torch.empty_like(y1)
-            C_.bn_cl_bwd(dz1, y1, mean1, inv1, g1f, be1f, part, nb1, dg1, db1, dy1, False)
+            C_.bn_cl_bwd(dz1, y1, mean1, inv1, g1f, be1f, part, dgrid, dg1, db1, dy1, False, part_ready=True)
         with TR.phase(TR.conv(1, True)):
             g1grid = max(1, min(N * ((T1 + 3) // 4), ctx.ncu))
             wpart1 = torch.empty(int(C_.conv1_wgrad_part_floats(g1grid)), **f32)

@@ -1236,10 +1236,12 @@ def input_projection_hip(layer, x: torch.Tensor, lens: torch.Tensor) -> torch.Te
 
 
 @torch.no_grad()
-def recurrent_layer_infer(layer, x: torch.Tensor, lens: torch.Tensor, h0: Optional[torch.Tensor] = None):
+def recurrent_layer_infer(layer, x: torch.Tensor, lens: torch.Tensor, h0: Optional[torch.Tensor] = None,
+                          h_out: Optional[torch.Tensor] = None):
     """Inference-only layer with state carry: returns (y [T, N, H], h_last [ndir, N, H] fp32).
     h_last holds each row's state after its last valid step (the kernels freeze the state
-    past an utterance's length), which is what a streaming caller carries to the next chunk."""
+    past an utterance's length), which is what a streaming caller carries to the next chunk;
+    with h_out ([ndir, N, H] fp32) it is written there (one copy) and h_out is returned."""
     ndir = 2 if layer.bw is not None else 1
     T, N, _ = x.shape
     plan = plan_for(N, layer.hidden, layer.cell, ndir, x.device)
@@ -1267,6 +1269,9 @@ def recurrent_layer_infer(layer, x: torch.Tensor, lens: torch.Tensor, h0: Option
         gx = _linear(x.to(torch.bfloat16).reshape(T * N, -1), W16, b16, alpha).view(T, N, -1)
     lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
     y, (hx, hs, gates) = _run_fwd(gx.contiguous(), lens, U, bh, plan, h0=h0)
+    if h_out is not None:
+        h_out.copy_(hs[:, T, :N])
+        return y, h_out
     return y, hs[:, T, :N].clone()
 
 

@@ -83,10 +83,28 @@ def test_conv2_dgrad_wgrad(cuda, N, T):
     wr = w.float().clone().requires_grad_(True)
     out = F.conv2d(xr, wr, None, stride=(2, 1))
     out.backward(dy.float().permute(0, 3, 1, 2))
-    for grid in (5, 64):
+    # conv1's BN state for the fused BN-backward sums of the dgrad epilogue
+    y1 = (torch.randn(N, T1, F1, 32, device=cuda) * 2).bfloat16()
+    mean, inv = torch.randn(32, device=cuda) * 0.3, torch.rand(32, device=cuda) + 0.5
+    gamma, beta = torch.randn(32, device=cuda), torch.randn(32, device=cuda)
+    for grid in (5, 64, 512):
         dx = torch.full((N, T1, F1, 32), float("nan"), device=cuda).bfloat16()
         C_.conv2_dgrad(dy, w, dx, grid)
         assert _rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2, ("dx", grid)
+        part = torch.full((grid * 64,), float("nan"), device=cuda)
+        dx2 = torch.empty_like(dx)
+        C_.conv2_dgrad(dy, w, dx2, grid, y1, mean, inv, gamma, beta, part)
+        assert torch.equal(dx2, dx)
+        outs = []
+        for ready in (True, False):
+            dg, db = torch.empty(32, device=cuda), torch.empty(32, device=cuda)
+            dyb = torch.empty_like(dx)
+            p2 = part.clone() if ready else torch.empty(1024 * 64, device=cuda)
+            C_.bn_cl_bwd(dx, y1, mean, inv, gamma, beta, p2, grid if ready else 64, dg, db, dyb, False,
+                         part_ready=ready)
+            outs.append((dg, db, dyb))
+        for a_, b_ in zip(outs[0], outs[1]):
+            assert _rel(a_, b_) < 1e-4, ("fused BN sums", grid, _rel(a_, b_))
         part = torch.empty(int(C_.conv2_wgrad_part_floats(grid)), device=cuda)
         dw = torch.full((32, 32, 10, 5), float("nan"), device=cuda)
         C_.conv2_wgrad(dy, x, part, dw, grid)

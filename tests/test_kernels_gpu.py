@@ -491,8 +491,9 @@ def _e4m3_pow2(x, amax):
 
 def _gru_bptt_fp8_emulation(dy, lens, U, hs, gates, H, ndir):
     """fp32 model of csrc/rnn_fp8.hip rnnf8_bwd_kernel on the forward's saved states: U^T in
-    e4m3 with the per-tensor power-of-two scale, the gate gradients of each (row, 64-unit
-    workgroup) requantised to e4m3 with one power-of-two scale every step; dgh / dgx exact."""
+    e4m3 with the per-tensor power-of-two scale, the gate gradients requantised to e4m3 every
+    step with one power-of-two scale per (row, 32-unit group) shared by the three gates; dgh /
+    dgx exact."""
     T, N, _ = dy.shape
     P = H // 64
     dgx = torch.zeros(T, N, ndir * 3 * H, device=dy.device)
@@ -521,8 +522,8 @@ def _gru_bptt_fp8_emulation(dy, lens, U, hs, gates, H, ndir):
             dgh[s] = ghv
             tt = torch.where(act, t, torch.full_like(t, s))
             dgx[tt, ar, d * 3 * H:(d + 1) * 3 * H] = gxs
-            blk = ghv.view(N, 3, P, 64).abs().amax(dim=(1, 3))             # [N, P]
-            am = blk[:, None, :, None].expand(N, 3, P, 64).reshape(N, 3 * H)
+            blk = ghv.abs().view(N, 3, H // 32, 32).amax(dim=(1, 3), keepdim=True)
+            am = blk.expand(N, 3, H // 32, 32).reshape(N, 3 * H)
             dhrec = _e4m3_pow2(ghv, am) @ uq
         dghs.append(dgh)
     return dgx, dghs
