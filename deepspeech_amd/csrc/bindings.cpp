@@ -709,11 +709,11 @@ void conv1_fwd(at::Tensor x, at::Tensor w, OptT bias, at::Tensor y, at::Tensor p
 }
 int64_t conv1_fwd_grid(int64_t N, int64_t T1) { return ds2_conv1_fwd_grid((int)N, (int)T1); }
 
-// per-tile phase stamps of workgroups 0..7 (optional int64 [8 * 16 * 5], tools/conv_timeline.py)
+// per-tile phase stamps of workgroups 0..7 (optional int64 [8 * 16 * 6], tools/conv_timeline.py)
 long long* trace_ptr(const OptT& trace) {
   if (!trace) return nullptr;
-  TORCH_CHECK(trace->is_cuda() && trace->scalar_type() == at::kLong && trace->numel() >= 8 * 16 * 5 &&
-                  trace->is_contiguous(), "trace must be a contiguous cuda int64 tensor of >= 640 elements");
+  TORCH_CHECK(trace->is_cuda() && trace->scalar_type() == at::kLong && trace->numel() >= 8 * 16 * 6 &&
+                  trace->is_contiguous(), "trace must be a contiguous cuda int64 tensor of >= 768 elements");
   return reinterpret_cast<long long*>(trace->data_ptr<int64_t>());
 }
 

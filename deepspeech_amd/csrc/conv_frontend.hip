@@ -130,8 +130,8 @@ struct Conv2Fwd {
 };
 constexpr int C2_KT = 10, C2_KF = 5;
 // per-tile phase stamps of workgroups 0..7 (wave 0, lane 0): tile start, rows landed, MFMA loop
-// done, partial sums reduced, outputs stored (tools/conv_timeline.py)
-constexpr int C2_TRACE = 5;
+// done, partial sums reduced, outputs stored, next tile's rows issued (tools/conv_timeline.py)
+constexpr int C2_TRACE = 6;
 __device__ __forceinline__ void c2_stamp(long long* tr, int it, int k) {
   if (tr != nullptr && blockIdx.x < 8 && threadIdx.x == 0 && it < 16)
     tr[((int)blockIdx.x * 16 + it) * C2_TRACE + k] = __builtin_amdgcn_s_memrealtime();
@@ -140,15 +140,18 @@ constexpr int PR = 80;                           // LDS bytes per position row (
 constexpr int C2F_KPW = 25;                      // k-steps per wave
 constexpr int C2F_PL = 80;                       // positions per plane (F1 <= 80)
 constexpr int C2F_BUF = (C2_KT * 4 * C2F_PL + 20) * 16;   // 40 planes + the last plane's overrun
-constexpr int C2F_RED = 2 * 12 * 64 * 16;        // two waves' partial sums (f32x4 per lane)
-constexpr int C2F_SMEM = C2F_BUF + C2F_RED;
+// after the MFMA loop the row buffer is scratch: 36 partial-sum slots (wave -> owner, m) of
+// 64 f32x4, then the bf16 output row
+constexpr int C2F_STG = 36 * 64 * 16;
+constexpr int C2F_SMEM = C2F_BUF;
+static_assert(C2F_STG + 32 * MT * 64 <= C2F_BUF, "partial sums and the output row fit in the row buffer");
 static_assert(C2F_SMEM >= 32 * 16 * C2_KT * C2_KF * 2, "one ci half of the weights is staged through LDS");
 
 template <int S0>
 __device__ __forceinline__ void conv2_fwd_body(const Conv2Fwd& a);
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv2_fwd_kernel(Conv2Fwd a) {
-  DS2_DCHECK(a.T2 == (a.T1 - C2_KT) / 2 + 1 && a.F2 == a.F1 - 4 && a.F1 <= C2F_PL && a.F2 <= 32 * MT);
+  DS2_DCHECK(a.T2 == (a.T1 - C2_KT) / 2 + 1 && a.F2 == a.F1 - 4 && a.F1 <= C2F_PL && a.F1 > 64);
   switch (uni(threadIdx.x >> 6)) {                   // k-step s = kt * 10 + kf * 2 + ci-half
     case 0: conv2_fwd_body<0>(a); break;
     case 1: conv2_fwd_body<C2F_KPW>(a); break;
@@ -161,10 +164,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 template <int S0>
 __device__ __forceinline__ void conv2_fwd_body(const Conv2Fwd& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, w = S0 / C2F_KPW;
+  constexpr int w = S0 / C2F_KPW;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int hi = lane >> 5, col = lane & 31;
   unsigned char* const buf = smem;
-  f32x4* red = (f32x4*)(smem + C2F_BUF);                             // [2 slots][12][64]
+  f32x4* red = (f32x4*)smem;                                         // [36 slots][64] after the loop
+  unsigned short* stg = (unsigned short*)(smem + C2F_STG);          // [F2][32] bf16 output row
 
   // weights -> VGPR fragments through LDS, one ci half at a time, as the image [16 ci][32 co][50]
   // (dword copies; consecutive co 100 B apart, so the 16-bit gathers are conflict-free)
@@ -189,21 +194,27 @@ __device__ __forceinline__ void conv2_fwd_body(const Conv2Fwd& a) {
       __syncthreads();
     }
   }
-  const float bco = (w == 0 && a.bias) ? a.bias[col] : 0.f;
+  const float bco = a.bias ? a.bias[col] : 0.f;
   const int ntiles = a.N * a.T2;
-  const int F1 = a.F1, nr = (F1 + 63) >> 6;               // wave rounds per plane
+  const int F1 = a.F1;
   const int X = (gridDim.x % 8 == 0) ? 8 : 1;
   const int per = (int)gridDim.x / X, xi = (int)blockIdx.x % X, wi = (int)blockIdx.x / X;
   const int t_lo = (int)((long long)ntiles * xi / X), t_hi = (int)((long long)ntiles * (xi + 1) / X);
 
-  // stage input rows 2 t2 .. 2 t2 + 9: plane p = (row j = p >> 2, chunk c = p & 3), positions
-  // 64 r + lane of round r (a wave round never crosses a plane, so its LDS run is lane-linear)
+  // stage input rows 2 t2 .. 2 t2 + 9: plane p = (row p >> 2, 16-B channel chunk p & 3), round r
+  // = positions 64 r + lane (F1 in (64, 80]: 2 rounds). Wave w issues rounds k = w + 4 i of the
+  // 80, i.e. planes (w >> 1) + 2 i in round w & 1: every offset but the tile base is a constant.
+  constexpr int R = w & 1;
+  const bool on = 64 * R + lane < F1;
   auto issue = [&](int t) {
     const int n = t / a.T2, t2 = t - n * a.T2;
-    const bf16_t* base = a.x + ((size_t)n * a.T1 + 2 * t2) * F1 * CC;
-    for (int k = w; k < C2_KT * 4 * nr; k += 4) {
-      const int p = k / nr, pos = 64 * (k - p * nr) + lane;
-      if (pos < F1) glds16(base + ((size_t)(p >> 2) * F1 + pos) * CC + (p & 3) * 8, buf + (p * C2F_PL + pos - lane) * 16);
+    const bf16_t* base = a.x + ((size_t)n * a.T1 + 2 * t2) * F1 * CC + (64 * R + lane) * CC;
+    if (on) {
+#pragma unroll
+      for (int i = 0; i < 20; ++i) {
+        const int p = (w >> 1) + 2 * i;
+        glds16(base + (size_t)(p >> 2) * F1 * CC + (p & 3) * 8, buf + (p * C2F_PL + 64 * R) * 16);
+      }
     }
   };
   const unsigned char* const lbase = buf + col * 16 + hi * C2F_PL * 16;
@@ -235,57 +246,54 @@ __device__ __forceinline__ void conv2_fwd_body(const Conv2Fwd& a) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = mfma32(af[i & 1][m], bfr[i], acc[m]);
     }
-    auto put = [&](int slot) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-          red[(slot * 12 + m * 4 + r4) * 64 + lane] =
-              (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
-    };
-    auto add = [&](int slot) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          const f32x4 v = red[(slot * 12 + m * 4 + r4) * 64 + lane];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[m][4 * r4 + e] += v[e];
-        }
-    };
-    // tree: w2 -> slot 0, w3 -> slot 1; w0 += 0, w1 += 1; then w1 -> slot 0; w0 += 0
+    // reduce-scatter: wave w owns accumulator group r4 = w of every m (output rows 32 m + 8 w +
+    // 4 hi + 0..3); slot (src, owner rank, m) with the owner's rank among src's 3 partners
     c2_stamp(a.trace, it, 2);
-    lds_barrier();                                     // buf free; the previous tile's red reads done
-    if (w >= 2) put(w - 2);
-    lds_barrier();
-    if (w < 2) add(w);
-    lds_barrier();
-    if (w == 1) put(0);
-    lds_barrier();
-    if (w == 0) add(0);
-    c2_stamp(a.trace, it, 3);
-    if (tile + per < t_hi) issue(tile + per);          // after every LDS read of this tile
-    if (w == 0) {
-      // the row goes through reduction slot 0 (wave 0 read it last) as bf16 [F2][32], then out
-      // in 16-B chunks (48 two-byte stores per lane otherwise)
-      unsigned short* stg = (unsigned short*)red;
+    lds_barrier();                                     // every MFMA read of buf done
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (o == w) continue;
+      const int rk = o - (o > w ? 1 : 0);
 #pragma unroll
       for (int m = 0; m < MT; ++m)
+        red[((w * 3 + rk) * MT + m) * 64 + lane] =
+            (f32x4){acc[m][4 * o], acc[m][4 * o + 1], acc[m][4 * o + 2], acc[m][4 * o + 3]};
+    }
+    lds_barrier();
+    f32x4 own[MT];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int f2 = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (m < 2 || f2 < a.F2) {
-            const bf16_t b = f2bf(acc[m][r] + bco);
-            stg[f2 * CC + col] = b;
-            const float vb = bf2f(b);
-            ssum += vb;
-            ssq += vb * vb;
-          }
+    for (int m = 0; m < MT; ++m)
+      own[m] = (f32x4){acc[m][4 * w], acc[m][4 * w + 1], acc[m][4 * w + 2], acc[m][4 * w + 3]};
+#pragma unroll
+    for (int src = 0; src < 4; ++src) {
+      if (src == w) continue;
+      const int rk = w - (w > src ? 1 : 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) own[m] += red[((src * 3 + rk) * MT + m) * 64 + lane];
+    }
+    c2_stamp(a.trace, it, 3);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int f2 = 32 * m + 8 * w + 4 * hi + e;
+        if (m < 2 || f2 < a.F2) {
+          const bf16_t b = f2bf(own[m][e] + bco);
+          stg[f2 * CC + col] = b;
+          const float vb = bf2f(b);
+          ssum += vb;
+          ssq += vb * vb;
         }
+      }
+    lds_barrier();
+    {
       i32x4* dst = (i32x4*)(a.y + ((size_t)n * a.T2 + t2) * a.F2 * CC);
-      for (int q = lane; q < a.F2 * 4; q += 64) dst[q] = ((const i32x4*)stg)[q];
+      for (int q = tid; q < a.F2 * 4; q += 256) dst[q] = ((const i32x4*)stg)[q];
     }
     c2_stamp(a.trace, it, 4);
+    lds_barrier();                                     // the row copy's reads done: buf is free
+    if (tile + per < t_hi) issue(tile + per);
+    c2_stamp(a.trace, it, 5);
   }
   __syncthreads();
   write_stats(ssum, ssq, (float*)red, 4, a.part);
@@ -320,28 +328,34 @@ struct Conv2Dgrad {
 constexpr int C2D_KPW = 25;                      // k-steps per wave (one parity's 50 in halves)
 constexpr int C2D_PR = 4 + 32 * MT;              // LDS position rows per dy row (positions -4 .. 95)
 constexpr int C2D_BUF = 5 * C2D_PR * PR;         // 40000 B
-constexpr int C2D_HALF = 12 * 64 * 16;           // one wave's partial sums (f32x4 per lane)
-constexpr int C2D_SMEM = C2D_BUF + 2 * C2D_HALF;
+constexpr int C2D_RED = 4 * 6 * 64 * 16;        // [wave][6 groups it hands over][64] f32x4
+constexpr int C2D_ROW = 80 * 64;                 // one bf16 output row [F1 <= 80][32]
+constexpr int C2D_SMEM = C2D_BUF + C2D_RED + 2 * C2D_ROW;
 static_assert(C2D_SMEM >= 16 * CC * C2_KT * C2_KF * 2, "one co half of the weights is staged through LDS");
 
-template <int S0>
-__device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a, int par);
+template <int W>
+__device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a);
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv2_dgrad_kernel(Conv2Dgrad a) {
-  DS2_DCHECK(a.F2 <= 32 * MT - 4 && a.F1 == a.F2 + 4 && a.F1 > 64);
-  const int w = uni(threadIdx.x >> 6), par = w & 1;
-  if (w >> 1) conv2_dgrad_body<C2D_KPW>(a, par);     // k-step s = ai * 10 + kf * 2 + co-half
-  else conv2_dgrad_body<0>(a, par);
+  DS2_DCHECK(a.F2 <= 32 * MT - 4 && a.F1 == a.F2 + 4 && a.F1 > 64 && a.F1 <= 80);
+  switch (uni(threadIdx.x >> 6)) {
+    case 0: conv2_dgrad_body<0>(a); break;
+    case 1: conv2_dgrad_body<1>(a); break;
+    case 2: conv2_dgrad_body<2>(a); break;
+    default: conv2_dgrad_body<3>(a); break;
+  }
 }
 
-// S0: the wave's first k-step (compile-time, so every LDS offset of the loop is an immediate)
-template <int S0>
-__device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a, const int par) {
+// W: the wave (parity W & 1, K half W >> 1), compile-time so every LDS offset is an immediate
+template <int W>
+__device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
+  constexpr int w = W, par = W & 1, kh = W >> 1, S0 = kh * C2D_KPW;   // k-step s = ai*10 + kf*2 + co-half
+  const int tid = threadIdx.x, lane = tid & 63;
   const int hi = lane >> 5, col = lane & 31;
   unsigned char* const buf = smem;
-  f32x4* red = (f32x4*)(smem + C2D_BUF);                             // [2 slots][12][64]
+  f32x4* red = (f32x4*)(smem + C2D_BUF);
+  unsigned short* stg = (unsigned short*)(smem + C2D_BUF + C2D_RED + par * C2D_ROW);   // this parity's row
 
   // weights -> VGPR fragments through LDS, one co half (51.2 KB of OIHW) at a time: coalesced
   // 16-B global loads, then 16-bit LDS gathers
@@ -368,7 +382,7 @@ __device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a, const int 
 
   const int U = (a.T1 + 1) >> 1;
   const int ntiles = a.N * U;
-  const int F2 = a.F2, nq = 5 * F2, nr = (nq + 63) >> 6;   // 16-B chunks per dy row, wave rounds
+  const int F2 = a.F2, nq = 5 * F2;                        // 16-B chunks per dy row (<= 6 rounds)
   // tiles: X contiguous ranges (one per XCD when the grid is a multiple of 8; workgroup b runs
   // on XCD b % 8), dealt round-robin to that XCD's workgroups
   const int X = (gridDim.x % 8 == 0) ? 8 : 1;
@@ -377,17 +391,22 @@ __device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a, const int 
 
   // stage dy rows u-4..u of tile t into the 5 slots (rows outside [0, T2) are clamped: their
   // k-steps are skipped); a lane's 16-B chunk q of a slot is position q / 5, chunk q % 5, and
-  // chunk 4 (the row's pad column, never read) repeats chunk 3
+  // chunk 4 (the row's pad column, never read) repeats chunk 3. Wave w issues rounds k = w + 4 i
+  // of the 30 (slot k / 6, round k % 6): compile-time slot and LDS offset.
   auto issue = [&](int t) {
     const int n = t / U, u = t - n * U;
     const bf16_t* base = a.dy + (size_t)n * a.T2 * F2 * CC;
-    for (int k = w; k < 5 * nr; k += 4) {
-      const int j = k / nr, r = k - j * nr;
-      const int q = 64 * r + lane;
-      if (q < nq) {
-        const int pos = (q * 52429) >> 18, c = min(q - 5 * pos, 3);    // q / 5 for q < 2^14
-        const int row = min(max(u - 4 + j, 0), a.T2 - 1);
-        glds16(base + ((size_t)row * F2 + pos) * CC + c * 8, buf + (j * C2D_PR + 4) * PR + 1024 * r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = w + 4 * i;
+      if (k < 30) {
+        const int j = k / 6, r = k % 6;
+        const int q = 64 * r + lane;
+        if (q < nq) {
+          const int pos = (q * 52429) >> 18, c = min(q - 5 * pos, 3);    // q / 5 for q < 2^14
+          const int row = min(max(u - 4 + j, 0), a.T2 - 1);
+          glds16(base + ((size_t)row * F2 + pos) * CC + c * 8, buf + (j * C2D_PR + 4) * PR + 1024 * r);
+        }
       }
     }
   };
@@ -428,79 +447,88 @@ __device__ __forceinline__ void conv2_dgrad_body(const Conv2Dgrad& a, const int 
       }
     }
     c2_stamp(a.trace, it, 2);
-    lds_barrier();                                     // buf free; the previous tile's red reads done
-    if (w >= 2) {
+    // the parity's two K halves reduce-scatter: K half kh owns accumulator groups r4 = 2 kh + j
+    // (j = 0, 1) of every m, i.e. output rows 32 m + 8 (2 kh + j) + 4 hi + 0..3, and hands the
+    // other two groups to its partner (wave W ^ 2) through red[wave][m][j]
+    lds_barrier();                                     // the previous tile's red / row reads done
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4)
-          red[(par * 12 + m * 4 + r4) * 64 + lane] =
-              (f32x4){acc[m][4 * r4], acc[m][4 * r4 + 1], acc[m][4 * r4 + 2], acc[m][4 * r4 + 3]};
-    }
+      for (int j = 0; j < 2; ++j) {
+        const int g = 2 * (1 - kh) + j;
+        red[((w * MT + m) * 2 + j) * 64 + lane] = (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+      }
     lds_barrier();
-    if (w < 2) {
+    f32x4 own[MT][2];
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          const f32x4 x = red[(par * 12 + m * 4 + r4) * 64 + lane];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[m][4 * r4 + e] += x[e];
-        }
-    }
+      for (int j = 0; j < 2; ++j) {
+        const int g = 2 * kh + j;
+        own[m][j] = (f32x4){acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]} +
+                    red[(((w ^ 2) * MT + m) * 2 + j) * 64 + lane];
+      }
     c2_stamp(a.trace, it, 3);
     const int t1 = 2 * u + par;
-    if (w < 2 && t1 < a.T1) {                          // wave-uniform
-      // the row goes through this wave's own reduction slot (read above) as bf16 [F1][32], then
-      // out in 16-B chunks: the epilogue issues no global store before its conv1 loads (a load
-      // behind a store to a possibly aliasing pointer would wait for the store)
-      const size_t rowoff = ((size_t)n * a.T1 + t1) * a.F1 * CC;
-      unsigned short* stg = (unsigned short*)(red + par * 12 * 64);
-      // one per-lane base; rows 0..63 at compile-time offsets (global-load immediates), the last
-      // m-tile's rows clamped to the row (they are neither stored nor counted past F1)
-      const unsigned short* yb = (const unsigned short*)a.y1 + rowoff + 4 * hi * CC + col;
-      const int lastoff = (a.F1 - 1 - 4 * hi) * CC;
+    const bool out = t1 < a.T1;                        // wave-uniform
+    const size_t rowoff = ((size_t)n * a.T1 + t1) * a.F1 * CC;
+    if (out) {
+      // conv1's outputs at the owned positions, loaded before any global store of the tile
+      // (one per-lane base, compile-time offsets; the last m-tile clamped to the row)
+      unsigned short yv[MT][2][4];
+      if (bn) {
+        const unsigned short* yb = (const unsigned short*)a.y1 + rowoff + 4 * hi * CC + col;
+        const int lastoff = (a.F1 - 1 - 4 * hi) * CC;
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        unsigned short yv[16];
-        if (bn) {
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int fo = (32 * m + (r & 3) + 8 * (r >> 2)) * CC;
-            yv[r] = m < 2 ? yb[fo] : yb[min(fo, lastoff)];
-          }
-        }
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int f1 = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (m < 2 || f1 < a.F1) {
-            const bf16_t d = f2bf(acc[m][r]);
-            stg[f1 * CC + col] = d;
-            if (bn) {
-              const float xh = (bf2f(yv[r]) - bmu) * bis;
-              const float zz = xh * bg + bbt;
-              const float dd = (zz > 0.f && zz < CLIP) ? bf2f(d) : 0.f;
-              bs += dd;
-              bq += dd * xh;
+            for (int e = 0; e < 4; ++e) {
+              const int fo = (32 * m + 8 * (2 * kh + j) + e) * CC;
+              yv[m][j][e] = m < 2 ? yb[fo] : yb[min(fo, lastoff)];
+            }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int f1 = 32 * m + 8 * (2 * kh + j) + 4 * hi + e;
+            if (m < 2 || f1 < a.F1) {
+              const bf16_t d = f2bf(own[m][j][e]);
+              stg[f1 * CC + col] = d;
+              if (bn) {
+                const float xh = (bf2f(yv[m][j][e]) - bmu) * bis;
+                const float zz = xh * bg + bbt;
+                const float dd = (zz > 0.f && zz < CLIP) ? bf2f(d) : 0.f;
+                bs += dd;
+                bq += dd * xh;
+              }
             }
           }
-        }
-      }
-      i32x4* dst = (i32x4*)(a.dx + rowoff);
-      for (int q = lane; q < a.F1 * 4; q += 64) dst[q] = ((const i32x4*)stg)[q];
     }
-    if (tile + per < t_hi) issue(tile + per);          // after every LDS read of this tile
+    lds_barrier();                                     // both halves of each parity row staged
+    if (out) {
+      i32x4* dst = (i32x4*)(a.dx + rowoff);
+      for (int q = kh * 64 + lane; q < a.F1 * 4; q += 128) dst[q] = ((const i32x4*)stg)[q];
+    }
     c2_stamp(a.trace, it, 4);
+    // the next tile's rows go out after every LDS access (and conv1 load) of this one: hipcc
+    // puts an s_waitcnt vmcnt(0) before any LDS access while LDS-DMA loads are in flight
+    if (tile + per < t_hi) issue(tile + per);
+    c2_stamp(a.trace, it, 5);
   }
   if (bn) {
-    // per-workgroup sums: lanes l, l ^ 32 and waves 0, 1 share a channel
+    // per-workgroup sums: lanes l, l ^ 32 and all 4 waves share a channel
     bs += __shfl_xor(bs, 32, 64);
     bq += __shfl_xor(bq, 32, 64);
     float* sh = (float*)red;
     __syncthreads();
-    if (w < 2 && lane < 32) { sh[(w * 32 + lane) * 2] = bs; sh[(w * 32 + lane) * 2 + 1] = bq; }
+    if (lane < 32) { sh[(w * 32 + lane) * 2] = bs; sh[(w * 32 + lane) * 2 + 1] = bq; }
     __syncthreads();
-    if (tid < 64) a.part[(size_t)blockIdx.x * 64 + tid] = sh[tid] + sh[64 + tid];
+    if (tid < 64) a.part[(size_t)blockIdx.x * 64 + tid] = sh[tid] + sh[64 + tid] + sh[128 + tid] + sh[192 + tid];
   }
 }
 

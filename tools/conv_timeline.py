@@ -13,11 +13,11 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-PHASES = ("wait rows", "mfma loop", "reduce", "epilogue")
+PHASES = ("wait rows", "mfma loop", "reduce", "epilogue", "issue next")
 
 
 def summarize(tr):
-    t = tr.view(8, 16, 5).double() / 100.0            # us
+    t = tr.view(8, 16, 6).double() / 100.0            # us
     out = {}
     for k, name in enumerate(PHASES):
         d = (t[:, :, k + 1] - t[:, :, k]).flatten()
@@ -57,7 +57,7 @@ def main():
                                                                 None, tr)),
                       ("conv2_dgrad+bn", lambda tr: C_.conv2_dgrad(dy, w, dx, grid, x, mean, inv, g, be, part,
                                                                    tr))):
-        tr = torch.zeros(8 * 16 * 5, device=dev, dtype=torch.int64)
+        tr = torch.zeros(8 * 16 * 6, device=dev, dtype=torch.int64)
         run(None)
         run(tr)
         torch.cuda.synchronize()
