@@ -113,6 +113,8 @@ struct DS2RnnF8B {
 int ds2_rnnf8_bwd_supported(int H, int N, int ndir);
 long long ds2_rnnf8_ring_words(int H, int BG, int R);
 int ds2_rnnf8_bwd(const DS2RnnF8B* d, hipStream_t st);
+int ds2_fp8_quant_u(int ndir, const void* const* x, int rows, int cols, void* const* q, void* const* qt, int* uexp,
+                    float* part, hipStream_t st);
 int ds2_fp8_quant_pow2_t(const void* x, int rows, int cols, void* q, int* uexp, unsigned* amax, hipStream_t st);
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs);
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
@@ -446,6 +448,38 @@ void fp8_quant_pow2(at::Tensor x, at::Tensor q, at::Tensor uexp, at::Tensor amax
   check(ds2_fp8_quant_pow2(x.data_ptr(), x.numel(), q.data_ptr(), uexp.data_ptr<int>(),
                            reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream()),
         "fp8_quant_pow2");
+}
+
+// csrc/rnn_fp8.hip: e4m3 copies of U_f (and U_b) [rows][cols] bf16 with one power-of-two scale per
+// direction: q [ndir, rows, cols] and / or qt [ndir, cols, rows] uint8, uexp int32 [>= ndir],
+// part fp32 [>= ndir * 256] scratch
+void fp8_quant_u(at::Tensor U_f, OptT U_b, OptT q, OptT qt, at::Tensor uexp, at::Tensor part) {
+  const int ndir = U_b.has_value() ? 2 : 1;
+  for (const at::Tensor* u : {&U_f, U_b.has_value() ? &*U_b : &U_f}) {
+    need_gpu(*u, "U");
+    TORCH_CHECK(u->scalar_type() == at::kBFloat16 && u->is_contiguous() && u->dim() == 2 && u->sizes() == U_f.sizes(),
+                "U must be contiguous bf16 2-D, both directions alike");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(u->data_ptr()) & 15) == 0, "U 16-B aligned");
+  }
+  const int64_t rows = U_f.size(0), cols = U_f.size(1);
+  TORCH_CHECK(rows % 64 == 0 && cols % 64 == 0, "fp8_quant_u: rows and cols multiples of 64");
+  TORCH_CHECK(q.has_value() || qt.has_value(), "fp8_quant_u: q or qt");
+  void* pq[2] = {nullptr, nullptr};
+  void* pqt[2] = {nullptr, nullptr};
+  if (q) {
+    TORCH_CHECK(q->scalar_type() == at::kByte && q->is_contiguous() && q->numel() == ndir * rows * cols, "q uint8 [ndir, rows, cols]");
+    for (int d = 0; d < ndir; ++d) pq[d] = static_cast<unsigned char*>(q->data_ptr()) + d * rows * cols;
+  }
+  if (qt) {
+    TORCH_CHECK(qt->scalar_type() == at::kByte && qt->is_contiguous() && qt->numel() == ndir * rows * cols &&
+                    (reinterpret_cast<uintptr_t>(qt->data_ptr()) & 15) == 0, "qt uint8 [ndir, cols, rows], 16-B aligned");
+    for (int d = 0; d < ndir; ++d) pqt[d] = static_cast<unsigned char*>(qt->data_ptr()) + d * rows * cols;
+  }
+  TORCH_CHECK(uexp.scalar_type() == at::kInt && uexp.numel() >= ndir, "uexp int32 [>= ndir]");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= ndir * 256, "part fp32 [>= ndir * 256]");
+  const void* px[2] = {U_f.data_ptr(), U_b.has_value() ? U_b->data_ptr() : U_f.data_ptr()};
+  check(ds2_fp8_quant_u(ndir, px, (int)rows, (int)cols, pq, pqt, uexp.data_ptr<int>(), part.data_ptr<float>(),
+                        cur_stream()), "fp8_quant_u");
 }
 
 // csrc/rnn_fp8.hip: transposed e4m3 copy q [cols][rows] of a bf16 [rows][cols] tensor scaled by
@@ -1209,6 +1243,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rnnf8_supported", [](int64_t H, int64_t N, int64_t ndir) { return ds2_rnnf8_supported((int)H, (int)N, (int)ndir); });
   m.def("fp8_quant_pow2", &fp8_quant_pow2);
   m.def("fp8_quant_pow2_t", &fp8_quant_pow2_t);
+  m.def("fp8_quant_u", &fp8_quant_u);
   m.def("rnnf8_bwd", &rnnf8_bwd);
   m.def("rnnf8_bwd_supported", [](int64_t H, int64_t N, int64_t ndir) {
     return ds2_rnnf8_bwd_supported((int)H, (int)N, (int)ndir);

@@ -1138,6 +1138,73 @@ __global__ __launch_bounds__(256) void quant_pow2_kernel(const bf16_t* __restric
   }
 }
 
+// ---- U of both directions in one pass each (config 5's fp8 layers): per-block |U| maxima, then
+// e4m3 copies in both layouts the recurrences read (row-major for the forward, transposed for
+// the BPTT, which keeps the forward's) from one read of U. No atomics and no zeroed scratch:
+// the quantiser reduces the QU_NB partials of its direction itself.
+constexpr int QU_NB = 256;
+
+__global__ __launch_bounds__(256) void amax_parts_kernel(const bf16_t* __restrict__ x0, const bf16_t* __restrict__ x1,
+                                                         long long n, float* __restrict__ part) {
+  const bf16_t* x = blockIdx.y ? x1 : x0;
+  float m = 0.f;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (long long)QU_NB * 256 * 8) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(bf2f((bf16_t)v[k])));
+  }
+  __shared__ float wm[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.y * QU_NB + blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+}
+
+// 64 x 64 tiles of direction blockIdx.z's [rows][cols] U: q row-major, qt [cols][rows] (either
+// may be null), both / 2^e with e from the direction's amax (uexp[d] = 127 + e, E8M0)
+__global__ __launch_bounds__(256) void quant_u_kernel(const bf16_t* __restrict__ x0, const bf16_t* __restrict__ x1,
+                                                      int rows, int cols, const float* __restrict__ part,
+                                                      unsigned char* q0, unsigned char* q1, unsigned char* qt0,
+                                                      unsigned char* qt1, int* __restrict__ uexp) {
+  const int d = blockIdx.z;
+  const bf16_t* x = d ? x1 : x0;
+  unsigned char* q = d ? q1 : q0;
+  unsigned char* qt = d ? qt1 : qt0;
+  __shared__ float wm[4];
+  __shared__ unsigned char t_s[64][64 + 16];
+  float m = part[d * QU_NB + threadIdx.x];               // QU_NB == blockDim.x
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  const int eb = e8m0_bits(__float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) uexp[d] = eb;
+  const float inv = __uint_as_float((unsigned)(254 - eb) << 23);          // 2^-(eb - 127)
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int k = threadIdx.x; k < 512; k += 256) {         // chunk k: row k >> 3, columns 8 (k & 7) ..
+    const int r = k >> 3, c = (k & 7) * 8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (size_t)(r0 + r) * cols + c0 + c);
+    unsigned w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)v[4 * h]) * inv, bf2f((bf16_t)v[4 * h + 1]) * inv, 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f((bf16_t)v[4 * h + 2]) * inv, bf2f((bf16_t)v[4 * h + 3]) * inv, lo, true);
+      w[h] = (unsigned)lo;
+    }
+    if (q) *reinterpret_cast<uint2*>(q + (size_t)(r0 + r) * cols + c0 + c) = make_uint2(w[0], w[1]);
+    *reinterpret_cast<uint2*>(&t_s[r][c]) = make_uint2(w[0], w[1]);
+  }
+  if (qt) {
+    __syncthreads();
+    const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 16;    // qt row c0 + c, 16 rows from rr
+    unsigned w4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w4[j] = (unsigned)t_s[rr + 4 * j][c] | ((unsigned)t_s[rr + 4 * j + 1][c] << 8) |
+              ((unsigned)t_s[rr + 4 * j + 2][c] << 16) | ((unsigned)t_s[rr + 4 * j + 3][c] << 24);
+    *reinterpret_cast<uint4*>(qt + (size_t)(c0 + c) * rows + r0 + rr) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1266,6 +1333,21 @@ int ds2_rnnf8_bwd(const DS2RnnF8B* d, hipStream_t st) {
     case 5: hipLaunchKernelGGL((rnnf8_bwd_kernel<12, 4>), dim3(grid), dim3(BTH8), 0, st, a); break;
     default: return -41;
   }
+  return (int)hipGetLastError();
+}
+
+// U of ndir directions ([rows][cols] bf16 each, rows and cols multiples of 64): row-major q[d]
+// and / or transposed qt[d] e4m3 copies with one power-of-two scale per direction, uexp[d] =
+// 127 + e; part: ndir * 256 floats of scratch. Two launches for all directions and layouts.
+int ds2_fp8_quant_u(int ndir, const void* const* x, int rows, int cols, void* const* q, void* const* qt, int* uexp,
+                    float* part, hipStream_t st) {
+  if (ndir < 1 || ndir > 2 || rows <= 0 || cols <= 0 || rows % 64 || cols % 64) return (int)hipErrorInvalidValue;
+  const bf16_t* x1 = (const bf16_t*)x[ndir - 1];
+  hipLaunchKernelGGL(amax_parts_kernel, dim3(QU_NB, ndir), dim3(256), 0, st, (const bf16_t*)x[0], x1,
+                     (long long)rows * cols, part);
+  hipLaunchKernelGGL(quant_u_kernel, dim3(cols / 64, rows / 64, ndir), dim3(256), 0, st, (const bf16_t*)x[0], x1,
+                     rows, cols, part, (unsigned char*)q[0], (unsigned char*)q[ndir - 1], (unsigned char*)qt[0],
+                     (unsigned char*)qt[ndir - 1], uexp);
   return (int)hipGetLastError();
 }
 

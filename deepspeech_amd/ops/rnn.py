@@ -417,10 +417,27 @@ def fp8_recurrence_ok(plan: RnnPlan, N: int) -> bool:
     return BG * (-(-N // BG)) == plan.NP
 
 
-def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan):
+def _quant_u(U, plan: RnnPlan, rowmajor: bool = True, transposed: bool = True):
+    """(U8 [ndir, 3H, H] | None, U8T [ndir, H, 3H] | None, uexp int32 [ndir]): e4m3 copies of the
+    recurrent weights with one power-of-two scale per direction, computed on the device: the
+    forward's layout and the BPTT's transposed one from one read of U (csrc/rnn_fp8.hip
+    quant_u_kernel; two launches for every direction and layout)."""
+    C = _ext.ext()
+    H, ndir = plan.H, plan.ndir
+    dev = U[0].device
+    U8 = torch.empty(ndir, 3 * H, H, device=dev, dtype=torch.uint8) if rowmajor else None
+    U8T = torch.empty(ndir, H, 3 * H, device=dev, dtype=torch.uint8) if transposed else None
+    words = torch.empty(ndir, device=dev, dtype=torch.int32)
+    part = torch.empty(ndir * 256, device=dev, dtype=torch.float32)
+    C.fp8_quant_u(U[0].contiguous(), U[1].contiguous() if ndir == 2 else None, U8, U8T, words, part)
+    return U8, U8T, words
+
+
+def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan, keep: Optional[dict] = None):
     """GRU forward with e4m3 recurrent weights (one power-of-two scale per direction, computed
     on the device) and an e4m3 hidden-state exchange: groups of H/64 workgroups on one XCD
-    (csrc/rnn_fp8.hip). Returns (y, (hx, hs, gates)) in the layout of _run_fwd."""
+    (csrc/rnn_fp8.hip). Returns (y, (hx, hs, gates)) in the layout of _run_fwd. With keep (a
+    dict), the transposed e4m3 U of the same quantisation goes into keep["quant"] for the BPTT."""
     C = _ext.ext()
     T, N, gstride = gx.shape
     H, ndir = plan.H, plan.ndir
@@ -428,10 +445,9 @@ def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan):
     R = -(-N // BG)
     NP = BG * R
     dev = gx.device
-    U8 = torch.empty(ndir, 3 * H, H, device=dev, dtype=torch.uint8)
-    words = torch.empty(4, device=dev, dtype=torch.int32)          # uexp[2], amax scratch
-    for d in range(ndir):
-        C.fp8_quant_pow2(U[d].contiguous(), U8[d], words[d:d + 1], words[3:4])
+    U8, U8T, words = _quant_u(U, plan, True, keep is not None)
+    if keep is not None:
+        keep["quant"] = (U8T, words)
     y2 = torch.empty(ndir, T, N, H, device=dev, dtype=torch.bfloat16)
     hq = torch.empty(ndir, T + 1, NP, H, device=dev, dtype=torch.uint8)
     hx = torch.empty(ndir, T + 1, NP, H, device=dev, dtype=torch.bfloat16)
@@ -461,10 +477,10 @@ def fp8_bptt_ok(plan: RnnPlan, N: int) -> bool:
 
 
 def _run_bwd_fp8(dy, lens, U, hs, gates, plan: RnnPlan, gstride: int, dgx_scale: float = 1.0,
-                 want_bias: bool = True):
+                 want_bias: bool = True, quant=None):
     """fp8 GRU BPTT (csrc/rnn_fp8.hip): groups of H/64 workgroups on one XCD, U^T in e4m3 with
-    a per-tensor power-of-two scale (computed here on the device), the gate gradients requantised
-    to e4m3 per batch row each step. Same outputs as _run_bwd: (dgx [T, N, gstride] bf16 x
+    a per-tensor power-of-two scale (the forward's, via quant, or computed here on the device), the
+    gate gradients requantised to e4m3 per (row, 32-unit group) each step. Same outputs as _run_bwd: (dgx [T, N, gstride] bf16 x
     dgx_scale, dgh [ndir, steps, NP, 3H] bf16, bias partials [2, ndir, BG, 3H] or None)."""
     C = _ext.ext()
     T, N, H = dy.shape
@@ -476,10 +492,8 @@ def _run_bwd_fp8(dy, lens, U, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
     dev = dy.device
     steps = T
     dy = dy.to(torch.bfloat16).contiguous()
-    U8T = torch.empty(ndir, H, 3 * H, device=dev, dtype=torch.uint8)
-    words = torch.empty(4, device=dev, dtype=torch.int32)          # uexp[2], amax scratch
-    for d in range(ndir):
-        C.fp8_quant_pow2_t(U[d].contiguous(), U8T[d], words[d:d + 1], words[3:4])
+    # quant: (U8T, uexp) of the forward's quantisation of the same U, else quantised here
+    U8T, words = quant if quant is not None else _quant_u(U, plan, False, True)[1:]
     dgh = torch.empty(ndir, steps, NP, 3 * H, device=dev, dtype=torch.bfloat16)
     dgx = torch.empty(T, N, gstride, device=dev, dtype=torch.bfloat16)
     census = torch.empty(ndir * BG * (H // 64), device=dev, dtype=torch.int32)
@@ -699,8 +713,10 @@ class FusedBiLayer(torch.autograd.Function):
             # gradient is straight-through with respect to the quantisation of the exchanged h and
             # of dg (no quantisation gradient); tests/test_convergence_gpu.py pins the resulting
             # 300-step loss curve against the bf16 recurrence
-            y, (hx, hs, gates) = _run_fwd_fp8(gx, lens, U, bh, plan)
             ctx.fp8_bwd = fp8_bptt_ok(plan, N)
+            keep = {} if ctx.fp8_bwd else None
+            y, (hx, hs, gates) = _run_fwd_fp8(gx, lens, U, bh, plan, keep)
+            ctx.fp8_quant = keep["quant"] if keep is not None else None
         else:
             y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
         dev = x.device
@@ -728,7 +744,8 @@ class FusedBiLayer(torch.autograd.Function):
         GH = GATES[plan.cell] * plan.H
         if getattr(ctx, "fp8_bwd", False):
             dgx, dgh, parts = _run_bwd_fp8(dy, lens, [U_f16, U_b16 if d1 else None], hs, gates, plan,
-                                           plan.ndir * GH, dgx_scale=ctx.alpha)
+                                           plan.ndir * GH, dgx_scale=ctx.alpha, quant=ctx.fp8_quant)
+            ctx.fp8_quant = None
         else:
             dgx, dgh, parts = _run_bwd(dy, lens, [U_f16, U_b16 if d1 else None], hx, hs, gates, plan,
                                        plan.ndir * GH, dgx_scale=ctx.alpha)

@@ -413,6 +413,32 @@ def test_fp8_quant_pow2(cuda):
         assert float((q != want).float().mean()) == 0.0
 
 
+@pytest.mark.parametrize("H,ndir", [(256, 2), (1280, 2), (1280, 1)])
+def test_fp8_quant_u_both_layouts(cuda, H, ndir):
+    """csrc/rnn_fp8.hip quant_u_kernel (the fp8 layers' U, both directions, one read): the
+    row-major and transposed e4m3 copies and each direction's exponent equal the per-tensor
+    quantiser's, bitwise; either layout alone gives the same bytes."""
+    from deepspeech_amd.ops import _ext
+    C = _ext.ext()
+    torch.manual_seed(H + ndir)
+    U = [(torch.randn(3 * H, H, device=cuda) * s).to(torch.bfloat16) for s in (0.05, 7.0)[:ndir]]
+    q = torch.empty(ndir, 3 * H, H, device=cuda, dtype=torch.uint8)
+    qt = torch.empty(ndir, H, 3 * H, device=cuda, dtype=torch.uint8)
+    uexp = torch.empty(ndir, device=cuda, dtype=torch.int32)
+    part = torch.empty(ndir * 256, device=cuda)
+    C.fp8_quant_u(U[0], U[1] if ndir == 2 else None, q, qt, uexp, part)
+    q2 = torch.empty_like(q)
+    C.fp8_quant_u(U[0], U[1] if ndir == 2 else None, q2, None, uexp, part)
+    assert torch.equal(q, q2)
+    for d in range(ndir):
+        ref = torch.empty(3 * H, H, device=cuda, dtype=torch.uint8)
+        w = torch.empty(2, device=cuda, dtype=torch.int32)
+        C.fp8_quant_pow2(U[d], ref, w[0:1], w[1:2])
+        assert int(uexp[d]) == int(w[0])
+        assert torch.equal(q[d], ref)
+        assert torch.equal(qt[d], ref.t().contiguous())
+
+
 def _gru_fp8_emulation(gx, lens, U, bh, H):
     """fp32 model of csrc/rnn_fp8.hip: U quantised to e4m3 with a power-of-two scale, h_{t-1}
     requantised to e4m3 every step for the recurrent product, the cell in fp32."""

@@ -69,17 +69,18 @@ def main():
             print("| %s | %.0f | %.1f |" % (ph, us, 100 * us / period))
 
 
-_PHASES = [
+_PHASES = [       # first match wins: BPTT before fwd (the fp8 kernels share the rnnf8 prefix)
+    ("recurrence BPTT", ("rnnf8_bwd", "rnnw_bwd", "rnnrs_bwd", "rnnx_bwd", "rnn_bwd")),
     ("recurrence fwd", ("rnne_fwd", "rnnw_fwd", "rnnf8", "rnnq_fwd", "rnnx_fwd", "rnn_fwd")),
-    ("recurrence BPTT", ("rnnw_bwd", "rnnrs_bwd", "rnnx_bwd", "rnn_bwd")),
+    ("fp8 quantisers", ("quant_pow2", "amax_")),
     ("weight-gradient GEMMs (gemm8 column mode)", ("gemm8_kernel<false, 1, 1>", "gemm8_kernel<false, 1, 0>")),
     ("projection / dx / FC GEMM (hand-written)", ("gemm_kernel", "gemm8_kernel", "transpose_bf16")),
     ("library GEMM (hipBLASLt) BBS = dx", ("_BBS_",)),
     ("library GEMM (hipBLASLt) BSS = weight grads", ("_BSS_",)),
     ("conv front-end fwd", ("conv1_fwd", "conv2_fwd", "bn_cl_apply", "bn_cl_finalize")),
-    ("conv front-end bwd", ("conv1_wgrad", "conv2_wgrad", "conv2_dgrad", "bn_cl_bwd")),
+    ("conv front-end bwd", ("conv1_wgrad", "conv2_wgrad", "conv2_dgrad", "bn_cl_bwd", "wgrad_reduce")),
     ("CTC + head", ("ctc_", "fc_lsm")),
-    ("optimizer", ("adam_ema", "grad_norm", "wgrad_reduce")),
+    ("optimizer", ("adam_ema", "grad_norm")),
     ("fills / copies", ("multi_fill", "rocclr_fill", "rocclr_copy", "FillFunctor", "copy_kernel")),
 ]
 
