@@ -188,8 +188,12 @@ int ds2_conv2_wgrad(const void* dy, const void* x, float* part, int grid, float*
                     int F2, hipStream_t st);
 int ds2_conv1_fwd(const void* x, const void* w, const float* bias, void* y, float* part, int N, int T, int F0,
                   int T1, int F1, hipStream_t st);
+struct DS2Conv1WgradBn {  // csrc/conv_frontend.hip: conv1's BN-backward apply in the wgrad staging
+  const void *dz, *y1;
+  const float *mean, *invstd, *gamma, *beta, *dbeta, *dgamma;
+};
 int ds2_conv1_wgrad(const void* dy, const void* x, float* part, int grid, float* dw, int N, int T, int F0, int T1,
-                    int F1, hipStream_t st);
+                    int F1, const DS2Conv1WgradBn* bn, hipStream_t st);
 int ds2_bn_cl_finalize(const float* part, int nb, double M, float eps, float* mean, float* invstd, float* run_mean,
                        float* run_var, float momentum, hipStream_t st);
 int ds2_bn_cl_apply(const void* y, const float* mean, const float* invstd, const float* gamma, const float* beta,
@@ -801,14 +805,29 @@ void conv2_wgrad(at::Tensor dy, at::Tensor x, at::Tensor part, at::Tensor dw, in
 }
 
 // dy [N,T1,F1,32], x [N,T,F0] -> dw (fp32, 32*20*5)
-void conv1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor part, at::Tensor dw, int64_t grid) {
+// bn (optional, all or none): dy is then dz = dL/d(clip(BN(y1))) and the kernel applies conv1's
+// BatchNorm backward (batch statistics mean / invstd, affine gamma / beta, dbeta / dgamma sums)
+// while staging it, bitwise as bn_cl_bwd's apply pass
+void conv1_wgrad(at::Tensor dy, at::Tensor x, at::Tensor part, at::Tensor dw, int64_t grid, OptT y1, OptT mean,
+                 OptT invstd, OptT gamma, OptT beta, OptT dbeta, OptT dgamma) {
   need_bf16(dy, "dy"); need_bf16(x, "x");
   TORCH_CHECK(grid > 0, "grid");
   need_f32(part, "part", ds2_conv1_wgrad_part_floats((int)grid));
   need_f32(dw, "dw", 32 * 100);
-  check(ds2_conv1_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), (int)grid, dw.data_ptr<float>(),
-                        (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)dy.size(1), (int)dy.size(2),
-                        cur_stream()), "conv1_wgrad");
+  DS2Conv1WgradBn bn{};
+  const bool with_bn = y1.has_value();
+  if (with_bn) {
+    TORCH_CHECK(mean && invstd && gamma && beta && dbeta && dgamma, "conv1_wgrad: the BN arguments come all or none");
+    need_bf16(*y1, "y1");
+    TORCH_CHECK(y1->sizes() == dy.sizes(), "y1 must have dz's shape");
+    for (const OptT* t : {&mean, &invstd, &gamma, &beta, &dbeta, &dgamma}) need_f32(**t, "bn vector", 32);
+    bn = DS2Conv1WgradBn{dy.data_ptr(), y1->data_ptr(), mean->data_ptr<float>(), invstd->data_ptr<float>(),
+                         gamma->data_ptr<float>(), beta->data_ptr<float>(), dbeta->data_ptr<float>(),
+                         dgamma->data_ptr<float>()};
+  }
+  check(ds2_conv1_wgrad(with_bn ? nullptr : dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), (int)grid,
+                        dw.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (int)x.size(2), (int)dy.size(1),
+                        (int)dy.size(2), with_bn ? &bn : nullptr, cur_stream()), "conv1_wgrad");
 }
 int64_t conv2_wgrad_part_floats(int64_t grid) { return ds2_conv2_wgrad_part_floats((int)grid); }
 int64_t conv1_wgrad_part_floats(int64_t grid) { return ds2_conv1_wgrad_part_floats((int)grid); }
@@ -833,10 +852,11 @@ void bn_cl_apply(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor ga
                         tmaj ? 1 : 0, cur_stream()), "bn_cl_apply");
 }
 
-// part_ready: part already holds nb partial sums (conv2_dgrad's bn epilogue), skip the reduce pass
+// part_ready: part already holds nb partial sums (conv2_dgrad's bn epilogue), skip the reduce pass;
+// 2: also skip the apply pass (dgamma / dbeta only: conv1_wgrad applies the backward itself)
 void bn_cl_bwd(at::Tensor dz, at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor beta,
                at::Tensor part, int64_t nb, at::Tensor dgamma, at::Tensor dbeta, at::Tensor dy, bool tmaj,
-               bool part_ready) {
+               int64_t part_ready) {
   need_bf16(dz, "dz"); need_bf16(y, "y"); need_bf16(dy, "dy");
   TORCH_CHECK(y.dim() == 4 && y.size(3) == 32 && dz.numel() == y.numel() && dy.numel() == y.numel(),
               "bn_cl_bwd shapes");
@@ -846,7 +866,7 @@ void bn_cl_bwd(at::Tensor dz, at::Tensor y, at::Tensor mean, at::Tensor invstd, 
   check(ds2_bn_cl_bwd(dz.data_ptr(), y.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
                       gamma.data_ptr<float>(), beta.data_ptr<float>(), part.data_ptr<float>(), (int)nb,
                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dy.data_ptr(), (int)y.size(0),
-                      (int)y.size(1), (int)y.size(2), tmaj ? 1 : 0, part_ready ? 1 : 0, cur_stream()), "bn_cl_bwd");
+                      (int)y.size(1), (int)y.size(2), tmaj ? 1 : 0, (int)part_ready, cur_stream()), "bn_cl_bwd");
 }
 
 // --------------------------------------------------------------------------- greedy CTC decode
@@ -1303,14 +1323,17 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("part") = py::none(),
         py::arg("trace") = py::none());
   m.def("conv2_wgrad", &conv2_wgrad);
-  m.def("conv1_wgrad", &conv1_wgrad);
+  m.def("conv1_wgrad", &conv1_wgrad, py::arg("dy"), py::arg("x"), py::arg("part"), py::arg("dw"), py::arg("grid"),
+        py::arg("y1") = py::none(), py::arg("mean") = py::none(), py::arg("invstd") = py::none(),
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("dbeta") = py::none(),
+        py::arg("dgamma") = py::none());
   m.def("conv2_wgrad_part_floats", &conv2_wgrad_part_floats);
   m.def("conv1_wgrad_part_floats", &conv1_wgrad_part_floats);
   m.def("bn_cl_finalize", &bn_cl_finalize);
   m.def("bn_cl_apply", &bn_cl_apply);
   m.def("bn_cl_bwd", &bn_cl_bwd, py::arg("dz"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"),
         py::arg("beta"), py::arg("part"), py::arg("nb"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dy"),
-        py::arg("tmaj"), py::arg("part_ready") = false);
+        py::arg("tmaj"), py::arg("part_ready") = 0);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
         py::arg("K"), py::arg("a_col"), py::arg("b_col"), py::arg("epi"), py::arg("alpha"), py::arg("cfg"),
         py::arg("alpha_dev") = py::none(), py::arg("Ml") = 0, py::arg("Nl") = 0, py::arg("Kl") = 0);

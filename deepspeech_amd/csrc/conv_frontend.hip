@@ -41,6 +41,12 @@
 
 using namespace ds2;
 
+// optional BatchNorm-backward apply fused into conv1's weight-gradient staging (bindings.cpp)
+struct DS2Conv1WgradBn {
+  const void *dz, *y1;                             // bf16 [N][T1][F1][32]
+  const float *mean, *invstd, *gamma, *beta, *dbeta, *dgamma;
+};
+
 // optional BatchNorm-backward sums fused into the conv2 data-gradient epilogue (bindings.cpp)
 struct DS2Conv2DgradBn {
   const void* y1;                                  // conv1 output [N][T1][F1][32] bf16
@@ -749,10 +755,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Fwd a) {
 // conv1 weight gradient
 // =====================================================================================
 struct Conv1Wgrad {
-  const bf16_t* dy;   // [N][T1][F1][32]
+  const bf16_t* dy;   // [N][T1][F1][32], or null with bn.dz: dy computed while staging
   const bf16_t* x;    // [N][T][F0]
   float* part;        // [grid][5][4][64][4]
   int N, T, F0, T1, F1;
+  // optional: conv1's BatchNorm backward applied in the staging (bn_cl_bwd_apply_kernel's
+  // arithmetic, so dy is bitwise the same): dz = dL/d(clip(BN(y1))) [N][T1][F1][32], y1
+  const bf16_t *dz, *y1;
+  const float *mean, *invstd, *gamma, *beta, *dbeta, *dgamma;
+  float M;            // N * T1 * F1
 };
 constexpr int C1W_XP = 88;                       // de-interleaved row stride (positions)
 constexpr int C1W_DY = C1_ROWS * 80 * 64;        // dy image bytes (4 rows x 80 positions)
@@ -774,6 +785,18 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(Conv1Wgrad a) {
   const unsigned lofs = (unsigned)((8 * h + q) * 64 + (cb + 4 * pp) * 2);
   const int bkt = col >> 3, bkf = col & 7;
 
+  // fused BN backward: a thread's chunks all hold channels 8 (tid & 3) .. + 7 (256 and 320 are
+  // multiples of 4), so their constants stay in registers
+  const bool bn = a.dz != nullptr;
+  float bmu[8], bis[8], bg[8], bbt[8], bmdb[8], bmdg[8];
+  if (bn) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = (tid & 3) * 8 + j;
+      bmu[j] = a.mean[c]; bis[j] = a.invstd[c]; bg[j] = a.gamma[c]; bbt[j] = a.beta[c];
+      bmdb[j] = a.dbeta[c] / a.M; bmdg[j] = a.dgamma[c] / a.M;
+    }
+  }
   f32x16 acc[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) acc[i] = (f32x16){};
@@ -785,8 +808,23 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(Conv1Wgrad a) {
       const int r = ch / 320, rem = ch - r * 320, pos = rem >> 2, c4 = rem & 3;
       const int t1 = t1_0 + r;
       i32x4 v = (i32x4){0, 0, 0, 0};
-      if (pos < a.F1 && t1 < a.T1)
-        v = *(const i32x4*)(a.dy + (((size_t)n * a.T1 + t1) * a.F1 + pos) * CC + c4 * 8);
+      if (pos < a.F1 && t1 < a.T1) {
+        const size_t off = (((size_t)n * a.T1 + t1) * a.F1 + pos) * CC + c4 * 8;
+        if (bn) {
+          const bf16x8 y = *(const bf16x8*)(a.y1 + off), d = *(const bf16x8*)(a.dz + off);
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = (bf2f((bf16_t)y[j]) - bmu[j]) * bis[j];
+            const float zz = xh * bg[j] + bbt[j];
+            const float dd = (zz > 0.f && zz < CLIP) ? bf2f((bf16_t)d[j]) : 0.f;
+            o[j] = (short)f2bf(bg[j] * bis[j] * (dd - bmdb[j] - xh * bmdg[j]));
+          }
+          v = __builtin_bit_cast(i32x4, o);
+        } else {
+          v = *(const i32x4*)(a.dy + off);
+        }
+      }
       *(i32x4*)(dys + ch * 16) = v;
     }
     // x rows 2*t1_0 + r: raw rows into LDS, then de-interleaved xd[r][kf'][p] = x[t][2p + kf']
@@ -1161,10 +1199,15 @@ int ds2_conv1_fwd(const void* x, const void* w, const float* bias, void* y, floa
 }
 
 int ds2_conv1_wgrad(const void* dy, const void* x, float* part, int grid, float* dw, int N, int T, int F0, int T1,
-                    int F1, hipStream_t st) {
+                    int F1, const DS2Conv1WgradBn* bn, hipStream_t st) {
   if (F1 > 80 || F1 != (F0 - 5) / 2 + 1 || T1 != (T - 20) / 2 + 1 || T1 < 1) return -43;
+  if ((dy == nullptr) == (bn == nullptr)) return -44;     // dy, or the BN backward's inputs
   DS2_HIP_CHECK((hipError_t)set_smem(conv1_wgrad_kernel, C1W_SMEM));
-  Conv1Wgrad a{(const bf16_t*)dy, (const bf16_t*)x, part, N, T, F0, T1, F1};
+  Conv1Wgrad a{(const bf16_t*)dy, (const bf16_t*)x, part, N, T, F0, T1, F1,
+               bn ? (const bf16_t*)bn->dz : nullptr, bn ? (const bf16_t*)bn->y1 : nullptr,
+               bn ? bn->mean : nullptr, bn ? bn->invstd : nullptr, bn ? bn->gamma : nullptr,
+               bn ? bn->beta : nullptr, bn ? bn->dbeta : nullptr, bn ? bn->dgamma : nullptr,
+               (float)((double)N * T1 * F1)};
   hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(grid), dim3(256), C1W_SMEM, st, a);
   hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(5 * 1024 / 256), dim3(256), 0, st, part, grid, 5 * 1024, dw);
   return (int)hipGetLastError();
@@ -1202,11 +1245,14 @@ int ds2_bn_cl_bwd(const void* dz, const void* y, const float* mean, const float*
   // time-major dz: the reduce pass (which transposes it through LDS anyway) leaves a
   // channels-last copy in dy, and the apply pass then works in place on dy, coalesced
   // (the apply's own per-row LDS transpose ran at ~1/9 of the bandwidth roofline)
-  if (!part_ready)   // else part holds nb partial sums already (conv2_dgrad_kernel's bn epilogue)
+  // part_ready: part holds nb partial sums already (conv2_dgrad_kernel's bn epilogue); 2: and
+  // no apply pass either (conv1_wgrad_kernel applies the BN backward while staging)
+  if (!part_ready)
     hipLaunchKernelGGL(bn_cl_bwd_reduce_kernel, dim3(nb), dim3(256), 0, st, (const bf16_t*)dz, (const bf16_t*)y,
                        mean, invstd, gamma, beta, part, N, T, F, tmaj, tmaj ? (bf16_t*)dy : (bf16_t*)nullptr);
   hipLaunchKernelGGL(bn_cl_bwd_finalize_kernel, dim3(CC), dim3(256), 0, st, part, nb, dbeta, dgamma);
   const int rows = N * T;
+  if (part_ready == 2) return (int)hipGetLastError();
   hipLaunchKernelGGL(bn_cl_bwd_apply_kernel, dim3(rows < 4096 ? rows : 4096), dim3(256), 0, st,
                      tmaj ? (const bf16_t*)dy : (const bf16_t*)dz, (const bf16_t*)y, mean, invstd, gamma, beta,
                      dbeta, dgamma, (bf16_t*)dy, N, T, F);

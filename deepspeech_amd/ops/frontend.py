@@ -292,13 +292,14 @@ class FrontendCL(torch.autograd.Function):
         gg2, gb2, gbias2 = _deliver(g2, dg2, ipg2), _deliver(be2, db2, ipb2), _zero_grad_of(b2)
         with TR.phase(TR.bn(1, True)):
             (dg1, ipg1), (db1, ipb1) = _grad_buffer(g1), _grad_buffer(be1)
-            dy1 = torch.empty_like(y1)
-            C_.bn_cl_bwd(dz1, y1, mean1, inv1, g1f, be1f, part, dgrid, dg1, db1, dy1, False, part_ready=True)
+            # the sums came out of the dgrad epilogue; the apply pass runs inside conv1_wgrad's
+            # staging (dy1 never materialised), so only dgamma / dbeta here
+            C_.bn_cl_bwd(dz1, y1, mean1, inv1, g1f, be1f, part, dgrid, dg1, db1, dz1, False, part_ready=2)
         with TR.phase(TR.conv(1, True)):
             g1grid = max(1, min(N * ((T1 + 3) // 4), ctx.ncu))
             wpart1 = torch.empty(int(C_.conv1_wgrad_part_floats(g1grid)), **f32)
             dw1, ip1 = _grad_buffer(w1)
-            C_.conv1_wgrad(dy1, x, wpart1, dw1, g1grid)
+            C_.conv1_wgrad(dz1, x, wpart1, dw1, g1grid, y1, mean1, inv1, g1f, be1f, db1, dg1)
             gw1 = _deliver(w1, dw1, ip1)
         gg1, gb1, gbias1 = _deliver(g1, dg1, ipg1), _deliver(be1, db1, ipb1), _zero_grad_of(b1)
         return None, gw1, gbias1, gg1, gb1, gw2, gbias2, gg2, gb2, None

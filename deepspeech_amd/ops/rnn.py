@@ -1132,11 +1132,12 @@ class WgradScheduler:
             items, self.deferred = self.deferred, []
             members = [m for d in items for m in d.members]
             fused = self._fused_opt(members)
+            cap = int(os.environ.get("DS2_GROUP_CUS", "0"))
             if fused is not None:
-                GM.gemm8_group(members, opt=fused[0])
+                GM.gemm8_group(members, opt=fused[0], max_grid=cap)
                 self.fused_ranges.extend(fused[1])
             else:
-                GM.gemm8_group(members)
+                GM.gemm8_group(members, max_grid=cap)
             for d in items:
                 d.done()
             return

@@ -126,6 +126,28 @@ def test_conv1_wgrad(cuda, N, T):
         dw = torch.full((32, 1, 20, 5), float("nan"), device=cuda)
         C_.conv1_wgrad(dy, x, part, dw, grid)
         assert _rel(dw, wr.grad) < 1e-2, ("dw1", grid, _rel(dw, wr.grad))
+    # the BatchNorm backward applied inside the staging: bitwise the weight gradient of the
+    # apply pass's dy (dz and y1 as conv1's BN sees them; sums from the reduce pass)
+    y1 = (torch.randn(N, T1, F1, 32, device=cuda) * 3 + 1).bfloat16()
+    dz = dy
+    yf = y1.float().reshape(-1, 32)
+    mean = yf.mean(0).contiguous()
+    inv = torch.rsqrt(yf.var(0, unbiased=False) + 1e-3).contiguous()
+    gamma, beta = torch.rand(32, device=cuda) + 0.5, torch.randn(32, device=cuda) * 0.3
+    bpart = torch.empty(64 * 64, device=cuda)
+    dg, db = torch.empty(32, device=cuda), torch.empty(32, device=cuda)
+    dy_bn = torch.empty_like(dz)
+    C_.bn_cl_bwd(dz, y1, mean, inv, gamma, beta, bpart, 64, dg, db, dy_bn, False)
+    dg2, db2 = torch.empty(32, device=cuda), torch.empty(32, device=cuda)
+    C_.bn_cl_bwd(dz, y1, mean, inv, gamma, beta, bpart, 64, dg2, db2, dz, False, part_ready=2)
+    assert torch.equal(dg, dg2) and torch.equal(db, db2)
+    for grid in (3, 64):
+        part = torch.empty(int(C_.conv1_wgrad_part_floats(grid)), device=cuda)
+        dw_a = torch.full((32, 1, 20, 5), float("nan"), device=cuda)
+        dw_b = torch.full((32, 1, 20, 5), float("nan"), device=cuda)
+        C_.conv1_wgrad(dy_bn, x, part, dw_a, grid)
+        C_.conv1_wgrad(dz, x, part, dw_b, grid, y1, mean, inv, gamma, beta, db, dg)
+        assert torch.equal(dw_a, dw_b), ("fused BN backward", grid, (dw_a - dw_b).abs().max())
 
 
 @pytest.mark.parametrize("tmaj", [False, True])
