@@ -30,11 +30,11 @@ _PERSISTENT = {6: 0, 7: 1, 8: 2}
 # measured picks: (M, N, K, a_col, b_col, batch) -> cfg
 TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
     # headline shapes (T2=241, N=32, H=800), tools/bench_gemm8.py on MI355X
-    # projection, layers 1-4: persistent 128x256 (cfg 7) 82.5 us, gemm8 82.4 (tie: kept); layer 0
-    # runs on gemm8 (182 vs 196 us)
-    (7712, 4800, 800, False, False, 1): 7,
+    # projection, layers 1-4: on gemm8 (not listed). Alone it ties the persistent 128x256 tile
+    # (82.4 vs 82.5 us); in the step, same box: 7.80-7.83 vs 7.84-7.85 ms/step (round 4)
     # dx = dgx W on the K-contiguous W^T shadow (ops/rnn.py _transpose_async), persistent
-    # 128x256: 67 / 197 us vs gemm8 82 / 203 (tools/bench_gemm8.py)
+    # 128x256: 67 / 197 us vs gemm8 82 / 203 (tools/bench_gemm8.py); in the step gemm8 loses
+    # too (7.90-7.94 vs 7.84-7.85 ms/step, round 4)
     (7712, 800, 4800, False, False, 1): 7,
     # layer 0's dx (7712, 2400, 4800) runs on gemm8 (non-persistent): it shares the chip with
     # the grouped weight-gradient launch, and a persistent grid's statically assigned tiles
@@ -141,10 +141,10 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
     orientation: a [M, K], b [K, N]; out fp32 (store / accumulate) or bf16 (store, optional
     bias). Returns False (nothing launched) when the shape or strides are not covered.
 
-    Routing (tools/bench_gemm8.py, MI355X): the headline's row-row projections keep their
-    measured csrc/gemm.hip persistent tile (TUNED); every other covered shape runs on
-    csrc/gemm8.hip — row-row projections, dx = dgx W with W read as stored (column-mode B),
-    and the column-column weight gradients with split-K sized to the CU count."""
+    Routing (tools/bench_gemm8.py, MI355X): the headline's dx GEMMs keep their measured
+    csrc/gemm.hip persistent tile (TUNED); every other covered shape runs on csrc/gemm8.hip —
+    row-row projections, dx = dgx W with W read as stored (column-mode B), and the
+    column-column weight gradients with split-K sized to the CU count."""
     if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
         return False
     M, K = a.shape[-2], a.shape[-1]

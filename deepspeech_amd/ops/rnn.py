@@ -1132,7 +1132,11 @@ class WgradScheduler:
             items, self.deferred = self.deferred, []
             members = [m for d in items for m in d.members]
             fused = self._fused_opt(members)
-            cap = int(os.environ.get("DS2_GROUP_CUS", "0"))
+            # the grouped launch on 3/4 of the CUs: the conv front-end's backward beside it
+            # (LDS-bound kernels that cannot share a CU with a group workgroup's 128 KB) gets
+            # the rest; headline, same box: 7.83-7.87 ms/step vs 7.89-7.90 on every CU, 7.94
+            # at 176, 7.84-7.92 at 208, 8.03 at 128
+            cap = (3 * _ext.num_cus(torch.cuda.current_device())) // 4
             if fused is not None:
                 GM.gemm8_group(members, opt=fused[0], max_grid=cap)
                 self.fused_ranges.extend(fused[1])
