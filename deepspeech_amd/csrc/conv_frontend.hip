@@ -699,6 +699,7 @@ __device__ __forceinline__ void stage_rows(bf16_t* xs, const bf16_t* xu, int t0,
 
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Fwd a) {
   __shared__ __attribute__((aligned(16))) bf16_t xs[C1_IN * C1_XS];
+  __shared__ __attribute__((aligned(16))) bf16_t ys[C1_ROWS][32 * MT * CC];   // each wave's output row (F1 <= 96)
   __shared__ float statsh[4 * 32 * 2];
   const int tid = threadIdx.x, lane = tid & 63, w = uni(tid >> 6);
   const int hi = lane >> 5, col = lane & 31;
@@ -733,7 +734,9 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Fwd a) {
         acc[m] = mfma32(av, bfr[s], acc[m]);
       }
     }
-    bf16_t* yrow = a.y + ((size_t)n * a.T1 + t1) * a.F1 * CC;
+    // the row goes through this wave's LDS row as bf16 [F1][32], then out in 16-B chunks
+    // (48 two-byte stores per lane otherwise)
+    bf16_t* yl = ys[w];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -741,12 +744,14 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Fwd a) {
         const int f1 = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hi;
         if (f1 < a.F1) {
           const bf16_t b = f2bf(acc[m][r] + bco);
-          yrow[f1 * CC + col] = b;
+          yl[f1 * CC + col] = b;
           const float vb = bf2f(b);
           ssum += vb;
           ssq += vb * vb;
         }
       }
+    i32x4* dst = (i32x4*)(a.y + ((size_t)n * a.T1 + t1) * a.F1 * CC);
+    for (int q = lane; q < a.F1 * 4; q += 64) dst[q] = ((const i32x4*)yl)[q];
   }
   write_stats(ssum, ssq, statsh, 4, a.part);
 }
