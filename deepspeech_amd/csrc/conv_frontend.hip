@@ -981,7 +981,7 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_reduce_kernel(const bf16_t* __r
                                                                const float* __restrict__ beta, float* part,
                                                                int N, int T, int F, int tmaj,
                                                                bf16_t* __restrict__ dz_cl) {
-  __shared__ bf16_t tr[32 * 97];
+  __shared__ float red[4 * 4 * 8];       // [wave][channel octet][8] per pass
   const int tid = threadIdx.x, c0 = (tid & 3) * 8;
   float mu[8], is[8], g[8], bt[8], s[8], q[8];
 #pragma unroll
@@ -1015,31 +1015,28 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_reduce_kernel(const bf16_t* __r
     }
     for (; e < total; e += step) acc8(y8[e], d8[e]);
   } else {
-    const int stride = F + 1;
-    for (int row = blockIdx.x; row < N * T; row += gridDim.x) {
+    // time-major dz [T][N][c * F + f]: chunk e of the channels-last stream is (row = n * T + t,
+    // position f, channels 8 (e & 3) ..): its 8 dz values are one time-major row's elements
+    // c * F + f (a 2-byte gather from one cache-resident row), and the channels-last copy the
+    // apply pass reads is written as one 16-B chunk. No LDS and no barriers, so the kernel
+    // streams beside the grouped weight-gradient GEMM in the step's tail.
+    const long long total = (long long)N * T * F * 4, step = (long long)gridDim.x * 256;
+    const bf16x8* y8 = (const bf16x8*)y;
+    const int c0 = (tid & 3) * 8;
+    for (long long e = (long long)blockIdx.x * 256 + tid; e < total; e += step) {
+      const long long rowf = e >> 2;
+      const int row = (int)(rowf / F), f = (int)(rowf - (long long)row * F);
       const int n = row / T, t = row - n * T;
-      const bf16_t* yr = y + (size_t)row * F * CC;
-      __syncthreads();
-      const bf16_t* dr = dz + ((size_t)t * N + n) * CC * F;
-      for (int e = tid; e < CC * F; e += 256) {
-        const int c = e / F, f = e - c * F;
-        tr[c * stride + f] = dr[e];
-      }
-      __syncthreads();
-      for (int ch = tid; ch < F * 4; ch += 256) {
-        const int f = ch >> 2;
-        bf16x8 d;
+      const bf16_t* dr = dz + ((size_t)t * N + n) * CC * F + f;
+      bf16x8 d;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = (short)tr[(c0 + j) * stride + f];
-        // the transposed (channels-last) copy, so the apply pass reads it coalesced
-        if (dz_cl != nullptr) *(bf16x8*)(dz_cl + (size_t)row * F * CC + ch * 8) = d;
-        acc8(*(const bf16x8*)(yr + ch * 8), d);
-      }
+      for (int j = 0; j < 8; ++j) d[j] = (short)dr[(c0 + j) * F];
+      if (dz_cl != nullptr) ((bf16x8*)dz_cl)[e] = d;
+      acc8(y8[e], d);
     }
   }
   // reduce over the 64 threads sharing a channel octet (tid & 3)
   __syncthreads();
-  float* red = (float*)tr;   // [4 waves][4 octets][8] floats, reused per pass
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     float* v = pass == 0 ? s : q;
