@@ -227,6 +227,40 @@ void check(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "deepspeech_amd kernel launch failed in ", what, " (code ", rc, ")");
 }
 
+// ---- cross-stream ordering on one device ------------------------------------------------
+// A default event's marker carries a system-scope release (L2 write-back + invalidate) and its
+// barrier a system-scope acquire: ~6 us of idle queue per record or wait, 80+ us when the
+// write-back meets a busy L2 (the grouped weight-gradient launch followed by the allocator's
+// record_stream events). Streams of one device only need a device-scope release.
+constexpr unsigned kLightEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+
+int64_t event_new(unsigned flags) {
+  hipEvent_t e = nullptr;
+  TORCH_CHECK(hipEventCreateWithFlags(&e, flags ? flags : kLightEvent) == hipSuccess, "hipEventCreateWithFlags");
+  return (int64_t)(intptr_t)e;
+}
+void event_free(int64_t e) { (void)hipEventDestroy((hipEvent_t)(intptr_t)e); }
+void event_record(int64_t e, int64_t stream) {
+  TORCH_CHECK(hipEventRecord((hipEvent_t)(intptr_t)e, (hipStream_t)(intptr_t)stream) == hipSuccess, "hipEventRecord");
+}
+void event_wait(int64_t stream, int64_t e) {
+  TORCH_CHECK(hipStreamWaitEvent((hipStream_t)(intptr_t)stream, (hipEvent_t)(intptr_t)e, 0) == hipSuccess,
+              "hipStreamWaitEvent");
+}
+bool event_query(int64_t e) { return hipEventQuery((hipEvent_t)(intptr_t)e) == hipSuccess; }
+
+// dst waits for everything enqueued on src so far: record + wait back to back, so one cached
+// event per host thread and device serves every pair (the wait binds to the record just made)
+void stream_wait(int64_t dst, int64_t src) {
+  if (dst == src) return;
+  static thread_local hipEvent_t evs[64] = {};
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "hipGetDevice");
+  if (evs[dev] == nullptr) TORCH_CHECK(hipEventCreateWithFlags(&evs[dev], kLightEvent) == hipSuccess, "event");
+  TORCH_CHECK(hipEventRecord(evs[dev], (hipStream_t)(intptr_t)src) == hipSuccess, "hipEventRecord");
+  TORCH_CHECK(hipStreamWaitEvent((hipStream_t)(intptr_t)dst, evs[dev], 0) == hipSuccess, "hipStreamWaitEvent");
+}
+
 void need_gpu(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
@@ -1312,6 +1346,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("store_g") = false);
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
+  m.def("event_new", &event_new, py::arg("flags") = 0);
+  m.def("event_free", &event_free);
+  m.def("event_record", &event_record);
+  m.def("event_wait", &event_wait);
+  m.def("event_query", &event_query);
+  m.def("stream_wait", &stream_wait);
   m.def("ctc_greedy", &ctc_greedy, py::arg("logits"), py::arg("lens"), py::arg("labels"), py::arg("counts"),
         py::arg("blank"), py::arg("score") = py::none());
   m.def("conv1_fwd", &conv1_fwd);

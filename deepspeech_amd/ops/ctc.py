@@ -115,7 +115,7 @@ class FusedHeadCTC(torch.autograd.Function):
     def _backward(ctx, gloss):
         from . import gemm as GM
         from .optim import arena_of, emit_grad
-        from .rnn import wgrad_stream
+        from .rnn import _stream_wait, wgrad_stream
         h, G, w16 = ctx.saved_tensors
         weight, bias = ctx.params
         T, N, H = h.shape
@@ -135,10 +135,9 @@ class FusedHeadCTC(torch.autograd.Function):
         if side is None:
             gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32 / N, K)
             return dh, gw, gb, None, None, None, None, None
-        side.wait_stream(torch.cuda.current_stream(h.device))
+        _stream_wait(side, torch.cuda.current_stream(h.device))
+        arena_of(weight).wgrad.hold(G, h2, g32)
         with torch.cuda.stream(side):
-            for t in (G, h2, g32):
-                t.record_stream(side)
             gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32 / N, K)
         return dh, gw, gb, None, None, None, None, None
 

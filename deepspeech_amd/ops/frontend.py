@@ -365,16 +365,15 @@ class FusedHead(torch.autograd.Function):
         # arena-managed weights: dW and the bias sum run on the weight-gradient side stream,
         # so the top recurrent layer's BPTT starts right after dh (they were ~75 us on the
         # critical path); the Trainer joins that stream before Adam
-        from .rnn import wgrad_stream
+        from .rnn import _stream_wait, wgrad_stream
         side = (wgrad_stream(d2.device, arena_of(weight)) if (arena_of(bias) is not None and _HEAD_SIDE)
                 else None)
         if side is None:
             gw, gb = FusedHead._weight_grads(weight, bias, d2, h2)
             return dh, gw, gb
-        side.wait_stream(torch.cuda.current_stream(d2.device))
+        _stream_wait(side, torch.cuda.current_stream(d2.device))
+        arena_of(weight).wgrad.hold(d2, h2)
         with torch.cuda.stream(side):
-            d2.record_stream(side)
-            h2.record_stream(side)
             gw, gb = FusedHead._weight_grads(weight, bias, d2, h2)
         return dh, gw, gb
 

@@ -275,6 +275,19 @@ def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], al
     return torch.addmm(b16, x2, W16.t(), alpha=alpha)
 
 
+def _stream_wait(dst, src) -> None:
+    """dst waits for the work enqueued on src so far: one event record + wait through
+    csrc/bindings.cpp stream_wait (a cached device-scope event; no event object created and
+    destroyed per call as torch's wait_stream does). Every record or wait still costs its
+    queue ~6 us (tools/probe_event_gap.py), so the backward issues as few as it can."""
+    if dst == src:
+        return
+    if src.device.index == torch.cuda.current_device():
+        _ext.ext().stream_wait(dst.cuda_stream, src.cuda_stream)
+    else:
+        dst.wait_stream(src)
+
+
 class _PendingT:
     """A queued W^T shadow: transposed on the side stream by WgradScheduler.flush_transposes."""
     __slots__ = ("W16", "wT", "side", "event")
@@ -757,9 +770,10 @@ class FusedBiLayer(torch.autograd.Function):
             if ctx.wT is not None:
                 wT = ctx.wT
                 if isinstance(wT, _PendingT):
+                    sch_t = arena_of(W_f).wgrad
                     if wT.event is None:                 # not flushed by the model: do it now
-                        arena_of(W_f).wgrad.flush_transposes()
-                    torch.cuda.current_stream(dgx.device).wait_event(wT.event)
+                        sch_t.flush_transposes()
+                    sch_t.wait_transposes(torch.cuda.current_stream(dgx.device), wT.event)
                     wT = wT.wT
                 return _mm_bf16(dgx2, wT.t()).view(T, N, D)
             return _mm_bf16(dgx2, W16).view(T, N, D)
@@ -776,11 +790,9 @@ class FusedBiLayer(torch.autograd.Function):
             # reads the transposed W^T copy, which the optimizer does not write; without that copy
             # dx would read the arena's bf16 shadow that the optimizer range rewrites, so this
             # ordering is taken only when ctx.wT exists)
-            side.wait_stream(torch.cuda.current_stream(x16.device))
+            _stream_wait(side, torch.cuda.current_stream(x16.device))
+            sch.hold(x16, dgx, dgh, hx, parts)
             with torch.cuda.stream(side):
-                for t in (x16, dgx, dgh, hx, parts):
-                    if t is not None:
-                        t.record_stream(side)
                 res = FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, None)
             dx = input_grad()
             ctx.wT = None
@@ -792,11 +804,9 @@ class FusedBiLayer(torch.autograd.Function):
         # The layer below only needs dx: its BPTT (200 of the 256 CUs, latency-bound) runs
         # while these GEMMs fill the idle CUs. Gradients land in the arena on the side
         # stream, and the bucket hooks fire inside it, so an all-reduce waits for them.
-        side.wait_stream(torch.cuda.current_stream(x16.device))
+        _stream_wait(side, torch.cuda.current_stream(x16.device))
+        sch.hold(x16, dgx, dgh, hx, parts)
         with torch.cuda.stream(side):
-            for t in (x16, dgx, dgh, hx, parts):
-                if t is not None:
-                    t.record_stream(side)
             return FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx)
 
     @staticmethod
@@ -995,6 +1005,9 @@ class WgradScheduler:
         self.early_upper_done = False
         self.early_upper_hi = 0
         self.transposes = []       # queued W^T shadows of this forward (_transpose_async)
+        self._t_events = {}        # device -> event of the last transposes flush
+        self._t_waited = set()     # streams that waited for it
+        self._hold = []            # tensors read on the side stream, released by join()
         self._fused = None         # (arena, tensors, constants, store_g): set_fused_update
         self.fused_ranges = []     # arena element ranges the grouped epilogue updated this step
         _schedulers.add(self)
@@ -1022,6 +1035,10 @@ class WgradScheduler:
 
     def discard(self) -> None:
         """Drop deferred GEMMs of an aborted backward (called at the start of a step)."""
+        if self._hold:
+            for idx, s in self.streams.items():
+                _stream_wait(torch.cuda.current_stream(idx), s)
+            self._hold.clear()
         self.deferred.clear()
         self.main_tail.clear()
         self._eob_queued = False
@@ -1043,14 +1060,35 @@ class WgradScheduler:
         C = _ext.ext()
         cur = torch.cuda.current_stream(jobs[0].W16.device)
         side = jobs[0].side
-        side.wait_stream(cur)
+        _stream_wait(side, cur)
         with torch.cuda.stream(side):
             for j in jobs:
-                j.W16.record_stream(side)
-                j.wT.record_stream(side)
+                self.hold(j.W16, j.wT)
                 C.transpose_bf16(j.W16, j.wT)
-                j.event = torch.cuda.Event()
-                j.event.record(side)
+        # one event for the whole flush, waited once per consumer stream (wait_transposes)
+        idx = side.device.index
+        ev = self._t_events.get(idx)
+        if ev is None:
+            ev = self._t_events[idx] = int(C.event_new(0))
+        C.event_record(ev, side.cuda_stream)
+        self._t_waited = set()
+        for j in jobs:
+            j.event = ev
+
+    def wait_transposes(self, stream, ev) -> None:
+        """Make ``stream`` wait for the flushed W^T transposes (once per flush and stream)."""
+        if stream.cuda_stream in self._t_waited:
+            return
+        _ext.ext().event_wait(stream.cuda_stream, ev)
+        self._t_waited.add(stream.cuda_stream)
+
+    def hold(self, *tensors) -> None:
+        """Keep tensors that side-stream work reads alive until join() has made the current
+        stream wait for the side stream, instead of record_stream: the caching allocator
+        records an event on the side stream for every such tensor it frees, and three of
+        those landing behind the grouped weight-gradient launch held the optimizer range
+        back by 80-85 us per step (tools/probe_event_gap.py: ~6 us per record alone)."""
+        self._hold.extend(t for t in tensors if t is not None)
 
     def set_early_upper(self, ranger, fn, grid: int = 0) -> None:
         """For THIS backward: once the lowest layer b whose weight gradients run beside the
@@ -1074,7 +1112,7 @@ class WgradScheduler:
         arena = arena_of(params[0]) if params else None
         if arena is None or any(arena.first_write(p) for p in params):
             return
-        torch.cuda.current_stream().wait_stream(main)    # readers of the weights issued so far
+        _stream_wait(torch.cuda.current_stream(), main)   # readers of the weights issued so far
         fn(hi, grid)
         self.early_upper_hi = hi
         self.early_upper_done = True
@@ -1098,7 +1136,7 @@ class WgradScheduler:
         arena = arena_of(params[0]) if params else None
         if arena is None or any(arena.first_write(p) for p in params):
             return
-        torch.cuda.current_stream().wait_stream(main)    # readers of the weights issued so far
+        _stream_wait(torch.cuda.current_stream(), main)   # readers of the weights issued so far
         fn()
         self.early_done = True
 
@@ -1155,7 +1193,7 @@ class WgradScheduler:
         layer's dU behind the front-end backward)."""
         if self.deferred:
             for idx, s in self.streams.items():
-                s.wait_stream(torch.cuda.current_stream(idx))
+                _stream_wait(s, torch.cuda.current_stream(idx))
                 with torch.cuda.stream(s):
                     self.flush()
             self.flush()
@@ -1187,7 +1225,8 @@ class WgradScheduler:
         """Make the current stream wait for every pending side-stream weight gradient."""
         self.drain()
         for idx, s in self.streams.items():
-            torch.cuda.current_stream(idx).wait_stream(s)
+            _stream_wait(torch.cuda.current_stream(idx), s)
+        self._hold.clear()           # frees on the current stream, ordered after the side work
 
 
 _schedulers = weakref.WeakSet()
