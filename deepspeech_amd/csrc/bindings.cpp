@@ -144,8 +144,14 @@ int ds2_fp8_quant_blocks(long long na, long long nb_el);
 int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev,
               const float* alpha_dev2, int M, int N, int K, int lda, int ldb, int ldc, int fp8, int a_col, int b_col,
               int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
-              unsigned* cnt, int cus, hipStream_t st);
+              unsigned* cnt, int cus, const struct DS2Fill* fill, hipStream_t st);
 int ds2_gemm8_splits(int K, int fp8, int S);
+struct DS2Fill {       // csrc/gemm8.hip: regions the launch's idle workgroups initialise
+  int n;
+  unsigned* ptr[8];
+  unsigned long long words[8];
+  unsigned pattern[8];
+};
 struct DS2G8Opt {      // csrc/gemm8.hip: Adam + EMA in the grouped GEMM's epilogue
   float* p;
   float* m;
@@ -1001,8 +1007,20 @@ static int dev_cus() {
 }
 
 void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, double alpha, OptT alpha_dev,
-           OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws, OptT cnt, int64_t max_grid) {
+           OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws, OptT cnt, int64_t max_grid,
+           std::vector<at::Tensor> fill, std::vector<int64_t> fill_pat) {
   const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  // fill: regions initialised by the launch's idle workgroups (multi_fill semantics)
+  TORCH_CHECK(fill.size() == fill_pat.size() && fill.size() <= 8, "gemm8: <= 8 (fill region, pattern) pairs");
+  DS2Fill fd{};
+  fd.n = (int)fill.size();
+  for (size_t i = 0; i < fill.size(); ++i) {
+    need_gpu(fill[i], "gemm8 fill region");
+    TORCH_CHECK((fill[i].numel() * fill[i].element_size()) % 4 == 0, "gemm8: fill regions of whole 32-bit words");
+    fd.ptr[i] = (unsigned*)fill[i].data_ptr();
+    fd.words[i] = (unsigned long long)fill[i].numel() * fill[i].element_size() / 4;
+    fd.pattern[i] = (unsigned)(uint32_t)fill_pat[i];
+  }
   TORCH_CHECK(fp8 ? B.scalar_type() == at::kFloat8_e4m3fn
                   : (A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16),
               "gemm8: bf16 or fp8 e4m3fn operands (both the same)");
@@ -1045,7 +1063,8 @@ void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, dou
   check(ds2_gemm8(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, dev_scalar(alpha_dev, "alpha_dev"),
                   dev_scalar(alpha_dev2, "alpha_dev2"), (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc,
                   fp8 ? 1 : 0, a_col ? 1 : 0, b_col ? 1 : 0, (int)epi, (float)alpha, (int)batch, sA, sB, sC, S, wsp,
-                  cntp, max_grid > 0 ? (int)std::min<int64_t>(max_grid, dev_cus()) : dev_cus(), cur_stream()),
+                  cntp, max_grid > 0 ? (int)std::min<int64_t>(max_grid, dev_cus()) : dev_cus(), fd.n ? &fd : nullptr,
+                  cur_stream()),
         "gemm8");
 }
 
@@ -1339,7 +1358,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm8", &gemm8, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("epi"),
         py::arg("alpha") = 1.0, py::arg("alpha_dev") = py::none(), py::arg("alpha_dev2") = py::none(),
         py::arg("a_col") = false, py::arg("b_col") = false, py::arg("splits") = 1, py::arg("ws") = py::none(),
-        py::arg("cnt") = py::none(), py::arg("max_grid") = 0);
+        py::arg("cnt") = py::none(), py::arg("max_grid") = 0, py::arg("fill") = std::vector<at::Tensor>{},
+        py::arg("fill_pat") = std::vector<int64_t>{});
   m.def("gemm8_group", &gemm8_group, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("epi"), py::arg("splits"),
         py::arg("a_col"), py::arg("b_col"), py::arg("ws"), py::arg("cnt"), py::arg("max_grid"),
         py::arg("opt") = std::vector<c10::optional<at::Tensor>>{}, py::arg("optf") = std::vector<double>{},

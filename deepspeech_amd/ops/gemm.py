@@ -136,7 +136,7 @@ def _operand(t: torch.Tensor, row_if_unit_last: bool):
 
 def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool = False,
            alpha: float = 1.0, bias: Optional[torch.Tensor] = None, max_grid: int = 0,
-           splits: Optional[int] = None) -> bool:
+           splits: Optional[int] = None, fill=None) -> bool:
     """out (=|+=) alpha * a @ b (+ bias) for 2-D (or batched 3-D) bf16 views of any unit-stride
     orientation: a [M, K], b [K, N]; out fp32 (store / accumulate) or bf16 (store, optional
     bias). Returns False (nothing launched) when the shape or strides are not covered.
@@ -144,7 +144,11 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
     Routing (tools/bench_gemm8.py, MI355X): the headline's dx GEMMs keep their measured
     csrc/gemm.hip persistent tile (TUNED); every other covered shape runs on csrc/gemm8.hip —
     row-row projections, dx = dgx W with W read as stored (column-mode B), and the
-    column-column weight gradients with split-K sized to the CU count."""
+    column-column weight gradients with split-K sized to the CU count.
+
+    fill = (regions, patterns): buffers the next kernel needs initialised (multi_fill
+    semantics), written by the gemm8 launch's idle workgroups, or by a multi_fill after the
+    GEMM on the other paths (done whenever True is returned)."""
     if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
         return False
     M, K = a.shape[-2], a.shape[-1]
@@ -168,11 +172,13 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
     batch = A.shape[0] if A.dim() == 3 else 1
     key = (M, N, K, a_col, b_col, batch)
     if _FORCE is None and key not in TUNED and gemm8_supported(M, N, K, False, a_col, b_col):
-        gemm8(A, B, out, epi, alpha, bias, a_col=a_col, b_col=b_col, max_grid=max_grid, splits=splits)
+        gemm8(A, B, out, epi, alpha, bias, a_col=a_col, b_col=b_col, max_grid=max_grid, splits=splits, fill=fill)
         return True
     if not supported(M, N, K, a_col, b_col):
         return False
     gemm(A, B, out, M, N, K, a_col, b_col, epi, alpha, bias)
+    if fill is not None:
+        _ext.ext().multi_fill(list(fill[0]), list(fill[1]))
     return True
 
 
@@ -230,7 +236,7 @@ def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_sli
 def gemm8(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = 0, alpha: float = 1.0,
           bias: Optional[torch.Tensor] = None, alpha_dev: Optional[torch.Tensor] = None,
           alpha_dev2: Optional[torch.Tensor] = None, a_col: bool = False, b_col: bool = False,
-          splits: Optional[int] = None, max_grid: int = 0) -> torch.Tensor:
+          splits: Optional[int] = None, max_grid: int = 0, fill=None) -> torch.Tensor:
     """out (=, or += for epi 2) alpha * alpha_dev * alpha_dev2 * A @ B^T (+ bias) on the stored
     operands (see the section comment); out bf16 (epi 0) or fp32 (epi 1 / 2). splits=None picks
     the k-slice count from the shape (gemm8_splits). max_grid > 0 caps the persistent grid
@@ -250,7 +256,9 @@ def gemm8(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = 0, alp
     if S > 1:
         ws = torch.empty(S * batch * M * N, device=A.device, dtype=torch.float32)
         cnt = _tile_counters(A.device, _cdiv(M, 256) * _cdiv(N, 256) * batch)
-    C.gemm8(A, B, out, bias, epi, float(alpha), alpha_dev, alpha_dev2, a_col, b_col, S, ws, cnt, max_grid)
+    regions, pats = (list(fill[0]), list(fill[1])) if fill is not None else ([], [])
+    C.gemm8(A, B, out, bias, epi, float(alpha), alpha_dev, alpha_dev2, a_col, b_col, S, ws, cnt, max_grid,
+            regions, pats)
     return out
 
 

@@ -260,19 +260,25 @@ def _stamps(kind: str, plan: "RnnPlan", grid: int, dev) -> Optional[torch.Tensor
     return t
 
 
-def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], alpha: float) -> torch.Tensor:
+def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], alpha: float,
+            fill=None) -> torch.Tensor:
     """gx = alpha * x2 W16^T + b16 (bf16): the hand-written MFMA GEMM (csrc/gemm.hip) with the
     sequence-BN scale and the bias fused in its epilogue; library GEMM only for shapes the
-    kernel does not cover (K % 32 != 0) or under DS2_GEMM=torch."""
+    kernel does not cover (K % 32 != 0) or under DS2_GEMM=torch. fill: (regions, patterns) of
+    the recurrence that follows, initialised by the GEMM launch (GM.matmul) or after it."""
     M, K = x2.shape
     N = W16.shape[0]
     if GM.enabled("proj") and x2.is_cuda:
         out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
-        if GM.matmul(x2, W16.t(), out, alpha=alpha, bias=b16):
+        if GM.matmul(x2, W16.t(), out, alpha=alpha, bias=b16, fill=fill):
             return out
     if b16 is None:
-        return torch.mm(x2, W16.t()) * alpha if alpha != 1.0 else torch.mm(x2, W16.t())
-    return torch.addmm(b16, x2, W16.t(), alpha=alpha)
+        out = torch.mm(x2, W16.t()) * alpha if alpha != 1.0 else torch.mm(x2, W16.t())
+    else:
+        out = torch.addmm(b16, x2, W16.t(), alpha=alpha)
+    if fill is not None:
+        _ext.ext().multi_fill(list(fill[0]), list(fill[1]))
+    return out
 
 
 def _stream_wait(dst, src) -> None:
@@ -360,18 +366,25 @@ def _alloc_fwd(T: int, N: int, plan: RnnPlan, dev) -> _FwdBufs:
     return b
 
 
-def _fill_fwd(b: _FwdBufs, plan: RnnPlan) -> None:
+def _fill_regions(b: _FwdBufs, plan: RnnPlan):
+    """(regions, patterns) that an XCD forward launch needs initialised."""
     ndir = plan.ndir
     hx, hs = b.hx, b.hs
     regions = ([hx[d, 0] for d in range(ndir)] + [hx[d, 1:] for d in range(ndir)] +
                [hs[d, 0] for d in range(ndir)] + [b.census] + ([b.ysum] if b.fuse else []))
-    _ext.ext().multi_fill(regions, [0] * ndir + [-1] * ndir + [0] * ndir + [-1] + ([-1] if b.fuse else []))
+    return regions, [0] * ndir + [-1] * ndir + [0] * ndir + [-1] + ([-1] if b.fuse else [])
 
 
-def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
+def _fill_fwd(b: _FwdBufs, plan: RnnPlan) -> None:
+    _ext.ext().multi_fill(*_fill_regions(b, plan))
+
+
+def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None, bufs: Optional[_FwdBufs] = None):
     """Launch the persistent forward recurrence over gx [T, N, ndir*G*H] (bf16).
     U / bh: per-direction lists (bf16 [G*H, H] / fp32 [G*H] or None).
     h0: optional initial state [ndir, N, H] (streaming state carry; zeros otherwise).
+    bufs: the launch's buffers, already initialised (the projection GEMM that produced gx
+    filled them: _alloc_fwd + _fill_regions); allocated and filled here when None.
     Returns (y [T, N, H] bf16 = sum of directions, saved-state tuple)."""
     C = _ext.ext()
     T, N, gstride = gx.shape
@@ -379,12 +392,13 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None):
     steps = T
     dev = gx.device
     d1 = ndir == 2
-    b = _alloc_fwd(T, N, plan, dev)
+    b = bufs if bufs is not None else _alloc_fwd(T, N, plan, dev)
     fuse, y2, ysum, hx, hs, gates = b.fuse, b.y2, b.ysum, b.hx, b.hs, b.gates
     if plan.kind == "xcd":
         census = b.census
         err = error_word(dev)
-        _fill_fwd(b, plan)
+        if bufs is None:
+            _fill_fwd(b, plan)
         if h0 is not None:
             hs[:, 0, :N].copy_(h0)
             hx[:, 0, :N].copy_(h0)
@@ -707,10 +721,19 @@ class FusedBiLayer(torch.autograd.Function):
         b16 = _bf16_group(dirs_b)                     # [ndir*G*H]
         x16 = x.to(torch.bfloat16).contiguous()
         x2 = x16.view(T * N, D)
+        fp8_rec = fp8 and x.is_cuda and fp8_recurrence_ok(plan, N)
+        bufs = fill = None
+        if x.is_cuda and not fp8_rec and plan.kind == "xcd":
+            # the recurrence's buffers are initialised by the projection GEMM's idle workgroups
+            # (csrc/gemm8.hip DS2Fill): no separate fill launch between the two
+            bufs = _alloc_fwd(T, N, plan, x.device)
+            fill = _fill_regions(bufs, plan)
         if fp8:
             gx = fp8_linear(x2, W16, b16, alpha).view(T, N, -1)
+            if fill is not None:
+                _ext.ext().multi_fill(*fill)
         else:
-            gx = _linear(x2, W16, b16, alpha).view(T, N, -1)
+            gx = _linear(x2, W16, b16, alpha, fill=fill).view(T, N, -1)
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
@@ -720,7 +743,7 @@ class FusedBiLayer(torch.autograd.Function):
             arena = arena_of(W_f)
             wT = _transpose_async(W16, wgrad_stream(x.device, arena), arena.wgrad if arena is not None else None)
         ctx.fp8_bwd = False
-        if fp8 and x.is_cuda and fp8_recurrence_ok(plan, N):
+        if fp8_rec:
             # config 5's fp8 mode: the recurrence too (e4m3 U and h exchange), and its BPTT on the
             # same geometry with the same e4m3 U (rnnf8_bwd_kernel; dg requantised per row). The
             # gradient is straight-through with respect to the quantisation of the exchanged h and
@@ -731,7 +754,7 @@ class FusedBiLayer(torch.autograd.Function):
             y, (hx, hs, gates) = _run_fwd_fp8(gx, lens, U, bh, plan, keep)
             ctx.fp8_quant = keep["quant"] if keep is not None else None
         else:
-            y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan)
+            y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan, bufs=bufs)
         dev = x.device
         ctx.save_for_backward(x16, lens, W16, U[0], U[1] if U[1] is not None else torch.empty(0, device=dev),
                               hx, hs, gates)

@@ -373,3 +373,36 @@ def test_adam_ema_ranges_bitwise():
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     assert torch.equal(b[0][1000:1024], bufs[0][1000:1024])
+
+
+@pytest.mark.parametrize("M,N,K", [(7712, 4800, 800), (4096, 4096, 256), (300, 328, 96)])
+def test_gemm8_idle_workgroup_fill(M, N, K):
+    """csrc/gemm8.hip DS2Fill: regions initialised by the launch's lighter workgroups — the GEMM
+    output bitwise that of a launch without fill, every region word its pattern (aligned,
+    unaligned-tail and 4-B-aligned regions), for uneven (589 tiles), even (256) and tiny grids."""
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).to(BF)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    b = torch.randn(N, device=DEV).to(BF)
+    ref = torch.empty(M, N, device=DEV, dtype=BF)
+    G.gemm8(x, w, ref, epi=0, alpha=0.5, bias=b)
+    big = torch.zeros(3 * 1024 * 1024 + 7, device=DEV, dtype=torch.int32)
+    odd = torch.zeros(1001, device=DEV, dtype=torch.int32)[1:]          # 4-B aligned, not 16-B
+    hb = torch.full((2, 242, 32, 800), 1.0, device=DEV, dtype=BF)
+    regions = [big, odd, hb[0, 0], hb[0, 1:], hb[1, 1:]]
+    pats = [-1, 0x12345678, 0, -1, -1]
+    out = torch.empty(M, N, device=DEV, dtype=BF)
+    G.gemm8(x, w, out, epi=0, alpha=0.5, bias=b, fill=(regions, pats))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert bool((big == -1).all()) and bool((odd == 0x12345678).all())
+    assert bool((hb[0, 0] == 0).all()) and bool((hb[1, 0] == 1.0).all())
+    assert bool((hb[:, 1:].view(torch.int16) == -1).all())
+
+
+def test_gemm8_fill_only_on_row_row():
+    a = torch.randn(256, 256, device=DEV).to(BF)
+    o = torch.empty(256, 256, device=DEV, dtype=torch.float32)
+    r = torch.zeros(64, device=DEV, dtype=torch.int32)
+    with pytest.raises(RuntimeError):
+        G.gemm8(a, a, o, epi=1, a_col=True, b_col=True, fill=([r], [-1]))
