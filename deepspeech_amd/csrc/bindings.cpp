@@ -209,7 +209,7 @@ int ds2_bn_cl_bwd(const void* dz, const void* y, const float* mean, const float*
                   int tmaj, int part_ready, hipStream_t st);
 int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev, int M, int N, int K,
              int lda, int ldb, int ldc, int Ml, int Nl, int Kl, int a_col, int b_col, int epi, float alpha, int batch,
-             long long sA, long long sB, long long sC, int cfg, hipStream_t st);
+             long long sA, long long sB, long long sC, int cfg, const DS2Fill* fill, hipStream_t st);
 int ds2_gemm_tile(int cfg, int* bm, int* bn);
 int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens, const int* labels,
                  const int* label_lens, float* loss, void* G, float* ws, int T, int N, int H, int K, int Lmax,
@@ -1006,21 +1006,28 @@ static int dev_cus() {
   return cus_of[dev];
 }
 
-void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, double alpha, OptT alpha_dev,
-           OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws, OptT cnt, int64_t max_grid,
-           std::vector<at::Tensor> fill, std::vector<int64_t> fill_pat) {
-  const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
-  // fill: regions initialised by the launch's idle workgroups (multi_fill semantics)
-  TORCH_CHECK(fill.size() == fill_pat.size() && fill.size() <= 8, "gemm8: <= 8 (fill region, pattern) pairs");
+// fill: regions the GEMM launch initialises for the next kernel (multi_fill semantics)
+DS2Fill make_fill(const std::vector<at::Tensor>& fill, const std::vector<int64_t>& fill_pat) {
+  TORCH_CHECK(fill.size() == fill_pat.size() && fill.size() <= 8, "<= 8 (fill region, pattern) pairs");
   DS2Fill fd{};
   fd.n = (int)fill.size();
   for (size_t i = 0; i < fill.size(); ++i) {
-    need_gpu(fill[i], "gemm8 fill region");
-    TORCH_CHECK((fill[i].numel() * fill[i].element_size()) % 4 == 0, "gemm8: fill regions of whole 32-bit words");
+    need_gpu(fill[i], "fill region");
+    TORCH_CHECK((fill[i].numel() * fill[i].element_size()) % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(fill[i].data_ptr()) & 3) == 0,
+                "fill regions of whole, aligned 32-bit words");
     fd.ptr[i] = (unsigned*)fill[i].data_ptr();
     fd.words[i] = (unsigned long long)fill[i].numel() * fill[i].element_size() / 4;
     fd.pattern[i] = (unsigned)(uint32_t)fill_pat[i];
   }
+  return fd;
+}
+
+void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, double alpha, OptT alpha_dev,
+           OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws, OptT cnt, int64_t max_grid,
+           std::vector<at::Tensor> fill, std::vector<int64_t> fill_pat) {
+  const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
+  const DS2Fill fd = make_fill(fill, fill_pat);
   TORCH_CHECK(fp8 ? B.scalar_type() == at::kFloat8_e4m3fn
                   : (A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16),
               "gemm8: bf16 or fp8 e4m3fn operands (both the same)");
@@ -1180,8 +1187,10 @@ int64_t ld_of(const at::Tensor& t, const char* name) {
 }
 
 void gemm(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t M, int64_t N, int64_t K, bool a_col,
-          bool b_col, int64_t epi, double alpha, int64_t cfg, OptT alpha_dev, int64_t Ml, int64_t Nl, int64_t Kl) {
+          bool b_col, int64_t epi, double alpha, int64_t cfg, OptT alpha_dev, int64_t Ml, int64_t Nl, int64_t Kl,
+          std::vector<at::Tensor> fill, std::vector<int64_t> fill_pat) {
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: bf16 operands");
+  const DS2Fill fd = make_fill(fill, fill_pat);
   TORCH_CHECK(epi >= 0 && epi <= 2, "gemm: epi 0..2");
   TORCH_CHECK(C.scalar_type() == (epi == 0 ? at::kBFloat16 : at::kFloat), "gemm: C dtype does not match epi");
   const int64_t lda = ld_of(A, "A"), ldb = ld_of(B, "B"), ldc = ld_of(C, "C");
@@ -1210,7 +1219,7 @@ void gemm(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t M, int64_
   const int64_t sA = batch > 1 ? A.stride(0) : 0, sB = batch > 1 ? B.stride(0) : 0, sC = batch > 1 ? C.stride(0) : 0;
   check(ds2_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), bp, ad, (int)M, (int)N, (int)K, (int)lda, (int)ldb,
                  (int)ldc, (int)Ml, (int)Nl, (int)Kl, a_col ? 1 : 0, b_col ? 1 : 0, (int)epi, (float)alpha, (int)batch,
-                 sA, sB, sC, (int)cfg, cur_stream()),
+                 sA, sB, sC, (int)cfg, fd.n ? &fd : nullptr, cur_stream()),
         "gemm");
 }
 
@@ -1396,7 +1405,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tmaj"), py::arg("part_ready") = 0);
   m.def("gemm", &gemm, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"),
         py::arg("K"), py::arg("a_col"), py::arg("b_col"), py::arg("epi"), py::arg("alpha"), py::arg("cfg"),
-        py::arg("alpha_dev") = py::none(), py::arg("Ml") = 0, py::arg("Nl") = 0, py::arg("Kl") = 0);
+        py::arg("alpha_dev") = py::none(), py::arg("Ml") = 0, py::arg("Nl") = 0, py::arg("Kl") = 0,
+        py::arg("fill") = std::vector<at::Tensor>{}, py::arg("fill_pat") = std::vector<int64_t>{});
   m.def("gemm_tile", &gemm_tile);
   m.def("head_ctc", &head_ctc);
   m.def("fc_logits", &fc_logits);

@@ -122,6 +122,52 @@ __device__ __forceinline__ float wave_max(float v) {
 
 }  // namespace ds2
 
+// Buffers the NEXT kernel of a stream needs initialised (a recurrence's h0 slots, sentinel-
+// filled exchange slots, census words, bias partials): written by a persistent GEMM launch's
+// lighter workgroups (one work unit fewer than the busiest) after their last unit, while the
+// others finish theirs, instead of by a separate multi_fill launch on the critical path
+// (csrc/fill.hip semantics: region r = words[r] 32-bit words of pattern[r]).
+struct DS2Fill {
+  int n;
+  unsigned* ptr[8];
+  unsigned long long words[8];
+  unsigned pattern[8];
+};
+
+// This workgroup's share of a DS2Fill in a persistent grid over `total` work units where XCD x
+// walks [x * tx, (x + 1) * tx) and its workgroup l (blockIdx = 8 l + x, per = gridDim / 8 of
+// them) owns units l, l + per, ...: a workgroup is light when it owns fewer than
+// ceil(tx / per), and the light ones (all of them when none is) split the regions' 16-B chunks
+// in (XCD, l) order. nthr: threads per workgroup.
+__device__ inline void fill_idle(const DS2Fill& f, int total, int tx, int nthr) {
+  const int per = gridDim.x >> 3, x = blockIdx.x & 7, l = blockIdx.x >> 3;
+  const int cmax = (tx + per - 1) / per;
+  int nl = 0, me = -1;
+  for (int xx = 0; xx < 8; ++xx) {             // uniform: scalar arithmetic
+    const int cnt = max(0, min(total, (xx + 1) * tx) - xx * tx);
+    // light workgroups of XCD xx: ceil((cnt - l) / per) < cmax, i.e. l >= cnt - (cmax - 1) * per
+    const int first = max(0, min(per, cnt - (cmax - 1) * per));
+    if (xx == x && l >= first) me = nl + (l - first);
+    nl += per - first;
+  }
+  if (nl == 0) {                               // every workgroup equally busy: all of them fill
+    nl = gridDim.x;
+    me = x * per + l;
+  }
+  if (me < 0) return;
+  const unsigned long long stride = (unsigned long long)nl * nthr;
+  const unsigned long long t0 = (unsigned long long)me * nthr + threadIdx.x;
+  for (int r = 0; r < f.n; ++r) {
+    unsigned* p = f.ptr[r];
+    const unsigned v = f.pattern[r];
+    const unsigned long long nw = f.words[r];
+    const unsigned long long n4 = ((reinterpret_cast<uintptr_t>(p) & 15) == 0) ? nw / 4 : 0;
+    const ds2::i32x4 v4 = {(int)v, (int)v, (int)v, (int)v};
+    for (unsigned long long i = t0; i < n4; i += stride) reinterpret_cast<ds2::i32x4*>(p)[i] = v4;
+    for (unsigned long long i = n4 * 4 + t0; i < nw; i += stride) p[i] = v;
+  }
+}
+
 #define DS2_HIP_CHECK(expr)                                                        \
   do {                                                                             \
     hipError_t _e = (expr);                                                        \

@@ -54,6 +54,7 @@ struct GemmArgs {
                           // for a col-mode operand whose k-rows past Kl multiply zeros)
   int epi;                // 0: bf16 = alpha*acc + bias; 1: fp32 = alpha*acc; 2: fp32 += alpha*acc
   float alpha;
+  DS2Fill fill;           // persistent configurations: regions the lighter workgroups initialise
 };
 
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
@@ -228,7 +229,12 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
     return true;
   };
   int m0, n0;
-  if (id >= id_end || !coords(id, m0, n0)) return;
+  if (id >= id_end || !coords(id, m0, n0)) {
+    if constexpr (PERS) {
+      if (g.fill.n > 0) fill_idle(g.fill, ntm * ntn, (ntm * ntn + 7) >> 3, NW * 64);
+    }
+    return;
+  }
   const bf16_t* A = g.A + (size_t)blockIdx.z * g.sA;
   const bf16_t* B = g.B + (size_t)blockIdx.z * g.sB;
   const int tid = threadIdx.x, lane = tid & 63, wave = uni(tid >> 6);
@@ -386,6 +392,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs g) {
       break;
     }
   }
+  if constexpr (PERS) {
+    if (g.fill.n > 0) fill_idle(g.fill, ntm * ntn, (ntm * ntn + 7) >> 3, NW * 64);
+  }
 }
 
 template <int AC, int BC, int FM, int FN, int WM, int WN, int NS, bool PERS = false>
@@ -440,6 +449,9 @@ int dispatch(const GemmArgs& a, int batch, int cfg, hipStream_t st) {
 
 extern "C" {
 
+int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
+                   hipStream_t st);
+
 // Returns the tile (BM, BN) of configuration cfg, or -1.
 int ds2_gemm_tile(int cfg, int* bm, int* bn) {
   static const int T[NCFG][2] = {{256, 256}, {128, 256}, {256, 128}, {128, 128}, {128, 128}, {128, 128},
@@ -455,7 +467,7 @@ int ds2_gemm_tile(int cfg, int* bm, int* bn) {
 // re-read row Kl-1 (their products must meet zeros in the other operand).
 int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev, int M, int N, int K,
              int lda, int ldb, int ldc, int Ml, int Nl, int Kl, int a_col, int b_col, int epi, float alpha, int batch,
-             long long sA, long long sB, long long sC, int cfg, hipStream_t st) {
+             long long sA, long long sB, long long sC, int cfg, const DS2Fill* fill, hipStream_t st) {
   Ml = Ml ? Ml : M;
   Nl = Nl ? Nl : N;
   Kl = Kl ? Kl : K;
@@ -477,10 +489,22 @@ int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const floa
   a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.epi = epi;
   a.alpha = alpha;
-  if (!a_col && !b_col) return dispatch<0, 0>(a, batch, cfg, st);
-  if (!a_col && b_col) return dispatch<0, 1>(a, batch, cfg, st);
-  if (a_col && b_col) return dispatch<1, 1>(a, batch, cfg, st);
-  return dispatch<1, 0>(a, batch, cfg, st);
+  a.fill = DS2Fill{};
+  // the persistent single-GEMM configurations fill from their lighter workgroups; any other
+  // launch is followed by the plain fill kernel
+  const bool fused_fill = fill != nullptr && fill->n > 0 && cfg >= 6 && batch == 1;
+  if (fused_fill) a.fill = *fill;
+  int rc;
+  if (!a_col && !b_col) rc = dispatch<0, 0>(a, batch, cfg, st);
+  else if (!a_col && b_col) rc = dispatch<0, 1>(a, batch, cfg, st);
+  else if (a_col && b_col) rc = dispatch<1, 1>(a, batch, cfg, st);
+  else rc = dispatch<1, 0>(a, batch, cfg, st);
+  if (rc == 0 && fill != nullptr && fill->n > 0 && !fused_fill) {
+    unsigned long long bytes[8];
+    for (int i = 0; i < fill->n; ++i) bytes[i] = fill->words[i] * 4;
+    rc = ds2_multi_fill(fill->n, (void* const*)fill->ptr, bytes, fill->pattern, st);
+  }
+  return rc;
 }
 
 }  // extern "C"

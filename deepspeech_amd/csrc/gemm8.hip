@@ -122,21 +122,6 @@ struct G8Prob {
 constexpr int G8_MAXP = 24;
 constexpr int G8_MAXFILL = 8;
 
-}  // namespace
-
-// Buffers the NEXT kernel of the stream needs initialised (the forward recurrence's h0 slots,
-// sentinel-filled exchange slots, census words): written by the launch's lighter workgroups
-// (one work unit fewer than the busiest) after their last unit, while the others finish theirs,
-// instead of by a separate multi_fill launch on the critical path (csrc/fill.hip semantics:
-// region r = words[r] 32-bit words of pattern[r]).
-struct DS2Fill {
-  int n;
-  unsigned* ptr[8];
-  unsigned long long words[8];
-  unsigned pattern[8];
-};
-
-namespace {
 
 using G8Opt = DS2G8Opt;
 
@@ -327,44 +312,6 @@ __device__ __forceinline__ void opt_update4(const G8Opt& o, long long e, f32x4 g
     *(uint2*)(p16 + e) = make_uint2(lo, hi);
   }
   if (o.store_g) __builtin_nontemporal_store(gv, (f32x4*)(const_cast<float*>(o.gbase) + e));
-}
-
-// the fill share of this workgroup: XCD x's workgroup l (blockIdx = 8 l + x) owns units
-// l, l + per, ... of the XCD's range, so it is light when it owns fewer than ceil(tx / per);
-// the light workgroups (all of them when none is) split the regions' 16-B chunks in
-// (XCD, l) order
-__device__ __forceinline__ int g8_units(int total, int tx, int per, int x, int l) {
-  const int cnt = max(0, min(total, (x + 1) * tx) - x * tx);
-  return cnt > l ? (cnt - l + per - 1) / per : 0;
-}
-
-__device__ void fill_idle(const DS2Fill& f, int total, int tx) {
-  const int per = gridDim.x >> 3, x = blockIdx.x & 7, l = blockIdx.x >> 3;
-  const int cmax = (tx + per - 1) / per;
-  int nl = 0, me = -1;
-  for (int xx = 0; xx < 8; ++xx) {             // uniform: scalar arithmetic
-    const int cnt = max(0, min(total, (xx + 1) * tx) - xx * tx);
-    // light workgroups of XCD xx: l with g8_units(..) < cmax, i.e. l >= cnt - (cmax - 1) * per
-    const int first = max(0, min(per, cnt - (cmax - 1) * per));
-    if (xx == x && l >= first) me = nl + (l - first);
-    nl += per - first;
-  }
-  if (nl == 0) {                               // every workgroup equally busy: all of them fill
-    nl = gridDim.x;
-    me = x * per + l;
-  }
-  if (me < 0) return;
-  const unsigned long long stride = (unsigned long long)nl * NTHR;
-  const unsigned long long t0 = (unsigned long long)me * NTHR + threadIdx.x;
-  for (int r = 0; r < f.n; ++r) {
-    unsigned* p = f.ptr[r];
-    const unsigned v = f.pattern[r];
-    const unsigned long long nw = f.words[r];
-    const unsigned long long n4 = ((reinterpret_cast<uintptr_t>(p) & 15) == 0) ? nw / 4 : 0;
-    const i32x4 v4 = {(int)v, (int)v, (int)v, (int)v};
-    for (unsigned long long i = t0; i < n4; i += stride) reinterpret_cast<i32x4*>(p)[i] = v4;
-    for (unsigned long long i = n4 * 4 + t0; i < nw; i += stride) p[i] = v;
-  }
 }
 
 template <bool FP8, int AC, int BC>
@@ -711,7 +658,7 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
   // only the row-row (projection) variant carries the fill: in the column-mode ones its live
   // values pushed the k-loop over 256 VGPRs
   if constexpr (!FP8 && AC == 0 && BC == 0) {
-    if (g.fill.n > 0) fill_idle(g.fill, total, tx);
+    if (g.fill.n > 0) fill_idle(g.fill, total, tx, NTHR);
   }
 }
 

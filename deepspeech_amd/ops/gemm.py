@@ -86,7 +86,7 @@ def _dev_cus(t: torch.Tensor) -> int:
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: int, a_col: bool, b_col: bool,
          epi: int, alpha: float = 1.0, bias: Optional[torch.Tensor] = None, cfg: Optional[int] = None,
-         alpha_dev: Optional[torch.Tensor] = None, Ml: int = 0, Nl: int = 0, Kl: int = 0) -> torch.Tensor:
+         alpha_dev: Optional[torch.Tensor] = None, Ml: int = 0, Nl: int = 0, Kl: int = 0, fill=None) -> torch.Tensor:
     """Raw launch. A/B are the STORED matrices (unit-stride last dim): A [M,K] (row) or
     [K,M] (col), B [N,K] (row) or [K,N] (col). alpha_dev: fp32 device scalar multiplied into
     alpha. Ml/Nl: a col-mode operand padded in memory to Ml/Nl columns; Kl: a col-mode
@@ -96,7 +96,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, M: int, N: int, K: i
         cfg = choose_cfg(M, N, K, a_col, b_col, batch, _dev_cus(A))
         if epi != 2 and cfg in (1, 2) and _FORCE is None:
             cfg += 6        # the persistent twin: same tile, next tile's loads under the stores
-    _ext.ext().gemm(A, B, C, bias, M, N, K, a_col, b_col, epi, float(alpha), cfg, alpha_dev, Ml, Nl, Kl)
+    regions, pats = (list(fill[0]), list(fill[1])) if fill is not None else ([], [])
+    _ext.ext().gemm(A, B, C, bias, M, N, K, a_col, b_col, epi, float(alpha), cfg, alpha_dev, Ml, Nl, Kl, regions, pats)
     return C
 
 
@@ -176,9 +177,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
         return True
     if not supported(M, N, K, a_col, b_col):
         return False
-    gemm(A, B, out, M, N, K, a_col, b_col, epi, alpha, bias)
-    if fill is not None:
-        _ext.ext().multi_fill(list(fill[0]), list(fill[1]))
+    gemm(A, B, out, M, N, K, a_col, b_col, epi, alpha, bias, fill=fill)
     return True
 
 

@@ -319,13 +319,17 @@ def _transpose_async(W16: torch.Tensor, side, sch=None):
     return job
 
 
-def _mm_bf16(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a @ b in bf16 through csrc/gemm.hip (library GEMM for uncovered shapes)."""
+def _mm_bf16(a: torch.Tensor, b: torch.Tensor, fill=None) -> torch.Tensor:
+    """a @ b in bf16 through csrc/gemm.hip (library GEMM for uncovered shapes). fill:
+    (regions, patterns) for the next kernel, initialised by the GEMM launch or after it."""
     if GM.enabled("dx") and a.is_cuda:
         out = torch.empty(a.shape[0], b.shape[1], device=a.device, dtype=torch.bfloat16)
-        if GM.matmul(a, b, out):
+        if GM.matmul(a, b, out, fill=fill):
             return out
-    return torch.mm(a, b)
+    out = torch.mm(a, b)
+    if fill is not None:
+        _ext.ext().multi_fill(list(fill[0]), list(fill[1]))
+    return out
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -545,12 +549,29 @@ def _alloc_bwd(plan: RnnPlan, want_bias: bool, dev) -> tuple:
     return census, parts, ring
 
 
-def _fill_bwd(census, parts, ring) -> None:
+def _bwd_fill_regions(census, parts, ring):
     regions, pats = [census], [-1]
     if parts is not None:
         regions.append(parts)
         pats.append(0)
-    _ext.ext().multi_fill(regions + [ring], pats + [-1])     # one launch for every init
+    return regions + [ring], pats + [-1]
+
+
+def _fill_bwd(census, parts, ring) -> None:
+    _ext.ext().multi_fill(*_bwd_fill_regions(census, parts, ring))     # one launch for every init
+
+
+# device index -> (plan, stream, (census, parts, ring)): the next BPTT's buffers, initialised by
+# the input-gradient GEMM of the layer above (FusedBiLayer._backward), so no fill launch sits
+# between that GEMM and the BPTT it feeds. Taken (once) by _run_bwd on the same plan and stream.
+_BWD_PREFILL = {}
+
+
+def _prefill_bwd(plan: "RnnPlan", dev):
+    """Allocate the next BPTT's buffers; returns the fill for the GEMM that precedes it."""
+    bufs = _alloc_bwd(plan, True, dev)
+    _BWD_PREFILL[dev.index] = (plan, torch.cuda.current_stream(dev).cuda_stream, bufs)
+    return _bwd_fill_regions(*bufs)
 
 
 def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale: float = 1.0,
@@ -572,8 +593,13 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
         err = error_word(dev)
         # generation-3 BPTT: reduce-scatter of partials through a 3-slot ring (readiness =
         # per-use tag in each word's LSB, ring filled with 0xFFFFFFFF); dgh is a plain output
-        census, parts, ring = _alloc_bwd(plan, want_bias, dev)
-        _fill_bwd(census, parts, ring)
+        pre = _BWD_PREFILL.pop(dev.index, None)
+        if (pre is not None and want_bias and pre[0] is plan and
+                pre[1] == torch.cuda.current_stream(dev).cuda_stream):
+            census, parts, ring = pre[2]
+        else:
+            census, parts, ring = _alloc_bwd(plan, want_bias, dev)
+            _fill_bwd(census, parts, ring)
         C.rnnx_bwd(dy, lens, U[0], U[1] if d1 else None, hs[0], hs[1] if d1 else None,
                    gates[0] if has_g else None, gates[1] if (has_g and d1) else None,
                    dgh[0], dgh[1] if d1 else None, dgx,
@@ -798,7 +824,11 @@ class FusedBiLayer(torch.autograd.Function):
                         sch_t.flush_transposes()
                     sch_t.wait_transposes(torch.cuda.current_stream(dgx.device), wT.event)
                     wT = wT.wT
-                return _mm_bf16(dgx2, wT.t()).view(T, N, D)
+                # the layer below's BPTT buffers ride on this GEMM (same plan in a DS2 stack;
+                # an fp8 or differently shaped layer below just leaves them unused)
+                fill = (_prefill_bwd(plan, dgx.device) if ctx.idx >= 1 and plan.kind == "xcd" and
+                        not getattr(ctx, "fp8_bwd", False) else None)
+                return _mm_bf16(dgx2, wT.t(), fill=fill).view(T, N, D)
             return _mm_bf16(dgx2, W16).view(T, N, D)
 
         # ---- weight gradients (off the critical path) ----
@@ -1111,6 +1141,12 @@ class WgradScheduler:
         records an event on the side stream for every such tensor it frees, and three of
         those landing behind the grouped weight-gradient launch held the optimizer range
         back by 80-85 us per step (tools/probe_event_gap.py: ~6 us per record alone)."""
+        if len(self._hold) > 512 and all(torch.cuda.current_stream(i) != st for i, st in self.streams.items()):
+            # a loop that never joins (bare loss.backward() without join_wgrad_streams): bound
+            # what is held by ordering the current stream after the side stream and letting go
+            for idx, st in self.streams.items():
+                _stream_wait(torch.cuda.current_stream(idx), st)
+            self._hold.clear()
         self._hold.extend(t for t in tensors if t is not None)
 
     def set_early_upper(self, ranger, fn, grid: int = 0) -> None:

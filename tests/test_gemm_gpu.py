@@ -406,3 +406,25 @@ def test_gemm8_fill_only_on_row_row():
     r = torch.zeros(64, device=DEV, dtype=torch.int32)
     with pytest.raises(RuntimeError):
         G.gemm8(a, a, o, epi=1, a_col=True, b_col=True, fill=([r], [-1]))
+
+
+@pytest.mark.parametrize("cfg", [7, 3])
+def test_gemm_fill_persistent_and_fallback(cfg):
+    """csrc/gemm.hip with a DS2Fill: the persistent configuration fills from its lighter
+    workgroups (the dx GEMM feeding the next BPTT: 244 tiles on 248 workgroups), any other runs
+    the fill kernel after; output bitwise that of a launch without fill."""
+    M, N, K = 7712, 800, 4800
+    torch.manual_seed(cfg)
+    a = torch.randn(M, K, device=DEV).to(BF)
+    wt = (torch.randn(N, K, device=DEV) * 0.05).to(BF)
+    ref = torch.empty(M, N, device=DEV, dtype=BF)
+    G.gemm(a, wt, ref, M, N, K, False, False, 0, 1.0, None, cfg=cfg)
+    census = torch.zeros(400, device=DEV, dtype=torch.int32)
+    parts = torch.full((2, 2, 4, 2400), 3.0, device=DEV)
+    ring = torch.zeros(2, 30001, device=DEV)
+    out = torch.empty(M, N, device=DEV, dtype=BF)
+    G.gemm(a, wt, out, M, N, K, False, False, 0, 1.0, None, cfg=cfg, fill=([census, parts, ring], [-1, 0, -1]))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert bool((census == -1).all()) and bool((parts == 0).all())
+    assert bool((ring.view(torch.int32) == -1).all())
