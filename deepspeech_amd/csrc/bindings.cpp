@@ -234,11 +234,12 @@ void check(int rc, const char* what) {
 }
 
 // ---- cross-stream ordering on one device ------------------------------------------------
-// A default event's marker carries a system-scope release (L2 write-back + invalidate) and its
-// barrier a system-scope acquire: ~6 us of idle queue per record or wait, 80+ us when the
-// write-back meets a busy L2 (the grouped weight-gradient launch followed by the allocator's
-// record_stream events). Streams of one device only need a device-scope release.
-constexpr unsigned kLightEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+// Events keep the default (system-scope) fences: with hipEventReleaseToDevice the next kernel
+// on the waiting queue could read lines another XCD's L2 still held stale (the ReLU
+// convergence test drifted 6-8 %), and the device-scope marker measured no cheaper (~6 us per
+// record or wait either way, tools/probe_event_gap.py). What these helpers save is the event
+// object churn of torch's wait_stream.
+constexpr unsigned kLightEvent = hipEventDisableTiming;
 
 int64_t event_new(unsigned flags) {
   hipEvent_t e = nullptr;
