@@ -60,6 +60,10 @@ def parse():
                    help="skip the streaming-inference RTF measured after the training timing "
                         "(BASELINE metric's inference half; rank 0, outside the timed region)")
     p.add_argument("--infer_seconds", type=float, default=10.0, help="audio per stream of the RTF runs")
+    p.add_argument("--no_walk", action="store_true",
+                   help="skip the SortaGrad epoch walk measured after the headline timing")
+    p.add_argument("--walk_scale", type=int, default=1,
+                   help="epoch-walk size: the reference dummy epoch's bucket counts x this (reference: 10)")
     p.add_argument("--fp8", action="store_true",
                    help="BASELINE config 5's fp8 mode: MX-fp8 e4m3 input projections and an e4m3 forward "
                         "recurrence (U and hidden-state exchange); BPTT, weight gradients and the "
@@ -145,6 +149,9 @@ def main():
     value = total_audio / elapsed
     flops = ctx.all_reduce_sum(flops)
     lossv = float(loss.float().item()) if loss is not None else float("nan")
+    walk = None
+    if not args.no_walk:
+        walk = epoch_walk(trainer, ctx, dev, args.batch_size, args.walk_scale)
     shutdown(ctx)
     infer = None
     if ctx.is_main and not args.no_infer:
@@ -176,9 +183,67 @@ def main():
             "achieved_tflops": round(flops / elapsed / 1e12, 2),
             "final_loss": round(lossv, 4),
         }
+        if walk is not None:
+            out["epoch_walk"] = walk
         if infer is not None:
             out["inference"] = infer
         print(json.dumps(out), flush=True)
+
+
+def epoch_walk(trainer, ctx, dev, batch_size: int, scale: int):
+    """SortaGrad epoch throughput, measured AFTER and outside
+    the headline timing: one dummy epoch in the reference's order — buckets of 100..1500
+    frames ascending, each bucket's batch count from src/deepSpeech_dummy.py:9-11 (x scale;
+    the reference uses 10), data/synthetic.py DummyBucketWalk — with the batches staged on
+    the device beforehand (the reference's dummy mode times data generation separately,
+    src/deepSpeech_train.py:309-312). The same trainer continues training; on one GPU it runs
+    the captured-step path with per-shape eager / replay selection (Trainer step_graphs
+    "auto"). A first pass captures and decides every shape untimed; the second pass is timed
+    (barrier + synchronize on both sides, max over ranks; audio summed over ranks). An eager
+    pass follows for comparison."""
+    import torch
+    from deepspeech_amd.data.synthetic import DummyBucketWalk, to_device
+    walk = DummyBucketWalk(batch_size, seed=77 + ctx.rank, scale_factor=scale)
+    n = walk.steps_per_epoch()
+    host = [walk.next() for _ in range(n)]
+    batches = [to_device(b, dev) for b in host]
+    audio = sum(b.audio_seconds for b in host)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def timed():
+        sync()
+        ctx.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for b in batches:
+            trainer.step(b)
+        sync()
+        ctx.barrier()
+        sync()
+        return ctx.all_reduce_max(time.perf_counter() - t0)
+
+    total_audio = ctx.all_reduce_sum(audio)
+    res = {"what": "one dummy epoch in SortaGrad order (100..1500-frame buckets ascending, "
+                   "src/deepSpeech_dummy.py counts x %d), audio-sec/sec whole job" % scale,
+           "steps": n, "audio_s": round(total_audio, 1)}
+    prev = trainer.step_graphs
+    if trainer.graphs_active() or (dev.type == "cuda" and ctx.world_size == 1):
+        trainer.step_graphs = "auto"
+    for b in batches:                     # untimed: plans, captures, per-shape decisions
+        trainer.step(b)
+    el = timed()
+    res["audio_s_per_s"] = round(total_audio / el, 1)
+    res["ms"] = round(1e3 * el, 1)
+    if trainer.graph_modes:
+        res["modes"] = {str(k[1]): m[0] for k, m in sorted(trainer.graph_modes.items())}
+    trainer.step_graphs = False
+    el_e = timed()
+    res["eager_audio_s_per_s"] = round(total_audio / el_e, 1)
+    trainer.step_graphs = prev
+    return res
 
 
 def streaming_rtf(dev, engine: str, seconds: float):

@@ -136,7 +136,7 @@ int ds2_bn_bwd(const void* dout, int dout_bf16, const void* y, int y_bf16, const
                int dy_bf16, int N, int C, int T, int F, int layout, hipStream_t st);
 int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
                  float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
-                 hipStream_t st);
+                 const float* hyper, hipStream_t st);
 int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
@@ -167,7 +167,7 @@ int ds2_gemm8_group(int np, const void* const* A, const void* const* B, void* co
                     hipStream_t st);
 int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema, void* p16, const long long* lohi,
                         int nr, float lr_t, float b1, float b2, float eps, float gscale, float ema_keep,
-                        hipStream_t st);
+                        const float* hyper, hipStream_t st);
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
                    void* a8, void* b8, float* part, float* scales, hipStream_t st);
 int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st);
@@ -717,7 +717,7 @@ void bn_bwd(at::Tensor dout, at::Tensor y, at::Tensor mean, at::Tensor invstd, a
 
 // --------------------------------------------------------------------------- optimizer
 void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, OptT p16, double lr_t, double b1,
-              double b2, double eps, double gscale, double ema_keep, OptT skip, int64_t max_grid) {
+              double b2, double eps, double gscale, double ema_keep, OptT skip, int64_t max_grid, OptT hyper) {
   need_gpu(p, "p");
   need_gpu(g, "g");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 arena expected");
@@ -726,14 +726,14 @@ void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, 
   check(ds2_adam_ema(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                      ptr_or_null<float>(ema, "ema"), ptr_or_null<void>(p16, "p16"), n, (float)lr_t, (float)b1,
                      (float)b2, (float)eps, (float)gscale, (float)ema_keep, ptr_or_null<const int>(skip, "skip"),
-                     (int)max_grid, cur_stream()),
+                     (int)max_grid, ptr_or_null<const float>(hyper, "hyper"), cur_stream()),
         "adam_ema");
 }
 
 // Adam + EMA over several (lo, hi) element ranges of whole-arena buffers in one launch
 void adam_ema_ranges(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, OptT p16,
                      std::vector<int64_t> lohi, double lr_t, double b1, double b2, double eps, double gscale,
-                     double ema_keep) {
+                     double ema_keep, OptT hyper) {
   need_gpu(p, "p");
   need_gpu(g, "g");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 arena expected");
@@ -745,7 +745,7 @@ void adam_ema_ranges(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, Opt
   check(ds2_adam_ema_ranges(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                             ptr_or_null<float>(ema, "ema"), ptr_or_null<void>(p16, "p16"), r.data(),
                             (int)(r.size() / 2), (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale,
-                            (float)ema_keep, cur_stream()),
+                            (float)ema_keep, ptr_or_null<const float>(hyper, "hyper"), cur_stream()),
         "adam_ema_ranges");
 }
 
@@ -1356,8 +1356,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_stats", &bn_stats);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);
-  m.def("adam_ema", &adam_ema);
-  m.def("adam_ema_ranges", &adam_ema_ranges);
+  m.def("adam_ema", &adam_ema, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("ema"),
+        py::arg("p16"), py::arg("lr_t"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("gscale"),
+        py::arg("ema_keep"), py::arg("skip"), py::arg("max_grid"), py::arg("hyper") = py::none());
+  m.def("adam_ema_ranges", &adam_ema_ranges, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"),
+        py::arg("ema"), py::arg("p16"), py::arg("lohi"), py::arg("lr_t"), py::arg("b1"), py::arg("b2"),
+        py::arg("eps"), py::arg("gscale"), py::arg("ema_keep"), py::arg("hyper") = py::none());
   m.def("grad_norm_blocks", &grad_norm_blocks);
   m.def("grad_norm", &grad_norm);
   m.def("cast_bf16", &cast_bf16);

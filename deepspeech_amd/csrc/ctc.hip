@@ -99,7 +99,7 @@ __global__ __launch_bounds__(64) void ctc_recur_kernel(const int* __restrict__ l
                                                        int SPmax, int blank) {
   const int b = blockIdx.x, beta = blockIdx.y, lane = threadIdx.x;
   const int len = min(lens[b], T);
-  const int L = label_lens[b];
+  const int L = min(label_lens[b], Lmax);   // a label length past the padded width reads no other row
   const int SP = 2 * L + 1;
   if (len <= 0 || L > len) {
     if (!beta && lane == 0) logp_out[b] = NEG_INF;
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const LT* __restrict__ lo
   if (w >= T * N) return;
   const int t = w / N, b = w % N;
   const int len = min(lens[b], T);
-  const int L = label_lens[b];
+  const int L = min(label_lens[b], Lmax);   // a label length past the padded width reads no other row
   const float logp = (len > 0 && L <= len) ? logp_in[b] : NEG_INF;
   const bool feasible = !(logp == NEG_INF);        // NaN stays "feasible": it must reach the loss
   if (t == 0 && lane == 0) loss[b] = feasible ? -logp : (zero_inf ? 0.f : INFINITY);
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256) void ctc_grad_lp_kernel(const int* __restrict_
   if (w >= T * N) return;
   const int t = w / N, b = w % N;
   const int len = min(lens[b], T);
-  const int L = label_lens[b];
+  const int L = min(label_lens[b], Lmax);   // a label length past the padded width reads no other row
   const float logp = (len > 0 && L <= len) ? logp_in[b] : NEG_INF;
   const bool feasible = !(logp == NEG_INF);        // NaN stays "feasible": it must reach the loss
   if (t == 0 && lane == 0) loss[b] = feasible ? -logp : (zero_inf ? 0.f : INFINITY);

@@ -11,6 +11,10 @@
 // bf16 compute copy of the weights). The gradient is pre-scaled by `gscale` (1/world for
 // the data-parallel mean, or a loss-scale inverse). A separate reduction kernel computes
 // the squared gradient norm and a non-finite flag for the NaN guard.
+// `hyper` (optional, device [2] fp32 = {lr_t, ema_keep}) replaces the two per-step scalars
+// of the argument list: a captured training step (Trainer step graphs) bakes its kernel
+// arguments into the graph, so the step-dependent values are read from device memory that
+// the host rewrites before each replay.
 #include <algorithm>
 
 #include "common.h"
@@ -76,8 +80,9 @@ __device__ __forceinline__ void adam_groups(float* __restrict__ p, const float* 
 __global__ __launch_bounds__(OPT_THREADS) void adam_ema_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ ema, bf16_t* __restrict__ p16, long long n, float lr_t, float b1, float b2, float eps,
-    float gscale, float ema_keep, const int* __restrict__ skip) {
+    float gscale, float ema_keep, const int* __restrict__ skip, const float* __restrict__ hyper) {
   if (skip != nullptr && *skip) return;
+  if (hyper != nullptr) { lr_t = hyper[0]; ema_keep = hyper[1]; }
   const long long n4 = n / 4;
   const long long stride = (long long)gridDim.x * OPT_THREADS;
   long long i = (long long)blockIdx.x * OPT_THREADS + threadIdx.x;
@@ -102,8 +107,10 @@ template <int U>
 __global__ __launch_bounds__(OPT_THREADS) void adam_ema_chunk_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ ema, bf16_t* __restrict__ p16, long long n, long long chunk4, float lr_t, float b1,
-    float b2, float eps, float gscale, float ema_keep, const int* __restrict__ skip) {
+    float b2, float eps, float gscale, float ema_keep, const int* __restrict__ skip,
+    const float* __restrict__ hyper) {
   if (skip != nullptr && *skip) return;
+  if (hyper != nullptr) { lr_t = hyper[0]; ema_keep = hyper[1]; }
   const long long n4 = n / 4;
   const long long lo = (long long)blockIdx.x * chunk4, hi = min(n4, lo + chunk4);
   long long i = lo + threadIdx.x;
@@ -135,7 +142,8 @@ struct AdamRanges {
 __global__ __launch_bounds__(OPT_THREADS) void adam_ema_ranges_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
     float* __restrict__ ema, bf16_t* __restrict__ p16, AdamRanges rg, float lr_t, float b1, float b2, float eps,
-    float gscale, float ema_keep) {
+    float gscale, float ema_keep, const float* __restrict__ hyper) {
+  if (hyper != nullptr) { lr_t = hyper[0]; ema_keep = hyper[1]; }
   const long long total = rg.pre4[rg.nr];
   const long long stride = (long long)gridDim.x * OPT_THREADS;
   int r = 0;
@@ -189,7 +197,7 @@ extern "C" {
 // of the CUs: a few workgroups stream the range instead of queueing behind it)
 int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
                  float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
-                 hipStream_t st) {
+                 const float* hyper, hipStream_t st) {
   // arenas past ~120 M parameters (config 5: 146 M) stream faster block-contiguous (1098 vs
   // 1200 us, interleaved A/B in tools/bench_adam.py); smaller ones (46 M: 278 vs 328 us, 89 M:
   // 634 vs 748) faster grid-strided
@@ -199,20 +207,20 @@ int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void*
     const int grid = (int)std::max<long long>(1, std::min<long long>(-max_grid, (n4 + OPT_THREADS - 1) / OPT_THREADS));
     const long long chunk4 = (n4 + grid - 1) / grid;
     hipLaunchKernelGGL(adam_ema_chunk_kernel<2>, dim3(grid), dim3(OPT_THREADS), 0, st, p, g, m, v, ema, (bf16_t*)p16,
-                       n, chunk4, lr_t, b1, b2, eps, gscale, ema_keep, skip);
+                       n, chunk4, lr_t, b1, b2, eps, gscale, ema_keep, skip, hyper);
     return (int)hipGetLastError();
   }
   int grid = grid_for(n);
   if (max_grid > 0 && grid > max_grid) grid = max_grid;
   hipLaunchKernelGGL(adam_ema_kernel, dim3(grid), dim3(OPT_THREADS), 0, st, p, g, m, v, ema, (bf16_t*)p16, n,
-                     lr_t, b1, b2, eps, gscale, ema_keep, skip);
+                     lr_t, b1, b2, eps, gscale, ema_keep, skip, hyper);
   return (int)hipGetLastError();
 }
 
 // lohi: nr (lo, hi) element ranges of the arena, each a multiple of 4 at both ends
 int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema, void* p16, const long long* lohi,
                         int nr, float lr_t, float b1, float b2, float eps, float gscale, float ema_keep,
-                        hipStream_t st) {
+                        const float* hyper, hipStream_t st) {
   if (nr < 0 || nr > ADAM_MAXR) return (int)hipErrorInvalidValue;
   AdamRanges rg;
   rg.nr = nr;
@@ -225,7 +233,7 @@ int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema
   }
   if (rg.pre4[nr] == 0) return 0;
   hipLaunchKernelGGL(adam_ema_ranges_kernel, dim3(grid_for(rg.pre4[nr] * 4)), dim3(OPT_THREADS), 0, st, p, g, m, v,
-                     ema, (bf16_t*)p16, rg, lr_t, b1, b2, eps, gscale, ema_keep);
+                     ema, (bf16_t*)p16, rg, lr_t, b1, b2, eps, gscale, ema_keep, hyper);
   return (int)hipGetLastError();
 }
 

@@ -284,11 +284,14 @@ class FrontendCL(torch.autograd.Function):
             wpart = torch.empty(int(C_.conv2_wgrad_part_floats(grid)), **f32)
             dw2, ip2 = _grad_buffer(w2)
             C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
-            gw2 = _deliver(w2, dw2, ip2)
             dz1 = torch.empty_like(y1)
             # two workgroups per CU; the epilogue also leaves conv1's BN-backward sums in part
             dgrid = max(1, min(N * ((T1 + 1) // 2), 2 * ctx.ncu))
             C_.conv2_dgrad(dy2, w2_16, dz1, dgrid, y1, mean1, inv1, g1f, be1f, part)
+            # reported only after the dgrad has been enqueued: a bucket whose last reporter is
+            # conv2.weight may launch its all-reduce + optimizer range (which rewrites the bf16
+            # shadow w2_16) at this call, so every reader of w2_16 must already be on the stream
+            gw2 = _deliver(w2, dw2, ip2)
         gg2, gb2, gbias2 = _deliver(g2, dg2, ipg2), _deliver(be2, db2, ipb2), _zero_grad_of(b2)
         with TR.phase(TR.bn(1, True)):
             (dg1, ipg1), (db1, ipb1) = _grad_buffer(g1), _grad_buffer(be1)

@@ -15,7 +15,7 @@ dispatch round. DS2_GEMM_CFG=<0..5> forces one tile for every call (tuning only)
 from __future__ import annotations
 
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -330,6 +330,9 @@ def gemm8_group(members, accumulate: bool = False, max_grid: int = 0, opt=None) 
 
 
 _counters: Dict[Tuple[int, int], torch.Tensor] = {}
+# replaced counter buffers stay allocated: a captured step graph (Trainer step graphs) keeps
+# the address it was captured with, so a buffer must never be freed and handed to another use
+_retired: List[torch.Tensor] = []
 
 
 def _tile_counters(dev: torch.device, n: int) -> torch.Tensor:
@@ -339,6 +342,8 @@ def _tile_counters(dev: torch.device, n: int) -> torch.Tensor:
     key = (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
     buf = _counters.get(key)
     if buf is None or buf.numel() < n:
+        if buf is not None:
+            _retired.append(buf)
         buf = torch.zeros(max(n, 4096), device=dev, dtype=torch.int32)
         _counters[key] = buf
     return buf

@@ -283,6 +283,21 @@ class FusedAdamEMA:
             _ext.ext().cast_bf16(arena.flat, self.p16)
         self._norm_part = None
         self._bad = None
+        # device {lr_t, ema_keep} read by the kernels instead of their scalar arguments while
+        # ``device_hyper`` is set (a captured step: Trainer step graphs); load_hyper() writes it
+        self.hyper = torch.zeros(2, device=dev, dtype=torch.float32) if self.use_hip else None
+        self.device_hyper = False
+
+    def load_hyper(self, lr_t: float, keep: float) -> None:
+        """Stage this update's (lr_t, ema_keep) into :attr:`hyper` on the current stream (an
+        async copy from a fresh pinned host tensor, which the caching host allocator keeps
+        alive until the copy has run). Both are rounded to fp32 exactly as the scalar kernel
+        arguments are, so a replayed update is bitwise the eager one."""
+        h = torch.tensor([lr_t, keep], dtype=torch.float32).pin_memory()
+        self.hyper.copy_(h, non_blocking=True)
+
+    def _hyper_arg(self):
+        return self.hyper if self.device_hyper else None
 
     # TF ExponentialMovingAverage with num_updates: min(decay, (1+n)/(10+n))
     def ema_keep(self, global_step: int) -> float:
@@ -338,7 +353,8 @@ class FusedAdamEMA:
         _ext.ext().adam_ema(a.flat[sl], a.grad[sl], self.m[sl], self.v[sl],
                             self.ema[sl] if self.ema is not None else None,
                             self.p16[sl] if self.p16 is not None else None,
-                            lr_t, self.b1, self.b2, self.eps, gscale, keep, skip_flag, int(max_grid))
+                            lr_t, self.b1, self.b2, self.eps, gscale, keep, skip_flag, int(max_grid),
+                            self._hyper_arg())
 
     @torch.no_grad()
     def apply_excluding(self, lo: int, hi: int, exclude, lr_t: float, keep: float, gscale: float = 1.0) -> None:
@@ -360,7 +376,8 @@ class FusedAdamEMA:
         if self.use_hip and len(todo) > 1 and len(todo) <= 64 and all(a % 4 == 0 and b % 4 == 0 for a, b in todo):
             ar = self.arena
             _ext.ext().adam_ema_ranges(ar.flat, ar.grad, self.m, self.v, self.ema, self.p16,
-                                       [x for r in todo for x in r], lr_t, self.b1, self.b2, self.eps, gscale, keep)
+                                       [x for r in todo for x in r], lr_t, self.b1, self.b2, self.eps, gscale, keep,
+                                       self._hyper_arg())
             return
         for a, b in todo:
             self.apply_range(a, b, lr_t, keep, gscale)

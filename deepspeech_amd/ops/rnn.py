@@ -1063,10 +1063,13 @@ class WgradScheduler:
         self._hold = []            # tensors read on the side stream, released by join()
         self._fused = None         # (arena, tensors, constants, store_g): set_fused_update
         self.fused_ranges = []     # arena element ranges the grouped epilogue updated this step
+        # every weight gradient on the current stream (a captured step graph: ROCm replays a
+        # graph's cross-stream edges as barrier packets between its queues)
+        self.single_stream = False
         _schedulers.add(self)
 
     def stream(self, device: torch.device) -> Optional["torch.cuda.Stream"]:
-        if device.type != "cuda" or os.environ.get("DS2_WGRAD_STREAM", "1") != "1":
+        if device.type != "cuda" or self.single_stream or os.environ.get("DS2_WGRAD_STREAM", "1") != "1":
             return None
         idx = device.index if device.index is not None else torch.cuda.current_device()
         s = self.streams.get(idx)
@@ -1089,8 +1092,9 @@ class WgradScheduler:
     def discard(self) -> None:
         """Drop deferred GEMMs of an aborted backward (called at the start of a step)."""
         if self._hold:
-            for idx, s in self.streams.items():
-                _stream_wait(torch.cuda.current_stream(idx), s)
+            if not self.single_stream:
+                for idx, s in self.streams.items():
+                    _stream_wait(torch.cuda.current_stream(idx), s)
             self._hold.clear()
         self.deferred.clear()
         self.main_tail.clear()
@@ -1283,8 +1287,9 @@ class WgradScheduler:
     def join(self) -> None:
         """Make the current stream wait for every pending side-stream weight gradient."""
         self.drain()
-        for idx, s in self.streams.items():
-            _stream_wait(torch.cuda.current_stream(idx), s)
+        if not self.single_stream:
+            for idx, s in self.streams.items():
+                _stream_wait(torch.cuda.current_stream(idx), s)
         self._hold.clear()           # frees on the current stream, ordered after the side work
 
 

@@ -17,8 +17,9 @@ No host synchronisation happens inside the step; the loss is returned as a devic
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 import os
+import time
 from typing import Dict, Optional
 
 import torch
@@ -80,10 +81,29 @@ def _check_hw_queues() -> None:
                       "call deepspeech_amd.utils.setenvs.setenvs() before anything initialises HIP" % q)
 
 
+@dataclass
+class _ShapeState:
+    seen: int = 0
+    graph: Optional["_StepGraph"] = None
+    mode: Optional[str] = None               # "eager" / "graph" once decided
+    trials: list = field(default_factory=list)
+
+
+@dataclass
+class _StepGraph:
+    graph: "torch.cuda.CUDAGraph"
+    feats: torch.Tensor
+    seq_lens: torch.Tensor
+    labels: torch.Tensor
+    label_lens: torch.Tensor
+    loss: torch.Tensor
+
+
 class Trainer:
     def __init__(self, model: DeepSpeech2, lr_schedule: LRSchedule, moving_avg_decay: Optional[float] = 0.9999,
                  world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
-                 nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False):
+                 nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False,
+                 step_graphs=False, graph_warmup: int = 2):
         self.model = model
         self._seed = {}            # (device, dtype) -> device scalar 1.0 (backward seed)
         # bf16 compute shadows of the weights only for the HIP engine (fused ops read them)
@@ -133,6 +153,14 @@ class Trainer:
                     self._layer_first.setdefault(int(n.split(".")[1]), i)
         if self.bucketer.enabled and self.arena.flat.is_cuda:
             _check_hw_queues()
+        # step graphs (False, True or "auto"): the whole single-device step (forward, CTC,
+        # backward, Adam + EMA) captured once per batch shape and replayed (see _graph_step)
+        self.step_graphs = step_graphs
+        self.graph_warmup = max(1, int(graph_warmup))
+        self._shapes: Dict[tuple, "_ShapeState"] = {}
+        # auto mode: shape key -> (chosen mode, best eager ms, best replay ms)
+        self.graph_modes: Dict[tuple, tuple] = {}
+        self._graph_pool = None
 
     def upper_range(self, b: int):
         """(end, params) of the arena range holding the FC head and the recurrent layers >= b:
@@ -147,7 +175,147 @@ class Trainer:
     def lr(self) -> float:
         return self.lr_schedule(self.global_step)
 
+    def graphs_active(self) -> bool:
+        """True when :meth:`step` runs captured step graphs: single device, HIP engine, no
+        gradient buckets (data parallelism keeps the eager step: its collectives are issued
+        from backward hooks as buckets fill)."""
+        return (self.step_graphs and self.arena.flat.is_cuda and self.model.engine == "hip"
+                and self.world == 1 and not self.bucketer.enabled and not _FUSED_OPT)
+
     def step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
+        # one Adam step count / EMA decay per training step, on the host, whatever runs it
+        lr_t, keep = self.opt.prepare(self.lr, self.global_step)
+        self.arena.ensure_bf16()      # outside any graph: a restore / EMA swap marks it dirty
+        if self.graphs_active():
+            loss = self._graph_step(batch, lr_t, keep)
+        else:
+            loss = self._body(batch, lr_t, keep)
+        self.global_step += 1
+        return loss
+
+    # ---- captured steps ---------------------------------------------------------------
+    @staticmethod
+    def graph_key(batch: Dict[str, torch.Tensor]) -> tuple:
+        """Shape key of a batch's step graph: features [N, T, F] and the label width rounded
+        up to 16 (the CTC kernels read each utterance's own label length, so zero padding
+        columns changes no result; rounding keeps one graph per length bucket)."""
+        S = int(batch["labels"].shape[1])
+        return tuple(batch["feats"].shape) + (max(16, -(-S // 16) * 16),)
+
+    @staticmethod
+    def _pad_labels(labels: torch.Tensor, width: int) -> torch.Tensor:
+        if labels.shape[1] == width:
+            return labels
+        return torch.nn.functional.pad(labels, (0, width - labels.shape[1]))
+
+    def _graph_step(self, batch: Dict[str, torch.Tensor], lr_t: float, keep: float) -> torch.Tensor:
+        """One step of this batch's shape, eager or through the shape's step graph.
+
+        The first ``graph_warmup`` steps of a new shape run eagerly (real training steps; they
+        build the recurrence plans, workspaces and split-K counters the capture then reuses),
+        the next one captures the step into a HIP graph and replays it. A replay copies the
+        batch into the graph's static inputs, stages (lr_t, ema_keep) into the optimizer's
+        device scalars and launches the graph: ~8 launches of host work instead of the eager
+        step's ~90 kernel launches, autograd and stream bookkeeping, so the short SortaGrad
+        buckets stop being host-bound (tools/host_overhead.py). ROCm replays a graph's
+        cross-stream edges as barrier packets, which costs the long buckets the overlap of the
+        weight-gradient side stream; with ``step_graphs="auto"`` each shape therefore times
+        three eager steps against three replays (host-synchronised, once per shape) and keeps
+        the faster (``graph_modes``). Both paths give bitwise the same step. All shapes share
+        one memory pool (replays never overlap, and each graph's outputs stay referenced)."""
+        key = self.graph_key(batch)
+        width = key[-1]
+        st = self._shapes.get(key)
+        if st is None:
+            st = self._shapes[key] = _ShapeState()
+        if st.mode == "eager" or (st.mode is None and st.seen < self.graph_warmup):
+            st.seen += 1
+            b = dict(batch)
+            b["labels"] = self._pad_labels(batch["labels"], width)
+            return self._body(b, lr_t, keep)
+        if st.graph is None:
+            st.graph = self._capture(batch, width)
+            if self.step_graphs != "auto":
+                st.mode = "graph"
+            return self._replay(st.graph, batch, width, lr_t, keep)
+        if st.mode == "graph":
+            return self._replay(st.graph, batch, width, lr_t, keep)
+        # auto: trial steps, alternating eager / replay, each timed between two synchronisations
+        kind = "eager" if len(st.trials) % 2 == 0 else "graph"
+        dev = self.arena.flat.device
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        if kind == "eager":
+            b = dict(batch)
+            b["labels"] = self._pad_labels(batch["labels"], width)
+            loss = self._body(b, lr_t, keep)
+        else:
+            loss = self._replay(st.graph, batch, width, lr_t, keep)
+        torch.cuda.synchronize(dev)
+        st.trials.append((kind, time.perf_counter() - t0))
+        if len(st.trials) >= 6:
+            te = min(t for k, t in st.trials if k == "eager")
+            tg = min(t for k, t in st.trials if k == "graph")
+            st.mode = "graph" if tg < te else "eager"
+            self.graph_modes[key] = (st.mode, 1e3 * te, 1e3 * tg)
+            if st.mode == "eager":
+                st.graph = None
+        return loss
+
+    def _replay(self, g: "_StepGraph", batch: Dict[str, torch.Tensor], width: int, lr_t: float,
+                keep: float) -> torch.Tensor:
+        g.feats.copy_(batch["feats"], non_blocking=True)
+        g.seq_lens.copy_(batch["seq_lens"], non_blocking=True)
+        g.label_lens.copy_(batch["label_lens"], non_blocking=True)
+        labels = batch["labels"]
+        if labels.shape[1] == width:
+            g.labels.copy_(labels, non_blocking=True)
+        else:
+            g.labels[:, labels.shape[1]:].zero_()
+            g.labels[:, :labels.shape[1]].copy_(labels, non_blocking=True)
+        self.opt.load_hyper(lr_t, keep)
+        g.graph.replay()
+        return g.loss.clone()
+
+    def _capture(self, batch: Dict[str, torch.Tensor], width: int) -> "_StepGraph":
+        dev = self.arena.flat.device
+        static = {
+            "feats": batch["feats"].clone(),
+            "seq_lens": batch["seq_lens"].clone(),
+            "labels": self._pad_labels(batch["labels"], width).clone(),
+            "label_lens": batch["label_lens"].clone(),
+        }
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(dev)
+        self.opt.device_hyper = True
+        sch = self.arena.wgrad
+        single = os.environ.get("DS2_GRAPH_STREAMS", "0") == "1"
+        sch.single_stream = single
+        try:
+            # thread_local: the train driver's prefetch thread may pin / copy while we capture
+            with torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
+                loss = self._body(static, 0.0, 0.0)
+        finally:
+            self.opt.device_hyper = False
+            sch.single_stream = False
+        return _StepGraph(graph, static["feats"], static["seq_lens"], static["labels"], static["label_lens"], loss)
+
+    def drop_graphs(self) -> None:
+        """Forget every captured step (after anything that re-allocates the arena, optimizer
+        state or model buffers the graphs were captured with)."""
+        self._shapes.clear()
+        self.graph_modes.clear()
+
+    @property
+    def _graphs(self) -> Dict[tuple, "_StepGraph"]:
+        """Captured step graphs by shape key."""
+        return {k: st.graph for k, st in self._shapes.items() if st.graph is not None}
+
+    def _body(self, batch: Dict[str, torch.Tensor], lr_t: float, keep: float) -> torch.Tensor:
+        """Forward, loss, backward and the optimizer update with a prepared (lr_t, keep): every
+        launch of a training step and no host synchronisation (capturable)."""
         model = self.model
         model.train()
         self.arena.ensure_bf16()
@@ -167,7 +335,6 @@ class Trainer:
         if per_bucket:
             # DP-native ordering: each gradient bucket's Adam + EMA range runs on the
             # bucketer's ordering stream right behind its all-reduce (bitwise the same update)
-            lr_t, keep = self.opt.prepare(self.lr, self.global_step)
             self.bucketer.set_optimizer(lambda lo, hi: self.opt.apply_range(lo, hi, lr_t, keep, gscale))
         early = (not per_bucket and self.nan_policy != "skip" and self._early_split > 0 and lazy and
                  self.arena.wgrad.grouped and self.arena.wgrad.defer_input)
@@ -175,7 +342,6 @@ class Trainer:
             # single device: the FC head's and recurrent stack's Adam + EMA range runs on the
             # weight-gradient stream right after the grouped tail GEMMs, beside the conv
             # front-end's backward (WgradScheduler.set_early_update); the front-end's range after
-            lr_t, keep = self.opt.prepare(self.lr, self.global_step)
             split, sch = self._early_split, self.arena.wgrad
             if _FUSED_OPT:
                 tensors, consts = self.opt.fused_constants(lr_t, keep, gscale)
@@ -209,8 +375,7 @@ class Trainer:
                 _, skip = self.opt.grad_norm_and_finite(gscale)
                 self.last_skip = skip
             with TR.phase(TR.EMA):
-                self.opt.step(self.lr, self.global_step, gscale=gscale, skip_flag=skip)
-        self.global_step += 1
+                self.opt.apply_range(0, self.arena.numel, lr_t, keep, gscale, skip)
         return loss.detach()
 
     def first_nonfinite_step(self) -> Optional[int]:

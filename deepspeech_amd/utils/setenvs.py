@@ -20,6 +20,12 @@ SURVEY §5.6; the CLI shims deepSpeech_train.py / deepSpeech_test.py call this f
                                          (measured at world size 1 with the DP machinery forced
                                          on: 10.01-10.08 ms/step at 4 queues, 9.39-9.43 at 8,
                                          9.35-9.45 without DP; profiles/r2_dp_readiness.md)
+          DEBUG_HIP_FORCE_GRAPH_QUEUES=1 replay a captured step graph (Trainer step graphs) on
+                                         one queue: HIP otherwise spreads a graph's parallel
+                                         branches over extra queues joined by barrier packets,
+                                         which made a 100-frame step 3.37 ms against 1.78 on
+                                         one queue (200 / 400 / 1000 frames: 2.44 / 4.85 / 7.94
+                                         against 2.43 / 3.67 / 8.08; profiles/r5_step_graphs.md)
 
 RCCL channel budget. Each RCCL channel is one workgroup that stays resident for the whole
 collective. The persistent recurrence needs P*groups co-resident workgroups, one per CU:
@@ -48,6 +54,7 @@ PLATFORMS: Dict[str, Dict[str, str]] = {
         "OMP_NUM_THREADS": "8",
         "NCCL_MAX_NCHANNELS": "32",
         "GPU_MAX_HW_QUEUES": "8",
+        "DEBUG_HIP_FORCE_GRAPH_QUEUES": "1",
     },
     "bdw": {
         "KMP_BLOCKTIME": "1", "KMP_SETTINGS": "1", "OMP_NUM_THREADS": "8", "MKL_NUM_THREADS": "8",

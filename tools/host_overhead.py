@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""Host enqueue time vs GPU time of the headline training step.
+"""Host enqueue time vs GPU time of the headline training step, per bucket length.
 
-Times K steps twice: the host-side loop alone (time until the Python loop has enqueued
-all K steps, no synchronisation inside) and the full wall time to the final
-synchronize. If host time per step approaches the GPU time per step the step is
-launch-bound and host overhead adds straight to ms/step.
-  python tools/host_overhead.py --steps 30
+For each padded length in --frames, times K steps twice: the host-side loop alone (time
+until the Python loop has enqueued all K steps, no synchronisation inside) and the full
+wall time to the final synchronize. If host time per step approaches the wall time per
+step the step is launch-bound and host overhead adds straight to ms/step (the short
+SortaGrad buckets of src/deepSpeech_dummy.py:9-11,54-87 are the case that matters).
+  python tools/host_overhead.py --steps 30 --frames 100,200,400,1000 [--graph]
+--graph times the captured-step path (Trainer(step_graphs=True)) instead of eager.
 """
 import argparse
 import os
@@ -20,6 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--num_hidden", type=int, default=800)
     ap.add_argument("--num_rnn_layers", type=int, default=5)
+    ap.add_argument("--frames", type=str, default="1000")
+    ap.add_argument("--graph", action="store_true")
     a = ap.parse_args()
     from deepspeech_amd.utils.setenvs import setenvs
     setenvs([])
@@ -31,18 +35,25 @@ def main():
     torch.manual_seed(0)
     m = DeepSpeech2(num_filters=32, num_hidden=a.num_hidden, num_rnn_layers=a.num_rnn_layers, cell="gru").to(dev)
     m.set_engine("hip", torch.bfloat16)
-    tr = Trainer(m, LRSchedule(1e-4, 10 ** 9, 0.9))
-    batch = to_device(FixedShapeBatches(32, max_frames=1000, seed=0, pool=1).next(), dev)
-    for _ in range(5):
-        tr.step(batch)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        tr.step(batch)
-    t1 = time.perf_counter()
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    print("host enqueue %.3f ms/step, wall %.3f ms/step" % (1e3 * (t1 - t0) / a.steps, 1e3 * (t2 - t0) / a.steps))
+    kw = {"step_graphs": True} if a.graph else {}
+    tr = Trainer(m, LRSchedule(1e-4, 10 ** 9, 0.9), **kw)
+    print("| frames | host enqueue ms/step | wall ms/step | audio-s/s |")
+    print("|---|---|---|---|")
+    for fr in [int(x) for x in a.frames.split(",")]:
+        batch = to_device(FixedShapeBatches(32, max_frames=fr, seed=0, pool=1).next(), dev)
+        audio = float(batch["seq_lens"].sum().item()) / 100.0
+        for _ in range(5):
+            tr.step(batch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            tr.step(batch)
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        wall = (t2 - t0) / a.steps
+        print("| %d | %.3f | %.3f | %.0f |" % (fr, 1e3 * (t1 - t0) / a.steps, 1e3 * wall, audio / wall),
+              flush=True)
 
 
 if __name__ == "__main__":
