@@ -150,7 +150,7 @@ def main():
     flops = ctx.all_reduce_sum(flops)
     lossv = float(loss.float().item()) if loss is not None else float("nan")
     walk = None
-    if not args.no_walk:
+    if not args.no_walk and dev.type == "cuda":
         walk = epoch_walk(trainer, ctx, dev, args.batch_size, args.walk_scale)
     shutdown(ctx)
     infer = None

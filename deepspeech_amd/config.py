@@ -121,6 +121,10 @@ def build_train_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--device", type=str, default="auto", help="auto | cpu | cuda")
     p.add_argument("--async_checkpoint", type=str2bool, default=True)
+    p.add_argument("--step_graphs", type=str, default="auto", choices=["auto", "on", "off"],
+                   help="single-GPU HIP engine: replay each batch shape's captured training step "
+                        "(HIP graph) instead of launching it eagerly; auto: time both once per "
+                        "shape and keep the faster (trainer.py _graph_step)")
     p.add_argument("--bucket_mb", type=float, default=32.0,
                    help="gradient all-reduce bucket size (MB) for data parallel")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", choices=["fp32", "bf16"])

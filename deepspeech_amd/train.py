@@ -171,7 +171,8 @@ def main(argv=None) -> int:
     data, steps_per_epoch = build_data(args, ctx, args.train_dir)
     trainer = Trainer(model, lr_schedule_from_args(args, steps_per_epoch), args.moving_avg_decay,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
-                      allreduce_bf16=args.allreduce_dtype == "bf16", nan_policy=args.nan_policy)
+                      allreduce_bf16=args.allreduce_dtype == "bf16", nan_policy=args.nan_policy,
+                      step_graphs={"auto": "auto", "on": True, "off": False}[args.step_graphs])
     start = 0
     rdir = resume_dir(args)
     if rdir is not None:
@@ -264,8 +265,11 @@ def main(argv=None) -> int:
             prof = None
         do_log = (step > 10 and step % args.log_every == 0) or step + 1 == args.max_steps
         do_sum = sum_on and step % args.summary_every == 0
-        do_ckpt = ctx.is_main and (step % args.checkpoint_every == 0 or step + 1 == args.max_steps)
-        if do_log or do_sum or do_ckpt:
+        # checkpoints need no host synchronisation (utils/checkpoint.py: device snapshot + side-
+        # stream copy + writer thread); --checkpoint_every 0 saves the last step only
+        do_ckpt = ctx.is_main and ((args.checkpoint_every > 0 and step % args.checkpoint_every == 0)
+                                   or step + 1 == args.max_steps)
+        if do_log or do_sum:
             lv = float(loss.item())          # host sync point
             if engine == "hip":
                 from .ops import rnn as RNN
@@ -307,13 +311,13 @@ def main(argv=None) -> int:
                 metrics.write(step, **rec)
             if do_sum:
                 write_summaries(events, step, trainer, model, args, lv, ema)
-            if do_ckpt:
-                ckpt.save(trainer, step)
+        if do_ckpt:
+            ckpt.save(trainer, step)
     if loss is not None:
         float(loss.item())
         check_divergence()
     if ckpt is not None:
-        ckpt.wait()
+        ckpt.close()
     if events is not None:
         events.close()
     source_free = prefetch.close() if prefetch is not None else True

@@ -86,7 +86,8 @@ class _ShapeState:
     seen: int = 0
     graph: Optional["_StepGraph"] = None
     mode: Optional[str] = None               # "eager" / "graph" once decided
-    trials: list = field(default_factory=list)
+    host_s: list = field(default_factory=list)     # host enqueue seconds of the eager steps
+    spans: list = field(default_factory=list)      # (start, end) events of undecided replays
 
 
 @dataclass
@@ -179,8 +180,9 @@ class Trainer:
         """True when :meth:`step` runs captured step graphs: single device, HIP engine, no
         gradient buckets (data parallelism keeps the eager step: its collectives are issued
         from backward hooks as buckets fill)."""
-        return (self.step_graphs and self.arena.flat.is_cuda and self.model.engine == "hip"
-                and self.world == 1 and not self.bucketer.enabled and not _FUSED_OPT)
+        return (bool(self.step_graphs) and self.arena.flat.is_cuda and self.model.engine == "hip"
+                and self.world == 1 and not self.bucketer.enabled and not _FUSED_OPT
+                and not getattr(self.model, "capture", False))     # activation taps: eager
 
     def step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         # one Adam step count / EMA decay per training step, on the host, whatever runs it
@@ -219,10 +221,12 @@ class Trainer:
         step's ~90 kernel launches, autograd and stream bookkeeping, so the short SortaGrad
         buckets stop being host-bound (tools/host_overhead.py). ROCm replays a graph's
         cross-stream edges as barrier packets, which costs the long buckets the overlap of the
-        weight-gradient side stream; with ``step_graphs="auto"`` each shape therefore times
-        three eager steps against three replays (host-synchronised, once per shape) and keeps
-        the faster (``graph_modes``). Both paths give bitwise the same step. All shapes share
-        one memory pool (replays never overlap, and each graph's outputs stay referenced)."""
+        weight-gradient side stream; with ``step_graphs="auto"`` each shape therefore compares
+        the device time of its first two replays (events, queried when done: no host
+        synchronisation) with the host enqueue time of its eager warm-up steps and keeps the
+        graph only when the eager step is host-bound (``graph_modes``: mode, eager host ms,
+        replay ms). Both paths give bitwise the same step. All shapes share one memory pool
+        (replays never overlap, and each graph's outputs stay referenced)."""
         key = self.graph_key(batch)
         width = key[-1]
         st = self._shapes.get(key)
@@ -232,38 +236,41 @@ class Trainer:
             st.seen += 1
             b = dict(batch)
             b["labels"] = self._pad_labels(batch["labels"], width)
-            return self._body(b, lr_t, keep)
+            t0 = time.perf_counter()
+            loss = self._body(b, lr_t, keep)
+            st.host_s.append(time.perf_counter() - t0)
+            return loss
         if st.graph is None:
             st.graph = self._capture(batch, width)
             if self.step_graphs != "auto":
                 st.mode = "graph"
-            return self._replay(st.graph, batch, width, lr_t, keep)
         if st.mode == "graph":
             return self._replay(st.graph, batch, width, lr_t, keep)
-        # auto: trial steps, alternating eager / replay, each timed between two synchronisations
-        kind = "eager" if len(st.trials) % 2 == 0 else "graph"
-        dev = self.arena.flat.device
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        if kind == "eager":
-            b = dict(batch)
-            b["labels"] = self._pad_labels(batch["labels"], width)
-            loss = self._body(b, lr_t, keep)
-        else:
-            loss = self._replay(st.graph, batch, width, lr_t, keep)
-        torch.cuda.synchronize(dev)
-        st.trials.append((kind, time.perf_counter() - t0))
-        if len(st.trials) >= 6:
-            te = min(t for k, t in st.trials if k == "eager")
-            tg = min(t for k, t in st.trials if k == "graph")
-            st.mode = "graph" if tg < te else "eager"
-            self.graph_modes[key] = (st.mode, 1e3 * te, 1e3 * tg)
+        # auto, undecided: replay between two events; decide once two replays have completed
+        # (queried, never waited for): keep the graph when its device time beats the eager
+        # step's host enqueue time — an eager step cannot finish faster than the host issues
+        # it, while a GPU-bound eager step keeps the side-stream overlap a replay loses
+        done = [(a, b) for a, b in st.spans if b.query()]
+        if len(done) >= 2:
+            tg = min(a.elapsed_time(b) for a, b in done)
+            te = 1e3 * min(st.host_s)
+            st.mode = "graph" if tg < 0.97 * te else "eager"
+            self.graph_modes[key] = (st.mode, te, tg)
+            st.spans = []
             if st.mode == "eager":
                 st.graph = None
+                b = dict(batch)
+                b["labels"] = self._pad_labels(batch["labels"], width)
+                return self._body(b, lr_t, keep)
+            return self._replay(st.graph, batch, width, lr_t, keep)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        loss = self._replay(st.graph, batch, width, lr_t, keep, events=(a, b))
+        st.spans.append((a, b))
         return loss
 
     def _replay(self, g: "_StepGraph", batch: Dict[str, torch.Tensor], width: int, lr_t: float,
-                keep: float) -> torch.Tensor:
+                keep: float, events=None) -> torch.Tensor:
         g.feats.copy_(batch["feats"], non_blocking=True)
         g.seq_lens.copy_(batch["seq_lens"], non_blocking=True)
         g.label_lens.copy_(batch["label_lens"], non_blocking=True)
@@ -274,7 +281,11 @@ class Trainer:
             g.labels[:, labels.shape[1]:].zero_()
             g.labels[:, :labels.shape[1]].copy_(labels, non_blocking=True)
         self.opt.load_hyper(lr_t, keep)
+        if events is not None:
+            events[0].record()
         g.graph.replay()
+        if events is not None:
+            events[1].record()
         return g.loss.clone()
 
     def _capture(self, batch: Dict[str, torch.Tensor], width: int) -> "_StepGraph":

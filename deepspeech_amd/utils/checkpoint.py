@@ -10,8 +10,9 @@ them: src/deepSpeech_test.py:217-220), BN moving stats.
 Here every entry is keyed by its TF variable name and stored in TF orientation (conv
 kernels HWIO), so checkpoints map 1:1 onto the reference graph's variables
 (SURVEY.md §5.4). Files are plain ``torch.save`` dicts of tensors/ints/strings that load
-with ``torch.load(weights_only=True)``. Saving is asynchronous: tensors are copied to
-host on the caller's thread (one device sync), the file write runs on a side thread.
+with ``torch.load(weights_only=True)``. Saving never blocks a GPU training thread
+(CheckpointManager: device snapshot -> side-stream copy into pinned double buffers ->
+writer thread).
 """
 from __future__ import annotations
 
@@ -221,7 +222,37 @@ def step_from_path(path: str) -> int:
     return int(path.split("/")[-1].split("-")[-1])
 
 
+class _HostSlot:
+    """One pinned host copy of the optimizer-visible state: the arena's fp32 weights, Adam m
+    and v, the EMA shadows (rows of ``flat``) and the model's buffers."""
+
+    def __init__(self, rows: int, numel: int, bufs: Dict[str, torch.Tensor]):
+        self.flat = torch.empty(rows, numel, dtype=torch.float32, pin_memory=True)
+        self.bufs = {n: torch.empty(b.shape, dtype=b.dtype, pin_memory=True) for n, b in bufs.items()}
+        self.bad = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        self.writing = False
+
+
 class CheckpointManager:
+    """model.ckpt-<step> files + the TF ``checkpoint`` state file (reference cadence: every 10
+    steps, src/deepSpeech_train.py:354-356, :471).
+
+    GPU saves never block the training thread:
+      1. on the training stream, one device-to-device copy of the arena's weights, Adam m / v
+         and EMA (plus the model buffers) into a device snapshot: ~0.3 ms per 0.74 GB (the
+         headline model) at HBM speed, ordered after the saved step's optimizer update and
+         before the next step's, so the snapshot is exactly step <step>'s state;
+      2. on a side stream, the snapshot's copy into one of two pinned host slots, and an
+         event; no host synchronisation on the training thread;
+      3. a writer thread waits for that event, maps the arena onto the TF variable names and
+         writes the file. If the writer falls behind (both slots busy), the newer snapshot
+         replaces the one still waiting and a warning is logged: the training thread never
+         waits for the disk.
+    The next save's device snapshot waits (on the stream, not the host) for the previous
+    host copy to have read the device snapshot. A save whose step, or an earlier one, had a
+    non-finite loss (the device-side watch, utils/stats.py) is not written.
+    CPU trainers (and async_save=False) take the synchronous snapshot() path."""
+
     def __init__(self, directory: str, max_to_keep: int = 100, async_save: bool = True):
         self.dir = directory
         self.max_to_keep = max_to_keep
@@ -234,57 +265,179 @@ class CheckpointManager:
         if os.path.exists(state):
             with open(state) as f:
                 self.kept = [m.group(1) for m in (re.match(r'\s*all_model_checkpoint_paths:\s*"(.*)"', l) for l in f) if m]
+        # asynchronous GPU path
+        self._cv = threading.Condition()
+        self._pending = None          # (slot, event, meta) waiting for the writer
+        self._busy = False            # the writer is writing a file
+        self._closed = False
+        self._slots: List[_HostSlot] = []
+        self._dev = None              # device snapshot: [rows, numel] + buffers + bad word
+        self._stream = None
+        self._d2h_done = None         # event: the last host copy has read the device snapshot
+        self.skipped: List[int] = []  # steps whose snapshot was replaced before it was written
+        self.written: List[int] = []
 
+    # ---- synchronous snapshot (CPU, tests, async_save=False) ------------------------------
     def snapshot(self, trainer) -> Dict[str, object]:
         out: Dict[str, object] = {}
         for k, v in model_to_tf(trainer.model).items():
             out[k] = v.detach().to("cpu", copy=True)
         for k, v in _arena_slots(trainer).items():
             out[k] = v.detach().to("cpu", copy=True)
-        if getattr(trainer.model, "param_layout", "tf") == "mkldnn":
+        return self._finish(trainer.model, out, _meta(trainer))
+
+    def _finish(self, model, out: Dict[str, object], meta: Dict[str, object]) -> Dict[str, object]:
+        if getattr(model, "param_layout", "tf") == "mkldnn":
             # engine=mkldnn_rnn / cudnn_rnn: the reference's MkldnnRNNCell blob per direction
             from .mkldnn_blob import to_mkldnn_layout
             tens = to_mkldnn_layout({k: v for k, v in out.items() if isinstance(v, torch.Tensor)})
             out = {k: v for k, v in out.items() if not isinstance(v, torch.Tensor)}
             out.update(tens)
-        out["global_step"] = int(trainer.global_step)
-        out["beta1_power"] = float(trainer.opt.b1 ** trainer.opt.t)
-        out["beta2_power"] = float(trainer.opt.b2 ** trainer.opt.t)
-        out["adam_t"] = int(trainer.opt.t)
-        out["format"] = "deepspeech_amd/tfnames/v1"
+        out.update(meta)
         return out
 
     def save(self, trainer, step: int) -> str:
-        self.wait()
-        snap = self.snapshot(trainer)
         name = "model.ckpt-%d" % step
         path = os.path.join(self.dir, name)
-
-        def write():
-            try:
-                tmp = path + ".tmp"
-                torch.save(snap, tmp)
-                os.replace(tmp, path)
-                if name in self.kept:
-                    self.kept.remove(name)
-                self.kept.append(name)
-                while len(self.kept) > self.max_to_keep:
-                    old = self.kept.pop(0)
-                    try:
-                        os.remove(os.path.join(self.dir, old))
-                    except FileNotFoundError:
-                        pass
-                write_state_file(self.dir, name, self.kept)
-            except BaseException as e:  # surfaced by wait()
-                self._error = e
-
+        if self.async_save and trainer.arena.flat.is_cuda:
+            self._save_async(trainer, step)
+            return path
+        self.wait()
+        snap = self.snapshot(trainer)
         if self.async_save:
-            self._thread = threading.Thread(target=write, daemon=True)
+            self._thread = threading.Thread(target=self._write_guarded, args=(snap, step), daemon=True)
             self._thread.start()
         else:
-            write()
-            self._raise()
+            self._write(snap, step)
         return path
+
+    # ---- file writing ----------------------------------------------------------------------
+    def _write(self, snap: Dict[str, object], step: int) -> None:
+        name = "model.ckpt-%d" % step
+        path = os.path.join(self.dir, name)
+        tmp = path + ".tmp"
+        torch.save(snap, tmp)
+        os.replace(tmp, path)
+        if name in self.kept:
+            self.kept.remove(name)
+        self.kept.append(name)
+        while len(self.kept) > self.max_to_keep:
+            old = self.kept.pop(0)
+            try:
+                os.remove(os.path.join(self.dir, old))
+            except FileNotFoundError:
+                pass
+        write_state_file(self.dir, name, self.kept)
+        self.written.append(step)
+
+    def _write_guarded(self, snap, step) -> None:
+        try:
+            self._write(snap, step)
+        except BaseException as e:  # surfaced by wait()
+            self._error = e
+
+    # ---- asynchronous GPU path -------------------------------------------------------------
+    def _save_async(self, trainer, step: int) -> None:
+        self._raise()
+        arena, opt = trainer.arena, trainer.opt
+        srcs = [arena.flat, opt.m, opt.v] + ([opt.ema] if opt.ema is not None else [])
+        bufs = {n: b for n, b in trainer.model.named_buffers()}
+        in_arena = set(arena.names)
+        bufs.update({n: p.detach() for n, p in trainer.model.named_parameters() if n not in in_arena})
+        dev = arena.flat.device
+        if self._dev is None or self._dev[0].shape != (len(srcs), arena.numel):
+            self.wait()
+            self._dev = (torch.empty(len(srcs), arena.numel, device=dev, dtype=torch.float32),
+                         {n: torch.empty_like(b) for n, b in bufs.items()},
+                         torch.empty(1, device=dev, dtype=torch.int32))
+            self._slots = [_HostSlot(len(srcs), arena.numel, bufs) for _ in range(2)]
+            self._stream = torch.cuda.Stream(device=dev)
+            self._d2h_done = None
+            self._start_writer()
+        dflat, dbufs, dbad = self._dev
+        main = torch.cuda.current_stream(dev)
+        if self._d2h_done is not None:
+            main.wait_event(self._d2h_done)       # the previous host copy has read the snapshot
+        for i, t in enumerate(srcs):
+            dflat[i].copy_(t)
+        for n, b in bufs.items():
+            dbufs[n].copy_(b)
+        dbad.copy_(trainer.watch.first_bad)
+        with self._cv:
+            slot = next((s for s in self._slots if not s.writing and
+                         (self._pending is None or s is not self._pending[0])), None)
+            if slot is None:
+                # both slots taken (one being written, one waiting): the newest state wins
+                slot = self._pending[0]
+                self.skipped.append(self._pending[2]["step"])
+                print("checkpoint writer behind: step %d replaced by step %d before it was written"
+                      % (self._pending[2]["step"], step), flush=True)
+                self._pending = None
+        side = self._stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            slot.flat.copy_(dflat, non_blocking=True)
+            for n, b in dbufs.items():
+                slot.bufs[n].copy_(b, non_blocking=True)
+            slot.bad.copy_(dbad, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        self._d2h_done = ev
+        meta = _meta(trainer)
+        meta["step"] = step
+        meta["watch_base"] = int(trainer.watch._base)
+        with self._cv:
+            self._pending = (slot, ev, meta, trainer.model, list(zip(arena.names, arena.offsets)), len(srcs))
+            self._cv.notify_all()
+
+    def _start_writer(self) -> None:
+        if self._thread is not None:
+            return
+        self._thread = threading.Thread(target=self._writer_loop, daemon=True)
+        self._thread.start()
+
+    def _writer_loop(self) -> None:
+        while True:
+            with self._cv:
+                while self._pending is None and not self._closed:
+                    self._cv.wait()
+                if self._pending is None and self._closed:
+                    return
+                job, self._pending = self._pending, None
+                slot = job[0]
+                slot.writing = True
+                self._busy = True
+            try:
+                self._write_job(*job)
+            except BaseException as e:   # surfaced by wait() / the next save()
+                self._error = e
+            finally:
+                with self._cv:
+                    slot.writing = False
+                    self._busy = False
+                    self._cv.notify_all()
+
+    def _write_job(self, slot: "_HostSlot", ev, meta, model, layout, rows) -> None:
+        ev.synchronize()
+        step = meta.pop("step")
+        base = meta.pop("watch_base")
+        bad = int(slot.bad[0])
+        if bad >= 0 and base + bad <= step:
+            print("checkpoint for step %d not written: non-finite loss at step %d" % (step, base + bad), flush=True)
+            return
+        names = {tn: (tf, to_tf) for tf, tn, to_tf, _ in tf_name_map(model)}
+        params = dict(model.named_parameters())
+        out: Dict[str, object] = {}
+        suffixes = ["", ADAM_M, ADAM_V] + ([EMA_SUFFIX] if rows == 4 else [])
+        for tn, (o, n) in layout:
+            tf, to_tf = names[tn]
+            shape = params[tn].shape
+            for r, suf in enumerate(suffixes):
+                out[tf + suf] = to_tf(slot.flat[r, o:o + n].view(shape)).clone()
+        for tf, tn, to_tf, _ in tf_name_map(model):
+            if tn in slot.bufs:
+                out[tf] = to_tf(slot.bufs[tn]).clone()
+        self._write(self._finish(model, out, meta), step)
 
     def _raise(self):
         if self._error is not None:
@@ -292,10 +445,33 @@ class CheckpointManager:
             raise e
 
     def wait(self) -> None:
-        if self._thread is not None:
+        """Block until every requested checkpoint is on disk (or surfaced its error)."""
+        if self._slots:
+            with self._cv:
+                while self._pending is not None or self._busy:
+                    self._cv.wait(timeout=1.0)
+        elif self._thread is not None:
             self._thread.join()
             self._thread = None
         self._raise()
+
+    def close(self) -> None:
+        self.wait()
+        if self._slots:
+            with self._cv:
+                self._closed = True
+                self._cv.notify_all()
+            if self._thread is not None:
+                self._thread.join()
+                self._thread = None
+
+
+def _meta(trainer) -> Dict[str, object]:
+    return {"global_step": int(trainer.global_step),
+            "beta1_power": float(trainer.opt.b1 ** trainer.opt.t),
+            "beta2_power": float(trainer.opt.b2 ** trainer.opt.t),
+            "adam_t": int(trainer.opt.t),
+            "format": "deepspeech_amd/tfnames/v1"}
 
 
 def load_checkpoint_file(path: str) -> Dict[str, object]:

@@ -67,7 +67,7 @@ def main():
                 pname = next((nm for nm, (o, c) in zip(A.arena.names, A.arena.offsets) if o <= idx < o + c), "?")
                 bad.append("%s(max %.3g at %s, %d elems)" % (n, float(d.max()), pname, int((d > 0).sum())))
         st = B._shapes.get(B.graph_key(b)) if hasattr(B, "_shapes") else None
-        phase = "" if st is None else "mode=%s seen=%d trials=%d graph=%s" % (st.mode, st.seen, len(st.trials), st.graph is not None)
+        phase = "" if st is None else "mode=%s seen=%d spans=%d graph=%s" % (st.mode, st.seen, len(st.spans), st.graph is not None)
         print("step %2d T=%d loss %s %s | %s %s" % (i, b["feats"].shape[1], float(la), float(lb),
                                                    "OK" if not bad else "DIFF " + " ".join(bad), phase), flush=True)
     print("modes", getattr(B, "graph_modes", None))
