@@ -3,6 +3,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Timing-only diagnostic switches of the persistent recurrence kernels (DS2_RNNX_KNOBS bits
+// 2, 4, 8, 32: skip output stores, waits, MFMAs or publishes — wrong results by design).
+// They exist only in a diagnostic build (python build.py --variant timing -D DS2_TIMING_KNOBS,
+// loaded with DS2_EXT_SO); the default build folds every such test to false, so no stray
+// environment variable can corrupt a training run (ops/rnn.py refuses those bits without it).
+#ifdef DS2_TIMING_KNOBS
+#define DS2_TKNOB(knobs, bit) (((knobs) & (bit)) != 0)
+#else
+#define DS2_TKNOB(knobs, bit) false
+#endif
+
 namespace ds2 {
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA 16x16x32 A/B fragment

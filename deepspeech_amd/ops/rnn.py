@@ -68,6 +68,19 @@ class RnnPlan:
 
 
 RNNX_KNOBS = int(os.environ.get("DS2_RNNX_KNOBS", "0"))   # diagnostic timing switches only
+# knob bits that skip work (wrong results): honoured only by a DS2_TIMING_KNOBS build
+TIMING_ONLY_KNOBS = 2 | 4 | 8 | 32
+
+
+def check_knobs() -> None:
+    """Refuse DS2_RNNX_KNOBS bits that skip work unless the loaded extension is the diagnostic
+    timing build (csrc/common.h DS2_TKNOB): the default build compiles those branches out, so
+    such a bit would silently time a different kernel than the caller believes."""
+    bad = RNNX_KNOBS & TIMING_ONLY_KNOBS
+    if bad and not bool(_ext.ext().timing_knobs_build()):
+        raise RuntimeError("DS2_RNNX_KNOBS bits 0x%x skip work (timing only, wrong results) and exist only in "
+                           "the diagnostic build: python build.py --variant timing -D DS2_TIMING_KNOBS, "
+                           "then DS2_EXT_SO=ab/_C_timing*.so" % bad)
 _FUSE_DIRSUM = True        # module switch: tests compare the fused direction sum with torch.add
 # split-K of a dU GEMM issued beside the next layer's BPTT (data-parallel runs, where the
 # weight gradients are not deferred): measured 2 (1: 9.21-9.29, 3: 9.09-9.15, 2: 8.98-9.03 ms/step)
@@ -1328,6 +1341,7 @@ def plan_for(N: int, H: int, cell: str, ndir: int, device: torch.device) -> RnnP
            os.environ.get("DS2_RNNX_MINR"))
     p = _plan_cache.get(key)
     if p is None:
+        check_knobs()
         p = make_plan(N, H, cell, ndir, _ext.num_cus(device.index or 0))
         _plan_cache[key] = p
     return p

@@ -312,7 +312,7 @@ def main(argv=None) -> int:
             if do_sum:
                 write_summaries(events, step, trainer, model, args, lv, ema)
         if do_ckpt:
-            ckpt.save(trainer, step)
+            ckpt.save(trainer, step, force=step + 1 == args.max_steps)
     if loss is not None:
         float(loss.item())
         check_divergence()

@@ -106,6 +106,9 @@ class Trainer:
                  nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False,
                  step_graphs=False, graph_warmup: int = 2):
         self.model = model
+        if model.engine == "hip":
+            from .ops.rnn import check_knobs
+            check_knobs()            # timing-only kernel switches never reach a training run
         self._seed = {}            # (device, dtype) -> device scalar 1.0 (backward seed)
         # bf16 compute shadows of the weights only for the HIP engine (fused ops read them)
         self.arena = ParamArena(model, bf16_shadow=(model.engine == "hip"))

@@ -242,15 +242,17 @@ class CheckpointManager:
          and EMA (plus the model buffers) into a device snapshot: ~0.3 ms per 0.74 GB (the
          headline model) at HBM speed, ordered after the saved step's optimizer update and
          before the next step's, so the snapshot is exactly step <step>'s state;
-      2. on a side stream, the snapshot's copy into one of two pinned host slots, and an
+      2. on a side stream, the snapshot's copy into a pinned host slot, and an
          event; no host synchronisation on the training thread;
       3. a writer thread waits for that event, maps the arena onto the TF variable names and
-         writes the file. If the writer falls behind (both slots busy), the newer snapshot
-         replaces the one still waiting and a warning is logged: the training thread never
-         waits for the disk.
-    The next save's device snapshot waits (on the stream, not the host) for the previous
-    host copy to have read the device snapshot. A save whose step, or an earlier one, had a
-    non-finite loss (the device-side watch, utils/stats.py) is not written.
+         writes the file.
+    The training thread never waits for the disk: a save requested while the writer is still
+    busy with an earlier file takes no snapshot at all (no copies; counted in ``skipped``,
+    logged once per stretch), so the file written next is the newest state at the first save
+    after the writer frees up. ``force=True`` (the last step of a run) waits for the writer
+    instead. The next save's device snapshot waits (on the stream, not the host) for the
+    previous host copy to have read the device snapshot. A save whose step, or an earlier
+    one, had a non-finite loss (the device-side watch, utils/stats.py) is not written.
     CPU trainers (and async_save=False) take the synchronous snapshot() path."""
 
     def __init__(self, directory: str, max_to_keep: int = 100, async_save: bool = True):
@@ -274,8 +276,9 @@ class CheckpointManager:
         self._dev = None              # device snapshot: [rows, numel] + buffers + bad word
         self._stream = None
         self._d2h_done = None         # event: the last host copy has read the device snapshot
-        self.skipped: List[int] = []  # steps whose snapshot was replaced before it was written
+        self.skipped: List[int] = []  # saves requested while the writer was busy (no snapshot)
         self.written: List[int] = []
+        self._behind = False
 
     # ---- synchronous snapshot (CPU, tests, async_save=False) ------------------------------
     def snapshot(self, trainer) -> Dict[str, object]:
@@ -296,12 +299,13 @@ class CheckpointManager:
         out.update(meta)
         return out
 
-    def save(self, trainer, step: int) -> str:
+    def save(self, trainer, step: int, force: bool = False) -> Optional[str]:
+        """Checkpoint ``trainer`` as model.ckpt-<step>; returns the path, or None when the save
+        was skipped because the writer is still busy (GPU, not forced)."""
         name = "model.ckpt-%d" % step
         path = os.path.join(self.dir, name)
         if self.async_save and trainer.arena.flat.is_cuda:
-            self._save_async(trainer, step)
-            return path
+            return path if self._save_async(trainer, step, force) else None
         self.wait()
         snap = self.snapshot(trainer)
         if self.async_save:
@@ -337,8 +341,20 @@ class CheckpointManager:
             self._error = e
 
     # ---- asynchronous GPU path -------------------------------------------------------------
-    def _save_async(self, trainer, step: int) -> None:
+    def _save_async(self, trainer, step: int, force: bool) -> bool:
         self._raise()
+        with self._cv:
+            if self._slots and (self._busy or self._pending is not None):
+                if not force:
+                    if not self._behind:
+                        print("checkpoint writer busy: skipping saves from step %d until it is free" % step,
+                              flush=True)
+                    self._behind = True
+                    self.skipped.append(step)
+                    return False
+                while self._busy or self._pending is not None:
+                    self._cv.wait(timeout=1.0)
+            self._behind = False
         arena, opt = trainer.arena, trainer.opt
         srcs = [arena.flat, opt.m, opt.v] + ([opt.ema] if opt.ema is not None else [])
         bufs = {n: b for n, b in trainer.model.named_buffers()}
@@ -350,7 +366,8 @@ class CheckpointManager:
             self._dev = (torch.empty(len(srcs), arena.numel, device=dev, dtype=torch.float32),
                          {n: torch.empty_like(b) for n, b in bufs.items()},
                          torch.empty(1, device=dev, dtype=torch.int32))
-            self._slots = [_HostSlot(len(srcs), arena.numel, bufs) for _ in range(2)]
+            # one pinned slot: a snapshot is only taken while the writer is idle (see save)
+            self._slots = [_HostSlot(len(srcs), arena.numel, bufs)]
             self._stream = torch.cuda.Stream(device=dev)
             self._d2h_done = None
             self._start_writer()
@@ -364,15 +381,7 @@ class CheckpointManager:
             dbufs[n].copy_(b)
         dbad.copy_(trainer.watch.first_bad)
         with self._cv:
-            slot = next((s for s in self._slots if not s.writing and
-                         (self._pending is None or s is not self._pending[0])), None)
-            if slot is None:
-                # both slots taken (one being written, one waiting): the newest state wins
-                slot = self._pending[0]
-                self.skipped.append(self._pending[2]["step"])
-                print("checkpoint writer behind: step %d replaced by step %d before it was written"
-                      % (self._pending[2]["step"], step), flush=True)
-                self._pending = None
+            slot = next(s for s in self._slots if not s.writing)
         side = self._stream
         side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -389,6 +398,7 @@ class CheckpointManager:
         with self._cv:
             self._pending = (slot, ev, meta, trainer.model, list(zip(arena.names, arena.offsets)), len(srcs))
             self._cv.notify_all()
+        return True
 
     def _start_writer(self) -> None:
         if self._thread is not None:

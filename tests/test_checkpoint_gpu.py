@@ -62,9 +62,9 @@ def test_async_checkpoint_is_bitwise_the_synchronous_snapshot(cuda, tmp_path, gr
     assert torch.equal(b.arena.flat, c.arena.flat) and torch.equal(b.opt.ema, c.opt.ema)
 
 
-def test_writer_behind_keeps_newest_snapshot(cuda, tmp_path):
-    """Both host slots busy: the snapshot still waiting is replaced by the newer one (logged)
-    instead of the training thread waiting for the disk."""
+def test_writer_behind_skips_saves_without_blocking(cuda, tmp_path):
+    """Writer busy: saves requested meanwhile take no snapshot and return at once (the training
+    thread never waits for the disk); a forced save (end of training) waits and is written."""
     from deepspeech_amd.utils import checkpoint as CK
     base = _base(cuda)
     batch = to_device(FixedShapeBatches(8, max_frames=300, seed=6, pool=1).next(), cuda)
@@ -77,12 +77,15 @@ def test_writer_behind_keeps_newest_snapshot(cuda, tmp_path):
         real(snap, step)
     ck._write = slow
     t0 = time.perf_counter()
+    paths = []
     for s in range(4):
         a.step(batch)
-        ck.save(a, s)
+        paths.append(ck.save(a, s))
     issued = time.perf_counter() - t0
+    a.step(batch)
+    assert ck.save(a, 4, force=True) is not None
     ck.close()
     assert issued < 1.0, issued                 # never waited for the 1 s writes
-    assert ck.written[0] == 0 and ck.written[-1] == 3
-    assert ck.skipped and set(ck.skipped) | set(ck.written) == {0, 1, 2, 3}
-    assert os.path.exists(str(tmp_path / "model.ckpt-3"))
+    assert paths[0] is not None and paths[1:] == [None] * 3
+    assert ck.written == [0, 4] and ck.skipped == [1, 2, 3]
+    assert CK.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-4")
