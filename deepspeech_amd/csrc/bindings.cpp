@@ -145,7 +145,7 @@ int ds2_fp8_quant_blocks(long long na, long long nb_el);
 int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev,
               const float* alpha_dev2, int M, int N, int K, int lda, int ldb, int ldc, int fp8, int a_col, int b_col,
               int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
-              unsigned* cnt, int cus, const struct DS2Fill* fill, hipStream_t st);
+              unsigned* cnt, int cus, const struct DS2Fill* fill, int ext_red, hipStream_t st);
 int ds2_gemm8_splits(int K, int fp8, int S);
 struct DS2Fill {       // csrc/gemm8.hip: regions the launch's idle workgroups initialise
   int n;
@@ -1027,7 +1027,7 @@ DS2Fill make_fill(const std::vector<at::Tensor>& fill, const std::vector<int64_t
 
 void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, double alpha, OptT alpha_dev,
            OptT alpha_dev2, bool a_col, bool b_col, int64_t splits, OptT ws, OptT cnt, int64_t max_grid,
-           std::vector<at::Tensor> fill, std::vector<int64_t> fill_pat) {
+           std::vector<at::Tensor> fill, std::vector<int64_t> fill_pat, bool ext_red) {
   const bool fp8 = A.scalar_type() == at::kFloat8_e4m3fn;
   const DS2Fill fd = make_fill(fill, fill_pat);
   TORCH_CHECK(fp8 ? B.scalar_type() == at::kFloat8_e4m3fn
@@ -1073,7 +1073,7 @@ void gemm8(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t epi, dou
                   dev_scalar(alpha_dev2, "alpha_dev2"), (int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)ldc,
                   fp8 ? 1 : 0, a_col ? 1 : 0, b_col ? 1 : 0, (int)epi, (float)alpha, (int)batch, sA, sB, sC, S, wsp,
                   cntp, max_grid > 0 ? (int)std::min<int64_t>(max_grid, dev_cus()) : dev_cus(), fd.n ? &fd : nullptr,
-                  cur_stream()),
+                  ext_red ? 1 : 0, cur_stream()),
         "gemm8");
 }
 
@@ -1374,7 +1374,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("alpha") = 1.0, py::arg("alpha_dev") = py::none(), py::arg("alpha_dev2") = py::none(),
         py::arg("a_col") = false, py::arg("b_col") = false, py::arg("splits") = 1, py::arg("ws") = py::none(),
         py::arg("cnt") = py::none(), py::arg("max_grid") = 0, py::arg("fill") = std::vector<at::Tensor>{},
-        py::arg("fill_pat") = std::vector<int64_t>{});
+        py::arg("fill_pat") = std::vector<int64_t>{}, py::arg("ext_red") = false);
   m.def("gemm8_group", &gemm8_group, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("epi"), py::arg("splits"),
         py::arg("a_col"), py::arg("b_col"), py::arg("ws"), py::arg("cnt"), py::arg("max_grid"),
         py::arg("opt") = std::vector<c10::optional<at::Tensor>>{}, py::arg("optf") = std::vector<double>{},

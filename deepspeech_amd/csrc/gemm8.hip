@@ -125,6 +125,21 @@ constexpr int G8_MAXFILL = 8;
 
 using G8Opt = DS2G8Opt;
 
+// Epilogue arithmetic with every rounding spelled out (no compiler-chosen contraction), shared
+// by the GEMM's own epilogue and g8_reduce_kernel so both give bitwise the same C
+__device__ __forceinline__ uint2 epi_bf16(float alpha, f32x4 v, const float (&bv)[4]) {
+  const unsigned lo = (unsigned)f2bf(__fmaf_rn(alpha, v[0], bv[0])) | ((unsigned)f2bf(__fmaf_rn(alpha, v[1], bv[1])) << 16);
+  const unsigned hi = (unsigned)f2bf(__fmaf_rn(alpha, v[2], bv[2])) | ((unsigned)f2bf(__fmaf_rn(alpha, v[3], bv[3])) << 16);
+  return make_uint2(lo, hi);
+}
+__device__ __forceinline__ float4 epi_f32(float alpha, f32x4 v) {
+  return make_float4(__fmul_rn(alpha, v[0]), __fmul_rn(alpha, v[1]), __fmul_rn(alpha, v[2]), __fmul_rn(alpha, v[3]));
+}
+__device__ __forceinline__ float4 epi_acc(float alpha, f32x4 v, float4 c) {
+  return make_float4(__fmaf_rn(alpha, v[0], c.x), __fmaf_rn(alpha, v[1], c.y), __fmaf_rn(alpha, v[2], c.z),
+                     __fmaf_rn(alpha, v[3], c.w));
+}
+
 struct G8Args {
   G8Prob p[G8_MAXP];
   G8Opt opt;
@@ -134,6 +149,7 @@ struct G8Args {
   const float* alpha_dev2;
   float alpha;
   int np, total;          // problems, work units of all problems
+  int ext_red;            // split units only store their fp32 partial; g8_reduce_kernel sums them
 };
 
 constexpr int NWV = 8;
@@ -586,17 +602,10 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
               const f32x4 v = value(qm, qn, j, i, m, n);
               const size_t off = (size_t)m * P.ldc + n;
               if (epi == 0) {
-                const unsigned lo = (unsigned)f2bf(alpha * v[0] + bv[0]) | ((unsigned)f2bf(alpha * v[1] + bv[1]) << 16);
-                const unsigned hi = (unsigned)f2bf(alpha * v[2] + bv[2]) | ((unsigned)f2bf(alpha * v[3] + bv[3]) << 16);
-                *(uint2*)(Cz + off * 2) = make_uint2(lo, hi);
+                *(uint2*)(Cz + off * 2) = epi_bf16(alpha, v, bv);
               } else {
-                float4 o = make_float4(alpha * v[0], alpha * v[1], alpha * v[2], alpha * v[3]);
                 float4* cp = (float4*)(Cz + off * 4);
-                if (epi == 2) {
-                  const float4 c = *cp;
-                  o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w;
-                }
-                *cp = o;
+                *cp = epi == 2 ? epi_acc(alpha, v, *cp) : epi_f32(alpha, v);
               }
             }
         }
@@ -631,6 +640,12 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
                              __builtin_bit_cast(i32x4, acc[qm][qn][j][i]));
             }
         }
+      if (g.ext_red) {
+        // g8_reduce_kernel (the next launch on the stream) sums the slabs: nothing to wait for
+        // here, and the next unit's prologue only rewrites LDS (every wave's last reads were
+        // retired by the final phase's barrier)
+        continue;
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       int* flag = (int*)smem;                       // LDS is free: the k-loop has finished
@@ -716,6 +731,44 @@ int dispatch8(const G8Args& a, int fp8, int a_col, int b_col, int cus, hipStream
 
 int units_of(const G8Prob& p) { return ((p.M + 255) / 256) * ((p.N + 255) / 256) * p.S; }
 
+// Split-K partials of one problem summed in slice order 0 .. S-1 (the same order and the
+// same epilogue arithmetic as the in-launch last-arriver reduction, so the result is bitwise
+// identical): every thread owns 4 consecutive columns of one row. Launched right behind the
+// GEMM on the same stream when its k-slices only stored their slabs (G8Args.ext_red): all
+// CUs reduce in parallel instead of each tile's last-arriving slice reading S slabs alone,
+// which dominated small-M launches (dx of a 100-frame batch: 12 tiles x 4 slices).
+__global__ __launch_bounds__(256) void g8_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                        void* __restrict__ C, int ldc, int epi,
+                                                        const bf16_t* __restrict__ bias, float alpha,
+                                                        const float* __restrict__ alpha_dev,
+                                                        const float* __restrict__ alpha_dev2) {
+  if (alpha_dev) alpha *= *alpha_dev;
+  if (alpha_dev2) alpha *= *alpha_dev2;
+  const int n4 = N >> 2;
+  const long long total = (long long)M * n4;
+  const size_t slab = (size_t)M * N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / n4), n = (int)(i - (long long)m * n4) * 4;
+    const size_t off = (size_t)m * N + n;
+    f32x4 v = __builtin_nontemporal_load((const f32x4*)(ws + off));
+    for (int s2 = 1; s2 < S; ++s2) v += __builtin_nontemporal_load((const f32x4*)(ws + off + s2 * slab));
+    const size_t co = (size_t)m * ldc + n;
+    if (epi == 0) {
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bias != nullptr) {
+        const uint2 b2 = *(const uint2*)(bias + n);
+        bv[0] = bf2f((bf16_t)(b2.x & 0xffff)); bv[1] = bf2f((bf16_t)(b2.x >> 16));
+        bv[2] = bf2f((bf16_t)(b2.y & 0xffff)); bv[3] = bf2f((bf16_t)(b2.y >> 16));
+      }
+      *(uint2*)((bf16_t*)C + co) = epi_bf16(alpha, v, bv);
+    } else {
+      float4* cp = (float4*)((float*)C + co);
+      *cp = epi == 2 ? epi_acc(alpha, v, *cp) : epi_f32(alpha, v);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -727,12 +780,15 @@ extern "C" {
 // S > 1: split-K over S k-slices through ws (fp32, >= S * batch * M * N floats) and cnt
 // (>= batch * tiles unsigned, all zero; every launch leaves them zero again). Launches that
 // may run concurrently (different streams) need separate cnt buffers.
+// ext_red (batch 1, S > 1): the k-slices only store their partials and g8_reduce_kernel,
+// launched right after on the same stream, sums them on the whole chip.
 int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const float* alpha_dev,
               const float* alpha_dev2, int M, int N, int K, int lda, int ldb, int ldc, int fp8, int a_col, int b_col,
               int epi, float alpha, int batch, long long sA, long long sB, long long sC, int S, float* ws,
-              unsigned* cnt, int cus, const DS2Fill* fill, hipStream_t st) {
+              unsigned* cnt, int cus, const DS2Fill* fill, int ext_red, hipStream_t st) {
   const int es = fp8 ? 1 : 2;
   if (batch <= 0 || batch > G8_MAXP || (epi != 0 && bias)) return (int)hipErrorInvalidValue;
+  if (ext_red && batch != 1) return (int)hipErrorInvalidValue;
   G8Args a;
   a.opt = G8Opt{};
   a.fill = DS2Fill{};
@@ -747,19 +803,28 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
   a.alpha_dev2 = alpha_dev2;
   a.alpha = alpha;
   a.np = batch;
+  a.ext_red = 0;
   int u = 0;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   for (int b = 0; b < batch; ++b) {
     G8Prob& p = a.p[b];
     const int rc = fill_prob(p, (const char*)A + b * sA * es, (const char*)B + b * sB * es,
-                             (char*)C + b * sC * (epi == 0 ? 2 : 4), ws, cnt ? cnt + (size_t)b * tiles : nullptr, M, N,
-                             K, lda, ldb, ldc, fp8, a_col, b_col, epi, S, u);
+                             (char*)C + b * sC * (epi == 0 ? 2 : 4), ws, cnt ? cnt + (size_t)b * tiles : nullptr, M,
+                             N, K, lda, ldb, ldc, fp8, a_col, b_col, epi, S, u);
     if (rc) return rc;
     if (ws) p.ws = ws + (size_t)b * p.S * M * N;
     u += units_of(p);
   }
   a.total = u;
-  return dispatch8(a, fp8, a_col, b_col, cus, st);
+  const G8Prob& red = a.p[a.np - 1];
+  a.ext_red = (ext_red && red.S > 1) ? 1 : 0;
+  int rc = dispatch8(a, fp8, a_col, b_col, cus, st);
+  if (rc || !a.ext_red) return rc;
+  const long long work = (long long)red.M * (N / 4);
+  const int grid = (int)std::max<long long>(1, std::min<long long>(4 * (long long)cus, (work + 255) / 256));
+  hipLaunchKernelGGL(g8_reduce_kernel, dim3(grid), dim3(256), 0, st, red.ws, red.S, red.M, N, red.C, ldc, epi,
+                     (const bf16_t*)bias, alpha, alpha_dev, alpha_dev2);
+  return (int)hipGetLastError();
 }
 
 // A group of independent bf16 GEMMs in one launch (one grid over all their work units): the
@@ -789,6 +854,7 @@ int ds2_gemm8_group(int np, const void* const* A, const void* const* B, void* co
   a.alpha_dev = a.alpha_dev2 = nullptr;
   a.alpha = 1.f;
   a.np = np;
+  a.ext_red = 0;
   int u = 0;
   for (int i = 0; i < np; ++i) {
     const int* d = dims + 8 * i;

@@ -232,32 +232,64 @@ def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_sli
     return best
 
 
+# Parallel split-K reduction (csrc/gemm8.hip ds2_gemm8 ext_red): a launch of few tiles that the
+# plain policy would already split (>= 2 k-slices, reduced by each tile's last-arriving slice
+# reading the S slabs alone) is cut into k-slices of >= _EXT_MIN_KT k-tiles until the units fill
+# the chip, and g8_reduce_kernel sums the partials on every CU. Measured (tools/bench_gemm8_plan.py,
+# profiles/r5_gemm.md): the dx GEMMs of the short SortaGrad buckets 68-109 -> 28-43 us, the 100-frame
+# layer-0 projection 56 -> 37 us; a K = 800 projection that the plain policy leaves unsplit lost
+# with any split (28 -> 31-34 us), and a row-split of an under-full last dispatch round (its rows as
+# k-sliced units taken round-robin by every workgroup) lost at every shape tried (54 -> 89 us at
+# M = 3712), so neither is planned. DS2_G8_PLAN=0 keeps the plain policy (A/B timing).
+_PLAN = os.environ.get("DS2_G8_PLAN", "1") != "0"
+_EXT_MIN_KT = 3
+
+
+def gemm8_plan(M: int, N: int, K: int, batch: int, cus: int, fp8: bool = False):
+    """(S, ext_red) of a gemm8 launch, or None when the plain gemm8_splits policy applies."""
+    if not _PLAN or batch != 1:
+        return None
+    tiles = _cdiv(M, 256) * _cdiv(N, 256)
+    if gemm8_splits(M, N, K, batch, cus) < 2:
+        return None
+    nkt = _cdiv(K * (1 if fp8 else 2), 128)
+    S = min(cus // tiles, nkt // _EXT_MIN_KT, 32)
+    return (S, True) if S >= 2 else None
+
+
 def gemm8(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, epi: int = 0, alpha: float = 1.0,
           bias: Optional[torch.Tensor] = None, alpha_dev: Optional[torch.Tensor] = None,
           alpha_dev2: Optional[torch.Tensor] = None, a_col: bool = False, b_col: bool = False,
-          splits: Optional[int] = None, max_grid: int = 0, fill=None) -> torch.Tensor:
+          splits: Optional[int] = None, max_grid: int = 0, fill=None, plan=None) -> torch.Tensor:
     """out (=, or += for epi 2) alpha * alpha_dev * alpha_dev2 * A @ B^T (+ bias) on the stored
     operands (see the section comment); out bf16 (epi 0) or fp32 (epi 1 / 2). splits=None picks
-    the k-slice count from the shape (gemm8_splits). max_grid > 0 caps the persistent grid
-    (workgroups loop over the units): a launch beside the persistent BPTT."""
+    the launch plan from the shape (gemm8_plan, else gemm8_splits); plan=(S, ext_red) forces
+    one. max_grid > 0 caps the persistent grid (workgroups loop over the units): a launch
+    beside the persistent BPTT."""
     batch = A.shape[0] if A.dim() == 3 else 1
     M = A.shape[-1] if a_col else A.shape[-2]
     K = A.shape[-2] if a_col else A.shape[-1]
     N = B.shape[-1] if b_col else B.shape[-2]
+    fp8 = A.dtype == torch.float8_e4m3fn
     cus = _dev_cus(A)
     if max_grid > 0:
         cus = min(cus, max_grid)
-    if splits is None:
+    ext_red = False
+    if plan is None:
+        plan = gemm8_plan(M, N, K, batch, cus, fp8) if splits is None else None
+    if plan is not None:
+        splits, ext_red = plan
+    elif splits is None:
         splits = gemm8_splits(M, N, K, batch, cus)
     C = _ext.ext()
-    S = int(C.gemm8_splits(K, A.dtype == torch.float8_e4m3fn, splits)) if splits > 1 else 1
+    S = int(C.gemm8_splits(K, fp8, splits)) if splits > 1 else 1
     ws = cnt = None
     if S > 1:
         ws = torch.empty(S * batch * M * N, device=A.device, dtype=torch.float32)
         cnt = _tile_counters(A.device, _cdiv(M, 256) * _cdiv(N, 256) * batch)
     regions, pats = (list(fill[0]), list(fill[1])) if fill is not None else ([], [])
     C.gemm8(A, B, out, bias, epi, float(alpha), alpha_dev, alpha_dev2, a_col, b_col, S, ws, cnt, max_grid,
-            regions, pats)
+            regions, pats, ext_red and S > 1)
     return out
 
 

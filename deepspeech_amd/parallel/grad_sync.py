@@ -45,9 +45,11 @@ import torch.distributed as dist
 
 class GradBucketer:
     def __init__(self, arena, bucket_mb: float = 32.0, compress_bf16: bool = False,
-                 process_group=None, world_size: Optional[int] = None, force: bool = False):
+                 process_group=None, world_size: Optional[int] = None, force: bool = False,
+                 split_after=()):
         """force: run the bucketed collectives even at world size 1 (needs an initialised
-        process group; measures the DP machinery's own overhead on one GPU)."""
+        process group; measures the DP machinery's own overhead on one GPU). split_after:
+        parameter names that also end a bucket (tests pin bucket layouts with it)."""
         self.arena = arena
         self.pg = process_group
         self.compress = compress_bf16
@@ -65,7 +67,7 @@ class GradBucketer:
                 start = off
             cur.append(i)
             end = off + n
-            if end - start >= limit:
+            if end - start >= limit or arena.names[i] in split_after:
                 self.buckets.append((start, arena.offsets[cur[-1]][0] + arena.offsets[cur[-1]][1], cur))
                 cur, start = [], None
         if cur:

@@ -104,7 +104,7 @@ class Trainer:
     def __init__(self, model: DeepSpeech2, lr_schedule: LRSchedule, moving_avg_decay: Optional[float] = 0.9999,
                  world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
                  nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False,
-                 step_graphs=False, graph_warmup: int = 2):
+                 step_graphs=False, graph_warmup: int = 2, bucket_split_after=()):
         self.model = model
         if model.engine == "hip":
             from .ops.rnn import check_knobs
@@ -116,7 +116,7 @@ class Trainer:
         self.lr_schedule = lr_schedule
         self.world = world_size
         self.bucketer = GradBucketer(self.arena, bucket_mb=bucket_mb, compress_bf16=allreduce_bf16,
-                                     world_size=world_size, force=force_buckets)
+                                     world_size=world_size, force=force_buckets, split_after=bucket_split_after)
         if world_size > 1:
             broadcast_params(self.arena)
             self.arena.mark_dirty()

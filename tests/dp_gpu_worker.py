@@ -18,10 +18,22 @@ from deepspeech_amd.parallel.dist import init_distributed, shutdown  # noqa: E40
 from deepspeech_amd.trainer import LRSchedule, Trainer  # noqa: E402
 
 
-def model(dev):
+# geometries: "small" (2 x BiGRU-64) and BASELINE config 5's (7 x BiGRU-1280 in fp8 mode: MX-fp8
+# projections, e4m3 forward recurrence, fp8 BPTT), selected by DS2_DP_GEOM
+GEOMS = {"small": dict(num_hidden=64, num_rnn_layers=2, fp8=False, batch=4, bucket_mb=0.05),
+         "config5": dict(num_hidden=1280, num_rnn_layers=7, fp8=True, batch=8, bucket_mb=32.0)}
+
+
+def geom(name=None):
+    return GEOMS[name or os.environ.get("DS2_DP_GEOM", "small")]
+
+
+def model(dev, name=None):
+    g = geom(name)
     torch.manual_seed(0)
-    m = DeepSpeech2(num_filters=32, num_hidden=64, num_rnn_layers=2, cell="gru").to(dev)
-    return m.set_engine("hip", torch.bfloat16)
+    m = DeepSpeech2(num_filters=32, num_hidden=g["num_hidden"], num_rnn_layers=g["num_rnn_layers"],
+                    cell="gru").to(dev)
+    return m.set_engine("hip", torch.bfloat16, fp8=g["fp8"])
 
 
 def step_grads(tr, batch):
@@ -65,10 +77,10 @@ def main():
     out = sys.argv[1]
     ctx = init_distributed("cuda")
     dev = ctx.device
-    batch = to_device(FixedShapeBatches(4, max_frames=300, seed=100 + ctx.rank, pool=1).next(), dev)
+    batch = to_device(FixedShapeBatches(geom()["batch"], max_frames=300, seed=100 + ctx.rank, pool=1).next(), dev)
     local = Trainer(model(dev), LRSchedule(1e-3, 10 ** 6, 0.9), world_size=1)
     g_local = grads(local, batch, dp=False)
-    bmb = float(os.environ.get("DS2_DP_BUCKET_MB", "0.05"))
+    bmb = float(os.environ.get("DS2_DP_BUCKET_MB", str(geom()["bucket_mb"])))
     dp = Trainer(model(dev), LRSchedule(1e-3, 10 ** 6, 0.9), world_size=ctx.world_size, bucket_mb=bmb)
     assert len(dp.bucketer.buckets) >= (3 if bmb < 1 else 1)
     if ctx.rank == 0 and os.environ.get("DS2_DP_DIAG"):

@@ -20,9 +20,14 @@ def _free_port():
     return p
 
 
-def test_dp2_gradients_equal_sum_of_local(cuda, tmp_path):
+@pytest.mark.parametrize("geom", ["small", "config5"])
+def test_dp2_gradients_equal_sum_of_local(cuda, tmp_path, geom):
+    """2 ranks on one GPU over gloo: the all-reduced gradient equals the sum of the local ones,
+    and a full per-bucket DP step equals one update of the averaged gradients. "config5":
+    BASELINE config 5's 7 x BiGRU-1280 in fp8 mode."""
     out = str(tmp_path / "g")
-    env = dict(os.environ, PYTHONPATH=ROOT, DS2_DIST_BACKEND="gloo", DS2_DEVICE_INDEX="0", OMP_NUM_THREADS="2")
+    env = dict(os.environ, PYTHONPATH=ROOT, DS2_DIST_BACKEND="gloo", DS2_DEVICE_INDEX="0", OMP_NUM_THREADS="2",
+               DS2_DP_GEOM=geom)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "dp_gpu_worker.py"), out]
@@ -39,7 +44,7 @@ def test_dp2_gradients_equal_sum_of_local(cuda, tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from deepspeech_amd.trainer import LRSchedule, Trainer
     import dp_gpu_worker as W
-    tr = Trainer(W.model(cuda), LRSchedule(1e-3, 10 ** 6, 0.9))
+    tr = Trainer(W.model(cuda, geom), LRSchedule(1e-3, 10 ** 6, 0.9))
     w0 = tr.arena.flat.clone()
     tr.arena.grad.copy_((g[0]["step_local"] + g[1]["step_local"]).to(cuda))
     tr.opt.step(tr.lr, 0, gscale=0.5)
@@ -50,6 +55,8 @@ def test_dp2_gradients_equal_sum_of_local(cuda, tmp_path):
     # gradient is ~eps-sized (float summation order)
     assert ((g[0]["w_step"] - w_ref).abs() > 1e-5).float().mean() < 1e-3
     assert (g[0]["w_step"] - w_ref).abs().max() < 2.5e-3
+    del tr
+    torch.cuda.empty_cache()
 
 
 def test_bench_gpus2_self_launch_on_one_gpu():

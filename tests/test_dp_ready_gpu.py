@@ -26,7 +26,30 @@ def test_recurrence_coresident_with_channel_blocks(cuda, blocks, lds):
         assert r["layer_ms"] < r["layer_ms_alone"] + 2.0 * r["spin_ms"] + 1.0, r
 
 
-def test_dp_machinery_world1_matches_plain_step(cuda):
+def test_fp8_recurrence_coresident_with_channel_blocks(cuda):
+    """BASELINE config 5's fp8 layer (BiGRU-1280, batch 32: e4m3 forward recurrence, fp8
+    BPTT, their projection and weight gradients) beside 32 RCCL-channel-shaped workgroups,
+    whichever launches first: no spin timeout, bounded delay."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import coresidency
+    res = coresidency.run([32], threads=256, lds=16384, spin_ms=2.0, iters=2, H=1280, N=32, T=121, fp8=True)
+    for r in res:
+        assert r["timeout"] is None, r
+        assert r["layer_ms"] < r["layer_ms_alone"] + 2.0 * r["spin_ms"] + 1.0, r
+
+
+# (hidden, layers, fp8, batch, bucket_split_after): the round-1 small GRU; the same with a bucket
+# that holds conv2.weight alone, so its Adam range (which rewrites the bf16 shadow conv2's data
+# gradient reads) is issued the moment conv2.weight reports (ADVICE r4); BASELINE config 5
+# (7 x BiGRU-1280, fp8 projections / recurrence / BPTT, batch 32)
+_DP_CASES = [(128, 2, False, 8, ()), (128, 2, False, 8, ("conv2.bias", "conv2.weight")),
+             (1280, 7, True, 32, ())]
+
+
+@pytest.mark.parametrize("H,layers,fp8,N,split_after", _DP_CASES)
+def test_dp_machinery_world1_matches_plain_step(cuda, H, layers, fp8, N, split_after):
     """force_buckets: gradient buckets + collectives at world size 1 give the plain update."""
     import copy
     from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
@@ -36,13 +59,17 @@ def test_dp_machinery_world1_matches_plain_step(cuda):
     ctx = init_distributed("cuda", force_group=True)
     try:
         torch.manual_seed(0)
-        base = DeepSpeech2(num_filters=32, num_hidden=128, num_rnn_layers=2, cell="gru").to(cuda)
-        batch = to_device(FixedShapeBatches(8, max_frames=300, seed=2, pool=1).next(), cuda)
+        base = DeepSpeech2(num_filters=32, num_hidden=H, num_rnn_layers=layers, cell="gru").to(cuda)
+        batch = to_device(FixedShapeBatches(N, max_frames=300, seed=2, pool=1).next(), cuda)
         outs = []
         # plain step; buckets + one update after finish(); buckets + per-bucket Adam ranges
         for force, per_bucket in ((False, False), (True, False), (True, True)):
-            m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
-            tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9), force_buckets=force)
+            m = copy.deepcopy(base).set_engine("hip", torch.bfloat16, fp8=fp8)
+            tr = Trainer(m, LRSchedule(1e-4, 1000, 0.9), force_buckets=force, bucket_split_after=split_after)
+            if split_after and force:
+                last = [tr.arena.names[idx[-1]] for _, _, idx in tr.bucketer.buckets]
+                assert [tr.arena.names[i] for i in tr.bucketer.buckets[last.index("conv2.weight")][2]] == \
+                    ["conv2.weight"]
             tr.per_bucket_update = per_bucket
             assert tr.bucketer.enabled == force
             for _ in range(2):
@@ -56,7 +83,14 @@ def test_dp_machinery_world1_matches_plain_step(cuda):
         # (full-K tiles) where the bucketed schedule runs them per layer (split-K beside the
         # BPTT): the same update up to fp32 summation order
         for x, y in zip(outs[0][:2], outs[1][:2]):
-            assert (x - y).abs().max() <= 1e-6 + 1e-5 * y.abs().max()
+            d = (x - y).abs()
+            tol = 1e-6 + 1e-5 * y.abs().max()
+            if not fp8:
+                assert d.max() <= tol
+            else:
+                # 146 M parameters: Adam's first steps move ~lr * sign(g), so an element whose
+                # gradient is ~0 may step the other way under a different summation order
+                assert (d > tol).float().mean() < 1e-4 and d.max() <= 4e-4
         assert (outs[0][2] != outs[1][2]).float().mean() < 1e-3     # bf16 shadows: rare 1-ulp flips
     finally:
         shutdown(ctx)           # later GPU tests must not run with a live RCCL group

@@ -428,3 +428,43 @@ def test_gemm_fill_persistent_and_fallback(cfg):
     assert torch.equal(out, ref)
     assert bool((census == -1).all()) and bool((parts == 0).all())
     assert bool((ring.view(torch.int32) == -1).all())
+
+
+# ------------------------------------------------ gemm8 launch plans (ops/gemm.py gemm8_plan)
+@pytest.mark.parametrize("M,N,K,a_col,b_col", [(672, 800, 4800, False, False), (672, 4800, 800, False, False),
+                                                (1312, 2400, 4800, False, True), (300, 328, 960, False, False),
+                                                (2400, 800, 672, True, True)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm8_parallel_reduce_bitwise_in_launch_reduce(M, N, K, a_col, b_col, epi):
+    """ext_red: the k-slices only store their partials and g8_reduce_kernel sums them on the
+    whole chip — bitwise the in-launch last-arriver reduction of the same slices (same order,
+    same epilogue), and close to the fp32 reference; bf16 (+ bias, alpha) and fp32 store /
+    accumulate epilogues, row- and column-mode operands."""
+    if epi == 0 and (a_col and b_col):
+        pytest.skip("column-column is the fp32 weight-gradient variant")
+    torch.manual_seed(M + N + K + epi)
+    A = torch.randn((K, M) if a_col else (M, K), device=DEV).to(BF)
+    B = (torch.randn((K, N) if b_col else (N, K), device=DEV) * 0.05 + 0.01).to(BF)
+    b = torch.randn(N, device=DEV).to(BF) if epi == 0 else None
+    dt = BF if epi == 0 else torch.float32
+    init = torch.randn(M, N, device=DEV).to(dt)
+    S = 6
+    o_in, o_ext = init.clone(), init.clone()
+    G.gemm8(A, B, o_in, epi, 0.75, b, a_col=a_col, b_col=b_col, plan=(S, False))
+    G.gemm8(A, B, o_ext, epi, 0.75, b, a_col=a_col, b_col=b_col, plan=(S, True))
+    torch.cuda.synchronize()
+    assert torch.equal(o_in, o_ext)
+    Af = A.float().t() if a_col else A.float()
+    Bf = B.float() if b_col else B.float().t()
+    ref = 0.75 * (Af @ Bf) + (b.float() if b is not None else 0.0) + (init.float() if epi == 2 else 0.0)
+    assert _rel(o_ext, ref) < (6e-3 if epi == 0 else 2e-5 * K ** 0.5 + 1e-4)
+
+
+def test_gemm8_plan_policy():
+    """The planner's choices at the DS2 shapes (256 CUs): parallel-reduce split-K where the plain
+    policy splits (a few tiles), nothing where it does not (full chip, K = 800 projections)."""
+    assert G.gemm8_plan(672, 800, 4800, 1, 256) == (21, True)
+    assert G.gemm8_plan(672, 4800, 2400, 1, 256) == (4, True)
+    assert G.gemm8_plan(672, 4800, 800, 1, 256) is None
+    assert G.gemm8_plan(7712, 4800, 800, 1, 256) is None
+    assert G.gemm8_plan(7712, 800, 4800, 2, 256) is None            # batched launches: plain policy

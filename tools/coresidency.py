@@ -24,26 +24,41 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 
-def run(blocks_list, threads, lds, spin_ms, iters, H=800, N=32, T=241):
+def run(blocks_list, threads, lds, spin_ms, iters, H=800, N=32, T=241, fp8=False):
+    """fp8: a whole BiGRU layer of BASELINE config 5's fp8 mode instead (e4m3 forward
+    recurrence and fp8 BPTT, csrc/rnn_fp8.hip; input projection and weight gradients
+    included), H = 1280 by default there."""
     from deepspeech_amd.ops import _ext
     from deepspeech_amd.ops import rnn as RNN
     C = _ext.ext()
     dev = torch.device("cuda")
     G = 3
-    plan = RNN.plan_for(N, H, "gru", 2, dev)
     torch.manual_seed(0)
-    gx = (torch.randn(T, N, 2 * G * H, device=dev) * 0.5).bfloat16().requires_grad_(True)
-    Us = [(torch.randn(G * H, H, device=dev) / H ** 0.5).bfloat16().requires_grad_(True) for _ in range(2)]
-    bh = [torch.zeros(G * H, device=dev, requires_grad=True) for _ in range(2)]
     lens = torch.full((N,), T, dtype=torch.int32, device=dev)
     dy = torch.randn(T, N, H, device=dev).bfloat16()
     done = torch.zeros(1, device=dev, dtype=torch.int32)
     side = torch.cuda.Stream()
     ticks = int(spin_ms * 1e5)           # s_memrealtime: 100 MHz
+    if fp8:
+        from deepspeech_amd.models import DeepSpeech2
+        m = DeepSpeech2(num_filters=32, num_hidden=H, num_rnn_layers=2, cell="gru").to(dev)
+        m.set_engine("hip", torch.bfloat16, fp8=True)
+        lay = m.rnn[1]
+        x = (torch.randn(T, N, H, device=dev) * 0.5).bfloat16().requires_grad_(True)
 
-    def layer():
-        y = RNN.BiRecurrence.apply(gx, lens, Us[0], Us[1], bh[0], bh[1], plan)
-        y.backward(dy)
+        def layer():
+            y = RNN.recurrent_layer_hip(lay, x, lens, 1)
+            y.backward(dy)
+            RNN.join_wgrad_streams()
+    else:
+        plan = RNN.plan_for(N, H, "gru", 2, dev)
+        gx = (torch.randn(T, N, 2 * G * H, device=dev) * 0.5).bfloat16().requires_grad_(True)
+        Us = [(torch.randn(G * H, H, device=dev) / H ** 0.5).bfloat16().requires_grad_(True) for _ in range(2)]
+        bh = [torch.zeros(G * H, device=dev, requires_grad=True) for _ in range(2)]
+
+        def layer():
+            y = RNN.BiRecurrence.apply(gx, lens, Us[0], Us[1], bh[0], bh[1], plan)
+            y.backward(dy)
 
     def case(blocks, order):
         torch.cuda.synchronize()
