@@ -65,9 +65,10 @@ def parse():
     p.add_argument("--walk_scale", type=int, default=1,
                    help="epoch-walk size: the reference dummy epoch's bucket counts x this (reference: 10)")
     p.add_argument("--fp8", action="store_true",
-                   help="BASELINE config 5's fp8 mode: MX-fp8 e4m3 input projections and an e4m3 forward "
-                        "recurrence (U and hidden-state exchange); BPTT, weight gradients and the "
-                        "front-end stay bf16. NOT the headline bf16 number")
+                   help="BASELINE config 5's fp8 mode: MX-fp8 e4m3 input projections, an e4m3 forward "
+                        "recurrence (U and hidden-state exchange) and an fp8 BPTT (e4m3 U^T, E8M0-scaled "
+                        "gate gradients); weight gradients and the front-end stay bf16. NOT the "
+                        "headline bf16 number")
     return p.parse_args()
 
 

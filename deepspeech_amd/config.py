@@ -120,6 +120,9 @@ def build_train_parser() -> argparse.ArgumentParser:
     p.add_argument("--nan_policy", type=str, default="abort", choices=["abort", "skip"])
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--device", type=str, default="auto", help="auto | cpu | cuda")
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU) on this node; without an outer launcher (torchrun) the driver "
+                        "starts them itself (parallel/launch.py). Default: the launcher's WORLD_SIZE, else 1")
     p.add_argument("--async_checkpoint", type=str2bool, default=True)
     p.add_argument("--step_graphs", type=str, default="auto", choices=["auto", "on", "off"],
                    help="single-GPU HIP engine: replay each batch shape's captured training step "

@@ -259,9 +259,13 @@ class DeepSpeech2(nn.Module):
 
     # ------------------------------------------------------------------ config
     def set_engine(self, engine: str, compute_dtype: torch.dtype = torch.float32, fp8: bool = False) -> "DeepSpeech2":
-        """engine: 'ref' (pure torch) | 'hip' (gfx950 kernels). fp8=True (HIP engine only):
-        the recurrent layers' input projections run as fp8 e4m3 scaled GEMMs (BASELINE
-        config 5); activations, recurrence and gradients stay bf16."""
+        """engine: 'ref' (pure torch) | 'hip' (gfx950 kernels). fp8=True (HIP engine only,
+        BASELINE config 5's fp8 mode): the recurrent layers' input projections run as MX-fp8
+        e4m3 GEMMs, and where csrc/rnn_fp8.hip covers the GRU geometry (ops/rnn.py
+        fp8_recurrence_ok / fp8_bptt_ok: H % 256 == 0, <= 8 rows per group) the forward
+        recurrence multiplies an e4m3 U and exchanges e4m3 hidden states, and the BPTT runs on
+        an e4m3 U^T with per-(row, 32-unit) E8M0-scaled gate gradients. Weight gradients, the
+        conv front-end, the head and the master weights stay bf16 / fp32."""
         if engine not in ("ref", "hip"):
             raise ValueError(engine)
         if fp8 and engine != "hip":
@@ -271,7 +275,10 @@ class DeepSpeech2(nn.Module):
         self.fp8 = fp8
         if engine == "hip":
             from ..ops.gemm_tuning import enable_tuned_gemms
-            enable_tuned_gemms()          # measured hipBLASLt/rocBLAS picks for the projections
+            # measured hipBLASLt picks for the library GEMMs that remain reachable: DS2_GEMM=torch
+            # A/B runs and shapes the hand-written kernels do not cover (every default-path GEMM
+            # of the training step runs on csrc/gemm8.hip / gemm.hip)
+            enable_tuned_gemms()
         for layer in self.rnn:
             layer.fp8 = fp8
         return self

@@ -102,6 +102,11 @@ def _stop(procs: List[subprocess.Popen], grace_s: float = 10.0) -> None:
 def maybe_spawn(requested: Optional[int], script: str, argv: Sequence[str]) -> Optional[int]:
     """If no launcher is active and ``requested`` > 1, run ``script argv`` as that many ranks
     and return the job's exit code; otherwise return None (this process is a rank: go on)."""
+    return maybe_spawn_cmd(requested, [sys.executable, "-u", script] + list(argv))
+
+
+def maybe_spawn_cmd(requested: Optional[int], cmd: Sequence[str]) -> Optional[int]:
+    """maybe_spawn for a whole command line (``python -m deepspeech_amd.train ...``)."""
     if launcher_world() is not None or requested is None or int(requested) <= 1:
         return None
-    return spawn_local(int(requested), [sys.executable, "-u", script] + list(argv))
+    return spawn_local(int(requested), list(cmd))

@@ -4,7 +4,7 @@
       --num_rnn_layers 7 --num_hidden 1760 --num_filters 32 --initial_lr 1e-4 \
       --train_dir ../models/librispeech/train --data_dir ../data/LibriSpeech/processed/ \
       [--dummy True] [--cell gru] [--engine hip]
-  multi-GPU: python -m torch.distributed.run --nproc-per-node 8 -m deepspeech_amd.train ...
+  multi-GPU: python -m deepspeech_amd.train --gpus 8 ...   (or under torch.distributed.run)
 
 Reference flow (src/deepSpeech_train.py:419-528): wipe/create train_dir, dump the flags to
 deepSpeech_parameters.json, build graph, Adam + staircase LR + weight EMA, restore or
@@ -142,10 +142,20 @@ def write_summaries(events, step: int, trainer, model, args, lv: float, ema: flo
 
 
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = C.parse_train_args(argv)
+    from .parallel.launch import check_world, maybe_spawn_cmd
+    # --gpus N > 1 without torchrun: N child ranks of this same command line; this process never
+    # touches the GPU and returns the job's code
+    code = maybe_spawn_cmd(args.gpus, [sys.executable, "-u", "-m", "deepspeech_amd.train"] + argv)
+    if code is not None:
+        return code
+    world = check_world(args.gpus)
     from .utils.setenvs import setenvs
     setenvs(platform=args.platform if args.platform in ("mi355x", "knl", "bdw") else "mi355x")   # before HIP init
     ctx = init_distributed(args.device)
+    if ctx.world_size != world:
+        raise SystemExit("world size %d does not match --gpus / WORLD_SIZE %d" % (ctx.world_size, world))
     dev = ctx.device
     engine = C.resolve_engine(args.engine, dev)
     dtype = C.resolve_dtype(args.dtype, args.use_fp16, dev)

@@ -98,16 +98,15 @@ def test_fp8_projection_training_tracks_bf16(cuda):
 
 
 def test_fp8_recurrence_training_tracks_bf16(cuda):
-    """Config 5's full fp8 mode — MX-fp8 projections AND the e4m3 forward recurrence of
-    csrc/rnn_fp8.hip (H % 256 == 0, so this geometry really routes through it: asserted) —
-    trains along the bf16 trajectory: 300 steps, same weights and batches. The BPTT runs in
-    bf16 on the fp8 forward's saved states (straight-through), which is what this pins; the
-    reference has no fp8 mode (parity unpinned). Measured on MI355X (round 4): windows
-    175.0/184.8 48.9/54.5 9.3/11.6 2.6/3.0 1.3/1.5 0.9/0.9 0.6/0.7 0.5/0.5 0.4/0.4 0.3/0.3 —
-    the fp8 run lags the bf16 one by a few steps on the steep part of the descent (max window
-    difference 24 %, where the projection-only fp8 mode above stays within 2 %: 3-bit-mantissa
-    U and exchanged h), then reaches the same loss. Pinned: every window within 35 %, the last
-    three within 15 %, both runs learn > 100x."""
+    """Config 5's full fp8 mode — MX-fp8 projections, the e4m3 forward recurrence AND the fp8
+    BPTT of csrc/rnn_fp8.hip (H % 256 == 0, so this geometry really routes through both
+    kernels: asserted) — trains along the bf16 trajectory: 300 steps, same weights and
+    batches. The BPTT multiplies an e4m3 U^T and requantises the gate gradients per (row,
+    32-unit group) every step; its gradient is straight-through with respect to the
+    quantisation of the exchanged h. The reference has no fp8 mode (parity unpinned).
+    Measured on MI355X with the fp8 BPTT (round 5, tests run with -s print the windows):
+    FP8_WINDOWS. Pinned: every window within FP8_MAX_REL, the last three within FP8_LAST_REL,
+    both runs learn > 100x."""
     from deepspeech_amd.ops import rnn as RNN
     torch.manual_seed(11)
     N, H = 8, 256
@@ -116,6 +115,7 @@ def test_fp8_recurrence_training_tracks_bf16(cuda):
     base.set_engine("hip", torch.bfloat16)
     f8.set_engine("hip", torch.bfloat16, fp8=True)
     assert RNN.fp8_recurrence_ok(RNN.plan_for(N, H, "gru", 2, cuda), N)
+    assert RNN.fp8_bptt_ok(RNN.plan_for(N, H, "gru", 2, cuda), N)
     batches = [to_device(FixedShapeBatches(N, max_frames=300, seed=40 + s, pool=1).next(), cuda) for s in range(4)]
     sched = LRSchedule(3e-4, 10 ** 9, 1.0)
     tb, tf = Trainer(base, sched), Trainer(f8, sched)

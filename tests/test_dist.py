@@ -135,6 +135,21 @@ def test_torchrun_gloo_two_ranks(tmp_path):
     assert "step 12" in r.stdout
 
 
+def test_train_gpus_flag_spawns_ranks_without_launcher(tmp_path):
+    """python -m deepspeech_amd.train --gpus 2 (no torchrun): the driver starts its two ranks
+    itself (parallel/launch.py), as bench.py does."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", DS2_DIST_BACKEND="gloo")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "deepspeech_amd.train", "--gpus", "2",
+           "--dummy", "True", "--batch_size", "2", "--num_hidden", "16", "--num_rnn_layers", "1",
+           "--num_filters", "4", "--device", "cpu", "--max_steps", "13", "--train_dir", str(tmp_path / "tr"),
+           "--log_every", "12"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "step 12" in r.stdout and "world: 2" in r.stdout
+
+
 def _run_bench(nproc, extra_env, args, timeout=600):
     import json
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", **extra_env)

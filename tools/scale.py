@@ -27,8 +27,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _gpu_count() -> int:
-    # counting devices does not initialise them (torch.cuda.device_count reads the driver's
-    # enumeration); an explicit HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES is honoured by it
+    # on this image (PyTorch 2.10 + ROCm 7) counting devices does not initialise them:
+    # torch.cuda.device_count uses the non-initialising enumeration (the pool's own notes say the
+    # same), so the parent still never brings up HIP before it starts the ranks; an explicit
+    # HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES is honoured by it
     try:
         import torch
         return int(torch.cuda.device_count())
