@@ -222,7 +222,8 @@ def emit_grad(p, g: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None
 
 
-def mm_into(p, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+def mm_into(p, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
+            max_grid: int = 0) -> Optional[torch.Tensor]:
     """Weight gradient ``a @ b`` (bf16 operands, fp32 accumulation) for parameter ``p``.
 
     Arena-managed: the GEMM writes fp32 straight into ``p.main_grad`` (``out`` may name a
@@ -240,7 +241,7 @@ def mm_into(p, a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = N
         except (RuntimeError, TypeError):
             return torch.mm(a.float(), b.float())
     dst = out if out is not None else p.main_grad.view(a.shape[0], b.shape[1])
-    if G.enabled("wgrad") and G.matmul(a, b, dst, accumulate=not arena.first_write(p)):
+    if G.enabled("wgrad") and G.matmul(a, b, dst, accumulate=not arena.first_write(p), max_grid=max_grid):
         return None
     if arena.first_write(p):
         try:

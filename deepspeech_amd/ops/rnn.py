@@ -890,13 +890,17 @@ class FusedBiLayer(torch.autograd.Function):
             def dw_done(W_f=W_f, W_b=W_b if d1 else None):
                 arena.grad_done(W_f, W_b)
 
-            def dw(grp=grp, dgx2=dgx2, x2=x2):
-                mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D))
-                dw_done()
             sch = arena.wgrad
             on_side = x16.is_cuda and sch.on_side(x16.device)
             grouped = sch.grouped and on_side
-            if sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device, ctx.idx):
+            defer_w = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device,
+                                                                                                  ctx.idx)
+            cap_w = _beside_grid(plan, x16.device) if (on_side and ctx.idx > 0 and not defer_w) else 0
+
+            def dw(grp=grp, dgx2=dgx2, x2=x2, cap=cap_w):
+                mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D), max_grid=cap)
+                dw_done()
+            if defer_w:
                 # run after the last recurrent layer's BPTT (grouped: every layer's, in one launch)
                 ops = GM.group_operands(dgx2.t(), x2, grp.view(plan.ndir * GH, D)) if grouped else None
                 sch.deferred.append(Deferred(dw, (dgx2, x2), [ops + (grp.view(plan.ndir * GH, D),)] if ops else None,
@@ -922,6 +926,7 @@ class FusedBiLayer(torch.autograd.Function):
             defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device, ctx.idx)
             beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
             splits = _DU_SPLITS if beside else None
+            cap_u = _beside_grid(plan, x16.device) if (beside and on_side) else 0
 
             steps = dgh.shape[1]
             g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
@@ -931,8 +936,8 @@ class FusedBiLayer(torch.autograd.Function):
             def du_done(U_f=U_f, U_b=U_b):
                 arena.grad_done(U_f, U_b)
 
-            def du(g3=g3, h3=h3, out=out, splits=splits):
-                if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out, splits=splits)):
+            def du(g3=g3, h3=h3, out=out, splits=splits, cap=cap_u):
+                if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out, splits=splits, max_grid=cap)):
                     try:
                         torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
                     except (RuntimeError, TypeError):
@@ -980,6 +985,22 @@ class FusedBiLayer(torch.autograd.Function):
 # 7 x BiGRU-1280 (160 CUs, 96 idle) 23.10 ms/step beside vs 24.53 deferred; 7 x bi-ReLU-1760
 # (generation-1 kernels) 20.95 deferred vs 21.64 beside.
 _BESIDE_MIN_IDLE_CUS = 96
+# weight-gradient GEMMs issued beside a later layer's BPTT (data parallelism, or wide layers
+# that leave >= _BESIDE_MIN_IDLE_CUS idle) run on a grid of at most the CUs the persistent BPTT
+# leaves idle (-1, the default), at most DS2_BESIDE_GRID workgroups (> 0), or the whole chip
+# (0), so that they fill the idle CUs instead of queueing workgroups behind the BPTT's.
+# Headline with the data-parallel machinery at world size 1 (same box, 3 alternating rounds,
+# scripts/ab_dp.sh): plain 7.731 / 7.745 / 7.739 ms/step; whole chip 7.821 / 7.809 / 7.822
+# (+1.1 %); 56 (= the idle CUs) 7.788 / 7.770 / 7.773 (+0.5 %); 32 9.21 / 9.13 / 9.15
+_BESIDE_GRID = int(os.environ.get("DS2_BESIDE_GRID", "-1"))
+
+
+def _beside_grid(plan: RnnPlan, device: torch.device) -> int:
+    if _BESIDE_GRID == 0:
+        return 0
+    idle = _ext.num_cus(device.index or 0) - _bptt_cus(plan)
+    cap = idle if _BESIDE_GRID < 0 else min(_BESIDE_GRID, idle)
+    return max(8, cap // 8 * 8)
 # bottom layer: the grouped launch before layer 0's dx GEMM (same-box A/B, 3 rounds: 8.025 /
 # 8.028 / 8.081 vs 8.091 / 8.024 / 8.101 ms/step after it)
 _GROUP_BEFORE_DX = True

@@ -105,8 +105,10 @@ def test_fp8_recurrence_training_tracks_bf16(cuda):
     32-unit group) every step; its gradient is straight-through with respect to the
     quantisation of the exchanged h. The reference has no fp8 mode (parity unpinned).
     Measured on MI355X with the fp8 BPTT (round 5, tests run with -s print the windows):
-    FP8_WINDOWS. Pinned: every window within FP8_MAX_REL, the last three within FP8_LAST_REL,
-    both runs learn > 100x."""
+    175.0/184.7 48.9/53.7 9.4/11.3 2.6/3.0 1.3/1.4 0.9/0.9 0.6/0.7 0.5/0.5 0.4/0.4 0.3/0.3,
+    max window difference 19 % (round 4, bf16 BPTT on the same fp8 forward: 24 %), again on
+    the steep part of the descent. Pinned: every window within 25 % (was 35 %), the last three
+    within 12 % (was 15 %), both runs learn > 100x."""
     from deepspeech_amd.ops import rnn as RNN
     torch.manual_seed(11)
     N, H = 8, 256
@@ -133,5 +135,5 @@ def test_fp8_recurrence_training_tracks_bf16(cuda):
     table = " ".join("%.1f/%.1f" % (a, c) for a, c in zip(wb.tolist(), wf.tolist()))
     print("fp8-recurrence windowed bf16/fp8 loss: %s; max rel %.4f" % (table, float(rel.max())))
     assert wf[-1] < 0.01 * wf[0] and wb[-1] < 0.01 * wb[0], table
-    assert float(rel.max()) < 0.35, table
-    assert float(rel[-3:].max()) < 0.15, table
+    assert float(rel.max()) < 0.25, table
+    assert float(rel[-3:].max()) < 0.12, table

@@ -118,8 +118,11 @@ def test_resume_auto_continues_instead_of_wiping(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "has checkpoint" in r.stdout
     assert CK.latest_checkpoint(d).endswith("model.ckpt-5")
+    # metrics rows are written at log / summary steps and the last step (checkpoint steps no
+    # longer synchronise the host): the first run's last row is step 3, the second run appends
+    # to the same file (not wiped) and its rows start after it
     steps = [json.loads(l)["step"] for l in open(os.path.join(d, "metrics.jsonl"))]
-    assert steps[0] == 0 and 4 in steps and steps.count(0) == 1      # the second run started at 4
+    assert steps[0] == 3 and steps[-1] == 5 and sorted(steps) == steps and steps.count(3) == 1
 
 
 def test_torchrun_restart_resumes_after_rank_kill(tmp_path):
