@@ -895,7 +895,9 @@ class FusedBiLayer(torch.autograd.Function):
             grouped = sch.grouped and on_side
             defer_w = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device,
                                                                                                   ctx.idx)
-            cap_w = _beside_grid(plan, x16.device) if (on_side and ctx.idx > 0 and not defer_w) else 0
+            fp8b = bool(getattr(ctx, "fp8_bwd", False))
+            cap_w = (_beside_grid(plan, x16.device, not sch.defer_input, fp8b)
+                     if (on_side and ctx.idx > 0 and not defer_w) else 0)
 
             def dw(grp=grp, dgx2=dgx2, x2=x2, cap=cap_w):
                 mm_into(W_f, dgx2.t(), x2, out=grp.view(plan.ndir * GH, D), max_grid=cap)
@@ -926,7 +928,8 @@ class FusedBiLayer(torch.autograd.Function):
             defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device, ctx.idx)
             beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
             splits = _DU_SPLITS if beside else None
-            cap_u = _beside_grid(plan, x16.device) if (beside and on_side) else 0
+            cap_u = (_beside_grid(plan, x16.device, not sch.defer_input, bool(getattr(ctx, "fp8_bwd", False)))
+                     if (beside and on_side) else 0)
 
             steps = dgh.shape[1]
             g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
@@ -987,16 +990,19 @@ class FusedBiLayer(torch.autograd.Function):
 _BESIDE_MIN_IDLE_CUS = 96
 # weight-gradient GEMMs issued beside a later layer's BPTT (data parallelism, or wide layers
 # that leave >= _BESIDE_MIN_IDLE_CUS idle) run on a grid of at most the CUs the persistent BPTT
-# leaves idle (-1, the default), at most DS2_BESIDE_GRID workgroups (> 0), or the whole chip
-# (0), so that they fill the idle CUs instead of queueing workgroups behind the BPTT's.
-# Headline with the data-parallel machinery at world size 1 (same box, 3 alternating rounds,
-# scripts/ab_dp.sh): plain 7.731 / 7.745 / 7.739 ms/step; whole chip 7.821 / 7.809 / 7.822
-# (+1.1 %); 56 (= the idle CUs) 7.788 / 7.770 / 7.773 (+0.5 %); 32 9.21 / 9.13 / 9.15
+# leaves idle, so that they fill the idle CUs instead of queueing workgroups behind the BPTT's:
+# with data parallelism and beside the fp8 BPTT (-1, the default), always (-2), at most
+# DS2_BESIDE_GRID workgroups (> 0), or never (0). Same box, alternating rounds
+# (scripts/ab_dp.sh, scripts/ab_beside.sh):
+#   headline, DP machinery at world 1: plain 7.731 / 7.745 / 7.739 ms/step; whole chip 7.821 /
+#     7.809 / 7.822 (+1.1 %); idle CUs (56) 7.788 / 7.770 / 7.773 (+0.5 %); 32: 9.13-9.21
+#   config 5 fp8: idle CUs (96) 18.13 / 18.14, whole chip 18.50 / 18.29
+#   config 5 bf16: idle CUs 23.37 / 23.42, whole chip 23.16 / 23.18 (kept uncapped)
 _BESIDE_GRID = int(os.environ.get("DS2_BESIDE_GRID", "-1"))
 
 
-def _beside_grid(plan: RnnPlan, device: torch.device) -> int:
-    if _BESIDE_GRID == 0:
+def _beside_grid(plan: RnnPlan, device: torch.device, dp: bool, fp8: bool) -> int:
+    if _BESIDE_GRID == 0 or (_BESIDE_GRID == -1 and not (dp or fp8)):
         return 0
     idle = _ext.num_cus(device.index or 0) - _bptt_cus(plan)
     cap = idle if _BESIDE_GRID < 0 else min(_BESIDE_GRID, idle)
