@@ -138,7 +138,6 @@ int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void*
                  float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
                  const float* hyper, hipStream_t st);
 int ds2_grad_norm_blocks(long long n);
-int ds2_timing_knobs_build();
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
 int ds2_fp8_quant_blocks(long long na, long long nb_el);
@@ -1381,7 +1380,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("store_g") = false);
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
-  m.def("timing_knobs_build", []() { return ds2_timing_knobs_build() != 0; });
   m.def("event_new", &event_new, py::arg("flags") = 0);
   m.def("event_free", &event_free);
   m.def("event_record", &event_record);

@@ -3,26 +3,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Timing-only diagnostic switches of the persistent recurrence kernels (DS2_RNNX_KNOBS bits
-// 2, 4, 8, 32: skip output stores, waits, MFMAs or publishes — wrong results by design).
-// They exist only in a diagnostic build (python build.py --variant timing -D DS2_TIMING_KNOBS,
-// loaded with DS2_EXT_SO); the default build folds every such test to false, so no stray
-// environment variable can corrupt a training run (ops/rnn.py refuses those bits without it).
-// In the default build the test is ANDed with a zero the compiler cannot see through (an
-// s_mov_b32 0 in asm: no input can set it), rather than folded to false: folding let hipcc
-// re-schedule the wide BPTT's gather loops into 70-112 spilled VGPRs (rnnrs_bwd_kernel<1, 12,
-// 6, *>, config 5 bf16 27.2 vs 22.2 ms/step), while the opaque zero keeps round 4's code.
-#ifdef DS2_TIMING_KNOBS
-#define DS2_TKNOB(knobs, bit) (((knobs) & (bit)) != 0)
-#else
-__device__ __forceinline__ int ds2_opaque_zero() {
-  int z;
-  asm("s_mov_b32 %0, 0" : "=s"(z));
-  return z;
-}
-#define DS2_TKNOB(knobs, bit) ((((knobs) & (bit)) & ds2_opaque_zero()) != 0)
-#endif
-
 namespace ds2 {
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA 16x16x32 A/B fragment

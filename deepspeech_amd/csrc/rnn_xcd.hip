@@ -1468,7 +1468,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
           for (int i = 0; i < GPT; ++i) {
             if (i + CHB < GPT) v[i + CHB < GPT ? i + CHB : 0] = load_sc1_b128(rs_ring, off[i + CHB < GPT ? i + CHB : 0]);
             if (pg7 + MW * i < P) {
-              while (!DS2_TKNOB(a.knobs, 4) && !granule_tagged16(v[i], want)) {
+              while (!(a.knobs & 4) && !granule_tagged16(v[i], want)) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
                 if (!(a.knobs & 16384)) __builtin_amdgcn_s_sleep(1);   // back-off (knob 16384: none; measured neutral)
                 v[i] = load_sc1_b128(rs_ring, off[i]);
@@ -1509,7 +1509,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 #pragma unroll
           for (int i = 0; i < NI; ++i) {
             if (pg7 + MW * (2 * i + h) < P) {
-              while (!DS2_TKNOB(a.knobs, 4) && !granule_tagged16(v[i], want)) {
+              while (!(a.knobs & 4) && !granule_tagged16(v[i], want)) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
                 if (!(a.knobs & 16384)) __builtin_amdgcn_s_sleep(1);   // back-off (knob 16384: none; measured neutral)
                 v[i] = load_sc1_b128(rs_ring, off[i]);
@@ -1549,7 +1549,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
 #pragma unroll
           for (int i = 0; i < GPT; ++i) {
             if (pg7 + MW * i < P) {
-              while (!DS2_TKNOB(a.knobs, 4) && !granule_tagged(v[i], want)) {   // knob 4: no wait (timing only)
+              while (!(a.knobs & 4) && !granule_tagged(v[i], want)) {   // knob 4: no wait (timing only)
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) { s_abort = 1; atomicOr(a.err, 1u); break; }
                 if (!(a.knobs & 16384)) __builtin_amdgcn_s_sleep(1);   // back-off (knob 16384: none; measured neutral)
                 v[i] = load_sc1_b128(rs_ring, off[i]);
@@ -1643,14 +1643,14 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
                              (int)((__float_as_uint(canon32(acc[2])) & ~1u) | tg),
                              (int)((__float_as_uint(canon32(acc[3])) & ~1u) | tg)};
             const unsigned off = ring_off(ws, mem, mt, lane & 15, 4 * (lane >> 4));
-            if (DS2_TKNOB(a.knobs, 32)) {                // knob 32 (timing only, with 4): no publish stores
+            if (a.knobs & 32) {                          // knob 32 (timing only, with 4): no publish stores
             } else if (plain) store_b128(rs_ring, off, v);
             else store_sc1_b128(rs_ring, off, v);
           }
         };
         if constexpr (PBF) {
           // unit pair p = wave + 7k: m-tiles 2p, 2p+1 -> one tagged-bf16 granule per lane
-          if (!DS2_TKNOB(a.knobs, 8) && !DS2_TKNOB(a.knobs, 32)) {
+          if (!(a.knobs & 40)) {
             // pair by pair: MFMA chains 2k, 2k+1, then the pair's convert/tag/store, so the
             // first granule leaves after 2G MFMAs. Measured against interleaving all MTU
             // chains (k-step outer, every store after the last MFMA; DS2_PUB_PIPE): 3.14 vs
@@ -1692,14 +1692,14 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
             const int pr = wave + MW * (i >> 1);
             if (2 * pr + 1 < MTS) {
               f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
-              if (!DS2_TKNOB(a.knobs, 8)) {
+              if (!(a.knobs & 8)) {
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                   a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], a0, 0, 0, 0);
                   a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i + 1][g], bfr[g], a1, 0, 0, 0);
                 }
               }
-              if (prow && !DS2_TKNOB(a.knobs, 32)) {
+              if (prow && !(a.knobs & 32)) {
                 i32x4 v;
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
@@ -1718,7 +1718,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
           const int mt0 = wave + MW * i, mt1 = wave + MW * (i + 1);
           if (mt1 < MTS) {
             f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
-            if (!DS2_TKNOB(a.knobs, 8)) {                // knob 8: no MFMA (timing only)
+            if (!(a.knobs & 8)) {                        // knob 8: no MFMA (timing only)
 #pragma unroll
               for (int g = 0; g < G; ++g) {
                 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ua[i][g], bfr[g], a0, 0, 0, 0);
@@ -2003,7 +2003,7 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
       f32x4 acc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bool nomfma = DS2_TKNOB(a.knobs, 4);        // knob 4: no MFMA (timing only, wrong results)
+      const bool nomfma = (a.knobs & 4) != 0;           // knob 4: no MFMA (timing only, wrong results)
       auto mfma_k = [&](int kk, bf16x8 af) {
         if (nomfma) { acc[0][0] += __builtin_bit_cast(float, (int)af[0]); return; }
 #pragma unroll
@@ -2057,7 +2057,7 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
       st.mark(-1);
       if (a.ysum != nullptr && s >= 2) mw_ysum_load(s - 2);
       if (s + 1 < a.steps) mw_put(s + 1);
-      if (s >= 2 && !DS2_TKNOB(a.knobs, 2)) mw_store(s - 2);   // knob 2: no output stores (timing only)
+      if (s >= 2 && !(a.knobs & 2)) mw_store(s - 2);     // knob 2: no output stores (timing only)
       if (s + 2 < a.steps) mw_load(s + 2);
       st.mark(0);
       lds_barrier();
@@ -2404,14 +2404,6 @@ static int set_smem_attr(F kernel, size_t smem) {
 }
 
 }  // namespace
-
-extern "C" int ds2_timing_knobs_build() {
-#ifdef DS2_TIMING_KNOBS
-  return 1;
-#else
-  return 0;
-#endif
-}
 
 extern "C" {
 

@@ -1,10 +1,10 @@
 """Register budget of the hand-written kernels (CPU: hipcc cross-compiles gfx950 here).
 
 A spilled persistent kernel runs far slower, and a harmless-looking source edit can tip one
-over: round 5's compile-time removal of the timing-only knob branches let hipcc re-schedule the
-config-5 BPTT (rnnrs_bwd_kernel<1, 12, 6, *>) into 70-112 spilled VGPRs, 22.2 -> 27.2 ms/step,
-which no functional test noticed. Every kernel that spills must be on the allowlist below
-(diagnostic stamp builds and variants no default plan launches)."""
+over: round 5's (reverted) compile-time removal of the timing-only knob branches let hipcc
+re-schedule the config-5 BPTT (rnnrs_bwd_kernel<1, 12, 6, *>) into 70-112 spilled VGPRs,
+22.2 -> 27.2 ms/step, which no functional test noticed. Every kernel that spills must be on
+the allowlist below (diagnostic stamp builds and variants no default plan launches)."""
 import os
 import shutil
 import sys

@@ -104,6 +104,8 @@ def main():
                     "BPTT: 4 no exchange wait, 8 no publish MFMA, 32 no publish stores (with 4), 64 fp32 "
                     "partials instead of tagged bf16 (results correct)")
     a = ap.parse_args()
+    if any(int(k) & 46 for k in a.knobs.split(",")):   # timing-only bits 2 | 4 | 8 | 32 (ops/rnn.py)
+        os.environ["DS2_TIMING_ONLY"] = "1"
     for proto in a.kernels.split(","):
       os.environ["DS2_RNN_KERNEL"] = proto
       for nw in ([int(x) for x in a.nw.split(",")] if proto == "v1" else [int(k) for k in a.knobs.split(",")]):
