@@ -172,6 +172,9 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
             return False
     batch = A.shape[0] if A.dim() == 3 else 1
     key = (M, N, K, a_col, b_col, batch)
+    if _FORCE is None and key not in TUNED and _small_rowrow(M, N, K, a_col, b_col, batch, epi, a):
+        gemm(A, B, out, M, N, K, a_col, b_col, epi, alpha, bias, fill=fill)
+        return True
     if _FORCE is None and key not in TUNED and gemm8_supported(M, N, K, False, a_col, b_col):
         gemm8(A, B, out, epi, alpha, bias, a_col=a_col, b_col=b_col, max_grid=max_grid, splits=splits, fill=fill)
         return True
@@ -179,6 +182,24 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
         return False
     gemm(A, B, out, M, N, K, a_col, b_col, epi, alpha, bias, fill=fill)
     return True
+
+
+# DS2_SMALL_M=0 keeps every covered shape on gemm8 (A/B timing)
+_SMALL_M = os.environ.get("DS2_SMALL_M", "1") != "0"
+
+
+def _small_rowrow(M: int, N: int, K: int, a_col: bool, b_col: bool, batch: int, epi: int,
+                  a: torch.Tensor) -> bool:
+    """Row-row bf16 GEMMs of few output tiles and short K (the projections of the short
+    SortaGrad buckets) run on csrc/gemm.hip's cost-model tile: with at most cus/2 256^2 tiles
+    gemm8 leaves half the chip idle, and at K <= 2400 its split-K plan does not recover that,
+    while 128-row tiles fill it. tools/bench_gemm_small_m.py, MI355X (profiles/r5_gemm.md):
+    projection (N 4800, K 800) at M 672: 12.8 vs 27.0 us, at 1312: 20.2 vs 28.5; (4800, 2400):
+    27.3 vs 36.9 and 42.3 vs 49.7; at M 2432 (190 tiles) gemm8 wins again (30.3 vs 32.6).
+    The input-gradient shapes (K 4800) keep gemm8's split-K, which wins there at every M."""
+    if not _SMALL_M or a_col or b_col or epi != 0 or batch != 1 or K > 2400 or not supported(M, N, K, a_col, b_col):
+        return False
+    return _cdiv(M, 256) * _cdiv(N, 256) * 2 <= _dev_cus(a)
 
 
 def mm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False,
