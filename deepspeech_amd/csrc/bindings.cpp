@@ -117,6 +117,8 @@ int ds2_fp8_quant_u(int ndir, const void* const* x, int rows, int cols, void* co
                     float* part, hipStream_t st);
 int ds2_fp8_quant_pow2_t(const void* x, int rows, int cols, void* q, int* uexp, unsigned* amax, hipStream_t st);
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs);
+int ds2_rnnx_fwd_family(int H, int cell, int mt, int knobs);
+int ds2_rnnx_bwd_family(int H, int cell, int mt, int R);
 int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st);
 long long ds2_rnnx_ring_floats(int H, int BG, int R);
 int ds2_rnnx_grid(int H, int cell, int ngroups, int xcd_map);
@@ -169,7 +171,7 @@ int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema
                         int nr, float lr_t, float b1, float b2, float eps, float gscale, float ema_keep,
                         const float* hyper, hipStream_t st);
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
-                   void* a8, void* b8, float* part, float* scales, hipStream_t st);
+                   void* a8, void* b8, float* part, float* scales, const void* a2, void* asum, hipStream_t st);
 int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st);
 int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                    hipStream_t st);
@@ -959,9 +961,21 @@ int64_t fp8_quant_blocks(int64_t na, int64_t nb) { return ds2_fp8_quant_blocks(n
 
 // per-tensor e4m3fn quantisation of two bf16 operands a [rows_a, K], b [rows_b, K] into
 // a8 [rows_a, Kp], b8 [rows_b, Kp] (columns >= K zero); scales[0] = amax_a/448,
-// scales[1] = amax_b/448 * alpha (device-side, for the fp8 GEMM's epilogue)
+// scales[1] = amax_b/448 * alpha (device-side, for the fp8 GEMM's epilogue). a2 / asum (given
+// together, a's shape): operand a is a + a2 (a bidirectional layer's two direction outputs),
+// its bf16 sum written to asum in the same pass (bitwise torch.add) and quantised from there.
 void fp8_quant2(at::Tensor a, at::Tensor b, double alpha, at::Tensor a8, at::Tensor b8, at::Tensor part,
-                at::Tensor scales) {
+                at::Tensor scales, c10::optional<at::Tensor> a2, c10::optional<at::Tensor> asum) {
+  TORCH_CHECK(a2.has_value() == asum.has_value(), "fp8_quant2: a2 and asum go together");
+  if (a2.has_value()) {
+    need_gpu(*a2, "a2");
+    need_gpu(*asum, "asum");
+    TORCH_CHECK(a2->scalar_type() == at::kBFloat16 && asum->scalar_type() == at::kBFloat16 && a2->is_contiguous() &&
+                    asum->is_contiguous() && a2->sizes() == a.sizes() && asum->sizes() == a.sizes() &&
+                    (reinterpret_cast<uintptr_t>(a2->data_ptr()) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(asum->data_ptr()) & 15) == 0,
+                "a2 / asum: contiguous 16-B aligned bf16 of a's shape");
+  }
   need_gpu(a, "a");
   need_gpu(b, "b");
   need_gpu(a8, "a8");
@@ -982,7 +996,9 @@ void fp8_quant2(at::Tensor a, at::Tensor b, double alpha, at::Tensor a8, at::Ten
   const int nb = ds2_fp8_quant_blocks(a.size(0) * Kp, b.size(0) * Kp);
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= 2 * nb, "part: 2*blocks floats");
   check(ds2_fp8_quant2(a.data_ptr(), a.size(0), b.data_ptr(), b.size(0), (int)K, (int)Kp, (float)alpha, a8.data_ptr(),
-                       b8.data_ptr(), part.data_ptr<float>(), scales.data_ptr<float>(), cur_stream()),
+                       b8.data_ptr(), part.data_ptr<float>(), scales.data_ptr<float>(),
+                       a2.has_value() ? a2->data_ptr() : nullptr, asum.has_value() ? asum->data_ptr() : nullptr,
+                       cur_stream()),
         "fp8_quant2");
 }
 
@@ -1338,6 +1354,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("N"), py::arg("NP"), py::arg("H"), py::arg("BG"), py::arg("R"), py::arg("steps"), py::arg("gstride"),
         py::arg("ndir"), py::arg("cell"), py::arg("mt"), py::arg("timeout"), py::arg("xcd_map"), py::arg("knobs"),
         py::arg("stamps") = py::none(), py::arg("ysum") = py::none());
+  m.def("rnnx_fwd_family", [](int64_t H, int64_t cell, int64_t mt, int64_t knobs) {
+    return ds2_rnnx_fwd_family((int)H, (int)cell, (int)mt, (int)knobs);
+  });
+  m.def("rnnx_bwd_family", [](int64_t H, int64_t cell, int64_t mt, int64_t R) {
+    return ds2_rnnx_bwd_family((int)H, (int)cell, (int)mt, (int)R);
+  });
   m.def("rnnx_fwd_fuses_sum", [](int64_t H, int64_t cell, int64_t mt, int64_t ndir, int64_t knobs) {
     return ds2_rnnx_fwd_fuses_sum((int)H, (int)cell, (int)mt, (int)ndir, (int)knobs) != 0;
   });
@@ -1367,7 +1389,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_bf16", &cast_bf16);
   m.def("device_info", &device_info);
   m.def("fp8_quant_blocks", &fp8_quant_blocks);
-  m.def("fp8_quant2", &fp8_quant2);
+  m.def("fp8_quant2", &fp8_quant2, py::arg("a"), py::arg("b"), py::arg("alpha"), py::arg("a8"), py::arg("b8"),
+        py::arg("part"), py::arg("scales"), py::arg("a2") = py::none(), py::arg("asum") = py::none());
   m.def("transpose_bf16", &transpose_bf16);
   m.def("gemm8", &gemm8, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("epi"),
         py::arg("alpha") = 1.0, py::arg("alpha_dev") = py::none(), py::arg("alpha_dev2") = py::none(),

@@ -11,6 +11,11 @@
 //   2. quant2_kernel  every block first reduces the partials of its operand (<= 1024
 //                     floats, L2-resident), then casts its slice; block 0 publishes
 //                     scales = {amax_a / 448, amax_b / 448 * alpha}.
+// Direction-sum form (an fp8 bidirectional layer feeding the next fp8 layer, SURVEY K12 /
+// src/custom_ops.py:94-95): operand a is given as its two addends a + a2 (the directions'
+// outputs); pass 1 writes the bf16 sum (the next layer's saved input, bitwise torch.add: fp32
+// add, one rounding) while it takes the amax, and pass 2 casts the sum. No separate add launch
+// and no extra read of the sum.
 #include <hip/hip_fp8.h>
 
 #include "common.h"
@@ -37,7 +42,8 @@ __device__ __forceinline__ float block_max(float v, float* sh) {
 
 __global__ __launch_bounds__(QT) void amax2_kernel(const bf16_t* __restrict__ a, long long na,
                                                    const bf16_t* __restrict__ b, long long nb_el, int nb,
-                                                   float* __restrict__ part) {
+                                                   float* __restrict__ part, const bf16_t* __restrict__ a2,
+                                                   bf16_t* __restrict__ asum) {
   __shared__ float sh[QT / 64];
   const bool second = blockIdx.x >= (unsigned)nb;
   const bf16_t* x = second ? b : a;
@@ -45,6 +51,29 @@ __global__ __launch_bounds__(QT) void amax2_kernel(const bf16_t* __restrict__ a,
   const int blk = second ? blockIdx.x - nb : blockIdx.x;
   float m = 0.f;
   const long long n8 = n / 8;
+  if (!second && a2 != nullptr) {
+    // direction-sum form: s = bf16(a + a2) stored, amax taken of the stored (rounded) sum
+    for (long long i = (long long)blk * QT + threadIdx.x; i < n8; i += (long long)nb * QT) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(a + i * 8);
+      const bf16x8 w = *reinterpret_cast<const bf16x8*>(a2 + i * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bf16_t r = f2bf(__fadd_rn(bf2f((bf16_t)v[j]), bf2f((bf16_t)w[j])));
+        o[j] = r;
+        m = fmaxf(m, fabsf(bf2f(r)));
+      }
+      *reinterpret_cast<bf16x8*>(asum + i * 8) = o;
+    }
+    for (long long i = n8 * 8 + (long long)blk * QT + threadIdx.x; i < n; i += (long long)nb * QT) {
+      const bf16_t r = f2bf(__fadd_rn(bf2f(a[i]), bf2f(a2[i])));
+      asum[i] = r;
+      m = fmaxf(m, fabsf(bf2f(r)));
+    }
+    m = block_max(m, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = m;
+    return;
+  }
   for (long long i = (long long)blk * QT + threadIdx.x; i < n8; i += (long long)nb * QT) {
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
 #pragma unroll
@@ -119,15 +148,17 @@ int ds2_fp8_quant_blocks(long long na, long long nb_el) {
 
 // a [rows_a][K], b [rows_b][K]: bf16 (16-B aligned, K % 8 == 0); a8 [rows_a][Kp], b8
 // [rows_b][Kp]: fp8 e4m3fn outputs, Kp % 8 == 0, columns >= K zero; part: 2*nb floats;
-// scales: {amax_a / 448, amax_b / 448 * alpha}
+// scales: {amax_a / 448, amax_b / 448 * alpha}. a2 / asum (both or neither, [rows_a][K]): the
+// operand is a + a2, written to asum (bf16) and quantised from there.
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
-                   void* a8, void* b8, float* part, float* scales, hipStream_t st) {
-  if (K % 8 || Kp % 8 || Kp < K) return (int)hipErrorInvalidValue;
+                   void* a8, void* b8, float* part, float* scales, const void* a2, void* asum, hipStream_t st) {
+  if (K % 8 || Kp % 8 || Kp < K || ((a2 == nullptr) != (asum == nullptr))) return (int)hipErrorInvalidValue;
   const long long na = rows_a * K, nb_el = rows_b * K;
   const int nb = ds2_fp8_quant_blocks(rows_a * Kp, rows_b * Kp);
   hipLaunchKernelGGL(amax2_kernel, dim3(2 * nb), dim3(QT), 0, st, (const bf16_t*)a, na, (const bf16_t*)b, nb_el, nb,
-                     part);
-  hipLaunchKernelGGL(quant2_kernel, dim3(2 * nb), dim3(QT), 0, st, (const bf16_t*)a, rows_a, (const bf16_t*)b, rows_b,
+                     part, (const bf16_t*)a2, (bf16_t*)asum);
+  const bf16_t* qa = (const bf16_t*)(asum != nullptr ? asum : a);
+  hipLaunchKernelGGL(quant2_kernel, dim3(2 * nb), dim3(QT), 0, st, qa, rows_a, (const bf16_t*)b, rows_b,
                      K, Kp, nb, (const float*)part, alpha, (unsigned char*)a8, (unsigned char*)b8, scales);
   return (int)hipGetLastError();
 }

@@ -2444,6 +2444,25 @@ static bool gen4_ok(int H, int cell, int mt, int knobs) {
   return kbq <= 8;
 }
 
+int ds2_rnnx_kb(int H, int G, int fwd);
+
+// Which forward kernel family ds2_rnnx_fwd launches for a geometry (the dispatch below and
+// the report binding rnnx_fwd_family share this one function): 6 rnnw (wide one-gate), 5 rnne
+// (GRU, K-eighths), 4 rnnq (K-quarters), 2 rnnx (generation 2); 0 = not covered (-30/-31/-33)
+int ds2_rnnx_fwd_family(int H, int cell, int mt, int knobs) {
+  if (wide_ok(H, cell)) return 6;
+  if (H % UPW != 0 || mt != 1 || ds2_rnnx_kb(H, cell == CELL_GRU ? 3 : 1, 1) < 0) return 0;
+  if (gen4_ok(H, cell, mt, knobs)) return (cell == CELL_GRU && H / 32 <= 32) ? 5 : 4;
+  return 2;
+}
+
+// BPTT family of ds2_rnnx_bwd_rs: 6 rnnw_bwd, 3 rnnrs (reduce-scatter), 0 = not covered
+int ds2_rnnx_bwd_family(int H, int cell, int mt, int R) {
+  if (wide_ok(H, cell)) return (R >= 1 && R <= 8 && mt == 1 && xcd_p(H, cell) <= 4 * MW) ? 6 : 0;
+  if (H % UPW != 0 || R < 1 || R > 16 || mt != 1 || H / UPW > 6 * MW) return 0;
+  return (H / 16 + MW - 1) / MW <= 12 ? 3 : 0;          // rnnrs_bwd_kernel's unit tiles (-36 past)
+}
+
 int ds2_rnnx_fwd_fuses_sum(int H, int cell, int mt, int ndir, int knobs) {
   return ndir == 2 && mt == 1 && (wide_ok(H, cell) || gen4_ok(H, cell, mt, knobs)) ? 1 : 0;
 }
@@ -2521,13 +2540,13 @@ int ds2_rnnx_fwd(const DS2RnnX* d, hipStream_t st) {
   const int kbq = (d->H / 32 + 3) / 4;
   // (GRU at kbq = 8 spills under the 3-waves-per-SIMD register budget: kbq 8..10 keep
   // kbq - 7 k-steps of U in LDS)
-  const bool gen4 = gen4_ok(d->H, d->cell, d->mt, d->knobs);
-  if (d->ysum != nullptr && (!gen4 || d->ndir != 2)) return -37;   // only gen 4 fuses the sum
-  // generation 5 (K-eighths, each granule polled once) for GRU layers with H <= 1024;
-  // knob 1 << 22 keeps generation 4 (A/B)
+  const int fam = ds2_rnnx_fwd_family(d->H, d->cell, d->mt, d->knobs);
+  const bool gen4 = fam == 4 || fam == 5;
+  if (d->ysum != nullptr && (!gen4 || d->ndir != 2)) return -37;   // only gen 4 / 5 fuse the sum
+  // generation 5 (K-eighths, each granule polled once) for GRU layers with H <= 1024
   // (H = 1280 measured slower on generation 5: 7.4 vs 5.75 us/step, its 40-workgroup groups
   // span XCDs and the U slice needs LDS k-steps and a single partial buffer)
-  if (gen4 && d->cell == CELL_GRU && d->H / 32 <= 32) {
+  if (fam == 5) {
     switch ((d->H / 32 + 7) / 8) {
 #define DS2_E(K, L, B)                                                                                    \
   case K:                                                                                                 \

@@ -347,7 +347,10 @@ class DeepSpeech2(nn.Module):
         for i, layer in enumerate(self.rnn):
             if self.engine == "hip":
                 from ..ops import rnn as RNN
-                out = RNN.recurrent_layer_hip(layer, inp, lens, i)
+                # an fp8 layer feeding an fp8 layer hands over its two direction outputs and
+                # the upper layer's quantiser sums them (no direction-sum launch)
+                pair = self.stack_fix and i + 1 < len(self.rnn) and RNN.pairs_ok(self.rnn[i + 1])
+                out = RNN.recurrent_layer_hip(layer, inp, lens, i, pair_out=pair)
             else:
                 from ..utils import trace as TR
                 with TR.phase(TR.rnn_cell(i)):

@@ -415,11 +415,14 @@ def fp8_pad(K: int) -> int:
     return -(-K // 128) * 128
 
 
-def linear_fp8(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], alpha: float) -> torch.Tensor:
+def linear_fp8(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], alpha: float,
+               x2b: Optional[torch.Tensor] = None, xsum: Optional[torch.Tensor] = None) -> torch.Tensor:
     """alpha * x2 @ W16^T + b16 with both operands quantised per tensor to OCP fp8 e4m3
     (csrc/quant.hip: amax, scale, saturating cast into K-padded copies, scales on the device)
     and multiplied by gemm8's fp8 path (v_mfma_scale_f32_16x16x128_f8f6f4: twice the bf16
-    MFMA rate); the two scales and alpha are applied in the epilogue. bf16 output."""
+    MFMA rate); the two scales and alpha are applied in the epilogue. bf16 output.
+    x2b / xsum: the input is x2 + x2b (a bidirectional layer's direction outputs), summed by
+    the quantiser's first pass into xsum (bf16, x2's shape; bitwise torch.add)."""
     C = _ext.ext()
     x2 = x2.contiguous()
     W16 = W16.contiguous()
@@ -431,6 +434,6 @@ def linear_fp8(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor],
     w8 = torch.empty(N, Kp, device=x2.device, dtype=f8)
     nb = int(C.fp8_quant_blocks(M * Kp, N * Kp))
     ws = torch.empty(2 * nb + 2, device=x2.device, dtype=torch.float32)
-    C.fp8_quant2(x2, W16, float(alpha), x8, w8, ws[:2 * nb], ws[2 * nb:])
+    C.fp8_quant2(x2, W16, float(alpha), x8, w8, ws[:2 * nb], ws[2 * nb:], x2b, xsum)
     out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
     return gemm8(x8, w8, out, 0, 1.0, b16, ws[2 * nb:2 * nb + 1], ws[2 * nb + 1:2 * nb + 2], splits=1)

@@ -28,7 +28,7 @@ import math
 import os
 import weakref
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -463,6 +463,27 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None, bufs: Optional[_FwdBufs] =
     return y, (hx, hs, gates if gates is not None else torch.empty(0, device=dev))
 
 
+_FWD_FAMILY = {6: "rnnw_fwd (wide one-gate)", 5: "rnne_fwd (gen 5)", 4: "rnnq_fwd (gen 4)", 2: "rnnx_fwd (gen 2)"}
+_BWD_FAMILY = {6: "rnnw_bwd (wide one-gate)", 3: "rnnrs_bwd (reduce-scatter)"}
+
+
+def kernel_families(plan: RnnPlan) -> Tuple[str, str]:
+    """(forward, BPTT) kernel family a bf16 plan launches: csrc/rnn_xcd.hip's dispatch
+    (ds2_rnnx_fwd_family / ds2_rnnx_bwd_family, the functions the launches themselves branch
+    on) or generation 1 (csrc/rnn_persistent.hip), persistent or one launch per step. The fp8
+    layers (fp8_recurrence_ok) run csrc/rnn_fp8.hip instead. Raises if the xcd dispatch would
+    refuse the plan."""
+    if plan.kind != "xcd":
+        g1 = "rnn_%s (gen 1, " + ("persistent)" if plan.persistent else "step launches)")
+        return g1 % "fwd", g1 % "bwd"
+    C = _ext.ext()
+    f = int(C.rnnx_fwd_family(plan.H, CELL_CODE[plan.cell], plan.mt, _kernel_knobs()))
+    b = int(C.rnnx_bwd_family(plan.H, CELL_CODE[plan.cell], plan.mt, plan.R))
+    if f not in _FWD_FAMILY or b not in _BWD_FAMILY:
+        raise ValueError("xcd plan not covered by csrc/rnn_xcd.hip: %r" % (plan,))
+    return _FWD_FAMILY[f], _BWD_FAMILY[b]
+
+
 def fp8_recurrence_ok(plan: RnnPlan, N: int) -> bool:
     """csrc/rnn_fp8.hip serves this GRU layer (config 5's fp8 mode): H % 256 == 0, H/64 <= 32
     workgroups per group (one XCD), 8 groups of <= 8 rows, and the same padded batch rows as
@@ -489,11 +510,13 @@ def _quant_u(U, plan: RnnPlan, rowmajor: bool = True, transposed: bool = True):
     return U8, U8T, words
 
 
-def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan, keep: Optional[dict] = None):
+def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan, keep: Optional[dict] = None, pair: bool = False):
     """GRU forward with e4m3 recurrent weights (one power-of-two scale per direction, computed
     on the device) and an e4m3 hidden-state exchange: groups of H/64 workgroups on one XCD
     (csrc/rnn_fp8.hip). Returns (y, (hx, hs, gates)) in the layout of _run_fwd. With keep (a
-    dict), the transposed e4m3 U of the same quantisation goes into keep["quant"] for the BPTT."""
+    dict), the transposed e4m3 U of the same quantisation goes into keep["quant"] for the BPTT.
+    pair (two directions): y is the [2, T, N, H] pair of direction outputs, unsummed — the next
+    fp8 layer's quantiser sums them (fp8_linear x2b)."""
     C = _ext.ext()
     T, N, gstride = gx.shape
     H, ndir = plan.H, plan.ndir
@@ -516,7 +539,7 @@ def _run_fwd_fp8(gx, lens, U, bh, plan: RnnPlan, keep: Optional[dict] = None):
     C.multi_fill([hx[d, 0] for d in range(ndir)] + [hs[d, 0] for d in range(ndir)], [0] * (2 * ndir))
     C.rnnf8_fwd(gx.contiguous(), lens, U8, words, bh[0], bh[1] if ndir == 2 else None, y2, hq, hx, hs, gates, census,
                 error_word(dev), T, N, NP, H, BG, R, T, gstride, ndir, TIMEOUT_TICKS, 1)
-    y = torch.add(y2[0], y2[1]) if ndir == 2 else y2[0]
+    y = (y2 if pair else torch.add(y2[0], y2[1])) if ndir == 2 else y2[0]
     return y, (hx, hs, gates)
 
 
@@ -697,12 +720,19 @@ class BiRecurrence(torch.autograd.Function):
 FP8_MAX = 448.0      # OCP e4m3 (gfx950 MFMA fp8 is OCP e4m3fn, not MI300's fnuz)
 
 
-def fp8_linear(x2: torch.Tensor, W16: torch.Tensor, b16: torch.Tensor, alpha: float) -> torch.Tensor:
+def fp8_linear(x2: torch.Tensor, W16: torch.Tensor, b16: torch.Tensor, alpha: float,
+               x2b: Optional[torch.Tensor] = None, xsum: Optional[torch.Tensor] = None) -> torch.Tensor:
     """alpha * x2 @ W16^T + b16 with both operands quantised to fp8 e4m3 (per-tensor amax
     scaling, scales kept on the device: no host sync) and multiplied on the CDNA4 fp8 MFMA
     path of the hand-written gemm8 kernel (ops/gemm.py linear_fp8); bf16 output. Forward-only
     precision reduction: the backward GEMMs keep the bf16 copies (fp8 'mixed precision',
-    BASELINE config 5). CPU: the same arithmetic in torch (dequantised fp32 product)."""
+    BASELINE config 5). CPU: the same arithmetic in torch (dequantised fp32 product).
+    x2b / xsum: the input is the direction sum x2 + x2b, written to xsum by the quantiser."""
+    if x2b is not None:
+        if x2.is_cuda and not (x2.shape[1] % 8 or W16.shape[0] % 4):
+            return GM.linear_fp8(x2, W16, b16, alpha, x2b, xsum)
+        torch.add(x2, x2b, out=xsum)
+        x2 = xsum
     if x2.is_cuda:
         if x2.shape[1] % 8 or W16.shape[0] % 4:
             return torch.addmm(b16, x2, W16.t(), alpha=alpha)      # outside the kernels' contract
@@ -760,18 +790,32 @@ class FusedBiLayer(torch.autograd.Function):
               dx = dgx [W_fw; W_bw]                             (critical path: feeds layer below)
               dW = dgx^T x, dU_d = dgh_d^T h_d                  (fp32 straight into main_grad)
     alpha = 1/sqrt(1+eps) folds the reference's frozen sequence-BN (quirk Q3); 1 for 'none'.
+
+    fp8 stacks (config 5): with pair_out an fp8 bidirectional layer returns its two direction
+    outputs unsummed, [2, T, N, H], and the next fp8 layer takes that pair as x: its quantiser
+    writes the sum (bitwise torch.add) while it takes the amax (fp8_linear x2b), so the
+    direction sum costs no launch of its own (the sum fused into an existing pass,
+    src/custom_ops.py:94-95). The pair's gradient is the sum's, shared by both halves.
     """
 
     @staticmethod
     def forward(ctx, x, lens, plan: RnnPlan, alpha: float, idx: int, fp8: bool, W_f, W_b, U_f, U_b, b_f, b_b,
-                bh_f, bh_b):
-        T, N, D = x.shape
+                bh_f, bh_b, pair_out: bool = False):
+        pair_in = x.dim() == 4
+        T, N, D = x.shape[-3:]
         dirs_W = [W_f] + ([W_b] if W_b is not None else [])
         dirs_b = [b_f] + ([b_b] if b_b is not None else [])
         W16 = _bf16_group(dirs_W)                     # [ndir*G*H, D]
         b16 = _bf16_group(dirs_b)                     # [ndir*G*H]
-        x16 = x.to(torch.bfloat16).contiguous()
+        if pair_in:
+            if not fp8:
+                raise ValueError("a direction pair feeds only an fp8 layer (its quantiser sums it)")
+            xa, xb = x[0].to(torch.bfloat16).contiguous(), x[1].to(torch.bfloat16).contiguous()
+            x16 = torch.empty(T, N, D, device=x.device, dtype=torch.bfloat16)     # written by the quantiser
+        else:
+            x16 = x.to(torch.bfloat16).contiguous()
         x2 = x16.view(T * N, D)
+        ctx.pair_in = pair_in
         fp8_rec = fp8 and x.is_cuda and fp8_recurrence_ok(plan, N)
         bufs = fill = None
         if x.is_cuda and not fp8_rec and plan.kind == "xcd":
@@ -779,7 +823,11 @@ class FusedBiLayer(torch.autograd.Function):
             # (csrc/gemm8.hip DS2Fill): no separate fill launch between the two
             bufs = _alloc_fwd(T, N, plan, x.device)
             fill = _fill_regions(bufs, plan)
-        if fp8:
+        if pair_in:
+            gx = fp8_linear(xa.view(T * N, D), W16, b16, alpha, xb.view(T * N, D), x2).view(T, N, -1)
+            if fill is not None:
+                _ext.ext().multi_fill(*fill)
+        elif fp8:
             gx = fp8_linear(x2, W16, b16, alpha).view(T, N, -1)
             if fill is not None:
                 _ext.ext().multi_fill(*fill)
@@ -802,7 +850,7 @@ class FusedBiLayer(torch.autograd.Function):
             # 300-step loss curve against the bf16 recurrence
             ctx.fp8_bwd = fp8_bptt_ok(plan, N)
             keep = {} if ctx.fp8_bwd else None
-            y, (hx, hs, gates) = _run_fwd_fp8(gx, lens, U, bh, plan, keep)
+            y, (hx, hs, gates) = _run_fwd_fp8(gx, lens, U, bh, plan, keep, pair=pair_out and plan.ndir == 2)
             ctx.fp8_quant = keep["quant"] if keep is not None else None
         else:
             y, (hx, hs, gates) = _run_fwd(gx, lens, U, bh, plan, bufs=bufs)
@@ -818,6 +866,12 @@ class FusedBiLayer(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if dy.dim() == 4:
+            # the pair output's gradient: the next layer returns the sum's gradient for both
+            # halves (one tensor expanded); anything else would need per-direction dy
+            if dy.stride(0) != 0 and not torch.equal(dy[0], dy[1]):
+                raise RuntimeError("direction-pair output with different gradients per direction")
+            dy = dy[0]
         with TR.phase(TR.rnn_cell(ctx.idx, True)):
             return FusedBiLayer._backward(ctx, dy)
 
@@ -853,8 +907,10 @@ class FusedBiLayer(torch.autograd.Function):
                 # an fp8 or differently shaped layer below just leaves them unused)
                 fill = (_prefill_bwd(plan, dgx.device) if ctx.idx >= 1 and plan.kind == "xcd" and
                         not getattr(ctx, "fp8_bwd", False) else None)
-                return _mm_bf16(dgx2, wT.t(), fill=fill).view(T, N, D)
-            return _mm_bf16(dgx2, W16).view(T, N, D)
+                dx = _mm_bf16(dgx2, wT.t(), fill=fill).view(T, N, D)
+            else:
+                dx = _mm_bf16(dgx2, W16).view(T, N, D)
+            return dx.unsqueeze(0).expand(2, T, N, D) if ctx.pair_in else dx
 
         # ---- weight gradients (off the critical path) ----
         # only arena-managed weights (gradients written to main_grad, nothing returned to
@@ -991,7 +1047,7 @@ class FusedBiLayer(torch.autograd.Function):
         elif (ctx.idx >= 1 and ctx.idx == _upper_trigger(plan, x16.device) and arena is not None and x16.is_cuda and
               arena.wgrad.defer_input and arena.wgrad.on_side(x16.device)):
             arena.wgrad.run_early_upper(ctx.idx)   # layers >= idx and the head, beside the next BPTT
-        return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1])
+        return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1], None)
 
 
 # A layer's weight gradients are deferred to the grouped tail launch only when its BPTT leaves
@@ -1453,14 +1509,27 @@ def recurrent_layer_infer(layer, x: torch.Tensor, lens: torch.Tensor, h0: Option
     return y, hs[:, T, :N].clone()
 
 
-def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int = 0) -> torch.Tensor:
+def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int = 0,
+                        pair_out: bool = False) -> torch.Tensor:
+    """One recurrent layer on the HIP engine. x: [T, N, D], or the [2, T, N, D] direction pair
+    of an fp8 layer below (pairs_ok). pair_out: return this layer's fp8 direction outputs as
+    such a pair when it has them (the caller feeds them to an fp8 layer), else the sum."""
     with TR.phase(TR.rnn_cell(idx)):
-        return _recurrent_layer_hip(layer, x, lens, idx)
+        return _recurrent_layer_hip(layer, x, lens, idx, pair_out)
 
 
-def _recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int) -> torch.Tensor:
+# DS2_FP8_PAIRS=0: every fp8 layer sums its directions with torch.add (A/B timing)
+_FP8_PAIRS = os.environ.get("DS2_FP8_PAIRS", "1") != "0"
+
+
+def pairs_ok(layer) -> bool:
+    """layer takes the unsummed direction pair of the layer below (FusedBiLayer's fp8 form)."""
+    return _FP8_PAIRS and bool(getattr(layer, "fp8", False)) and layer.seq_bn in ("frozen", "none")
+
+
+def _recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int, pair_out: bool = False) -> torch.Tensor:
     ndir = 2 if layer.bw is not None else 1
-    plan = plan_for(x.shape[1], layer.hidden, layer.cell, ndir, x.device)
+    plan = plan_for(x.shape[-2], layer.hidden, layer.cell, ndir, x.device)
     fw, bw = layer.fw, layer.bw
     if layer.seq_bn in ("frozen", "none"):
         alpha = sbn_scale() if layer.seq_bn == "frozen" else 1.0
@@ -1468,7 +1537,9 @@ def _recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int) -
                                   fw.W, bw.W if bw is not None else None,
                                   fw.U, bw.U if bw is not None else None,
                                   fw.b, bw.b if bw is not None else None,
-                                  fw.b_h, bw.b_h if bw is not None else None)
+                                  fw.b_h, bw.b_h if bw is not None else None, pair_out)
+    if x.dim() == 4:
+        x = x[0] + x[1]
     x = x.to(torch.bfloat16)
     gx = input_projection_hip(layer, x, lens)
     U_f = fw.U.to(torch.bfloat16)

@@ -349,6 +349,44 @@ def test_fp8_recurrence_model_close_to_bf16(cuda):
     RNN.check_errors()
 
 
+def test_fp8_direction_pairs_are_bitwise_the_summed_stack(cuda, monkeypatch):
+    """fp8 stack (config 5's mode at its width, 3 layers): each fp8 layer hands its two
+    direction outputs to the next one, whose quantiser sums them (FusedBiLayer pair_out), instead
+    of a torch.add per layer. Loss and every gradient are bitwise those of the summed stack, and
+    the pair path leaves exactly one direction-sum add (the top layer's, feeding the head)."""
+    from deepspeech_amd.ops import rnn as RNN
+    torch.manual_seed(3)
+    base = DeepSpeech2(num_filters=32, num_hidden=1280, num_rnn_layers=3, cell="gru").to(cuda)
+    base.set_engine("hip", torch.bfloat16, fp8=True)
+    batch = to_device(FixedShapeBatches(32, max_frames=200, seed=8, pool=1).next(), cuda)
+    assert RNN.fp8_recurrence_ok(RNN.plan_for(32, 1280, "gru", 2, cuda), 32)
+    res = []
+    for pairs in (False, True):
+        m = copy.deepcopy(base)
+        if not pairs:
+            monkeypatch.setattr(RNN, "pairs_ok", lambda layer: False)
+        adds = []
+        real_add = torch.add
+
+        def counting_add(*a, **k):
+            adds.append(1)
+            return real_add(*a, **k)
+        monkeypatch.setattr(torch, "add", counting_add)
+        loss = _loss(m, batch)
+        loss.backward()
+        monkeypatch.setattr(torch, "add", real_add)
+        monkeypatch.undo()
+        RNN.join_wgrad_streams()
+        torch.cuda.synchronize()
+        RNN.check_errors()
+        res.append((loss.detach(), {n: p.grad.clone() for n, p in m.named_parameters()}, len(adds)))
+    (l0, g0, n0), (l1, g1, n1) = res
+    assert torch.equal(l0, l1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+    assert n0 - n1 == 2, (n0, n1)          # 3 layers: two sums moved into the quantisers
+
+
 def test_step_is_bitwise_reproducible(cuda):
     """Two trainers from the same initial state on the same batch produce bitwise-identical
     losses, gradients and updated weights (every fused kernel reduces in a fixed order; the
@@ -471,9 +509,18 @@ def test_prefetcher_matches_direct_upload(cuda):
     pf.close()
 
 
-@pytest.mark.parametrize("cell,H,D,T", [("gru", 800, 800, 241), ("gru", 800, 2400, 241), ("gru", 1280, 1280, 241),
-                                        ("rnn_relu", 800, 800, 241), ("rnn_relu", 1760, 1760, 241)])
-def test_recurrent_layer_same_upstream(cuda, cell, H, D, T):
+# every recurrence kernel family a bf16 plan can reach, at T = 241 and batch 32 (VERDICT r4
+# item 6): (cell, H, input width, T, DS2_RNN_MODE, expected forward family)
+_LAYER_CASES = [("gru", 800, 800, 241, "auto", "rnne_fwd"), ("gru", 800, 2400, 241, "auto", "rnne_fwd"),
+                ("gru", 1280, 1280, 241, "auto", "rnnq_fwd"), ("rnn_relu", 800, 800, 241, "auto", "rnnq_fwd"),
+                ("rnn_relu", 1760, 1760, 241, "auto", "rnnw_fwd"),
+                ("gru", 1056, 1056, 241, "auto", "rnnx_fwd"),        # generation 2: H / 32 = 33
+                ("rnn_relu", 2048, 2048, 241, "auto", "rnn_fwd"),    # wider than rnnw: generation 1
+                ("gru", 800, 800, 241, "step", "rnn_fwd")]           # the non-persistent fallback
+
+
+@pytest.mark.parametrize("cell,H,D,T,mode,family", _LAYER_CASES)
+def test_recurrent_layer_same_upstream(cuda, monkeypatch, cell, H, D, T, mode, family):
     """ONE bidirectional recurrent layer at the production geometries (batch 32, ragged
     lengths) with the same bf16 input and the same upstream gradient fed to the HIP layer
     (projection GEMM, persistent recurrence, BPTT, dx / dW / dU GEMMs, in-kernel bias sums)
@@ -495,8 +542,11 @@ def test_recurrent_layer_same_upstream(cuda, cell, H, D, T):
     from deepspeech_amd.models.deepspeech2 import RecurrentLayer
     from deepspeech_amd.ops import reference as R
     from deepspeech_amd.ops import rnn as RNN
+    monkeypatch.setenv("DS2_RNN_MODE", mode)
     torch.manual_seed(H + D)
     N = 32
+    fams = RNN.kernel_families(RNN.plan_for(N, H, cell, 2, cuda))
+    assert fams[0].startswith(family), fams
     ref = RecurrentLayer(D, H, cell, True, "frozen").to(cuda)
     with torch.no_grad():
         for d in ref.directions():
@@ -541,6 +591,6 @@ def test_recurrent_layer_same_upstream(cuda, cell, H, D, T):
     else:
         spread = reference(False)
         tol = {k: 0.015 if k == "y" else max(0.03, 1.6 * _rel(spread[k], want[k])) for k in want}
-    print({k: (round(errs[k], 5), round(tol[k], 4)) for k in errs})
+    print(fams, {k: (round(errs[k], 5), round(tol[k], 4)) for k in errs})
     bad = {k: (errs[k], tol[k]) for k in errs if errs[k] > tol[k]}
     assert not bad, (bad, errs)

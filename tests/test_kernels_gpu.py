@@ -357,6 +357,36 @@ def test_fp8_quant2_matches_torch(cuda):
         assert ((got - ref).abs()[bad] <= ref.abs()[bad] * 0.125 + 1e-6).all()
 
 
+def test_fp8_quant2_direction_sum_is_torch_add_then_quant(cuda):
+    """The quantiser's direction-sum form (operand a given as a + a2, an fp8 layer's two
+    direction outputs): the bf16 sum it writes is bitwise torch.add, and the scales and e4m3
+    copies are bitwise those of quantising that sum (ragged element count included)."""
+    from deepspeech_amd.ops import _ext
+    C = _ext.ext()
+    torch.manual_seed(1)
+    f8 = torch.float8_e4m3fn
+    for rows, K, Kp in ((1000, 136, 256), (77, 1280, 1280)):
+        ya = (torch.randn(rows, K) * 2).bfloat16().to(cuda)
+        yb = (torch.randn(rows, K) * 2).bfloat16().to(cuda)
+        w = (torch.randn(384, K) * 0.05).bfloat16().to(cuda)
+        nb = int(C.fp8_quant_blocks(rows * Kp, 384 * Kp))
+        outs = []
+        for fused in (False, True):
+            a8 = torch.empty(rows, Kp, device=cuda, dtype=f8)
+            w8 = torch.empty(384, Kp, device=cuda, dtype=f8)
+            ws = torch.empty(2 * nb + 2, device=cuda, dtype=torch.float32)
+            if fused:
+                s = torch.full((rows, K), float("nan"), device=cuda).bfloat16()
+                C.fp8_quant2(ya, w, 0.5, a8, w8, ws[:2 * nb], ws[2 * nb:], yb, s)
+            else:
+                s = torch.add(ya, yb)
+                C.fp8_quant2(s, w, 0.5, a8, w8, ws[:2 * nb], ws[2 * nb:])
+            outs.append((s, a8.view(torch.uint8), w8.view(torch.uint8), ws[2 * nb:]))
+        torch.cuda.synchronize()
+        for x, y in zip(outs[0], outs[1]):
+            assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("cell", ["gru", "rnn_relu"])
 def test_fused_direction_sum_bitwise(cuda, cell):
     """The gen-4 forward's in-kernel direction sum (one direction writes its bf16 value, the

@@ -166,3 +166,24 @@ def test_xcd_plans_for_wide_and_deferral_rule():
     c5 = RNN.make_xcd_plan(32, 1280, "gru", 2, 256)                         # config 5: 160 CUs
     assert RNN._bptt_cus(head) == 200 and RNN._bptt_cus(c5) == 160
     assert 256 - RNN._bptt_cus(head) < RNN._BESIDE_MIN_IDLE_CUS <= 256 - RNN._bptt_cus(c5)
+
+
+def test_recurrence_kernel_family_map():
+    """Which kernel family every bf16 plan launches (no GPU: the host dispatch functions of
+    csrc/rnn_xcd.hip that the launches branch on). Every family on this map is reachable by a
+    geometry someone can configure, and tests/test_engine_gpu.py runs each one at T = 241 and
+    batch 32 against the fp32 reference."""
+    from deepspeech_amd.ops import rnn as RNN
+    want = {("gru", 800, "auto"): "rnne_fwd", ("gru", 256, "auto"): "rnne_fwd",
+            ("gru", 1280, "auto"): "rnnq_fwd", ("rnn_relu", 800, "auto"): "rnnq_fwd",
+            ("rnn_relu", 1760, "auto"): "rnnw_fwd", ("gru", 1056, "auto"): "rnnx_fwd",
+            ("gru", 1344, "auto"): "rnnx_fwd", ("rnn_relu", 2048, "auto"): "rnn_fwd (gen 1, persistent)",
+            ("gru", 800, "step"): "rnn_fwd (gen 1, step"}
+    for (cell, H, mode), fam in want.items():
+        fw, bw = RNN.kernel_families(RNN.make_plan(32, H, cell, 2, 256, mode))
+        assert fw.startswith(fam), (cell, H, mode, fw)
+        assert bw.startswith({"rnnw_fwd": "rnnw_bwd"}.get(fam, "rnn_bwd" if fam.startswith("rnn_fwd") else "rnnrs_bwd"))
+    # the timing-only knob bits never reach the family choice, the selector bit 256 does
+    p = RNN.make_plan(32, 800, "gru", 2, 256)
+    assert int(RNN._ext.ext().rnnx_fwd_family(800, 1, 1, 256)) == 2
+    assert RNN.kernel_families(p)[0].startswith("rnne_fwd")
