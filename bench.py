@@ -150,6 +150,8 @@ def main():
     value = total_audio / elapsed
     flops = ctx.all_reduce_sum(flops)
     lossv = float(loss.float().item()) if loss is not None else float("nan")
+    # device memory high-water mark of the headline steps (caching allocator; this rank)
+    peak_gib = torch.cuda.max_memory_allocated(dev) / 2 ** 30 if dev.type == "cuda" else None
     walk = None
     if not args.no_walk and dev.type == "cuda":
         walk = epoch_walk(trainer, ctx, dev, args.batch_size, args.walk_scale)
@@ -184,6 +186,8 @@ def main():
             "achieved_tflops": round(flops / elapsed / 1e12, 2),
             "final_loss": round(lossv, 4),
         }
+        if peak_gib is not None:
+            out["peak_mem_gib"] = round(peak_gib, 2)
         if walk is not None:
             out["epoch_walk"] = walk
         if infer is not None:
