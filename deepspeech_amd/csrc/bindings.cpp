@@ -173,6 +173,9 @@ int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
                    void* a8, void* b8, float* part, float* scales, const void* a2, void* asum, hipStream_t st);
 int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st);
+int ds2_multi_copy(int n, void* const* dst, const void* const* src, const unsigned long long* rows,
+                   const unsigned* src_row, const unsigned* dst_row, const unsigned* src_pitch,
+                   const unsigned* dst_pitch, float* sdst, const float* svals, int ns, hipStream_t st);
 int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                    hipStream_t st);
 int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
@@ -942,6 +945,53 @@ void transpose_bf16(at::Tensor in, at::Tensor out) {
         "transpose_bf16");
 }
 
+// dst_i[r, :] = src_i[r, :] then zeros to dst_i's row end, for 2-D (or 1-D: one row) tensors of
+// one dtype with unit-stride rows and src cols <= dst cols; plus ns <= 4 fp32 scalars into
+// sdst. ONE launch (csrc/fill.hip multi_copy_kernel).
+void multi_copy(std::vector<at::Tensor> dsts, std::vector<at::Tensor> srcs, c10::optional<at::Tensor> sdst,
+                std::vector<double> svals) {
+  TORCH_CHECK(dsts.size() == srcs.size() && dsts.size() <= 8 && svals.size() <= 4, "multi_copy: <= 8 pairs, <= 4 scalars");
+  void* dp[8];
+  const void* sp[8];
+  unsigned long long rows[8];
+  unsigned srow[8], drow[8], spitch[8], dpitch[8];
+  for (size_t i = 0; i < dsts.size(); ++i) {
+    at::Tensor d = dsts[i], s = srcs[i];
+    need_gpu(d, "multi_copy dst");
+    need_gpu(s, "multi_copy src");
+    TORCH_CHECK(d.scalar_type() == s.scalar_type() && d.dim() == s.dim() && (d.dim() == 1 || d.dim() == 2),
+                "multi_copy: same dtype, 1-D or 2-D");
+    const int64_t es = d.element_size();
+    if (d.dim() == 1) {
+      TORCH_CHECK(d.is_contiguous() && s.is_contiguous() && s.numel() <= d.numel(), "multi_copy: 1-D contiguous");
+      rows[i] = 1;
+      srow[i] = (unsigned)(s.numel() * es); drow[i] = (unsigned)(d.numel() * es);
+      spitch[i] = srow[i]; dpitch[i] = drow[i];
+    } else {
+      TORCH_CHECK(d.size(0) == s.size(0) && s.size(1) <= d.size(1) && d.stride(1) == 1 && s.stride(1) == 1,
+                  "multi_copy: rows match, unit-stride rows, src cols <= dst cols");
+      rows[i] = (unsigned long long)d.size(0);
+      srow[i] = (unsigned)(s.size(1) * es); drow[i] = (unsigned)(d.size(1) * es);
+      spitch[i] = (unsigned)(std::max<int64_t>(s.stride(0), s.size(1)) * es);
+      dpitch[i] = (unsigned)(std::max<int64_t>(d.stride(0), d.size(1)) * es);
+    }
+    dp[i] = d.data_ptr();
+    sp[i] = s.data_ptr();
+  }
+  float sv[4] = {0.f, 0.f, 0.f, 0.f};
+  for (size_t i = 0; i < svals.size(); ++i) sv[i] = (float)svals[i];
+  float* sd = nullptr;
+  if (sdst.has_value()) {
+    need_gpu(*sdst, "multi_copy scalars");
+    TORCH_CHECK(sdst->scalar_type() == at::kFloat && sdst->is_contiguous() && sdst->numel() >= (int64_t)svals.size(),
+                "multi_copy: fp32 scalar slot");
+    sd = sdst->data_ptr<float>();
+  }
+  check(ds2_multi_copy((int)dsts.size(), dp, sp, rows, srow, drow, spitch, dpitch, sd, sv, (int)svals.size(),
+                       cur_stream()),
+        "multi_copy");
+}
+
 void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
   TORCH_CHECK(ts.size() == patterns.size() && ts.size() <= 8, "multi_fill: <= 8 (tensor, pattern) pairs");
   void* ptrs[8];
@@ -1389,6 +1439,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_bf16", &cast_bf16);
   m.def("device_info", &device_info);
   m.def("fp8_quant_blocks", &fp8_quant_blocks);
+  m.def("multi_copy", &multi_copy, py::arg("dsts"), py::arg("srcs"), py::arg("sdst") = py::none(),
+        py::arg("svals") = std::vector<double>{});
   m.def("fp8_quant2", &fp8_quant2, py::arg("a"), py::arg("b"), py::arg("alpha"), py::arg("a8"), py::arg("b8"),
         py::arg("part"), py::arg("scales"), py::arg("a2") = py::none(), py::arg("asum") = py::none());
   m.def("transpose_bf16", &transpose_bf16);

@@ -25,6 +25,7 @@ from typing import Dict, Optional
 import torch
 
 from .models import DeepSpeech2
+from .ops import _ext
 from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
 from .parallel.grad_sync import GradBucketer, broadcast_params
 from .utils import trace as TR
@@ -274,16 +275,25 @@ class Trainer:
 
     def _replay(self, g: "_StepGraph", batch: Dict[str, torch.Tensor], width: int, lr_t: float,
                 keep: float, events=None) -> torch.Tensor:
-        g.feats.copy_(batch["feats"], non_blocking=True)
-        g.seq_lens.copy_(batch["seq_lens"], non_blocking=True)
-        g.label_lens.copy_(batch["label_lens"], non_blocking=True)
-        labels = batch["labels"]
-        if labels.shape[1] == width:
-            g.labels.copy_(labels, non_blocking=True)
+        feats, labels = batch["feats"], batch["labels"]
+        pairs = [(g.feats, feats), (g.seq_lens, batch["seq_lens"]), (g.label_lens, batch["label_lens"]),
+                 (g.labels, labels)]
+        if all(s.is_cuda and s.dtype == d.dtype and s.is_contiguous() for d, s in pairs):
+            # the graph's inputs and the optimizer's step constants in ONE launch
+            # (csrc/fill.hip multi_copy_kernel; labels narrower than the captured width zero-padded)
+            _ext.ext().multi_copy([g.feats.view(-1), g.seq_lens, g.label_lens, g.labels],
+                                  [feats.reshape(-1), batch["seq_lens"], batch["label_lens"], labels],
+                                  self.opt.hyper, [lr_t, keep])
         else:
-            g.labels[:, labels.shape[1]:].zero_()
-            g.labels[:, :labels.shape[1]].copy_(labels, non_blocking=True)
-        self.opt.load_hyper(lr_t, keep)
+            g.feats.copy_(feats, non_blocking=True)
+            g.seq_lens.copy_(batch["seq_lens"], non_blocking=True)
+            g.label_lens.copy_(batch["label_lens"], non_blocking=True)
+            if labels.shape[1] == width:
+                g.labels.copy_(labels, non_blocking=True)
+            else:
+                g.labels[:, labels.shape[1]:].zero_()
+                g.labels[:, :labels.shape[1]].copy_(labels, non_blocking=True)
+            self.opt.load_hyper(lr_t, keep)
         if events is not None:
             events[0].record()
         g.graph.replay()

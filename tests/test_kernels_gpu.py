@@ -629,3 +629,25 @@ def test_fp8_bptt_matches_emulation(cuda, N, H, ndir):
         dgx16, _, _ = RNN._run_bwd(dy, lens, U + [None] * (2 - ndir), hx, hs, gates, plan, ndir * 3 * H)
         torch.cuda.synchronize()
         assert _rel(dgx.float(), dgx16.float()) < 8e-2, _rel(dgx.float(), dgx16.float())
+
+
+def test_multi_copy_rows_padding_and_scalars(cuda):
+    """csrc/fill.hip multi_copy: row copies into wider rows (rest of each row zeroed), 1-D
+    copies of several dtypes and the fp32 scalar slot, all in one launch (graph-replay inputs)."""
+    from deepspeech_amd.ops import _ext
+    C = _ext.ext()
+    torch.manual_seed(2)
+    f_src = torch.randn(3 * 7 * 5, device=cuda)
+    f_dst = torch.full_like(f_src, float("nan"))
+    lab_src = torch.randint(1, 28, (6, 9), device=cuda, dtype=torch.int32)
+    lab_dst = torch.full((6, 16), -1, device=cuda, dtype=torch.int32)
+    l_src = torch.randint(0, 100, (6,), device=cuda, dtype=torch.int32)
+    l_dst = torch.zeros_like(l_src)
+    h_src = torch.randn(40, device=cuda).bfloat16()
+    h_dst = torch.zeros_like(h_src)
+    hyper = torch.zeros(2, device=cuda)
+    C.multi_copy([f_dst, lab_dst, l_dst, h_dst], [f_src, lab_src, l_src, h_src], hyper, [1e-3 / 3, 0.9999])
+    torch.cuda.synchronize()
+    assert torch.equal(f_dst, f_src) and torch.equal(l_dst, l_src) and torch.equal(h_dst, h_src)
+    assert torch.equal(lab_dst[:, :9], lab_src) and bool((lab_dst[:, 9:] == 0).all())
+    assert torch.equal(hyper.cpu(), torch.tensor([1e-3 / 3, 0.9999], dtype=torch.float32))
