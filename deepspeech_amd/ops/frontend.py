@@ -26,6 +26,10 @@ BN_EPS = 1e-3
 BN_MOMENTUM = 0.01
 
 
+
+# conv1 weight-gradient workgroups per CU (its 67.5 KB of LDS allows two)
+_C1W_BPC = int(os.environ.get("DS2_C1W_BPC", "1"))
+
 def bn_eval_stats(block, eps: float):
     """(mean, invstd) for eval: running statistics (fused variant) or the debiased EMA of
     the moments (moments_ema variant, NHWC graph)."""
@@ -299,7 +303,7 @@ class FrontendCL(torch.autograd.Function):
             # staging (dy1 never materialised), so only dgamma / dbeta here
             C_.bn_cl_bwd(dz1, y1, mean1, inv1, g1f, be1f, part, dgrid, dg1, db1, dz1, False, part_ready=2)
         with TR.phase(TR.conv(1, True)):
-            g1grid = max(1, min(N * ((T1 + 3) // 4), ctx.ncu))
+            g1grid = max(1, min(N * ((T1 + 3) // 4), _C1W_BPC * ctx.ncu))
             wpart1 = torch.empty(int(C_.conv1_wgrad_part_floats(g1grid)), **f32)
             dw1, ip1 = _grad_buffer(w1)
             C_.conv1_wgrad(dz1, x, wpart1, dw1, g1grid, y1, mean1, inv1, g1f, be1f, db1, dg1)

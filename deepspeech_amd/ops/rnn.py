@@ -1076,8 +1076,8 @@ def _beside_grid(plan: RnnPlan, device: torch.device, dp: bool, fp8: bool) -> in
     cap = idle if _BESIDE_GRID < 0 else min(_BESIDE_GRID, idle)
     return max(8, cap // 8 * 8)
 # bottom layer: the grouped launch before layer 0's dx GEMM (same-box A/B, 3 rounds: 8.025 /
-# 8.028 / 8.081 vs 8.091 / 8.024 / 8.101 ms/step after it)
-_GROUP_BEFORE_DX = True
+# 8.028 / 8.081 vs 8.091 / 8.024 / 8.101 ms/step after it); DS2_GROUP_BEFORE_DX=0: after it
+_GROUP_BEFORE_DX = os.environ.get("DS2_GROUP_BEFORE_DX", "1") != "0"
 
 
 def _bptt_cus(plan: RnnPlan) -> int:
