@@ -32,6 +32,10 @@ from .utils import trace as TR
 from .utils.stats import NonfiniteWatch
 
 
+# host clock of the eager/graph decision (tests freeze it)
+_clock = time.perf_counter
+
+
 @dataclass
 class LRSchedule:
     initial_lr: float
@@ -240,9 +244,9 @@ class Trainer:
             st.seen += 1
             b = dict(batch)
             b["labels"] = self._pad_labels(batch["labels"], width)
-            t0 = time.perf_counter()
+            t0 = _clock()
             loss = self._body(b, lr_t, keep)
-            st.host_s.append(time.perf_counter() - t0)
+            st.host_s.append(_clock() - t0)
             return loss
         if st.graph is None:
             st.graph = self._capture(batch, width)
@@ -263,6 +267,11 @@ class Trainer:
             st.spans = []
             if st.mode == "eager":
                 st.graph = None
+                if not any(o.graph is not None for o in self._shapes.values()):
+                    # the last graph of the shared memory pool is gone, and with it the pool
+                    # (PyTorch frees a private pool with its last graph): the next capture must
+                    # not name the dead pool's handle (allocator assert at capture_begin)
+                    self._graph_pool = None
                 b = dict(batch)
                 b["labels"] = self._pad_labels(batch["labels"], width)
                 return self._body(b, lr_t, keep)
