@@ -93,6 +93,8 @@ def main():
     assert tr.bucketer.enabled and tr.per_bucket_update
     tr.step(batch)
     torch.cuda.synchronize()
+    from deepspeech_amd.ops.rnn import check_errors
+    check_errors()           # a recurrence that timed out (grid not co-resident) fails loudly
     torch.save({"local": g_local.cpu(), "dp": g_dp.cpu(), "step_local": g_step.cpu(),
                 "w_step": tr.arena.flat.cpu(), "ema_step": tr.opt.ema.cpu()}, "%s.%d" % (out, ctx.rank))
     torch.distributed.barrier()
