@@ -358,7 +358,8 @@ class FusedAdamEMA:
                             self._hyper_arg())
 
     @torch.no_grad()
-    def apply_excluding(self, lo: int, hi: int, exclude, lr_t: float, keep: float, gscale: float = 1.0) -> None:
+    def apply_excluding(self, lo: int, hi: int, exclude, lr_t: float, keep: float, gscale: float = 1.0,
+                        max_grid: int = 0) -> None:
         """Adam + EMA of arena elements [lo, hi) except the ``exclude`` ranges (already updated
         this step, e.g. by the grouped weight-gradient GEMM's fused epilogue): the remaining
         intervals in one launch (csrc/optim.hip adam_ema_ranges) when they fit its table."""
@@ -381,7 +382,7 @@ class FusedAdamEMA:
                                        self._hyper_arg())
             return
         for a, b in todo:
-            self.apply_range(a, b, lr_t, keep, gscale)
+            self.apply_range(a, b, lr_t, keep, gscale, max_grid=max_grid)
 
     def fused_constants(self, lr_t: float, keep: float, gscale: float = 1.0):
         """(tensors, constants) of a fused-epilogue update (gemm.gemm8_group ``opt``)."""

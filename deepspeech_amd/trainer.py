@@ -67,6 +67,14 @@ _UPPER_GRID = 512
 # epilogue streams its 2.2 MB of optimizer state at the same moment (HBM-bound, +450 us on the
 # group) instead of overlapping the MFMA work; off until that is staggered
 _FUSED_OPT = False
+# grid cap (blocks) of that early optimizer range: it streams beside the conv front-end's
+# backward, whose latency-bound conv1 weight gradient it slowed 3x on the full grid (headline,
+# same box, 4 rounds: 7.745-7.773 ms/step at 384 vs 7.788-7.817 uncapped and 7.793-7.821 at 512;
+# another box 3 rounds: 384 -0.45 %, 256 -0.2 to -0.3 %). Only when the range is the whole head
+# + recurrent stack (every weight gradient deferred to the grouped tail): config 5, whose upper
+# range already ran beside layer 0's BPTT, measured +0.15-0.3 % with the cap on its remainder.
+# DS2_EARLY_OPT_GRID=0: uncapped
+_EARLY_GRID = int(os.environ.get("DS2_EARLY_OPT_GRID", "384"))
 
 
 def _check_hw_queues() -> None:
@@ -381,7 +389,8 @@ class Trainer:
                 sch.set_fused_update(self.arena, tensors, consts, store_g=self.keep_grads)
             self.arena.wgrad.set_early_update(
                 lambda: self.opt.apply_excluding(sch.early_upper_hi if sch.early_upper_done else 0, split,
-                                                 sch.fused_ranges, lr_t, keep, gscale),
+                                                 sch.fused_ranges, lr_t, keep, gscale,
+                                                 max_grid=0 if sch.early_upper_done else _EARLY_GRID),
                 self._early_params)
             if self._layer_first and _EARLY_UPPER:
                 # the head and the layers whose weight gradients ran beside the BPTT (not in the
