@@ -173,6 +173,8 @@ int ds2_adam_ema_ranges(float* p, const float* g, float* m, float* v, float* ema
 int ds2_fp8_quant2(const void* a, long long rows_a, const void* b, long long rows_b, int K, int Kp, float alpha,
                    void* a8, void* b8, float* part, float* scales, const void* a2, void* asum, hipStream_t st);
 int ds2_transpose_bf16(const void* in, void* out, int R, int C, int ldi, int ldo, hipStream_t st);
+int ds2_prep_inputs(const float* x, void* y, long long n, const int* lens_in, int* lens_out, int nl,
+                    hipStream_t st);
 int ds2_multi_copy(int n, void* const* dst, const void* const* src, const unsigned long long* rows,
                    const unsigned* src_row, const unsigned* dst_row, const unsigned* src_pitch,
                    const unsigned* dst_pitch, float* sdst, const float* svals, int ns, hipStream_t st);
@@ -992,6 +994,21 @@ void multi_copy(std::vector<at::Tensor> dsts, std::vector<at::Tensor> srcs, c10:
         "multi_copy");
 }
 
+// feats fp32 -> bf16 (same shape, contiguous) and rnn lengths floor((seq_lens - 34) / 4), int32
+void prep_inputs(at::Tensor x, at::Tensor y, at::Tensor lens_in, at::Tensor lens_out) {
+  need_gpu(x, "feats");
+  need_gpu(y, "feats bf16");
+  need_gpu(lens_in, "seq_lens");
+  need_gpu(lens_out, "rnn lens");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && y.scalar_type() == at::kBFloat16 && x.is_contiguous() &&
+                  y.is_contiguous() && x.numel() == y.numel(), "prep_inputs: fp32 feats -> bf16 of the same size");
+  TORCH_CHECK(lens_in.scalar_type() == at::kInt && lens_out.scalar_type() == at::kInt && lens_in.is_contiguous() &&
+                  lens_out.is_contiguous() && lens_in.numel() == lens_out.numel(), "prep_inputs: int32 lengths");
+  check(ds2_prep_inputs(x.data_ptr<float>(), y.data_ptr(), x.numel(), lens_in.data_ptr<int>(),
+                        lens_out.data_ptr<int>(), (int)lens_in.numel(), cur_stream()),
+        "prep_inputs");
+}
+
 void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
   TORCH_CHECK(ts.size() == patterns.size() && ts.size() <= 8, "multi_fill: <= 8 (tensor, pattern) pairs");
   void* ptrs[8];
@@ -1439,6 +1456,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast_bf16", &cast_bf16);
   m.def("device_info", &device_info);
   m.def("fp8_quant_blocks", &fp8_quant_blocks);
+  m.def("prep_inputs", &prep_inputs);
   m.def("multi_copy", &multi_copy, py::arg("dsts"), py::arg("srcs"), py::arg("sdst") = py::none(),
         py::arg("svals") = std::vector<double>{});
   m.def("fp8_quant2", &fp8_quant2, py::arg("a"), py::arg("b"), py::arg("alpha"), py::arg("a8"), py::arg("b8"),

@@ -127,6 +127,46 @@ extern "C" int ds2_multi_copy(int n, void* const* dst, const void* const* src, c
 }
 
 // ---------------------------------------------------------------------------------------
+// Step inputs in one launch: the features cast to the compute dtype (fp32 -> bf16, 4 per
+// thread) and the recurrence lengths T2 = floor((T - 34) / 4) of the conv front-end
+// (ops/reference.py get_rnn_seqlen; src/deepSpeech.py:38-48) from the utterance lengths,
+// instead of a cast kernel and two integer kernels in front of every step.
+namespace {
+
+__global__ __launch_bounds__(256) void prep_inputs_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                          long long n, const int* __restrict__ lens_in,
+                                                          int* __restrict__ lens_out, int nl) {
+  const long long tid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (tid < nl) {
+    const int t = lens_in[tid] - 34;
+    lens_out[tid] = t >= 0 ? t / 4 : -((-t + 3) / 4);          // floor division
+  }
+  const long long stride = (long long)gridDim.x * 256;
+  const long long n4 = n / 4;
+  for (long long i = tid; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    uint2 o;
+    o.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
+    o.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+    reinterpret_cast<uint2*>(y)[i] = o;
+  }
+  for (long long i = n4 * 4 + tid; i < n; i += stride) y[i] = f2bf(x[i]);
+}
+
+}  // namespace
+
+extern "C" int ds2_prep_inputs(const float* x, void* y, long long n, const int* lens_in, int* lens_out, int nl,
+                               hipStream_t st) {
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 7)) return -52;
+  long long blocks = (n / 4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(prep_inputs_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, (bf16_t*)y, n, lens_in,
+                     lens_out, nl);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // bf16 transpose out[c][r] = in[r][c] ([R][C] -> [C][R], both row-major, unit-stride rows):
 // the K-contiguous W^T shadow of a recurrent layer's [W_fw; W_bw] that the input-gradient
 // GEMM dx = dgx W reads as a row-major operand (csrc/gemm.hip measured faster on it than on

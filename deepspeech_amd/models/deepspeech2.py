@@ -19,6 +19,7 @@ Reference quirks handled explicitly:
 """
 from __future__ import annotations
 
+import os
 import math
 from typing import Dict, List, Optional, Tuple
 
@@ -77,6 +78,10 @@ def freq_out(F_in: int = FREQ_BINS) -> Tuple[int, int]:
 NHWC_BN_EPS = 1e-5
 NHWC_BN_DECAY = 0.5
 
+
+
+# DS2_PREP_FUSED=0: the features' cast and the rnn lengths as torch ops (A/B)
+_PREP_FUSED = os.environ.get("DS2_PREP_FUSED", "1") != "0"
 
 class ConvBlock(nn.Module):
     """conv + bias + BatchNorm + clipped ReLU.
@@ -390,18 +395,33 @@ class DeepSpeech2(nn.Module):
         b = self.fc_bias.to(h.dtype)
         return torch.addmm(b, h.reshape(T * N, H), w.t()).view(T, N, -1)
 
+    def _hip_inputs(self, feats: torch.Tensor, seq_lens: torch.Tensor):
+        """(features in the compute dtype, rnn lengths int32) of the HIP engine: one fused launch
+        (csrc/fill.hip prep_inputs_kernel) for fp32 device features, else the torch ops."""
+        seq_lens = seq_lens.to(feats.device)
+        if (_PREP_FUSED and feats.is_cuda and feats.dtype == torch.float32 and self.compute_dtype == torch.bfloat16 and
+                feats.is_contiguous() and feats.data_ptr() % 16 == 0 and seq_lens.dtype == torch.int32 and
+                seq_lens.is_contiguous()):
+            from ..ops import _ext
+            x = torch.empty(feats.shape, device=feats.device, dtype=torch.bfloat16)
+            lens = torch.empty_like(seq_lens)
+            _ext.ext().prep_inputs(feats, x, seq_lens, lens)
+            return x, lens
+        return feats.to(self.compute_dtype), R.get_rnn_seqlen(seq_lens)
+
     def forward(self, feats: torch.Tensor, seq_lens: torch.Tensor
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
         """Returns (logits [T2, N, K] time-major, rnn lengths [N] int32)."""
-        lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
+        if self.engine == "hip":
+            feats, lens = self._hip_inputs(feats, seq_lens)
+        else:
+            lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
         if self.engine == "ref" and feats.device.type == "cuda" and self.compute_dtype != torch.float32:
             with torch.autocast("cuda", dtype=self.compute_dtype):
                 x = self.frontend(feats)
                 h = self.recurrent(x, lens)
                 logits = self.head(h)
             return logits.float(), lens
-        if self.engine == "hip":
-            feats = feats.to(self.compute_dtype)
         x = self.frontend(feats)
         h = self.recurrent(x, lens.to(x.device))
         logits = self.head(h)
@@ -415,8 +435,8 @@ class DeepSpeech2(nn.Module):
         otherwise forward() + loss()."""
         if self.engine == "hip" and self.num_classes <= 32 and self.num_hidden % 32 == 0:
             from ..ops import ctc as CTC
-            lens = R.get_rnn_seqlen(seq_lens.to(feats.device))
-            x = self.frontend(feats.to(self.compute_dtype))
+            xin, lens = self._hip_inputs(feats, seq_lens)
+            x = self.frontend(xin)
             h = self.recurrent(x, lens.to(x.device))
             from ..ops import rnn as RNN
             RNN.flush_transposes()      # the dx GEMMs' W^T shadows, beside the head + CTC

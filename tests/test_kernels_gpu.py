@@ -651,3 +651,20 @@ def test_multi_copy_rows_padding_and_scalars(cuda):
     assert torch.equal(f_dst, f_src) and torch.equal(l_dst, l_src) and torch.equal(h_dst, h_src)
     assert torch.equal(lab_dst[:, :9], lab_src) and bool((lab_dst[:, 9:] == 0).all())
     assert torch.equal(hyper.cpu(), torch.tensor([1e-3 / 3, 0.9999], dtype=torch.float32))
+
+
+def test_prep_inputs_matches_torch(cuda):
+    """csrc/fill.hip prep_inputs: fp32 -> bf16 features bitwise torch's cast (ragged tail
+    included) and the recurrence lengths bitwise ops/reference.py get_rnn_seqlen (negative
+    and non-multiple-of-4 lengths included)."""
+    from deepspeech_amd.ops import _ext
+    from deepspeech_amd.ops import reference as R
+    torch.manual_seed(3)
+    x = torch.randn(3, 101, 161, device=cuda) * 7
+    y = torch.empty(x.shape, device=cuda, dtype=torch.bfloat16)
+    lens = torch.tensor([0, 1, 33, 34, 35, 37, 38, 1000, 999], device=cuda, dtype=torch.int32)
+    out = torch.empty_like(lens)
+    _ext.ext().prep_inputs(x, y, lens, out)
+    torch.cuda.synchronize()
+    assert torch.equal(y, x.to(torch.bfloat16))
+    assert torch.equal(out, R.get_rnn_seqlen(lens))
