@@ -1345,7 +1345,7 @@ class WgradScheduler:
             # (LDS-bound kernels that cannot share a CU with a group workgroup's 128 KB) gets
             # the rest; headline, same box: 7.83-7.87 ms/step vs 7.89-7.90 on every CU, 7.94
             # at 176, 7.84-7.92 at 208, 8.03 at 128
-            cap = (3 * _ext.num_cus(torch.cuda.current_device())) // 4
+            cap = _GROUP_CAP or (3 * _ext.num_cus(torch.cuda.current_device())) // 4
             if fused is not None:
                 GM.gemm8_group(members, opt=fused[0], max_grid=cap)
                 self.fused_ranges.extend(fused[1])
@@ -1517,6 +1517,9 @@ def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int = 0
     with TR.phase(TR.rnn_cell(idx)):
         return _recurrent_layer_hip(layer, x, lens, idx, pair_out)
 
+
+# grid cap of the grouped tail launch (0: 3/4 of the CUs; A/B only)
+_GROUP_CAP = int(os.environ.get("DS2_GROUP_CAP", "0"))
 
 # DS2_FP8_PAIRS=0: every fp8 layer sums its directions with torch.add (A/B timing)
 _FP8_PAIRS = os.environ.get("DS2_FP8_PAIRS", "1") != "0"
