@@ -468,3 +468,22 @@ def test_gemm8_plan_policy():
     assert G.gemm8_plan(672, 4800, 800, 1, 256) is None
     assert G.gemm8_plan(7712, 4800, 800, 1, 256) is None
     assert G.gemm8_plan(7712, 800, 4800, 2, 256) is None            # batched launches: plain policy
+
+
+@pytest.mark.parametrize("M,N,K", [(672, 4800, 800), (672, 4800, 2400), (1312, 4800, 800), (672, 7680, 1280),
+                                   (2432, 4800, 800)])
+def test_short_bucket_projection_routing(cuda, M, N, K):
+    """matmul's short-bucket rule (ops/gemm.py _small_rowrow): row-row bf16 projections of few
+    256^2 tiles and K <= 2400 run on csrc/gemm.hip's cost-model tile, the rest on gemm8; either
+    way alpha * x W^T + bias within bf16 rounding of the fp32 product."""
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16)
+    W = (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    small = G._small_rowrow(M, N, K, False, False, 1, 0, x)
+    assert small == (M <= 1312 and (K <= 2400) and (-(-M // 256)) * (-(-N // 256)) * 2 <= G._dev_cus(x))
+    assert G.matmul(x, W.t(), out, alpha=0.5, bias=b)
+    torch.cuda.synchronize()
+    ref = 0.5 * (x.float() @ W.float().t()) + b.float()
+    assert _rel(out, ref) < 6e-3
