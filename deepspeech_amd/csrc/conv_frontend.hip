@@ -835,8 +835,12 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(Conv1Wgrad a) {
     // x rows 2*t1_0 + r: raw rows into LDS, then de-interleaved xd[r][kf'][p] = x[t][2p + kf']
     stage_rows(raw, a.x + (size_t)n * a.T * a.F0, 2 * t1_0, a.T, a.F0);
     __syncthreads();
+    // kf fastest: the 8 lanes of one (row, position block) read 8 consecutive raw elements per j
+    // (one LDS word for two of them), so a wave's 2-byte reads hit 32 distinct banks; with the
+    // position block fastest, lanes sat 32 B apart (8-way bank conflicts: 42 % of the kernel's
+    // LDS cycles, PMC SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE)
     for (int ch = tid; ch < C1_IN * 8 * 10; ch += 256) {
-      const int r = ch / 80, rem = ch - r * 80, kf = rem / 10, p0 = (rem - kf * 10) * 8;
+      const int kf = ch & 7, q = ch >> 3, r = q / 10, p0 = (q - r * 10) * 8;
       bf16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (short)raw[r * C1_XS + min(2 * (p0 + j) + kf, C1_XS - 1)];
