@@ -1070,7 +1070,7 @@ _BESIDE_GRID = int(os.environ.get("DS2_BESIDE_GRID", "-1"))
 
 
 def _beside_grid(plan: RnnPlan, device: torch.device, dp: bool, fp8: bool) -> int:
-    if _BESIDE_GRID == 0 or (_BESIDE_GRID == -1 and not (dp or fp8)):
+    if _BESIDE_GRID == 0 or (_BESIDE_GRID == -1 and not (dp or fp8 or _defer_wgrad(plan, device))):
         return 0
     idle = _ext.num_cus(device.index or 0) - _bptt_cus(plan)
     cap = idle if _BESIDE_GRID < 0 else min(_BESIDE_GRID, idle)
@@ -1093,22 +1093,36 @@ def _defer_wgrad(plan: RnnPlan, device: torch.device) -> bool:
     return _ext.num_cus(device.index or 0) - _bptt_cus(plan) < _BESIDE_MIN_IDLE_CUS
 
 
-# with deferral, only the bottom _DEFER_LAYERS layers' weight gradients join the grouped tail
-# launch; the layers above run theirs beside the next BPTT (and their optimizer range goes out
-# once the lowest of them has issued its gradients). Headline, same box, round 4: all deferred
-# 8.101 / 8.076 ms/step, bottom 3 8.077 / 8.089, bottom 2 8.129 / 8.122, bottom 1 8.125 / 8.115:
-# the tail shrinks (1.69 -> 1.24 ms at 2) but the BPTT chain grows as much (2.50 -> 2.93 ms of
-# kernel time: shared L2 / fabric), profiles/r4_negative_results.md. Kept: all deferred.
-_DEFER_LAYERS = 1 << 30
+# with deferral, only the bottom _defer_layers() layers' weight gradients join the grouped tail
+# launch; the layers above run theirs beside the next BPTT, on the CUs it leaves idle
+# (_beside_grid), and their optimizer range goes out once the lowest of them has issued its
+# gradients. Round 4, beside GEMMs on the whole chip: all deferred 8.101 / 8.076 ms/step, bottom
+# 1 8.125 / 8.115 (the BPTT chain grew by what the tail lost: shared L2 / fabric). Round 5, the
+# beside GEMMs capped to the BPTT's 56 idle CUs, same box, 3 rounds each on two boxes: all
+# deferred 7.696-7.723 / 7.709-7.717, bottom 1 7.652-7.653 / 7.578-7.599, bottom 2 7.627-7.693,
+# bottom 0 7.593-7.605; a 48-workgroup cap 8.49-8.54 (the GEMMs outlast the BPTT). Plans whose
+# BPTT leaves fewer than _PARTIAL_MIN_IDLE CUs (ReLU-1760: 32) keep everything deferred.
+# DS2_DEFER_LAYERS overrides.
+_DEFER_LAYERS = int(os.environ.get("DS2_DEFER_LAYERS", "-1"))
+_PARTIAL_MIN_IDLE = 56
+
+
+def _defer_layers(plan: RnnPlan, device: torch.device) -> int:
+    if _DEFER_LAYERS >= 0:
+        return _DEFER_LAYERS
+    if device.type != "cuda":
+        return 1 << 30
+    idle = _ext.num_cus(device.index or 0) - _bptt_cus(plan)
+    return 1 if idle >= _PARTIAL_MIN_IDLE else 1 << 30
 
 
 def _defer_layer(plan: RnnPlan, device: torch.device, idx: int) -> bool:
-    return _defer_wgrad(plan, device) and idx < _DEFER_LAYERS
+    return _defer_wgrad(plan, device) and idx < _defer_layers(plan, device)
 
 
 def _upper_trigger(plan: RnnPlan, device: torch.device) -> int:
     """Layer whose issued weight gradients complete the head + every layer above it."""
-    return _DEFER_LAYERS if _defer_wgrad(plan, device) else 1
+    return _defer_layers(plan, device) if _defer_wgrad(plan, device) else 1
 
 
 class Deferred:

@@ -416,7 +416,9 @@ def test_early_optimizer_range_is_bitwise_whole_update(cuda, H):
     moments and EMA of one whole-arena update after backward (three steps). H = 256: the
     BPTT leaves >= 96 CUs idle, so the weight gradients run beside each BPTT and the range of
     the head + layers >= 1 goes out beside layer 0's BPTT (two early ranges); H = 800 (the
-    headline width, 8 rows per group): deferred grouped launch, one early range."""
+    headline width, 8 rows per group, 56 idle CUs): layer 0's weight gradients in the grouped
+    launch, the upper layers' beside the next BPTT on the idle CUs — two early ranges as well
+    (DS2_DEFER_LAYERS unset); with every layer deferred, one."""
     from deepspeech_amd.ops import rnn as RNN
     from deepspeech_amd.trainer import Trainer, LRSchedule
     torch.manual_seed(0)
@@ -424,8 +426,8 @@ def test_early_optimizer_range_is_bitwise_whole_update(cuda, H):
     base = DeepSpeech2(num_filters=32, num_hidden=H, num_rnn_layers=3, cell="gru").to(cuda)
     batch = to_device(FixedShapeBatches(N, max_frames=300, seed=3, pool=1).next(), cuda)
     plan = RNN.plan_for(N, H, "gru", 2, cuda)
-    two_stage = not RNN._defer_wgrad(plan, cuda)
-    assert two_stage == (H == 256)
+    two_stage = not RNN._defer_wgrad(plan, cuda) or RNN._defer_layers(plan, cuda) < 3
+    assert (not RNN._defer_wgrad(plan, cuda)) == (H == 256)
     runs = []
     # "upper_only": the lower early range is skipped after the upper one ran (the
     # fallback update must not apply [0, usplit) a second time)
