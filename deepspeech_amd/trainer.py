@@ -58,7 +58,7 @@ def lr_schedule_from_args(args, steps_per_epoch: int) -> LRSchedule:
 # not deferred, on a capped grid (same box, config 5 fp8, 2 rounds: off 21.77 / 21.39 ms/step,
 # full grid 21.16 / 21.08, 192 blocks 21.04 / 20.99, 512 blocks 21.04 / 20.98)
 _EARLY_UPPER = True
-_UPPER_GRID = 512
+_UPPER_GRID = int(os.environ.get("DS2_UPPER_OPT_GRID", "512"))
 # single device, weight gradients deferred to the grouped tail launch: that launch can apply Adam +
 # EMA to the recurrent weights in its epilogue (csrc/gemm8.hip "Fused optimizer epilogue")
 # instead of storing their gradients for a separate optimizer pass to read back. Bitwise the
@@ -75,6 +75,8 @@ _FUSED_OPT = False
 # range already ran beside layer 0's BPTT, measured +0.15-0.3 % with the cap on its remainder.
 # DS2_EARLY_OPT_GRID=0: uncapped
 _EARLY_GRID = int(os.environ.get("DS2_EARLY_OPT_GRID", "384"))
+# the same range when the upper part already ran beside layer 0's BPTT (A/B)
+_LOWER_GRID = int(os.environ.get("DS2_LOWER_OPT_GRID", "0"))
 
 
 def _check_hw_queues() -> None:
@@ -390,7 +392,7 @@ class Trainer:
             self.arena.wgrad.set_early_update(
                 lambda: self.opt.apply_excluding(sch.early_upper_hi if sch.early_upper_done else 0, split,
                                                  sch.fused_ranges, lr_t, keep, gscale,
-                                                 max_grid=0 if sch.early_upper_done else _EARLY_GRID),
+                                                 max_grid=_LOWER_GRID if sch.early_upper_done else _EARLY_GRID),
                 self._early_params)
             if self._layer_first and _EARLY_UPPER:
                 # the head and the layers whose weight gradients ran beside the BPTT (not in the
