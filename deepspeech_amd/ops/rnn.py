@@ -962,7 +962,7 @@ class FusedBiLayer(torch.autograd.Function):
             on_side = x16.is_cuda and sch.on_side(x16.device)
             grouped = sch.grouped and on_side
             defer_w = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device,
-                                                                                                  ctx.idx)
+                                                                                                  ctx.idx, T)
             fp8b = bool(getattr(ctx, "fp8_bwd", False))
             cap_w = (_beside_grid(plan, x16.device, not sch.defer_input, fp8b)
                      if (on_side and ctx.idx > 0 and not defer_w) else 0)
@@ -993,7 +993,7 @@ class FusedBiLayer(torch.autograd.Function):
             sch = arena.wgrad
             on_side = x16.is_cuda and sch.on_side(x16.device)
             grouped = sch.grouped and on_side
-            defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device, ctx.idx)
+            defer = sch.defer_input and on_side and (ctx.idx >= 1 or grouped) and _defer_layer(plan, x16.device, ctx.idx, T)
             beside = ctx.idx > 0 and not defer            # runs beside the next layer's BPTT
             splits = _DU_SPLITS if beside else None
             cap_u = (_beside_grid(plan, x16.device, not sch.defer_input, bool(getattr(ctx, "fp8_bwd", False)))
@@ -1044,7 +1044,7 @@ class FusedBiLayer(torch.autograd.Function):
         gbh = _bias_grads([bh_f, bh_b] if d1 else [bh_f], parts[1]) if parts.shape[0] > 1 else [None, None]
         if tail:
             arena.wgrad.run_early_update()  # the recurrent stack's optimizer range, beside the front-end
-        elif (ctx.idx >= 1 and ctx.idx == _upper_trigger(plan, x16.device) and arena is not None and x16.is_cuda and
+        elif (ctx.idx >= 1 and ctx.idx == _upper_trigger(plan, x16.device, T) and arena is not None and x16.is_cuda and
               arena.wgrad.defer_input and arena.wgrad.on_side(x16.device)):
             arena.wgrad.run_early_upper(ctx.idx)   # layers >= idx and the head, beside the next BPTT
         return (dx, None, None, None, None, None, gW[0], gW[1], gU[0], gU[1], gb[0], gb[1], gbh[0], gbh[1], None)
@@ -1101,28 +1101,37 @@ def _defer_wgrad(plan: RnnPlan, device: torch.device) -> bool:
 # beside GEMMs capped to the BPTT's 56 idle CUs, same box, 3 rounds each on two boxes: all
 # deferred 7.696-7.723 / 7.709-7.717, bottom 1 7.652-7.653 / 7.578-7.599, bottom 2 7.627-7.693,
 # bottom 0 7.593-7.605; a 48-workgroup cap 8.49-8.54 (the GEMMs outlast the BPTT). Plans whose
-# BPTT leaves fewer than _PARTIAL_MIN_IDLE CUs (ReLU-1760: 32) keep everything deferred.
-# DS2_DEFER_LAYERS overrides.
+# BPTT leaves fewer than _PARTIAL_MIN_IDLE CUs (ReLU-1760: 32) keep everything deferred, and so do
+# sequences shorter than _PARTIAL_MIN_T recurrence steps: per-length eager A/B (same box, 2
+# rounds, tools/host_overhead.py, ms/step bottom-1 vs all deferred): 400 frames 3.62 vs 3.41,
+# 600 4.88 vs 4.79, 800 6.14 vs 6.22, 1000 7.64 vs 7.74, 1500 11.36 vs 11.68; a second box:
+# 700 5.67-5.68 vs 5.60-5.64, 800 6.24-6.29 vs 6.30-6.31 -- over a short BPTT the beside GEMMs
+# cannot hide and the split tail loses its one-launch efficiency; the cut sits past 800 frames
+# (191 steps).
+# DS2_DEFER_LAYERS / DS2_PARTIAL_MIN_T override.
 _DEFER_LAYERS = int(os.environ.get("DS2_DEFER_LAYERS", "-1"))
 _PARTIAL_MIN_IDLE = 56
+_PARTIAL_MIN_T = int(os.environ.get("DS2_PARTIAL_MIN_T", "200"))
 
 
-def _defer_layers(plan: RnnPlan, device: torch.device) -> int:
+def _defer_layers(plan: RnnPlan, device: torch.device, T: int) -> int:
+    """How many of the bottom layers defer their weight gradients to the grouped tail launch
+    at recurrence length ``T`` (everything deferred: 1 << 30)."""
     if _DEFER_LAYERS >= 0:
         return _DEFER_LAYERS
     if device.type != "cuda":
         return 1 << 30
     idle = _ext.num_cus(device.index or 0) - _bptt_cus(plan)
-    return 1 if idle >= _PARTIAL_MIN_IDLE else 1 << 30
+    return 1 if idle >= _PARTIAL_MIN_IDLE and T >= _PARTIAL_MIN_T else 1 << 30
 
 
-def _defer_layer(plan: RnnPlan, device: torch.device, idx: int) -> bool:
-    return _defer_wgrad(plan, device) and idx < _defer_layers(plan, device)
+def _defer_layer(plan: RnnPlan, device: torch.device, idx: int, T: int) -> bool:
+    return _defer_wgrad(plan, device) and idx < _defer_layers(plan, device, T)
 
 
-def _upper_trigger(plan: RnnPlan, device: torch.device) -> int:
+def _upper_trigger(plan: RnnPlan, device: torch.device, T: int) -> int:
     """Layer whose issued weight gradients complete the head + every layer above it."""
-    return _defer_layers(plan, device) if _defer_wgrad(plan, device) else 1
+    return _defer_layers(plan, device, T) if _defer_wgrad(plan, device) else 1
 
 
 class Deferred:

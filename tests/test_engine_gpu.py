@@ -409,8 +409,8 @@ def test_step_is_bitwise_reproducible(cuda):
     assert torch.equal(w0, w1)
 
 
-@pytest.mark.parametrize("H", [256, 800])
-def test_early_optimizer_range_is_bitwise_whole_update(cuda, H):
+@pytest.mark.parametrize("H,partial", [(256, True), (800, True), (800, False)])
+def test_early_optimizer_range_is_bitwise_whole_update(cuda, H, partial, monkeypatch):
     """Single device: the FC head's and recurrent stack's Adam + EMA range, issued on the
     weight-gradient stream beside the conv front-end's backward, gives bitwise the weights,
     moments and EMA of one whole-arena update after backward (three steps). H = 256: the
@@ -418,16 +418,20 @@ def test_early_optimizer_range_is_bitwise_whole_update(cuda, H):
     the head + layers >= 1 goes out beside layer 0's BPTT (two early ranges); H = 800 (the
     headline width, 8 rows per group, 56 idle CUs): layer 0's weight gradients in the grouped
     launch, the upper layers' beside the next BPTT on the idle CUs — two early ranges as well
-    (DS2_DEFER_LAYERS unset); with every layer deferred, one."""
+    (DS2_DEFER_LAYERS unset, sequences of >= _PARTIAL_MIN_T steps); with every layer
+    deferred (shorter sequences: ``partial`` False), one."""
     from deepspeech_amd.ops import rnn as RNN
     from deepspeech_amd.trainer import Trainer, LRSchedule
+    monkeypatch.setattr(RNN, "_PARTIAL_MIN_T", 0 if partial else 1 << 30)
     torch.manual_seed(0)
     N = 8 if H == 256 else 32
     base = DeepSpeech2(num_filters=32, num_hidden=H, num_rnn_layers=3, cell="gru").to(cuda)
     batch = to_device(FixedShapeBatches(N, max_frames=300, seed=3, pool=1).next(), cuda)
     plan = RNN.plan_for(N, H, "gru", 2, cuda)
-    two_stage = not RNN._defer_wgrad(plan, cuda) or RNN._defer_layers(plan, cuda) < 3
+    two_stage = not RNN._defer_wgrad(plan, cuda) or RNN._defer_layers(plan, cuda, 64) < 3
     assert (not RNN._defer_wgrad(plan, cuda)) == (H == 256)
+    if H == 800 and RNN._DEFER_LAYERS < 0:
+        assert two_stage == partial
     runs = []
     # "upper_only": the lower early range is skipped after the upper one ran (ADVICE r3: the
     # fallback update must not apply [0, usplit) a second time)
