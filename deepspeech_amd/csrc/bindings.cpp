@@ -263,6 +263,14 @@ void event_wait(int64_t stream, int64_t e) {
 }
 bool event_query(int64_t e) { return hipEventQuery((hipEvent_t)(intptr_t)e) == hipSuccess; }
 
+// The next kernel launched through ds2_launch (the GEMMs, the BPTT, multi_fill) completes event
+// e itself (hipExtLaunchKernel stop event) instead of a marker packet recorded behind it.
+// disarm_stop_event: True if no launch took it (the op ran elsewhere: record it the usual way).
+extern "C" hipEvent_t ds2_take_stop_event();
+extern "C" void ds2_arm_stop_event(hipEvent_t e);
+void arm_stop_event(int64_t e) { ds2_arm_stop_event((hipEvent_t)(intptr_t)e); }
+bool disarm_stop_event() { return ds2_take_stop_event() != nullptr; }
+
 // dst waits for everything enqueued on src so far: record + wait back to back, so one cached
 // event per host thread and device serves every pair (the wait binds to the record just made)
 void stream_wait(int64_t dst, int64_t src) {
@@ -1474,6 +1482,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
   m.def("event_new", &event_new, py::arg("flags") = 0);
+  m.def("arm_stop_event", &arm_stop_event);
+  m.def("disarm_stop_event", &disarm_stop_event);
   m.def("event_free", &event_free);
   m.def("event_record", &event_record);
   m.def("event_wait", &event_wait);

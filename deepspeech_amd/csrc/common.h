@@ -1,6 +1,7 @@
 // Shared device helpers for the deepspeech_amd gfx950 kernels.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace ds2 {
@@ -166,6 +167,21 @@ __device__ inline void fill_idle(const DS2Fill& f, int total, int tx, int nthr) 
     for (unsigned long long i = t0; i < n4; i += stride) reinterpret_cast<ds2::i32x4*>(p)[i] = v4;
     for (unsigned long long i = n4 * 4 + t0; i < nw; i += stride) p[i] = v;
   }
+}
+
+// Completion event armed for the next launch made through ds2_launch (hipExtLaunchKernel's stop
+// event; fill.hip ds2_arm_stop_event / ds2_take_stop_event): another stream can wait for that
+// kernel without a marker packet in this kernel's queue, each of which holds the queue ~6 us
+// between two kernels (tools/probe_event_gap.py). The host launchers whose kernel is the last
+// of an op take the event themselves and hand it to that launch.
+extern "C" hipEvent_t ds2_take_stop_event();
+extern "C" void ds2_arm_stop_event(hipEvent_t e);
+
+template <typename F, typename... Args>
+inline void ds2_launch(F kern, dim3 grid, dim3 block, unsigned lds, hipStream_t st, Args... args) {
+  hipEvent_t e = ds2_take_stop_event();
+  if (e != nullptr) hipExtLaunchKernelGGL(kern, grid, block, lds, st, nullptr, e, 0, args...);
+  else hipLaunchKernelGGL(kern, grid, block, lds, st, args...);
 }
 
 #define DS2_HIP_CHECK(expr)                                                        \

@@ -32,7 +32,16 @@ __global__ __launch_bounds__(256) void multi_fill_kernel(MultiFill f) {
   }
 }
 
+thread_local hipEvent_t g_stop_event = nullptr;
+
 }  // namespace
+
+extern "C" void ds2_arm_stop_event(hipEvent_t e) { g_stop_event = e; }
+extern "C" hipEvent_t ds2_take_stop_event() {
+  hipEvent_t e = g_stop_event;
+  g_stop_event = nullptr;
+  return e;
+}
 
 extern "C" int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                               hipStream_t st) {
@@ -51,7 +60,7 @@ extern "C" int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long
   unsigned long long blocks = (total / 4 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(multi_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, st, f);
+  ds2_launch(multi_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, st, f);
   return (int)hipGetLastError();
 }
 

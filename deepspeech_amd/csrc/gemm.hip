@@ -419,7 +419,7 @@ int launch(const GemmArgs& a, int batch, hipStream_t st) {
     grid = min(cus, (tiles + 7) & ~7);          // one workgroup per CU (>= 96 KB of LDS), x8 for the XCD map
     grid = max(8, grid & ~7);
   }
-  hipLaunchKernelGGL(kern, dim3(grid, 1, batch), dim3(WM * WN * 64), lds, st, a);
+  ds2_launch(kern, dim3(grid, 1, batch), dim3(WM * WN * 64), (unsigned)lds, st, a);
   return (int)hipGetLastError();
 }
 
@@ -494,6 +494,9 @@ int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const floa
   // launch is followed by the plain fill kernel
   const bool fused_fill = fill != nullptr && fill->n > 0 && cfg >= 6 && batch == 1;
   if (fused_fill) a.fill = *fill;
+  // an armed stop event belongs to the op's last launch: the plain fill kernel when one follows
+  const bool tail_fill = fill != nullptr && fill->n > 0 && !fused_fill;
+  hipEvent_t stop = tail_fill ? ds2_take_stop_event() : nullptr;
   int rc;
   if (!a_col && !b_col) rc = dispatch<0, 0>(a, batch, cfg, st);
   else if (!a_col && b_col) rc = dispatch<0, 1>(a, batch, cfg, st);
@@ -502,7 +505,10 @@ int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const floa
   if (rc == 0 && fill != nullptr && fill->n > 0 && !fused_fill) {
     unsigned long long bytes[8];
     for (int i = 0; i < fill->n; ++i) bytes[i] = fill->words[i] * 4;
+    ds2_arm_stop_event(stop);
     rc = ds2_multi_fill(fill->n, (void* const*)fill->ptr, bytes, fill->pattern, st);
+  } else if (stop != nullptr) {
+    ds2_arm_stop_event(stop);          // not launched: left armed for the caller to see
   }
   return rc;
 }

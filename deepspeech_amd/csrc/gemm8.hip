@@ -687,7 +687,7 @@ int launch8(const G8Args& a, int cus, hipStream_t st) {
   }
   int grid = min(cus, (a.total + 7) & ~7);          // cus: the CU budget (device CUs or a cap)
   grid = max(8, grid & ~7);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NTHR), LDS_BYTES, st, a);
+  ds2_launch(kern, dim3(grid), dim3(NTHR), (unsigned)LDS_BYTES, st, a);
   return (int)hipGetLastError();
 }
 
@@ -818,12 +818,18 @@ int ds2_gemm8(const void* A, const void* B, void* C, const void* bias, const flo
   a.total = u;
   const G8Prob& red = a.p[a.np - 1];
   a.ext_red = (ext_red && red.S > 1) ? 1 : 0;
+  // an armed stop event belongs to the op's last launch: the reduction when one follows
+  hipEvent_t stop = a.ext_red ? ds2_take_stop_event() : nullptr;
   int rc = dispatch8(a, fp8, a_col, b_col, cus, st);
-  if (rc || !a.ext_red) return rc;
+  if (rc || !a.ext_red) {
+    if (stop != nullptr) ds2_arm_stop_event(stop);
+    return rc;
+  }
   const long long work = (long long)red.M * (N / 4);
   const int grid = (int)std::max<long long>(1, std::min<long long>(4 * (long long)cus, (work + 255) / 256));
-  hipLaunchKernelGGL(g8_reduce_kernel, dim3(grid), dim3(256), 0, st, red.ws, red.S, red.M, N, red.C, ldc, epi,
-                     (const bf16_t*)bias, alpha, alpha_dev, alpha_dev2);
+  ds2_arm_stop_event(stop);
+  ds2_launch(g8_reduce_kernel, dim3(grid), dim3(256), 0u, st, (const float*)red.ws, red.S, red.M, N, red.C, ldc, epi,
+             (const bf16_t*)bias, alpha, alpha_dev, alpha_dev2);
   return (int)hipGetLastError();
 }
 

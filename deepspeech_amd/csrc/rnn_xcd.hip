@@ -2628,14 +2628,14 @@ static int rnnw_bwd(const DS2RnnX* d, hipStream_t st) {
   const int grid = ds2_rnnx_grid(d->H, d->cell, a.ngroups, a.xcd_map);
   const int npw = (d->H / 32 + MW - 1) / MW;          // unit pairs per publishing wave
   if (a.stamps != nullptr && npw == 8) {
-    hipLaunchKernelGGL((rnnw_bwd_kernel<16, 4, true>), dim3(grid), dim3(NTH), 0, st, a);
+    ds2_launch((rnnw_bwd_kernel<16, 4, true>), dim3(grid), dim3(NTH), 0u, st, a);
     return (int)hipGetLastError();
   }
   switch (2 * npw) {
-    case 10: hipLaunchKernelGGL((rnnw_bwd_kernel<10, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
-    case 12: hipLaunchKernelGGL((rnnw_bwd_kernel<12, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
-    case 14: hipLaunchKernelGGL((rnnw_bwd_kernel<14, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
-    case 16: hipLaunchKernelGGL((rnnw_bwd_kernel<16, 4>), dim3(grid), dim3(NTH), 0, st, a); break;
+    case 10: ds2_launch((rnnw_bwd_kernel<10, 4>), dim3(grid), dim3(NTH), 0u, st, a); break;
+    case 12: ds2_launch((rnnw_bwd_kernel<12, 4>), dim3(grid), dim3(NTH), 0u, st, a); break;
+    case 14: ds2_launch((rnnw_bwd_kernel<14, 4>), dim3(grid), dim3(NTH), 0u, st, a); break;
+    case 16: ds2_launch((rnnw_bwd_kernel<16, 4>), dim3(grid), dim3(NTH), 0u, st, a); break;
     default: return -36;
   }
   return (int)hipGetLastError();
@@ -2666,9 +2666,9 @@ int ds2_rnnx_bwd_rs(const DS2RnnX* d, hipStream_t st) {
   const int pbf = ((d->H / 16) % 2 != 0 || (d->knobs & 64)) ? 0 : (d->R <= 8 ? 1 : 2);
 #define DS2_RS(C, M, GP)                                                                    \
   do {                                                                                      \
-    if (pbf == 1) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP, 1>), dim3(grid), dim3(NTH), 0, st, a); \
-    else if (pbf == 2) hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP, 2>), dim3(grid), dim3(NTH), 0, st, a); \
-    else hipLaunchKernelGGL((rnnrs_bwd_kernel<C, M, GP, 0>), dim3(grid), dim3(NTH), 0, st, a);     \
+    if (pbf == 1) ds2_launch((rnnrs_bwd_kernel<C, M, GP, 1>), dim3(grid), dim3(NTH), 0u, st, a); \
+    else if (pbf == 2) ds2_launch((rnnrs_bwd_kernel<C, M, GP, 2>), dim3(grid), dim3(NTH), 0u, st, a); \
+    else ds2_launch((rnnrs_bwd_kernel<C, M, GP, 0>), dim3(grid), dim3(NTH), 0u, st, a);     \
   } while (0)
 #define DS2_RS_CELL(C)                                  \
   if (mtu_need <= 2) DS2_RS(C, 2, 4);                   \
