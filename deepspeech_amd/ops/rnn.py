@@ -998,6 +998,8 @@ class FusedBiLayer(torch.autograd.Function):
             splits = _DU_SPLITS if beside else None
             cap_u = (_beside_grid(plan, x16.device, not sch.defer_input, bool(getattr(ctx, "fp8_bwd", False)))
                      if (beside and on_side) else 0)
+            if cap_u and not _LOW_DU_CAP and ctx.idx == (_upper_trigger(plan, x16.device, T) if sch.defer_input else 1):
+                cap_u = 0
 
             steps = dgh.shape[1]
             g3 = dgh.view(2, steps * plan.NP, GH).transpose(1, 2)
@@ -1543,6 +1545,12 @@ def recurrent_layer_hip(layer, x: torch.Tensor, lens: torch.Tensor, idx: int = 0
 
 # grid cap of the grouped tail launch (0: 3/4 of the CUs; A/B only)
 _GROUP_CAP = int(os.environ.get("DS2_GROUP_CAP", "0"))
+# The lowest beside layer's dU is issued behind its dW and mostly runs after the last BPTT has
+# ended: on the whole chip, not the BPTT's idle CUs (capped it took 381 us on 56 CUs while the
+# tail's side stream waited for it). Same box, 3 rounds: 7.560 / 7.583 / 7.595 vs capped 7.609 /
+# 7.601 / 7.609 ms/step (an uncapped grouped tail launch on top: no further gain).
+# DS2_LOW_DU_CAP=1: capped (A/B)
+_LOW_DU_CAP = os.environ.get("DS2_LOW_DU_CAP", "0") != "0"
 
 # DS2_FP8_PAIRS=0: every fp8 layer sums its directions with torch.add (A/B timing)
 _FP8_PAIRS = os.environ.get("DS2_FP8_PAIRS", "1") != "0"
