@@ -998,7 +998,8 @@ class FusedBiLayer(torch.autograd.Function):
             splits = _DU_SPLITS if beside else None
             cap_u = (_beside_grid(plan, x16.device, not sch.defer_input, bool(getattr(ctx, "fp8_bwd", False)))
                      if (beside and on_side) else 0)
-            if cap_u and not _LOW_DU_CAP and ctx.idx == (_upper_trigger(plan, x16.device, T) if sch.defer_input else 1):
+            if cap_u and (_DU_UNCAP == "all" or (_DU_UNCAP == "low" and ctx.idx == (
+                    _upper_trigger(plan, x16.device, T) if sch.defer_input else 1))):
                 cap_u = 0
 
             steps = dgh.shape[1]
@@ -1549,8 +1550,10 @@ _GROUP_CAP = int(os.environ.get("DS2_GROUP_CAP", "0"))
 # ended: on the whole chip, not the BPTT's idle CUs (capped it took 381 us on 56 CUs while the
 # tail's side stream waited for it). Same box, 3 rounds: 7.560 / 7.583 / 7.595 vs capped 7.609 /
 # 7.601 / 7.609 ms/step (an uncapped grouped tail launch on top: no further gain).
-# DS2_LOW_DU_CAP=1: capped (A/B)
-_LOW_DU_CAP = os.environ.get("DS2_LOW_DU_CAP", "0") != "0"
+# DS2_DU_UNCAP=none: capped; =all: every beside layer's dU uncapped (A/B: 7.639 / 7.695 / 7.690
+# vs 7.535 / 7.554 / 7.563 ms/step for "low": an upper layer's dU then waits for the BPTT's CUs
+# and lands on the next dx GEMM and BPTT)
+_DU_UNCAP = os.environ.get("DS2_DU_UNCAP", "low")
 
 # DS2_FP8_PAIRS=0: every fp8 layer sums its directions with torch.add (A/B timing)
 _FP8_PAIRS = os.environ.get("DS2_FP8_PAIRS", "1") != "0"
