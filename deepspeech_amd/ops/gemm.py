@@ -42,6 +42,13 @@ TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
     # gemm8; 197 us alone; round 4 timeline, profiles/r4_headline.md)
     (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
 }
+# DS2_DX_CFG: the headline dx GEMM's configuration for an A/B (a csrc/gemm.hip cfg, or "g8")
+_DX_CFG = os.environ.get("DS2_DX_CFG")
+if _DX_CFG:
+    if _DX_CFG == "g8":
+        TUNED.pop((7712, 800, 4800, False, False, 1), None)
+    else:
+        TUNED[(7712, 800, 4800, False, False, 1)] = int(_DX_CFG)
 _FORCE = os.environ.get("DS2_GEMM_CFG")
 # DS2_GEMM selects which engine GEMM classes run on the hand-written kernels: "hip" (all, the
 # default), "torch" (none: library GEMMs, A/B timing only) or a comma list of {proj, dx, wgrad}.
