@@ -77,6 +77,10 @@ _FUSED_OPT = False
 _EARLY_GRID = int(os.environ.get("DS2_EARLY_OPT_GRID", "384"))
 # the same range when the upper part already ran beside layer 0's BPTT (A/B)
 _LOWER_GRID = int(os.environ.get("DS2_LOWER_OPT_GRID", "0"))
+# grid cap (blocks) of the data-parallel per-bucket Adam + EMA ranges, which stream beside the
+# BPTTs (0: uncapped). --force_dp at world 1, same box, 3 rounds: uncapped 7.754 / 7.747 / 7.705,
+# 512 7.782 / 7.725 / 7.719, 256 7.771 / 7.790 / 7.814, 128 7.86-7.88 ms/step
+_BUCKET_GRID = int(os.environ.get("DS2_BUCKET_OPT_GRID", "0"))
 
 
 def _check_hw_queues() -> None:
@@ -378,7 +382,8 @@ class Trainer:
         if per_bucket:
             # DP-native ordering: each gradient bucket's Adam + EMA range runs on the
             # bucketer's ordering stream right behind its all-reduce (bitwise the same update)
-            self.bucketer.set_optimizer(lambda lo, hi: self.opt.apply_range(lo, hi, lr_t, keep, gscale))
+            self.bucketer.set_optimizer(lambda lo, hi: self.opt.apply_range(lo, hi, lr_t, keep, gscale,
+                                                                            max_grid=_BUCKET_GRID))
         early = (not per_bucket and self.nan_policy != "skip" and self._early_split > 0 and lazy and
                  self.arena.wgrad.grouped and self.arena.wgrad.defer_input)
         if early:
