@@ -168,6 +168,31 @@ def test_xcd_plans_for_wide_and_deferral_rule():
     assert 256 - RNN._bptt_cus(head) < RNN._BESIDE_MIN_IDLE_CUS <= 256 - RNN._bptt_cus(c5)
 
 
+def test_partial_deferral_rule(monkeypatch):
+    """Which layers' weight gradients join the grouped tail launch (no GPU: the host rule of
+    ops/rnn.py _defer_layers). Headline (56 idle CUs): only layer 0's, and only for sequences of
+    >= _PARTIAL_MIN_T recurrence steps (the 10-s batch has 241); shorter buckets defer every
+    layer's. ReLU-1760 (32 idle CUs) defers everything; config 5 (96 idle) defers nothing."""
+    from deepspeech_amd.ops import rnn as RNN
+    monkeypatch.setenv("DS2_NUM_CUS", "256")
+    monkeypatch.setattr(RNN, "_DEFER_LAYERS", -1)
+    cuda = torch.device("cuda", 0)
+    head = RNN.make_xcd_plan(32, 800, "gru", 2, 256)
+    relu = RNN.make_xcd_plan(32, 1760, "rnn_relu", 2, 256)
+    c5 = RNN.make_xcd_plan(32, 1280, "gru", 2, 256)
+    assert RNN._PARTIAL_MIN_T <= 241
+    assert RNN._defer_wgrad(head, cuda) and RNN._defer_layers(head, cuda, 241) == 1
+    assert [RNN._defer_layer(head, cuda, i, 241) for i in range(5)] == [True] + [False] * 4
+    assert RNN._upper_trigger(head, cuda, 241) == 1
+    short = RNN._PARTIAL_MIN_T - 1
+    assert all(RNN._defer_layer(head, cuda, i, short) for i in range(5))
+    assert RNN._upper_trigger(head, cuda, short) >= 5
+    assert all(RNN._defer_layer(relu, cuda, i, 241) for i in range(7))
+    assert not RNN._defer_wgrad(c5, cuda) and RNN._upper_trigger(c5, cuda, 241) == 1
+    assert not any(RNN._defer_layer(c5, cuda, i, 241) for i in range(7))
+    assert RNN._defer_layers(head, torch.device("cpu"), 241) >= 5          # CPU: all deferred
+
+
 def test_recurrence_kernel_family_map():
     """Which kernel family every bf16 plan launches (no GPU: the host dispatch functions of
     csrc/rnn_xcd.hip that the launches branch on). Every family on this map is reachable by a
