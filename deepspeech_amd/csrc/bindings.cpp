@@ -220,7 +220,7 @@ int ds2_gemm(const void* A, const void* B, void* C, const void* bias, const floa
 int ds2_gemm_tile(int cfg, int* bm, int* bn);
 int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens, const int* labels,
                  const int* label_lens, float* loss, void* G, float* ws, int T, int N, int H, int K, int Lmax,
-                 int blank, int zero_inf, hipStream_t st);
+                 int blank, int zero_inf, float* mean, int* counter, int* first_bad, hipStream_t st);
 int ds2_hist_nbucket();
 int ds2_hist_blocks(long long n);
 int ds2_hist_stats(const void* x, int bf16, long long n, unsigned* counts, float* part, int blocks, hipStream_t st);
@@ -1317,8 +1317,11 @@ void gemm(at::Tensor A, at::Tensor B, at::Tensor C, OptT bias, int64_t M, int64_
 
 // FC head + CTC (training): h [T, N, H] bf16, W [K, H] bf16, bias [K] bf16 -> loss [N] fp32,
 // G [T*N, 32] bf16 (per-utterance dloss/dlogits, zero-padded classes)
+// mean (optional, [1] fp32): the batch-mean loss written by the same launch; counter / first_bad
+// (optional, [1] int32 each): the per-step divergence watch of utils/stats.py NonfiniteWatch
 void head_ctc(at::Tensor h, at::Tensor W, at::Tensor bias, at::Tensor lens, at::Tensor labels, at::Tensor label_lens,
-              at::Tensor loss, at::Tensor G, at::Tensor ws, int64_t blank, bool zero_inf) {
+              at::Tensor loss, at::Tensor G, at::Tensor ws, int64_t blank, bool zero_inf, OptT mean, OptT counter,
+              OptT first_bad) {
   for (auto* t : {&h, &W, &bias, &lens, &labels, &label_lens, &loss, &G, &ws}) need_gpu(*t, "head_ctc operand");
   TORCH_CHECK(h.dim() == 3 && h.scalar_type() == at::kBFloat16, "h: [T, N, H] bf16");
   const int64_t T = h.size(0), N = h.size(1), H = h.size(2), K = W.size(0);
@@ -1333,9 +1336,27 @@ void head_ctc(at::Tensor h, at::Tensor W, at::Tensor bias, at::Tensor lens, at::
   const int64_t Lmax = labels.size(1);
   TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= ds2_ctc_ws_floats((int)T, (int)N, (int)Lmax),
               "head_ctc: workspace too small");
+  float* mean_p = nullptr;
+  int *counter_p = nullptr, *first_p = nullptr;
+  if (mean.has_value()) {
+    need_gpu(*mean, "head_ctc mean");
+    TORCH_CHECK(mean->scalar_type() == at::kFloat && mean->numel() == 1, "mean: [1] fp32");
+    mean_p = mean->data_ptr<float>();
+  }
+  if (counter.has_value() || first_bad.has_value()) {
+    TORCH_CHECK(mean_p != nullptr && counter.has_value() && first_bad.has_value(),
+                "head_ctc: the watch needs mean, counter and first_bad");
+    need_gpu(*counter, "head_ctc counter");
+    need_gpu(*first_bad, "head_ctc first_bad");
+    TORCH_CHECK(counter->scalar_type() == at::kInt && counter->numel() == 1 && first_bad->scalar_type() == at::kInt &&
+                    first_bad->numel() == 1, "counter / first_bad: [1] int32");
+    counter_p = counter->data_ptr<int>();
+    first_p = first_bad->data_ptr<int>();
+  }
   check(ds2_head_ctc(h.data_ptr(), W.data_ptr(), bias.data_ptr(), lens.data_ptr<int>(), labels.data_ptr<int>(),
                      label_lens.data_ptr<int>(), loss.data_ptr<float>(), G.data_ptr(), ws.data_ptr<float>(), (int)T,
-                     (int)N, (int)H, (int)K, (int)Lmax, (int)blank, zero_inf ? 1 : 0, cur_stream()),
+                     (int)N, (int)H, (int)K, (int)Lmax, (int)blank, zero_inf ? 1 : 0, mean_p, counter_p, first_p,
+                     cur_stream()),
         "head_ctc");
 }
 
@@ -1516,7 +1537,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("alpha_dev") = py::none(), py::arg("Ml") = 0, py::arg("Nl") = 0, py::arg("Kl") = 0,
         py::arg("fill") = std::vector<at::Tensor>{}, py::arg("fill_pat") = std::vector<int64_t>{});
   m.def("gemm_tile", &gemm_tile);
-  m.def("head_ctc", &head_ctc);
+  m.def("head_ctc", &head_ctc, py::arg("h"), py::arg("W"), py::arg("bias"), py::arg("lens"), py::arg("labels"),
+        py::arg("label_lens"), py::arg("loss"), py::arg("G"), py::arg("ws"), py::arg("blank"), py::arg("zero_inf"),
+        py::arg("mean") = py::none(), py::arg("counter") = py::none(), py::arg("first_bad") = py::none());
   m.def("fc_logits", &fc_logits);
   m.def("hist_stats", &hist_stats);
   m.def("hist_nbucket", []() { return ds2_hist_nbucket(); });

@@ -382,9 +382,35 @@ __global__ __launch_bounds__(256) void ctc_grad_lp_kernel(const int* __restrict_
                                                         const float* __restrict__ ab_ws,
                                                         const float* __restrict__ logp_in, float* __restrict__ loss,
                                                         bf16_t* __restrict__ G, int T, int N, int K, int Lmax, int SPS,
-                                                        int blank, int zero_inf) {
+                                                        int blank, int zero_inf, float* __restrict__ mean_out,
+                                                        int* __restrict__ counter, int* __restrict__ first_bad) {
   __shared__ float occ_s[4][KPAD];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (mean_out != nullptr && blockIdx.x == 0 && wv == 0) {
+    // the batch-mean loss (every per-utterance loss is final: ctc_recur wrote logp) and the
+    // per-step divergence watch (stats.hip nonfinite_watch_kernel) in this launch instead of a
+    // reduction kernel and a 1-thread kernel behind it on the step's critical path
+    float s = 0.f;
+    for (int b0 = 0; b0 < N; b0 += 64) {
+      const int bb = b0 + lane;
+      float l = 0.f;
+      if (bb < N) {
+        const int lb = min(lens[bb], T), Lb = min(label_lens[bb], Lmax);
+        const float lp = (lb > 0 && Lb <= lb) ? logp_in[bb] : NEG_INF;
+        l = !(lp == NEG_INF) ? -lp : (zero_inf ? 0.f : INFINITY);
+      }
+      s += wave_sum(l);
+    }
+    if (lane == 0) {
+      const float m = s / (float)N;
+      *mean_out = m;
+      if (counter != nullptr) {
+        const int st = counter[0];
+        if (!(fabsf(m) <= 3.402823466e38f) && first_bad[0] < 0) first_bad[0] = st;   // NaN or +-inf
+        counter[0] = st + 1;
+      }
+    }
+  }
   const int w = blockIdx.x * 4 + wv;
   if (w >= T * N) return;
   const int t = w / N, b = w % N;
@@ -519,7 +545,7 @@ static int fc_attr(int lds) {
 // Outputs loss [N] and G [T*N][32] bf16 (dloss_b/dlogits, zero-padded). ws as ds2_ctc_ws_floats.
 int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens, const int* labels,
                  const int* label_lens, float* loss, void* G, float* ws, int T, int N, int H, int K, int Lmax,
-                 int blank, int zero_inf, hipStream_t st) {
+                 int blank, int zero_inf, float* mean, int* counter, int* first_bad, hipStream_t st) {
   if (K > KPAD || H % 32 != 0) return -20;
   const int SPmax = 2 * Lmax + 1;
   if (SPmax > 64 * 32) return -21;
@@ -536,7 +562,7 @@ int ds2_head_ctc(const void* h, const void* W, const void* bias, const int* lens
                      H, K);
   launch_recur_spl(spl, lens, labels, label_lens, lp_ws, ab_ws, logp, T, N, Lmax, SPmax, blank, st);
   hipLaunchKernelGGL(ctc_grad_lp_kernel, dim3((M + 3) / 4), dim3(256), 0, st, lens, labels, label_lens, lp_ws, ab_ws,
-                     logp, loss, (bf16_t*)G, T, N, K, Lmax, SPS, blank, zero_inf);
+                     logp, loss, (bf16_t*)G, T, N, K, Lmax, SPS, blank, zero_inf, mean, counter, first_bad);
   return (int)hipGetLastError();
 }
 

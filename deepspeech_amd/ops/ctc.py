@@ -5,6 +5,9 @@ to the logits is produced by the forward kernel and only scaled in backward.
 """
 from __future__ import annotations
 
+import os
+import threading
+
 import torch
 
 _FC_SPLIT_MAX = 16         # split-K ceiling of the FC head's weight-gradient GEMM
@@ -69,6 +72,35 @@ class CTCMeanFused(CTCLossFused):
             return grad * (gloss / ctx.n), None, None, None, None, None
 
 
+_watch_ctx = threading.local()
+# DS2_FUSED_LOSS=0: torch's mean and a separate watch launch (A/B; same box, 3 rounds, graph
+# steps: 100 frames 1.483-1.485 vs 1.486-1.495 ms, 200 frames 2.171-2.174 vs 2.177-2.182 ms;
+# headline within run-to-run spread)
+_FUSE_LOSS = os.environ.get("DS2_FUSED_LOSS", "1") != "0"
+
+
+class loss_watch:
+    """Context of one training step's forward: the fused head + CTC (FusedHeadCTC) writes the
+    batch-mean loss and runs the step's divergence watch (utils/stats.py NonfiniteWatch:
+    counter / first-bad words) inside its gradient launch, instead of a reduction kernel and a
+    1-thread kernel behind it. ``consumed`` is False when no fused head took it (the reference
+    engine, a CPU watch): the caller then runs ``watch.update(loss)`` itself."""
+
+    def __init__(self, watch):
+        self.watch = watch
+        self.consumed = False
+        self._prev = None
+
+    def __enter__(self):
+        self._prev = getattr(_watch_ctx, "cur", None)
+        _watch_ctx.cur = self
+        return self
+
+    def __exit__(self, *exc):
+        _watch_ctx.cur = self._prev
+        return False
+
+
 class FusedHeadCTC(torch.autograd.Function):
     """Mean CTC loss of the FC head's logits without materialising them (training path).
 
@@ -100,11 +132,23 @@ class FusedHeadCTC(torch.autograd.Function):
         loss = torch.empty(N, device=dev, dtype=torch.float32)
         G = torch.empty(T * N, 32, device=dev, dtype=torch.bfloat16)
         ws = torch.empty(int(C.ctc_ws_floats(T, N, labels.shape[1])), device=dev, dtype=torch.float32)
-        C.head_ctc(h, w16, b16, lens, labels, label_lens, loss, G, ws, blank, zero_infinity)
+        if not _FUSE_LOSS:
+            C.head_ctc(h, w16, b16, lens, labels, label_lens, loss, G, ws, blank, zero_infinity)
+            ctx.save_for_backward(h, G, w16)
+            ctx.params = (weight, bias)
+            ctx.K = K
+            return loss.mean()
+        mean = torch.empty((), device=dev, dtype=torch.float32)
+        lw = getattr(_watch_ctx, "cur", None)
+        watch = {}
+        if lw is not None and not lw.consumed and lw.watch.counter.device == dev:
+            watch = dict(counter=lw.watch.counter, first_bad=lw.watch.first_bad)
+            lw.consumed = True
+        C.head_ctc(h, w16, b16, lens, labels, label_lens, loss, G, ws, blank, zero_infinity, mean=mean, **watch)
         ctx.save_for_backward(h, G, w16)
         ctx.params = (weight, bias)
         ctx.K = K
-        return loss.mean()
+        return mean
 
     @staticmethod
     def backward(ctx, gloss):

@@ -26,6 +26,7 @@ import torch
 
 from .models import DeepSpeech2
 from .ops import _ext
+from .ops import ctc as _CTC
 from .ops.optim import FusedAdamEMA, ParamArena, exponential_decay
 from .parallel.grad_sync import GradBucketer, broadcast_params
 from .utils import trace as TR
@@ -371,8 +372,10 @@ class Trainer:
         lazy = model.engine == "hip"
         self.arena.wgrad.discard()
         self.arena.zero_grad(lazy=lazy)
-        loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
-        self.watch.update(loss)
+        with _CTC.loss_watch(self.watch) as lw:
+            loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
+        if not lw.consumed:
+            self.watch.update(loss)
         # a cached device 1.0 as the backward seed: autograd would launch a fill for ones_like
         one = self._seed.get((loss.device, loss.dtype))
         if one is None:

@@ -64,3 +64,31 @@ def test_nan_logits_reach_the_loss_and_the_watch(cuda, fused):
     w.update(torch.tensor(1.0, device=cuda))
     w.update(loss.detach())
     assert w.first_bad_step() == 8
+
+
+def test_trainer_fused_loss_watch(cuda):
+    """The HIP engine's head + CTC writes the batch-mean loss and runs the step's divergence
+    watch in its gradient launch (ops/ctc.py loss_watch): the watch counts every step, records
+    the first NaN step, and the loss is the mean of the per-utterance losses."""
+    from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.ops import ctc as CTC
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    torch.manual_seed(0)
+    m = DeepSpeech2(num_filters=32, num_hidden=128, num_rnn_layers=2, cell="gru").to(cuda).set_engine("hip", torch.bfloat16)
+    tr = Trainer(m, LRSchedule(1e-4, 100, 0.9))
+    b = to_device(FixedShapeBatches(4, max_frames=200, seed=0, pool=1).next(), cuda)
+    with CTC.loss_watch(tr.watch) as lw:
+        loss = m.forward_loss(b["feats"], b["seq_lens"], b["labels"], b["label_lens"])
+    assert lw.consumed and loss.dim() == 0 and torch.isfinite(loss).item()
+    assert int(tr.watch.counter.item()) == 1
+    tr.watch.reset(0)
+    for _ in range(3):
+        tr.step(b)
+    assert int(tr.watch.counter.item()) == 3 and tr.first_nonfinite_step() is None
+    with torch.no_grad():
+        m.fc_weight.data.fill_(float("nan"))
+    tr.arena.mark_dirty()
+    tr.step(b)
+    tr.step(b)
+    assert int(tr.watch.counter.item()) == 5 and tr.first_nonfinite_step() == 3
