@@ -124,6 +124,9 @@ def build_train_parser() -> argparse.ArgumentParser:
                    help="ranks (one per GPU) on this node; without an outer launcher (torchrun) the driver "
                         "starts them itself (parallel/launch.py). Default: the launcher's WORLD_SIZE, else 1")
     p.add_argument("--async_checkpoint", type=str2bool, default=True)
+    p.add_argument("--checkpoint_format", type=str, default="tf", choices=["tf", "torch"],
+                   help="tf: TF Saver-V2 bundle (model.ckpt-<step>.index + .data-00000-of-00001, "
+                        "readable by the reference's tf.train.Saver); torch: one torch.save file")
     p.add_argument("--step_graphs", type=str, default="auto", choices=["auto", "on", "off"],
                    help="single-GPU HIP engine: replay each batch shape's captured training step "
                         "(HIP graph) instead of launching it eagerly; auto: time both once per "

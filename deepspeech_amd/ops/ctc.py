@@ -119,6 +119,8 @@ class FusedHeadCTC(torch.autograd.Function):
         T, N, H = h.shape
         K = weight.shape[0]
         dev = h.device
+        if arena_of(weight) is not None:
+            arena_of(weight).await_params(weight, bias)      # a carried optimizer update (Trainer)
         h = h.to(torch.bfloat16).contiguous()
         w16 = weight.bf16 if arena_of(weight) is not None else weight.detach().to(torch.bfloat16).contiguous()
         b16 = bias.bf16 if arena_of(bias) is not None else bias.detach().to(torch.bfloat16).contiguous()

@@ -214,6 +214,8 @@ class FrontendCL(torch.autograd.Function):
     def forward(ctx, feats, w1, b1, g1, be1, w2, b2, g2, be2, model):
         C_ = _ext.ext()
         dev = feats.device
+        if arena_of(w1) is not None:
+            arena_of(w1).await_params(w1, b1, g1, be1, w2, b2, g2, be2)
         x = feats.to(torch.bfloat16).contiguous()
         N, T, F0 = x.shape
         T1, F1 = (T - 20) // 2 + 1, (F0 - 5) // 2 + 1
@@ -343,6 +345,8 @@ class FusedHead(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, weight, bias):
         T, N, H = h.shape
+        if arena_of(weight) is not None:
+            arena_of(weight).await_params(weight, bias)      # a carried optimizer update (Trainer)
         w16 = weight.bf16 if arena_of(weight) is not None else weight.to(torch.bfloat16)
         b16 = bias.bf16 if arena_of(bias) is not None else bias.to(torch.bfloat16)
         h2 = h.to(torch.bfloat16).reshape(T * N, H).contiguous()

@@ -88,6 +88,90 @@ class ParamArena:
                 p._ds2_arena = self
         self._dirty = True
         self.ensure_bf16()
+        # optimizer update carried into the next step (Trainer defer_update): chunks not issued
+        # yet ([(fn, params)] in the order the next forward reads them), and the events of the
+        # issued ones that readers of their weights still have to wait for
+        self._pending_chunks: List[tuple] = []
+        self._update_events: Dict[int, "torch.cuda.Event"] = {}
+        self._event_pool: List["torch.cuda.Event"] = []
+        self._event_next = 0
+
+    # ---- deferred optimizer update ----------------------------------------------------
+    def set_pending_update(self, chunks) -> None:
+        """Carry an optimizer update into the next forward: ``chunks`` = [(fn, params)] in the
+        order the next forward reads their weights; ``fn(grid)`` enqueues one chunk's update on
+        the current stream (grid: block cap, 0 = uncapped)."""
+        self._pending_chunks = list(chunks)
+        self._event_next = 0
+
+    def has_pending_update(self) -> bool:
+        return bool(self._pending_chunks) or bool(self._update_events)
+
+    def _event(self) -> "torch.cuda.Event":
+        if self._event_next == len(self._event_pool):
+            self._event_pool.append(torch.cuda.Event())
+        ev = self._event_pool[self._event_next]
+        self._event_next += 1
+        return ev
+
+    def issue_pending_update(self, grid: int = 0, count: int = 1) -> None:
+        """Enqueue the next ``count`` chunks of the carried update on the weight-gradient side
+        stream, behind everything the current stream has enqueued (a recurrent layer's
+        projection): each then runs on the CUs that layer's persistent recurrence leaves idle,
+        and the reader of its weights waits only for its own chunk (:meth:`await_params`)."""
+        if not self._pending_chunks:
+            return
+        take, self._pending_chunks = self._pending_chunks[:count], self._pending_chunks[count:]
+        dev = self.flat.device
+        side = self.wgrad.stream(dev) if dev.type == "cuda" else None
+        if side is None:
+            for fn, _ in take:
+                fn(0)
+            return
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for fn, params in take:
+                fn(grid)
+                ev = self._event()
+                ev.record(side)
+                for p in params:
+                    self._update_events[id(p)] = ev
+
+    def await_params(self, *params) -> None:
+        """Make the current stream wait for the carried update of ``params`` (no-op when none
+        is in flight); chunks holding any of them that were not issued yet are issued first.
+        Every fused op that reads arena weights calls this before it reads them."""
+        if not (self._update_events or self._pending_chunks):
+            return
+        ids = {id(p) for p in params if p is not None}
+        last = -1
+        for j, (_, ps) in enumerate(self._pending_chunks):
+            if any(id(p) in ids for p in ps):
+                last = j
+        if last >= 0:
+            self.issue_pending_update(0, last + 1)
+        cur = None
+        waited = set()
+        for i in ids:
+            ev = self._update_events.pop(i, None)
+            if ev is not None and id(ev) not in waited:
+                if cur is None:
+                    cur = torch.cuda.current_stream(self.flat.device)
+                cur.wait_event(ev)
+                waited.add(id(ev))
+
+    def settle_updates(self) -> None:
+        """Complete the carried update from the current stream's point of view: issue the
+        chunks nothing issued yet here, and wait for every chunk still in flight. After this
+        the master weights, bf16 shadows, Adam moments and EMA are those of the last step."""
+        take, self._pending_chunks = self._pending_chunks, []
+        for fn, _ in take:
+            fn(0)
+        if self._update_events:
+            cur = torch.cuda.current_stream(self.flat.device)
+            for ev in {id(e): e for e in self._update_events.values()}.values():
+                cur.wait_event(ev)
+            self._update_events.clear()
 
     # ---- bf16 shadow ------------------------------------------------------------
     def mark_dirty(self) -> None:

@@ -803,6 +803,11 @@ class FusedBiLayer(torch.autograd.Function):
                 bh_f, bh_b, pair_out: bool = False):
         pair_in = x.dim() == 4
         T, N, D = x.shape[-3:]
+        arena = arena_of(W_f)
+        if arena is not None:
+            # an optimizer update carried over from the previous step (Trainer defer_update)
+            # may still be writing these weights on the side stream
+            arena.await_params(W_f, W_b, U_f, U_b, b_f, b_b, bh_f, bh_b)
         dirs_W = [W_f] + ([W_b] if W_b is not None else [])
         dirs_b = [b_f] + ([b_b] if b_b is not None else [])
         W16 = _bf16_group(dirs_W)                     # [ndir*G*H, D]
@@ -833,6 +838,11 @@ class FusedBiLayer(torch.autograd.Function):
                 _ext.ext().multi_fill(*fill)
         else:
             gx = _linear(x2, W16, b16, alpha, fill=fill).view(T, N, -1)
+        if arena is not None and x.is_cuda:
+            # the next chunk of the optimizer update carried over from the previous step (the
+            # layer above's, or the head's): on the side stream behind this projection, i.e.
+            # beside this layer's recurrence on the CUs it leaves idle
+            arena.issue_pending_update(_idle_cus(plan, x.device))
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
@@ -1088,6 +1098,15 @@ def _bptt_cus(plan: RnnPlan) -> int:
     if plan.kind == "xcd":
         return plan.ndir * plan.BG * _xcd_p(plan.H, plan.cell)
     return plan.ndir * plan.BG * plan.S if plan.persistent else 1 << 30
+
+
+def _idle_cus(plan: RnnPlan, device: torch.device) -> int:
+    """Block cap for work beside this plan's persistent recurrence: the CUs it leaves idle
+    (rounded down to whole XCD rounds), 0 (uncapped) when that is not a useful bound."""
+    if device.type != "cuda" or plan.kind != "xcd":
+        return 0
+    idle = _ext.num_cus(device.index or 0) - _bptt_cus(plan)
+    return idle // 8 * 8 if idle >= 16 else 0
 
 
 def _defer_wgrad(plan: RnnPlan, device: torch.device) -> bool:

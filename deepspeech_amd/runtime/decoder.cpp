@@ -306,6 +306,7 @@ class BatchBeamSearch {
 #ifndef DS2_NO_PYBIND
 void register_loader(py::module_& m);
 void register_tfrecord(py::module_& m);
+void register_bundle(py::module_& m);
 
 PYBIND11_MODULE(_native, m) {
   m.doc() = "deepspeech_amd native host runtime";
@@ -328,5 +329,6 @@ PYBIND11_MODULE(_native, m) {
       .def("best", &ds2rt::PrefixBeamSearch::best);
   register_loader(m);
   register_tfrecord(m);
+  register_bundle(m);
 }
 #endif  // DS2_NO_PYBIND

@@ -182,7 +182,8 @@ def main(argv=None) -> int:
     trainer = Trainer(model, lr_schedule_from_args(args, steps_per_epoch), args.moving_avg_decay,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
                       allreduce_bf16=args.allreduce_dtype == "bf16", nan_policy=args.nan_policy,
-                      step_graphs={"auto": "auto", "on": True, "off": False}[args.step_graphs])
+                      step_graphs={"auto": "auto", "on": True, "off": False}[args.step_graphs],
+                      defer_update=True)
     start = 0
     rdir = resume_dir(args)
     if rdir is not None:
@@ -198,7 +199,8 @@ def main(argv=None) -> int:
             print("Variable: ", n, tuple(p.shape))
         print("parameters: %d" % model.num_params())
 
-    ckpt = CK.CheckpointManager(args.train_dir, args.max_to_keep, args.async_checkpoint) if ctx.is_main else None
+    ckpt = (CK.CheckpointManager(args.train_dir, args.max_to_keep, args.async_checkpoint, fmt=args.checkpoint_format,
+                                 nan_policy=args.nan_policy) if ctx.is_main else None)
     events = EventWriter(args.train_dir) if ctx.is_main else None
     metrics = JsonlWriter(os.path.join(args.train_dir, "metrics.jsonl")) if ctx.is_main else None
     durations = []
@@ -265,6 +267,7 @@ def main(argv=None) -> int:
         steps_since += 1
         audio_since += hb.audio_seconds
         if prof is not None:
+            trainer.flush()
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             prof.__exit__(None, None, None)
@@ -320,14 +323,24 @@ def main(argv=None) -> int:
                                tflops=round(step_fl * ctx.world_size / (ms.sum() / 1e3) / 1e12, 3))
                 metrics.write(step, **rec)
             if do_sum:
+                trainer.flush()              # variable histograms read the updated weights
                 write_summaries(events, step, trainer, model, args, lv, ema)
         if do_ckpt:
-            ckpt.save(trainer, step, force=step + 1 == args.max_steps)
+            trainer.flush()                  # the snapshot is step <step>'s full update
+            if ckpt.save(trainer, step, force=step + 1 == args.max_steps) is None:
+                # the writer was still busy with an earlier file: no snapshot (CheckpointManager)
+                metrics.write(step, event="checkpoint_skipped", checkpoints_written=len(ckpt.written))
+    trainer.flush()
     if loss is not None:
         float(loss.item())
         check_divergence()
     if ckpt is not None:
         ckpt.close()
+        if ckpt.written:
+            # the effective save cadence of the run
+            metrics.write(args.max_steps - 1, event="checkpoint_summary", checkpoints_written=len(ckpt.written),
+                          checkpoints_skipped=len(ckpt.skipped), checkpoints_dropped=len(ckpt.dropped),
+                          checkpoint_write_s_mean=round(sum(ckpt.write_s) / len(ckpt.write_s), 4))
     if events is not None:
         events.close()
     source_free = prefetch.close() if prefetch is not None else True

@@ -124,8 +124,11 @@ class Trainer:
     def __init__(self, model: DeepSpeech2, lr_schedule: LRSchedule, moving_avg_decay: Optional[float] = 0.9999,
                  world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
                  nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False,
-                 step_graphs=False, graph_warmup: int = 2, bucket_split_after=()):
+                 step_graphs=False, graph_warmup: int = 2, bucket_split_after=(), defer_update: bool = False):
         self.model = model
+        # carry the optimizer update of the FC head and recurrent layers >= 1 into the next
+        # step's forward (see _body); readers of the weights between steps call flush()
+        self.defer_update = bool(defer_update)
         if model.engine == "hip":
             from .ops.rnn import check_knobs
             check_knobs()            # timing-only kernel switches never reach a training run
@@ -185,6 +188,7 @@ class Trainer:
         # auto mode: shape key -> (chosen mode, best eager ms, best replay ms)
         self.graph_modes: Dict[tuple, tuple] = {}
         self._graph_pool = None
+        self._chunk_cache = {}
 
     def upper_range(self, b: int):
         """(end, params) of the arena range holding the FC head and the recurrent layers >= b:
@@ -194,6 +198,45 @@ class Trainer:
         if not i:
             return None
         return self.arena.offsets[i][0], list(self.arena.params[:i])
+
+    def _chunks(self, hi: int):
+        """[(lo, hi, params)] of arena range [0, hi) split per recurrent layer, in the order the
+        next forward reads them: layer 1, 2, ..., the top layer, then the FC head."""
+        key = ("chunks", hi)
+        c = self._chunk_cache.get(key)
+        if c is not None:
+            return c
+        starts = sorted((self.arena.offsets[i][0], k) for k, i in self._layer_first.items())
+        bounds = [0] + [s for s, _ in starts if 0 < s < hi] + [hi]
+        out = []
+        for lo, up in zip(bounds[:-1], bounds[1:]):
+            params = [p for p, (o, n) in zip(self.arena.params, self.arena.offsets) if lo <= o < up]
+            if up > lo:
+                out.append((lo, up, params))
+        c = self._chunk_cache[key] = list(reversed(out))
+        return c
+
+    def _carry_update(self, hi: int, lr_t: float, keep: float, gscale: float) -> None:
+        """Register the optimizer update of arena range [0, hi) (FC head + recurrent layers >= 1,
+        whose gradients are final once layer 1's weight gradients are issued) with the arena, to
+        be enqueued by the NEXT forward one chunk beside each recurrence (ops/rnn.py FusedBiLayer:
+        layer k's chunk beside layer k-1's recurrence, the head's beside the top layer's), each
+        projection waiting only for its own chunk. In this
+        step's tail it ran beside the conv front-end's backward and the bottom layer's weight
+        gradients, which it slowed (r5 profile: 387 us of HBM-bound work on the critical tail).
+        Bitwise the same update (every element's Adam + EMA is independent of the launch split)."""
+        opt = self.opt
+
+        def chunk(lo, up):
+            return lambda grid: opt.apply_range(lo, up, lr_t, keep, gscale, max_grid=grid)
+        self.arena.set_pending_update([(chunk(lo, up), params) for lo, up, params in self._chunks(hi)])
+
+    def flush(self) -> None:
+        """Complete an optimizer update carried into the next step (``defer_update``): after
+        this, on the current stream, the weights, Adam moments, EMA and bf16 shadows are those
+        of the last step. Call before anything reads them between steps: checkpoints, EMA
+        swaps, eval, summaries, graph capture, and the end of a timed region."""
+        self.arena.settle_updates()
 
     @property
     def lr(self) -> float:
@@ -299,6 +342,7 @@ class Trainer:
 
     def _replay(self, g: "_StepGraph", batch: Dict[str, torch.Tensor], width: int, lr_t: float,
                 keep: float, events=None) -> torch.Tensor:
+        self.flush()           # a graph never carries or consumes an update across steps
         feats, labels = batch["feats"], batch["labels"]
         pairs = [(g.feats, feats), (g.seq_lens, batch["seq_lens"]), (g.label_lens, batch["label_lens"]),
                  (g.labels, labels)]
@@ -327,6 +371,7 @@ class Trainer:
 
     def _capture(self, batch: Dict[str, torch.Tensor], width: int) -> "_StepGraph":
         dev = self.arena.flat.device
+        self.flush()           # never capture the previous step's carried update into the graph
         static = {
             "feats": batch["feats"].clone(),
             "seq_lens": batch["seq_lens"].clone(),
@@ -374,6 +419,9 @@ class Trainer:
         self.arena.zero_grad(lazy=lazy)
         with _CTC.loss_watch(self.watch) as lw:
             loss = model.forward_loss(batch["feats"], batch["seq_lens"], batch["labels"], batch["label_lens"])
+        # a carried update whose weights no fused op awaited (another model path) completes
+        # here, before backward writes this step's gradients over the ones it reads
+        self.arena.settle_updates()
         if not lw.consumed:
             self.watch.update(loss)
         # a cached device 1.0 as the backward seed: autograd would launch a fill for ones_like
@@ -389,6 +437,8 @@ class Trainer:
                                                                             max_grid=_BUCKET_GRID))
         early = (not per_bucket and self.nan_policy != "skip" and self._early_split > 0 and lazy and
                  self.arena.wgrad.grouped and self.arena.wgrad.defer_input)
+        carry = early and self.defer_update and not torch.cuda.is_current_stream_capturing()
+        carried = [0]
         if early:
             # single device: the FC head's and recurrent stack's Adam + EMA range runs on the
             # weight-gradient stream right after the grouped tail GEMMs, beside the conv
@@ -404,10 +454,15 @@ class Trainer:
                 self._early_params)
             if self._layer_first and _EARLY_UPPER:
                 # the head and the layers whose weight gradients ran beside the BPTT (not in the
-                # grouped tail launch): their range goes out beside the next BPTT, on a capped grid
-                sch.set_early_upper(self.upper_range,
-                                    lambda hi, grid: self.opt.apply_range(0, hi, lr_t, keep, gscale, max_grid=grid),
-                                    _UPPER_GRID)
+                # grouped tail launch): their range goes out beside the next BPTT, on a capped grid,
+                # or (defer_update) beside the next step's first recurrence
+                if carry:
+                    def upper(hi, grid):
+                        carried[0] = hi
+                else:
+                    def upper(hi, grid):
+                        self.opt.apply_range(0, hi, lr_t, keep, gscale, max_grid=grid)
+                sch.set_early_upper(self.upper_range, upper, _UPPER_GRID)
         loss.backward(one)
         self.arena.wgrad.join()
         if lazy:
@@ -421,6 +476,8 @@ class Trainer:
                 sch = self.arena.wgrad
                 lo = split if sch.early_done else (sch.early_upper_hi if sch.early_upper_done else 0)
                 self.opt.apply_excluding(lo, self.arena.numel, sch.fused_ranges, lr_t, keep, gscale)
+            if carried[0] > 0:
+                self._carry_update(carried[0], lr_t, keep, gscale)
         elif not per_bucket:
             skip = None
             if self.nan_policy == "skip":
@@ -445,6 +502,7 @@ class Trainer:
 
     # ---- EMA weights for eval (reference evaluates the shadow variables) -------------
     def swap_ema(self) -> None:
+        self.flush()
         if self.opt.ema is None:
             return
         tmp = self.arena.flat.clone()

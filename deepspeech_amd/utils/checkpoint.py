@@ -9,14 +9,19 @@ them: src/deepSpeech_test.py:217-220), BN moving stats.
 
 Here every entry is keyed by its TF variable name and stored in TF orientation (conv
 kernels HWIO), so checkpoints map 1:1 onto the reference graph's variables
-(SURVEY.md §5.4). Files are plain ``torch.save`` dicts of tensors/ints/strings that load
-with ``torch.load(weights_only=True)``. Saving never blocks a GPU training thread
-(CheckpointManager: device snapshot -> side-stream copy into pinned double buffers ->
-writer thread).
+(SURVEY.md §5.4). The default file format is TF's own Saver-V2 tensor bundle
+(``model.ckpt-<step>.index`` + ``model.ckpt-<step>.data-00000-of-00001``, utils/tf_bundle.py):
+``global_step``, ``beta1_power`` / ``beta2_power`` (Adam's non-slot variables), ``<var>/Adam``,
+``<var>/Adam_1`` and ``<var>/ExponentialMovingAverage`` as TF 1.x names them, plus one extra
+``deepspeech_amd/adam_t``. ``fmt="torch"`` writes the earlier single ``torch.save`` file instead;
+restore and eval read either. Saving never blocks a GPU training thread (CheckpointManager:
+device snapshot -> side-stream copy into pinned buffers -> writer thread, which streams the
+bundle's data shard straight from the pinned buffer).
 """
 from __future__ import annotations
 
 import glob
+import math
 import os
 import re
 import threading
@@ -25,6 +30,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 import torch
 
 from ..models.deepspeech2 import DeepSpeech2
+from . import tf_bundle as TB
 
 EMA_SUFFIX = "/ExponentialMovingAverage"
 ADAM_M = "/Adam"
@@ -211,10 +217,14 @@ def latest_checkpoint(directory: str) -> Optional[str]:
                 if m:
                     p = m.group(1)
                     return p if os.path.isabs(p) else os.path.join(directory, p)
-    cands = glob.glob(os.path.join(directory, "model.ckpt-*"))
+    cands = {}
+    for p in glob.glob(os.path.join(directory, "model.ckpt-*")):
+        m = re.match(r"^(.*model\.ckpt-(\d+))(\.index)?$", p)
+        if m:
+            cands[m.group(1)] = int(m.group(2))
     if not cands:
         return None
-    return max(cands, key=lambda p: int(re.findall(r"-(\d+)$", p)[0]) if re.findall(r"-(\d+)$", p) else -1)
+    return max(cands, key=cands.get)
 
 
 def step_from_path(path: str) -> int:
@@ -255,10 +265,18 @@ class CheckpointManager:
     one, had a non-finite loss (the device-side watch, utils/stats.py) is not written.
     CPU trainers (and async_save=False) take the synchronous snapshot() path."""
 
-    def __init__(self, directory: str, max_to_keep: int = 100, async_save: bool = True):
+    def __init__(self, directory: str, max_to_keep: int = 100, async_save: bool = True, fmt: str = "tf",
+                 nan_policy: str = "abort"):
+        if fmt not in ("tf", "torch"):
+            raise ValueError("checkpoint format must be 'tf' (TF Saver-V2 bundle) or 'torch'")
         self.dir = directory
         self.max_to_keep = max_to_keep
         self.async_save = async_save
+        self.fmt = fmt
+        # a save after a non-finite loss is dropped only when that loss ends the run
+        # (nan_policy "abort"); under "skip" the skipped updates left the weights finite
+        self.nan_policy = nan_policy
+        self.dropped: List[int] = []
         self._thread: Optional[threading.Thread] = None
         self._error: Optional[BaseException] = None
         os.makedirs(directory, exist_ok=True)
@@ -277,6 +295,7 @@ class CheckpointManager:
         self._stream = None
         self._d2h_done = None         # event: the last host copy has read the device snapshot
         self.skipped: List[int] = []  # saves requested while the writer was busy (no snapshot)
+        self.write_s: List[float] = []    # seconds per file written (the effective save cadence)
         self.written: List[int] = []
         self._behind = False
 
@@ -304,9 +323,16 @@ class CheckpointManager:
         was skipped because the writer is still busy (GPU, not forced)."""
         name = "model.ckpt-%d" % step
         path = os.path.join(self.dir, name)
+        if hasattr(trainer, "flush"):
+            trainer.flush()       # an optimizer update carried into the next step (Trainer)
         if self.async_save and trainer.arena.flat.is_cuda:
             return path if self._save_async(trainer, step, force) else None
         self.wait()
+        if self.nan_policy == "abort" and hasattr(trainer, "first_nonfinite_step"):
+            bad = trainer.first_nonfinite_step()
+            if bad is not None and bad <= step:
+                self._drop(step, bad)
+                return None
         snap = self.snapshot(trainer)
         if self.async_save:
             self._thread = threading.Thread(target=self._write_guarded, args=(snap, step), daemon=True)
@@ -316,23 +342,35 @@ class CheckpointManager:
         return path
 
     # ---- file writing ----------------------------------------------------------------------
+    def _drop(self, step: int, bad: int) -> None:
+        self.dropped.append(step)
+        print("checkpoint for step %d not written: non-finite loss at step %d (nan_policy abort)" % (step, bad),
+              flush=True)
+
     def _write(self, snap: Dict[str, object], step: int) -> None:
+        import time
+        t0 = time.perf_counter()
         name = "model.ckpt-%d" % step
         path = os.path.join(self.dir, name)
-        tmp = path + ".tmp"
-        torch.save(snap, tmp)
-        os.replace(tmp, path)
+        if self.fmt == "tf":
+            TB.write_bundle(path, bundle_tensors(snap))
+        else:
+            tmp = path + ".tmp"
+            torch.save(snap, tmp)
+            os.replace(tmp, path)
         if name in self.kept:
             self.kept.remove(name)
         self.kept.append(name)
         while len(self.kept) > self.max_to_keep:
-            old = self.kept.pop(0)
-            try:
-                os.remove(os.path.join(self.dir, old))
-            except FileNotFoundError:
-                pass
+            old = os.path.join(self.dir, self.kept.pop(0))
+            for f in [old] + TB.bundle_files(old):
+                try:
+                    os.remove(f)
+                except FileNotFoundError:
+                    pass
         write_state_file(self.dir, name, self.kept)
         self.written.append(step)
+        self.write_s.append(time.perf_counter() - t0)
 
     def _write_guarded(self, snap, step) -> None:
         try:
@@ -432,9 +470,12 @@ class CheckpointManager:
         step = meta.pop("step")
         base = meta.pop("watch_base")
         bad = int(slot.bad[0])
-        if bad >= 0 and base + bad <= step:
-            print("checkpoint for step %d not written: non-finite loss at step %d" % (step, base + bad), flush=True)
+        if self.nan_policy == "abort" and bad >= 0 and base + bad <= step:
+            self._drop(step, base + bad)
             return
+        # the bundle writer streams views of the pinned slot (it is not reused before this job
+        # returns); torch.save would serialise a view's whole storage, so that format copies
+        own = (lambda t: t) if self.fmt == "tf" else (lambda t: t.clone())
         names = {tn: (tf, to_tf) for tf, tn, to_tf, _ in tf_name_map(model)}
         params = dict(model.named_parameters())
         out: Dict[str, object] = {}
@@ -443,10 +484,10 @@ class CheckpointManager:
             tf, to_tf = names[tn]
             shape = params[tn].shape
             for r, suf in enumerate(suffixes):
-                out[tf + suf] = to_tf(slot.flat[r, o:o + n].view(shape)).clone()
+                out[tf + suf] = own(to_tf(slot.flat[r, o:o + n].view(shape)))
         for tf, tn, to_tf, _ in tf_name_map(model):
             if tn in slot.bufs:
-                out[tf] = to_tf(slot.bufs[tn]).clone()
+                out[tf] = own(to_tf(slot.bufs[tn]))
         self._write(self._finish(model, out, meta), step)
 
     def _raise(self):
@@ -484,8 +525,50 @@ def _meta(trainer) -> Dict[str, object]:
             "format": "deepspeech_amd/tfnames/v1"}
 
 
+ADAM_T = "deepspeech_amd/adam_t"
+
+
+def bundle_tensors(snap: Dict[str, object]) -> Dict[str, torch.Tensor]:
+    """Tensors of a TF bundle for a snapshot dict: its tensors plus the scalar variables TF's
+    graph holds (global_step int64, Adam's beta1_power / beta2_power fp32) and adam_t."""
+    out = {k: v for k, v in snap.items() if isinstance(v, torch.Tensor)}
+    if "global_step" in snap:
+        out["global_step"] = torch.tensor(int(snap["global_step"]), dtype=torch.int64)
+    for k in ("beta1_power", "beta2_power"):
+        if k in snap:
+            out[k] = torch.tensor(float(snap[k]), dtype=torch.float32)
+    if "adam_t" in snap:
+        out[ADAM_T] = torch.tensor(int(snap["adam_t"]), dtype=torch.int64)
+    return out
+
+
+def _from_bundle(prefix: str) -> Dict[str, object]:
+    data: Dict[str, object] = dict(TB.read_bundle(prefix))
+    out: Dict[str, object] = {k: v for k, v in data.items()
+                              if k not in ("global_step", "beta1_power", "beta2_power", ADAM_T)}
+    out["format"] = "tf_bundle"
+    if "global_step" in data:
+        out["global_step"] = int(data["global_step"])
+    for k in ("beta1_power", "beta2_power"):
+        if k in data:
+            out[k] = float(data[k])
+    if ADAM_T in data:
+        out["adam_t"] = int(data[ADAM_T])
+    elif "beta1_power" in data and 0.0 < float(data["beta1_power"]) < 1.0:
+        # a TF-written checkpoint: Adam's step count from beta1_power = 0.9^t (default beta1)
+        out["adam_t"] = int(round(math.log(float(data["beta1_power"])) / math.log(0.9)))
+    return out
+
+
 def load_checkpoint_file(path: str) -> Dict[str, object]:
+    """A checkpoint by path or prefix: a TF Saver-V2 bundle (``<path>.index`` exists: ours or
+    TF-written) or a ``torch.save`` file (loaded with weights_only=True)."""
+    if TB.bundle_exists(path):
+        return _from_bundle(path)
     return torch.load(path, map_location="cpu", weights_only=True)
+
+
+read_checkpoint = load_checkpoint_file
 
 
 def restore(trainer, directory_or_file: str) -> Optional[int]:
@@ -497,13 +580,15 @@ def restore(trainer, directory_or_file: str) -> Optional[int]:
             print("No checkpoint file found")
             return None
     data = load_checkpoint_file(path)
+    if hasattr(trainer, "flush"):
+        trainer.flush()          # a carried optimizer update lands before the restored state
     tensors = normalize_layout(trainer.model, {k: v for k, v in data.items() if isinstance(v, torch.Tensor)})
     load_model_from_tf(trainer.model, tensors, strict=True)
     _load_arena_slots(trainer, tensors)
     trainer.arena.mark_dirty()
     step = step_from_path(path)
-    if data.get("format"):
-        # snapshot() stores trainer.global_step as it stood after the saved step
+    if data.get("format") and "global_step" in data:
+        # snapshot() (and TF's Saver, whose global_step apply_gradients already advanced) stores trainer.global_step as it stood after the saved step
         # (Trainer.step already counted it), i.e. the index of the next step to run
         trainer.global_step = int(data["global_step"])
     else:

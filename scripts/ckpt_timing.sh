@@ -16,6 +16,7 @@ for r in $(seq 1 "${ROUNDS}"); do
       --num_hidden 800 --cell gru --max_steps "${STEPS}" --checkpoint_every "${every}" --max_to_keep 3 \
       --train_dir "${d}" ${EXTRA} > "${OUT}/every${every}_r${r}.log" 2>&1
     echo "checkpoint_every=${every} round ${r}: $(grep -E 'audio-sec/sec' "${OUT}/every${every}_r${r}.log" | tail -n 1)"
-    echo "  files: $(ls ${d} | grep -c model.ckpt) checkpoints kept; $(grep -c 'skipping saves' "${OUT}/every${every}_r${r}.log" || true) stretches of saves skipped while the writer was busy"
+    echo "  files: $(ls ${d} | grep -c 'model.ckpt.*index') checkpoints kept; $(grep -c 'skipping saves' "${OUT}/every${every}_r${r}.log" || true) stretches of saves skipped while the writer was busy"
+    python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if 'checkpoint_summary' in l]; print('  cadence:', r[-1] if r else 'no checkpoint written')" "${d}/metrics.jsonl"
   done
 done

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 6: optimizer update carried into the next forward (Trainer defer_update).
+# Tests, same-box A/B against the in-step update, then a kernel-trace profile + timeline.
+set -o pipefail
+out=gpurun_out/r6_defer
+mkdir -p $out
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_defer_update_gpu.py \
+  > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
+tail -5 $out/tests.log
+for r in 1 2 3; do
+  for a in "" "--no_defer_update"; do
+    o=$(timeout -k 10 150 python bench.py --steps 30 --warmup 10 --no_infer --no_walk $a | tail -1) || exit 1
+    echo "defer${a:+ off} $(echo "$o" | grep -o '"ms_per_step": [0-9.]*')" | tee -a $out/ab.txt
+  done
+done
+timeout -k 10 300 bash scripts/rocprof.sh $out/prof 8 -- python3 bench.py --steps 5 --warmup 3 --no_infer --no_walk > $out/prof.log 2>&1 || exit 1
+db=$(ls $out/prof/*.db | head -1)
+python3 tools/rocpd_timeline.py $db --index 5 --phases > $out/timeline.txt 2>&1 || exit 1
+tail -30 $out/timeline.txt

@@ -83,19 +83,30 @@ def test_tf_names_and_orientation(cell):
     assert tuple(names["softmax_linear/weights"].shape) == (29, 16)
 
 
-def test_checkpoint_roundtrip_and_state_file(tmp_path):
+@pytest.mark.parametrize("fmt", ["tf", "torch"])
+def test_checkpoint_roundtrip_and_state_file(tmp_path, fmt):
     t = _trainer()
     b = _batch()
     for _ in range(3):
         t.step(b)
-    mgr = CK.CheckpointManager(str(tmp_path), max_to_keep=2, async_save=True)
+    mgr = CK.CheckpointManager(str(tmp_path), max_to_keep=2, async_save=True, fmt=fmt)
     for s in (1, 2, 3):
         mgr.save(t, s)
     mgr.wait()
     files = sorted(os.listdir(tmp_path))
-    assert "model.ckpt-1" not in files and "model.ckpt-3" in files and "checkpoint" in files
+    if fmt == "tf":
+        # TF Saver-V2 layout: <prefix>.index + <prefix>.data-00000-of-00001, old ones deleted
+        assert "model.ckpt-3.index" in files and "model.ckpt-3.data-00000-of-00001" in files
+        assert not any(f.startswith("model.ckpt-1") for f in files) and "checkpoint" in files
+        from deepspeech_amd.utils import tf_bundle as TB
+        raw = TB.read_bundle(str(tmp_path / "model.ckpt-3"))
+        assert raw["global_step"].dtype == torch.int64 and int(raw["global_step"]) == 3
+        assert abs(float(raw["beta1_power"]) - 0.9 ** 3) < 1e-7
+        data = CK.load_checkpoint_file(str(tmp_path / "model.ckpt-3"))
+    else:
+        assert "model.ckpt-1" not in files and "model.ckpt-3" in files and "checkpoint" in files
+        data = torch.load(str(tmp_path / "model.ckpt-3"), weights_only=True)
     assert CK.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-3")
-    data = torch.load(str(tmp_path / "model.ckpt-3"), weights_only=True)
     assert "conv1/weights/ExponentialMovingAverage" in data and "conv1/weights/Adam" in data
     # restore into a fresh trainer: identical weights, slots and continued trajectory
     t2 = _trainer()

@@ -121,7 +121,9 @@ def test_resume_auto_continues_instead_of_wiping(tmp_path):
     # metrics rows are written at log / summary steps and the last step (checkpoint steps no
     # longer synchronise the host): the first run's last row is step 3, the second run appends
     # to the same file (not wiped) and its rows start after it
-    steps = [json.loads(l)["step"] for l in open(os.path.join(d, "metrics.jsonl"))]
+    rows = [json.loads(l) for l in open(os.path.join(d, "metrics.jsonl"))]
+    steps = [r["step"] for r in rows if "event" not in r]        # checkpoint events are extra rows
+    assert any(r.get("event") == "checkpoint_summary" and r["checkpoints_written"] >= 1 for r in rows)
     assert steps[0] == 3 and steps[-1] == 5 and sorted(steps) == steps and steps.count(3) == 1
 
 
