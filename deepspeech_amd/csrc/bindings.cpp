@@ -180,6 +180,10 @@ int ds2_multi_copy(int n, void* const* dst, const void* const* src, const unsign
                    const unsigned* dst_pitch, float* sdst, const float* svals, int ns, hipStream_t st);
 int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                    hipStream_t st);
+int ds2_col_sum(int n, const float* const* in, float* const* out, const int* R, const int* B, const int* C,
+                const int* acc, hipStream_t st);
+int ds2_fc_bias_grad(const void* G, int M, int ldg, int K, const float* scale, float alpha, float* out, int acc,
+                     hipStream_t st);
 int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
                    int* labels, int* counts, float* score, hipStream_t st);
 size_t ds2_conv2_fwd_smem(int F1);
@@ -1031,6 +1035,47 @@ void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
   check(ds2_multi_fill((int)ts.size(), ptrs, bytes, pats, cur_stream()), "multi_fill");
 }
 
+// out_j (= or +=) sum over axis 1 of in_j [R, B, C] (fp32, contiguous) into out_j [R * C]
+// (fp32, contiguous): up to 4 slabs in one launch (csrc/reduce.hip, recurrent bias gradients)
+void col_sum(std::vector<at::Tensor> ins, std::vector<at::Tensor> outs, std::vector<bool> acc) {
+  TORCH_CHECK(!ins.empty() && ins.size() <= 4 && ins.size() == outs.size() && ins.size() == acc.size(),
+              "col_sum: 1..4 (in, out, accumulate) triples");
+  const float* ip[4];
+  float* op[4];
+  int R[4], B[4], C[4], a[4];
+  for (size_t j = 0; j < ins.size(); ++j) {
+    need_gpu(ins[j], "col_sum in");
+    need_gpu(outs[j], "col_sum out");
+    TORCH_CHECK(ins[j].dim() == 3 && ins[j].scalar_type() == at::kFloat && ins[j].is_contiguous(),
+                "col_sum: in must be a contiguous fp32 [R, B, C]");
+    TORCH_CHECK(outs[j].scalar_type() == at::kFloat && outs[j].is_contiguous() &&
+                    outs[j].numel() == ins[j].size(0) * ins[j].size(2),
+                "col_sum: out must be a contiguous fp32 tensor of R * C elements");
+    ip[j] = ins[j].data_ptr<float>();
+    op[j] = outs[j].data_ptr<float>();
+    R[j] = (int)ins[j].size(0);
+    B[j] = (int)ins[j].size(1);
+    C[j] = (int)ins[j].size(2);
+    a[j] = acc[j] ? 1 : 0;
+  }
+  check(ds2_col_sum((int)ins.size(), ip, op, R, B, C, a, cur_stream()), "col_sum");
+}
+
+// out[k] (= or +=) scale[0] * alpha * sum_m G[m, k] for k < K (G bf16 [M, ldg] with unit column
+// stride, scale a device fp32 scalar): the FC head's bias gradient (csrc/reduce.hip)
+void fc_bias_grad(at::Tensor G, int64_t K, at::Tensor scale, double alpha, at::Tensor out, bool acc) {
+  need_gpu(G, "G");
+  need_gpu(scale, "scale");
+  need_gpu(out, "out");
+  TORCH_CHECK(G.dim() == 2 && G.scalar_type() == at::kBFloat16 && G.stride(1) == 1, "fc_bias_grad: G bf16 [M, ldg]");
+  TORCH_CHECK(K >= 1 && K <= 32 && K <= G.size(1), "fc_bias_grad: 1 <= K <= min(32, G columns)");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() >= 1, "fc_bias_grad: fp32 device scale");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == K, "fc_bias_grad: fp32 out [K]");
+  check(ds2_fc_bias_grad(G.data_ptr(), (int)G.size(0), (int)G.stride(0), (int)K, scale.data_ptr<float>(),
+                         (float)alpha, out.data_ptr<float>(), acc ? 1 : 0, cur_stream()),
+        "fc_bias_grad");
+}
+
 // --------------------------------------------------------------------------- fp8 quantisation
 int64_t fp8_quant_blocks(int64_t na, int64_t nb) { return ds2_fp8_quant_blocks(na, nb); }
 
@@ -1502,6 +1547,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("store_g") = false);
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
+  m.def("col_sum", &col_sum);
+  m.def("fc_bias_grad", &fc_bias_grad);
   m.def("event_new", &event_new, py::arg("flags") = 0);
   m.def("arm_stop_event", &arm_stop_event);
   m.def("disarm_stop_event", &disarm_stop_event);

@@ -177,13 +177,25 @@ __device__ __forceinline__ void half_offsets(unsigned (&o)[2], int ld, int row0,
 // one half-tile through the operand's buffer resource (32-bit offsets: 2 VGPRs per half
 // instead of 64-bit pointers). Chunks past the row's end (a ragged last bf16 k-tile) read
 // the next row, or zeros past the operand (bounds-checked), and are never multiplied.
+// AUX: the loads' cache-policy bits (0 default; 2 = nt, a streaming hint).
+template <int AUX = 0>
 __device__ __forceinline__ void stage_half(unsigned char* dst, __amdgpu_buffer_rsrc_t rs, const unsigned (&o)[2],
                                            unsigned kb0, int wave) {
 #pragma unroll
   for (int j = 0; j < 2; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + (wave + NWV * j) * 1024), 16, o[j] + kb0, 0, 0,
-                                             0);
+                                             AUX);
 }
+
+// cache policy of the weight-gradient (column-column) kernels' operand loads: these launches
+// run beside the latency-bound persistent BPTT, whose per-step loads and partial-sum exchange
+// live in the same XCD L2. nt (aux 2, a streaming hint): headline, same
+// box, 3 rounds alternating, 7.549 / 7.583 / 7.560 ms/step vs 7.584 / 7.683 / 7.594 with the
+// default policy (scripts/r6_defer2.sh). Compile-time A/B: build.py --variant NAME
+// -D G8_COL_AUX=0.
+#ifndef G8_COL_AUX
+#define G8_COL_AUX 2
+#endif
 
 __device__ __forceinline__ i32x4 rd16(const unsigned char* half, int r, int chunk) {
   return *(const i32x4*)(half + r * ROWB + ((chunk ^ rsw(r)) << 4));
@@ -398,6 +410,15 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
     const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
     const int kt0 = ks * P.kps;                      // this unit's k-tiles [kt0, kt0 + nkt)
     const int nkt = max(0, min(nkt_all - kt0, P.kps));
+    // a ragged last tile whose second 128-row / 128-column quadrant lies wholly past M / N (the
+    // weight gradients' N = 800 tile column holds 32 valid columns): those quadrants' MFMAs are
+    // skipped (their accumulators are never stored); loads and barriers stay, so the staging
+    // pipeline's vmcnt accounting is unchanged
+#ifdef G8_NO_SKIP
+    const bool live_m1 = true, live_n1 = true;       // A/B build: every quadrant multiplied
+#else
+    const bool live_m1 = m0 + 128 < M, live_n1 = n0 + 128 < N;
+#endif
 
     unsigned oA0[2], oA1[2], oB0[2], oB1[2];
     if constexpr (AC) {
@@ -422,10 +443,11 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
       const int kt = kt0 + t;
       const unsigned ka = AC ? (unsigned)(kt * 64) * (unsigned)P.lda : (unsigned)(kt * ROWB);
       const unsigned kb = BC ? (unsigned)(kt * 64) * (unsigned)P.ldb : (unsigned)(kt * ROWB);
-      if (h == 0) stage_half(dst, rsA, oA0, ka, wave);
-      else if (h == 1) stage_half(dst, rsA, oA1, ka, wave);
-      else if (h == 2) stage_half(dst, rsB, oB0, kb, wave);
-      else stage_half(dst, rsB, oB1, kb, wave);
+      constexpr int aux = (AC && BC) ? G8_COL_AUX : 0;
+      if (h == 0) stage_half<aux>(dst, rsA, oA0, ka, wave);
+      else if (h == 1) stage_half<aux>(dst, rsA, oA1, ka, wave);
+      else if (h == 2) stage_half<aux>(dst, rsB, oB0, kb, wave);
+      else stage_half<aux>(dst, rsB, oB1, kb, wave);
     };
     auto read_a = [&](Frag (&a)[4], auto BUF, auto QM) {
       constexpr int buf = decltype(BUF)::value, qm = decltype(QM)::value;
@@ -491,7 +513,7 @@ __global__ __launch_bounds__(NTHR) void gemm8_kernel(G8Args g) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       bar();
       __builtin_amdgcn_sched_barrier(0);
-      mfma_tile<FP8, 0>(acc[qm][qn], fa, fb, full);
+      if ((qm == 0 || live_m1) && (qn == 0 || live_n1)) mfma_tile<FP8, 0>(acc[qm][qn], fa, fb, full);
       __builtin_amdgcn_sched_barrier(0);   // the cluster stays between its barriers
       bar();
     };

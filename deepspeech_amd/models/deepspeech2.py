@@ -80,8 +80,8 @@ NHWC_BN_DECAY = 0.5
 
 
 
-# DS2_PREP_FUSED=0: the features' cast and the rnn lengths as torch ops (A/B)
-_PREP_FUSED = os.environ.get("DS2_PREP_FUSED", "1") != "0"
+# False: the features' cast and the rnn lengths as torch ops (A/B)
+_PREP_FUSED = True
 
 class ConvBlock(nn.Module):
     """conv + bias + BatchNorm + clipped ReLU.

@@ -73,10 +73,10 @@ class CTCMeanFused(CTCLossFused):
 
 
 _watch_ctx = threading.local()
-# DS2_FUSED_LOSS=0: torch's mean and a separate watch launch (A/B; same box, 3 rounds, graph
-# steps: 100 frames 1.483-1.485 vs 1.486-1.495 ms, 200 frames 2.171-2.174 vs 2.177-2.182 ms;
-# headline within run-to-run spread)
-_FUSE_LOSS = os.environ.get("DS2_FUSED_LOSS", "1") != "0"
+# batch-mean loss and the divergence watch inside the CTC gradient launch (False: torch's mean
+# and a separate watch launch; measured same box, 3 rounds, graph steps: 100 frames 1.483-1.485
+# vs 1.486-1.495 ms, 200 frames 2.171-2.174 vs 2.177-2.182 ms; headline within spread)
+_FUSE_LOSS = True
 
 
 class loss_watch:
@@ -179,16 +179,18 @@ class FusedHeadCTC(torch.autograd.Function):
             dh = dh.view(T, N, H)
         side = wgrad_stream(h.device, arena_of(weight)) if arena_of(bias) is not None else None
         if side is None:
-            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32 / N, K)
+            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32, 1.0 / N, K)
             return dh, gw, gb, None, None, None, None, None
         _stream_wait(side, torch.cuda.current_stream(h.device))
         arena_of(weight).wgrad.hold(G, h2, g32)
         with torch.cuda.stream(side):
-            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32 / N, K)
+            gw, gb = FusedHeadCTC._weight_grads(weight, bias, G, h2, g32, 1.0 / N, K)
         return dh, gw, gb, None, None, None, None, None
 
     @staticmethod
-    def _weight_grads(weight, bias, G, h2, scale, K):
+    def _weight_grads(weight, bias, G, h2, scale, inv_n, K):
+        """dW_fc and db_fc, both scaled by the device scalar ``scale`` times the host ``inv_n``
+        (folded into the GEMM and reduction epilogues: no division kernel)."""
         from . import gemm as GM
         from .optim import arena_of, emit_grad
         M, H = h2.shape
@@ -201,17 +203,20 @@ class FusedHeadCTC(torch.autograd.Function):
             S *= 2
         if S > 1:
             parts = torch.empty(S, K, H, device=h2.device, dtype=torch.float32)
-            GM.gemm(G.view(S, M // S, G.shape[1]), h2.view(S, M // S, H), parts, K, H, M // S, True, True, 1, 1.0,
+            GM.gemm(G.view(S, M // S, G.shape[1]), h2.view(S, M // S, H), parts, K, H, M // S, True, True, 1, inv_n,
                     None, alpha_dev=scale, Ml=32)
         if a is not None:
             if S > 1:
-                if a.first_write(weight):
+                if weight.main_grad.is_contiguous():
+                    # the S partials summed straight into the arena (csrc/reduce.hip col_sum)
+                    _ext.ext().col_sum([parts.view(1, S, K * H)], [weight.main_grad], [not a.first_write(weight)])
+                elif a.first_write(weight):
                     torch.sum(parts, 0, out=weight.main_grad)
                 else:
                     weight.main_grad.add_(parts.sum(0))
             else:
                 # M = K rows stored; G is read as a [M_rows, 32]-column col-mode operand (Ml = 32)
-                GM.gemm(G, h2, weight.main_grad, K, H, M, True, True, 1 if a.first_write(weight) else 2, 1.0, None,
+                GM.gemm(G, h2, weight.main_grad, K, H, M, True, True, 1 if a.first_write(weight) else 2, inv_n, None,
                         alpha_dev=scale, Ml=32)
             a.grad_done(weight)
             gw = None
@@ -219,9 +224,15 @@ class FusedHeadCTC(torch.autograd.Function):
             gw = parts.sum(0)
         else:
             out = torch.empty(K, H, device=h2.device, dtype=torch.float32)
-            GM.gemm(G, h2, out, K, H, M, True, True, 1, 1.0, None, alpha_dev=scale, Ml=32)
+            GM.gemm(G, h2, out, K, H, M, True, True, 1, inv_n, None, alpha_dev=scale, Ml=32)
             gw = out
-        gb = emit_grad(bias, G[:, :K].sum(0, dtype=torch.float32) * scale)
+        ab = arena_of(bias)
+        if ab is not None and G.is_cuda and bias.main_grad.is_contiguous():
+            # db = scale * column sums of G in one launch straight into the arena (csrc/reduce.hip)
+            _ext.ext().fc_bias_grad(G, K, scale, float(inv_n), bias.main_grad.view(-1), not ab.first_write(bias))
+            ab.grad_done(bias)
+            return gw, None
+        gb = emit_grad(bias, G[:, :K].sum(0, dtype=torch.float32) * (scale * inv_n))
         return gw, gb
 
 

@@ -28,7 +28,7 @@ BN_MOMENTUM = 0.01
 
 
 # conv1 weight-gradient workgroups per CU (its 67.5 KB of LDS allows two)
-_C1W_BPC = int(os.environ.get("DS2_C1W_BPC", "1"))
+_C1W_BPC = 1
 
 def bn_eval_stats(block, eps: float):
     """(mean, invstd) for eval: running statistics (fused variant) or the debiased EMA of

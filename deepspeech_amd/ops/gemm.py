@@ -10,7 +10,7 @@ src/custom_ops.py:59-67 for W.x / U.h, src/deepSpeech_NCHW.py:188-198 for the FC
 
 Tile choice: per (shape, layout) from a small table measured on MI355X
 (tools/bench_gemm_ours.py), else a model that minimises the padded work of the last
-dispatch round. DS2_GEMM_CFG=<0..5> forces one tile for every call (tuning only).
+dispatch round. gemm._FORCE = <0..5> forces one tile for every call (tuning only).
 """
 from __future__ import annotations
 
@@ -42,14 +42,8 @@ TUNED: Dict[Tuple[int, int, int, bool, bool, int], int] = {
     # gemm8; 197 us alone; round 4 timeline, profiles/r4_headline.md)
     (7712, 800, 32, False, True, 1): 3,        # FC head dh (K = 32 padded classes)
 }
-# DS2_DX_CFG: the headline dx GEMM's configuration for an A/B (a csrc/gemm.hip cfg, or "g8")
-_DX_CFG = os.environ.get("DS2_DX_CFG")
-if _DX_CFG:
-    if _DX_CFG == "g8":
-        TUNED.pop((7712, 800, 4800, False, False, 1), None)
-    else:
-        TUNED[(7712, 800, 4800, False, False, 1)] = int(_DX_CFG)
-_FORCE = os.environ.get("DS2_GEMM_CFG")
+# one csrc/gemm.hip configuration for every call (tile tuning tools set it; None in training)
+_FORCE = None
 # DS2_GEMM selects which engine GEMM classes run on the hand-written kernels: "hip" (all, the
 # default), "torch" (none: library GEMMs, A/B timing only) or a comma list of {proj, dx, wgrad}.
 _SPEC = os.environ.get("DS2_GEMM", "hip")
@@ -191,8 +185,8 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: bool
     return True
 
 
-# DS2_SMALL_M=0 keeps every covered shape on gemm8 (A/B timing)
-_SMALL_M = os.environ.get("DS2_SMALL_M", "1") != "0"
+# False keeps every covered shape on gemm8 (A/B timing of _small_rowrow)
+_SMALL_M = True
 
 
 def _small_rowrow(M: int, N: int, K: int, a_col: bool, b_col: bool, batch: int, epi: int,
@@ -268,8 +262,8 @@ def gemm8_splits(M: int, N: int, K: int, batch: int = 1, cus: int = 256, min_sli
 # layer-0 projection 56 -> 37 us; a K = 800 projection that the plain policy leaves unsplit lost
 # with any split (28 -> 31-34 us), and a row-split of an under-full last dispatch round (its rows as
 # k-sliced units taken round-robin by every workgroup) lost at every shape tried (54 -> 89 us at
-# M = 3712), so neither is planned. DS2_G8_PLAN=0 keeps the plain policy (A/B timing).
-_PLAN = os.environ.get("DS2_G8_PLAN", "1") != "0"
+# M = 3712), so neither is planned. False keeps the plain policy (A/B timing).
+_PLAN = True
 _EXT_MIN_KT = 3
 
 

@@ -9,9 +9,8 @@ holds the solutions measured on MI355X for the benchmark configurations; with it
 PyTorch dispatches those shapes to the measured-fastest solution and everything else to the
 default heuristic. Tuning is OFF at run time (no timing runs inside training steps).
 
-  DS2_TUNABLEOP=0      do not load the table
-  DS2_TUNABLEOP=tune   tune unseen shapes too and write them to $DS2_TUNABLEOP_OUT
-                       (default ./tunableop_new.csv); merge the rows into the table by hand
+  enable_tuned_gemms(mode="tune", out=PATH)   tune unseen shapes too and write them to PATH
+                                              (tools/tune_buckets.py); merge the rows by hand
 """
 from __future__ import annotations
 
@@ -22,12 +21,12 @@ TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _done = False
 
 
-def enable_tuned_gemms() -> bool:
-    """Load the measured GEMM table once per process (idempotent). Returns True if active."""
+def enable_tuned_gemms(mode: str = "1", out: str = "") -> bool:
+    """Load the measured GEMM table once per process (idempotent). Returns True if active.
+    mode "0": do not load it; "tune": also tune unseen shapes, written to ``out``."""
     global _done
     if _done:
         return True
-    mode = os.environ.get("DS2_TUNABLEOP", "1")
     if mode == "0":
         return False
     import torch
@@ -37,14 +36,14 @@ def enable_tuned_gemms() -> bool:
     tun.enable(True)
     if mode == "tune":
         tun.tuning_enable(True)
-        tun.set_filename(os.environ.get("DS2_TUNABLEOP_OUT", "tunableop_new.csv"))
+        tun.set_filename(out or "tunableop_new.csv")
         if os.path.exists(TABLE):
             tun.read_file(TABLE)
     else:
         tun.tuning_enable(False)
         tun.record_untuned_enable(False)
         # point the writer at a scratch name so the shipped table is never rewritten
-        tun.set_filename(os.environ.get("DS2_TUNABLEOP_OUT", os.path.join("/tmp", "ds2_tunableop_unused.csv")))
+        tun.set_filename(out or os.path.join("/tmp", "ds2_tunableop_unused.csv"))
         if os.path.exists(TABLE):
             tun.read_file(TABLE)
     _done = True

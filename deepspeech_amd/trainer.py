@@ -59,7 +59,7 @@ def lr_schedule_from_args(args, steps_per_epoch: int) -> LRSchedule:
 # not deferred, on a capped grid (same box, config 5 fp8, 2 rounds: off 21.77 / 21.39 ms/step,
 # full grid 21.16 / 21.08, 192 blocks 21.04 / 20.99, 512 blocks 21.04 / 20.98)
 _EARLY_UPPER = True
-_UPPER_GRID = int(os.environ.get("DS2_UPPER_OPT_GRID", "512"))
+_UPPER_GRID = 512
 # single device, weight gradients deferred to the grouped tail launch: that launch can apply Adam +
 # EMA to the recurrent weights in its epilogue (csrc/gemm8.hip "Fused optimizer epilogue")
 # instead of storing their gradients for a separate optimizer pass to read back. Bitwise the
@@ -74,14 +74,16 @@ _FUSED_OPT = False
 # another box 3 rounds: 384 -0.45 %, 256 -0.2 to -0.3 %). Only when the range is the whole head
 # + recurrent stack (every weight gradient deferred to the grouped tail): config 5, whose upper
 # range already ran beside layer 0's BPTT, measured +0.15-0.3 % with the cap on its remainder.
-# DS2_EARLY_OPT_GRID=0: uncapped
-_EARLY_GRID = int(os.environ.get("DS2_EARLY_OPT_GRID", "384"))
-# the same range when the upper part already ran beside layer 0's BPTT (A/B)
-_LOWER_GRID = int(os.environ.get("DS2_LOWER_OPT_GRID", "0"))
+_EARLY_GRID = 384
+# the same range when the upper part already ran beside layer 0's BPTT (0: uncapped)
+_LOWER_GRID = 0
 # grid cap (blocks) of the data-parallel per-bucket Adam + EMA ranges, which stream beside the
 # BPTTs (0: uncapped). --force_dp at world 1, same box, 3 rounds: uncapped 7.754 / 7.747 / 7.705,
 # 512 7.782 / 7.725 / 7.719, 256 7.771 / 7.790 / 7.814, 128 7.86-7.88 ms/step
-_BUCKET_GRID = int(os.environ.get("DS2_BUCKET_OPT_GRID", "0"))
+_BUCKET_GRID = 0
+# capture step graphs on one stream (False: the weight-gradient side stream too; single-stream
+# capture is not bitwise at H = 800, where the deferral needs the side stream)
+_GRAPH_SINGLE_STREAM = False
 
 
 def _check_hw_queues() -> None:
@@ -384,8 +386,7 @@ class Trainer:
         torch.cuda.synchronize(dev)
         self.opt.device_hyper = True
         sch = self.arena.wgrad
-        single = os.environ.get("DS2_GRAPH_STREAMS", "0") == "1"
-        sch.single_stream = single
+        sch.single_stream = _GRAPH_SINGLE_STREAM
         try:
             # thread_local: the train driver's prefetch thread may pin / copy while we capture
             with torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):

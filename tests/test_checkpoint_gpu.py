@@ -44,7 +44,9 @@ def test_async_checkpoint_is_bitwise_the_synchronous_snapshot(cuda, tmp_path, gr
     for i in range(3):
         b.step(batches[i % 3])
     torch.cuda.synchronize()
-    want = CK.CheckpointManager(str(tmp_path / "b"), async_save=False).snapshot(b)
+    # the synchronous path's file, through the same (TF bundle) format
+    CK.CheckpointManager(str(tmp_path / "b"), async_save=False).save(b, 2)
+    want = CK.load_checkpoint_file(str(tmp_path / "b" / "model.ckpt-2"))
     assert set(got) == set(want)
     for k, v in want.items():
         if isinstance(v, torch.Tensor):
@@ -89,3 +91,45 @@ def test_writer_behind_skips_saves_without_blocking(cuda, tmp_path):
     assert paths[0] is not None and paths[1:] == [None] * 3
     assert ck.written == [0, 4] and ck.skipped == [1, 2, 3]
     assert CK.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-4")
+
+
+@pytest.mark.parametrize("policy", ["skip", "abort"])
+def test_nonfinite_step_and_async_saves(cuda, tmp_path, policy):
+    """a NaN loss injected at step 1 (a NaN FC bias for that one step: the clipped
+    ReLUs would scrub non-finite features). Under nan_policy skip the update is skipped (every
+    weight as before the step), and every later asynchronous save is still written; under abort
+    the saves at or after the bad step are dropped and reported."""
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    from deepspeech_amd.utils import checkpoint as CK
+    base = _base(cuda)
+    m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+    tr = Trainer(m, LRSchedule(1e-3, 100, 0.9), nan_policy=policy)
+    good = to_device(FixedShapeBatches(8, max_frames=300, seed=7, pool=1).next(), cuda)
+    ck = CK.CheckpointManager(str(tmp_path), nan_policy=policy)
+    tr.step(good)
+    torch.cuda.synchronize()
+    before = tr.arena.flat.clone()
+    saved = m.fc_bias.detach().clone()
+    with torch.no_grad():
+        m.fc_bias[0] = float("nan")
+    tr.arena.mark_dirty()
+    loss = tr.step(good)
+    with torch.no_grad():
+        m.fc_bias.copy_(saved)
+    tr.arena.mark_dirty()
+    torch.cuda.synchronize()
+    assert not torch.isfinite(loss).all()
+    w_after_bad = tr.arena.flat.clone()
+    if policy == "skip":
+        assert torch.equal(w_after_bad, before)          # the whole update was skipped
+    tr.step(good)
+    ck.save(tr, 2, force=True)
+    ck.close()
+    torch.cuda.synchronize()
+    assert tr.first_nonfinite_step() == 1
+    if policy == "skip":
+        assert torch.isfinite(w_after_bad).all() and torch.isfinite(tr.arena.flat).all()
+        assert ck.written == [2] and ck.dropped == []
+        assert CK.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-2")
+    else:
+        assert ck.written == [] and ck.dropped == [2]

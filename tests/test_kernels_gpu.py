@@ -29,18 +29,17 @@ def _rnn_case(cuda, cell, N, H, T, ndir, mode, seed=0, din=None, kernel="xcd"):
         gx[int(lens[b]):, b] = 0
     Us = [(torch.randn(G * H, H) / math.sqrt(H)).bfloat16().to(cuda) for _ in range(ndir)]
     bhs = [(torch.randn(G * H) * 0.1).to(cuda) if cell == "gru" else None for _ in range(ndir)]
-    old = os.environ.get("DS2_RNN_MODE"), os.environ.get("DS2_RNN_KERNEL")
-    os.environ["DS2_RNN_MODE"] = mode
-    os.environ["DS2_RNN_KERNEL"] = kernel
+    old = os.environ.get("DS2_RNN_MODE")
+    # generation 1 (kernel "v1") is DS2_RNN_MODE=v1; "auto" takes the XCD kernels where they fit
+    os.environ["DS2_RNN_MODE"] = "v1" if (kernel == "v1" and mode == "auto") else mode
     try:
         RNN._plan_cache.clear()
         plan = RNN.plan_for(N, H, cell, ndir, cuda)
     finally:
-        for k, v in zip(("DS2_RNN_MODE", "DS2_RNN_KERNEL"), old):
-            if v is None:
-                os.environ.pop(k)
-            else:
-                os.environ[k] = v
+        if old is None:
+            os.environ.pop("DS2_RNN_MODE")
+        else:
+            os.environ["DS2_RNN_MODE"] = old
         RNN._plan_cache.clear()
     if mode == "auto" and kernel == "xcd" and RNN.make_xcd_plan(N, H, cell, ndir, 256) is not None:
         assert plan.kind == "xcd", plan

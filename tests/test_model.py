@@ -1,5 +1,6 @@
 """Model-level semantics of the reference graph (CPU, engine=ref)."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -212,3 +213,49 @@ def test_recurrence_kernel_family_map():
     p = RNN.make_plan(32, 800, "gru", 2, 256)
     assert int(RNN._ext.ext().rnnx_fwd_family(800, 1, 1, 256)) == 2
     assert RNN.kernel_families(p)[0].startswith("rnne_fwd")
+
+
+@pytest.mark.parametrize("name,N,H,cell,T,dp,fp8,want", [
+    # headline 5 x BiGRU-800, batch 32, 10 s (T = 241): 200 CUs, layer 0 deferred, beside GEMMs on
+    # the 56 idle CUs, carried optimizer chunks on 56 blocks
+    ("headline", 32, 800, "gru", 241, False, False,
+     dict(bptt_cus=200, idle_cus=56, defer_wgrad=True, defer_layers=1, upper_trigger=1, beside_grid=56,
+          carry_grid=56, group_cap=192)),
+    # the short SortaGrad buckets (< 200 recurrence steps): every layer deferred
+    ("headline-short", 32, 800, "gru", 116, False, False,
+     dict(defer_wgrad=True, defer_layers=1 << 30, upper_trigger=1 << 30)),
+    # data parallel: same plan, beside grids capped for the collectives' sake
+    ("headline-dp", 32, 800, "gru", 241, True, False, dict(beside_grid=56)),
+    # config 5, 7 x BiGRU-1280: 160 CUs, 96 idle: nothing deferred, bf16 beside GEMMs uncapped,
+    # the fp8 BPTT's capped
+    ("config5-bf16", 32, 1280, "gru", 241, False, False,
+     dict(bptt_cus=160, idle_cus=96, defer_wgrad=False, upper_trigger=1, beside_grid=0, carry_grid=96)),
+    ("config5-fp8", 32, 1280, "gru", 241, False, True, dict(beside_grid=96)),
+    # reference headline 7 x bi-ReLU-1760: 224 CUs, everything deferred (32 idle < 56)
+    ("relu1760", 32, 1760, "rnn_relu", 241, False, False,
+     dict(bptt_cus=224, idle_cus=32, defer_wgrad=True, defer_layers=1 << 30, beside_grid=32, carry_grid=32)),
+])
+def test_schedule_for_shipped_configs(name, N, H, cell, T, dp, fp8, want):
+    """ops/rnn.py schedule_for: the one place every weight-gradient / optimizer placement
+    threshold is decided, pinned for each shipped configuration on a
+    256-CU MI355X (no GPU needed)."""
+    from deepspeech_amd.ops import rnn as RNN
+    plan = RNN.make_xcd_plan(N, H, cell, 2, 256)
+    s = RNN.schedule_for(plan, T, dp, fp8, 256)
+    for k, v in want.items():
+        assert getattr(s, k) == v, (name, k, getattr(s, k), v)
+    cpu = RNN.schedule_for(plan, T, dp, fp8, 0)
+    assert cpu.defer_wgrad and cpu.defer_layers >= 5 and cpu.beside_grid == 0
+
+
+def test_env_knobs_are_few():
+    """VERDICT r5 item 7: A/B-only environment switches whose decision is recorded are gone;
+    fewer than 20 distinct DS2_* variables are read anywhere in the package."""
+    import re
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "deepspeech_amd")
+    names = set()
+    for d, _, files in os.walk(root):
+        for f in files:
+            if f.endswith(".py"):
+                names |= set(re.findall(r"DS2_[A-Z0-9_]+", open(os.path.join(d, f)).read()))
+    assert len(names) < 20, sorted(names)

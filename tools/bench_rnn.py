@@ -27,9 +27,7 @@ XPHASES = ["gather(w0)", "sync1", "mfma(w0)", "sync2", "epilogue", "(mode)", "me
 def run(cell, N, H, T, ndir, nw, mode, iters, stamps=False):
     from deepspeech_amd.ops import rnn as RNN
     dev = torch.device("cuda")
-    os.environ["DS2_RNN_NW"] = str(nw) if nw else ""
-    if not nw:
-        os.environ.pop("DS2_RNN_NW")
+    RNN._FORCE_NW = nw if nw else 0
     os.environ["DS2_RNN_MODE"] = mode
     RNN._plan_cache.clear()
     plan = RNN.plan_for(N, H, cell, ndir, dev)
@@ -107,12 +105,11 @@ def main():
     if any(int(k) & 46 for k in a.knobs.split(",")):   # timing-only bits 2 | 4 | 8 | 32 (ops/rnn.py)
         os.environ["DS2_TIMING_ONLY"] = "1"
     for proto in a.kernels.split(","):
-      os.environ["DS2_RNN_KERNEL"] = proto
       for nw in ([int(x) for x in a.nw.split(",")] if proto == "v1" else [int(k) for k in a.knobs.split(",")]):
         if proto == "xcd":
             RNN_mod = __import__("deepspeech_amd.ops.rnn", fromlist=["x"])
             RNN_mod.RNNX_KNOBS = nw
-        for mode in ("auto",):
+        for mode in (("v1",) if proto == "v1" else ("auto",)):
             try:
                 r = run(a.cell, a.N, a.H, a.T, a.ndir, nw, mode, a.iters)
                 print(json.dumps({"kernel": proto, "nw": nw, "mode": mode,

@@ -41,11 +41,11 @@ def merge(path: str) -> None:
 
 
 def tune(out: str, frames, batch: int) -> None:
-    os.environ["DS2_TUNABLEOP"] = "tune"
-    os.environ["DS2_TUNABLEOP_OUT"] = out
+    from deepspeech_amd.ops.gemm_tuning import enable_tuned_gemms
     from deepspeech_amd.utils.setenvs import setenvs
     setenvs([])
     import torch
+    enable_tuned_gemms(mode="tune", out=out)     # before the model's own (idempotent) call
     from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
     from deepspeech_amd.models import DeepSpeech2
     from deepspeech_amd.trainer import LRSchedule, Trainer
