@@ -67,6 +67,12 @@ def parse():
     p.add_argument("--no_defer_update", action="store_true",
                    help="apply every step's whole optimizer update inside that step instead of carrying "
                         "the head's and upper layers' range into the next forward (A/B)")
+    p.add_argument("--no_carry_du", action="store_true",
+                   help="with the carried update, keep the upper layers' dU GEMMs beside the next BPTT (A/B)")
+    p.add_argument("--no_gate", action="store_true",
+                   help="side-stream work beside a persistent recurrence without the residency gate (A/B)")
+    p.add_argument("--carry_blocks", type=int, default=0,
+                   help="blocks per idle CU of the carried optimizer chunks (A/B; 0: the default)")
     p.add_argument("--fp8", action="store_true",
                    help="BASELINE config 5's fp8 mode: MX-fp8 e4m3 input projections, an e4m3 forward "
                         "recurrence (U and hidden-state exchange) and an fp8 BPTT (e4m3 U^T, E8M0-scaled "
@@ -102,6 +108,14 @@ def main():
                         stack_fix=True, seq_bn="frozen").to(dev)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     model.set_engine(args.engine, dtype, fp8=bool(args.fp8 and args.engine == "hip"))
+    if args.no_carry_du:
+        import deepspeech_amd.trainer as _T
+        _T._CARRY_DU = False
+    if args.no_gate:
+        RNN._RESIDENCY_GATE = False
+    if args.carry_blocks:
+        import deepspeech_amd.trainer as _T
+        _T._CARRY_BLOCKS_PER_CU, _T._CARRY_LDS = args.carry_blocks, 32768
     trainer = Trainer(model, LRSchedule(1e-4, 10 ** 9, 0.9), moving_avg_decay=0.9999,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
                       allreduce_bf16=args.allreduce_bf16, force_buckets=args.force_dp,

@@ -138,7 +138,7 @@ int ds2_bn_bwd(const void* dout, int dout_bf16, const void* y, int y_bf16, const
                int dy_bf16, int N, int C, int T, int F, int layout, hipStream_t st);
 int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
                  float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
-                 const float* hyper, hipStream_t st);
+                 const float* hyper, int lds_reserve, hipStream_t st);
 int ds2_grad_norm_blocks(long long n);
 int ds2_grad_norm(const float* g, long long n, float gscale, float* part, int nblocks, int* bad, hipStream_t st);
 int ds2_cast_bf16(const float* x, void* y, long long n, hipStream_t st);
@@ -180,6 +180,7 @@ int ds2_multi_copy(int n, void* const* dst, const void* const* src, const unsign
                    const unsigned* dst_pitch, float* sdst, const float* svals, int ns, hipStream_t st);
 int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                    hipStream_t st);
+int ds2_wait_resident(const unsigned* word, long long timeout, hipStream_t st);
 int ds2_col_sum(int n, const float* const* in, float* const* out, const int* R, const int* B, const int* C,
                 const int* acc, hipStream_t st);
 int ds2_fc_bias_grad(const void* G, int M, int ldg, int K, const float* scale, float alpha, float* out, int acc,
@@ -736,8 +737,10 @@ void bn_bwd(at::Tensor dout, at::Tensor y, at::Tensor mean, at::Tensor invstd, a
 
 // --------------------------------------------------------------------------- optimizer
 void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, OptT p16, double lr_t, double b1,
-              double b2, double eps, double gscale, double ema_keep, OptT skip, int64_t max_grid, OptT hyper) {
+              double b2, double eps, double gscale, double ema_keep, OptT skip, int64_t max_grid, OptT hyper,
+              int64_t lds_reserve) {
   need_gpu(p, "p");
+  TORCH_CHECK(lds_reserve >= 0 && lds_reserve <= 65536, "adam_ema: lds_reserve in [0, 64 KB]");
   need_gpu(g, "g");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "fp32 arena expected");
   const long long n = p.numel();
@@ -745,7 +748,7 @@ void adam_ema(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, OptT ema, 
   check(ds2_adam_ema(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
                      ptr_or_null<float>(ema, "ema"), ptr_or_null<void>(p16, "p16"), n, (float)lr_t, (float)b1,
                      (float)b2, (float)eps, (float)gscale, (float)ema_keep, ptr_or_null<const int>(skip, "skip"),
-                     (int)max_grid, ptr_or_null<const float>(hyper, "hyper"), cur_stream()),
+                     (int)max_grid, ptr_or_null<const float>(hyper, "hyper"), (int)lds_reserve, cur_stream()),
         "adam_ema");
 }
 
@@ -1021,6 +1024,16 @@ void prep_inputs(at::Tensor x, at::Tensor y, at::Tensor lens_in, at::Tensor lens
         "prep_inputs");
 }
 
+// a wave on the current stream that waits (bounded by `timeout` s_memrealtime ticks) until census
+// word `word` (int32, one element) is no longer -1: the persistent launch owning it is resident
+// (csrc/fill.hip)
+void wait_resident(at::Tensor word, int64_t timeout) {
+  need_gpu(word, "census word");
+  TORCH_CHECK(word.scalar_type() == at::kInt && word.numel() == 1, "wait_resident: one int32 census word");
+  check(ds2_wait_resident(reinterpret_cast<const unsigned*>(word.data_ptr<int>()), (long long)timeout, cur_stream()),
+        "wait_resident");
+}
+
 void multi_fill(std::vector<at::Tensor> ts, std::vector<int64_t> patterns) {
   TORCH_CHECK(ts.size() == patterns.size() && ts.size() <= 8, "multi_fill: <= 8 (tensor, pattern) pairs");
   void* ptrs[8];
@@ -1068,7 +1081,9 @@ void fc_bias_grad(at::Tensor G, int64_t K, at::Tensor scale, double alpha, at::T
   need_gpu(scale, "scale");
   need_gpu(out, "out");
   TORCH_CHECK(G.dim() == 2 && G.scalar_type() == at::kBFloat16 && G.stride(1) == 1, "fc_bias_grad: G bf16 [M, ldg]");
-  TORCH_CHECK(K >= 1 && K <= 32 && K <= G.size(1), "fc_bias_grad: 1 <= K <= min(32, G columns)");
+  TORCH_CHECK(K >= 1 && K <= 32 && G.size(1) >= 32 && G.stride(0) % 8 == 0 && G.data_ptr<at::BFloat16>() != nullptr &&
+                  reinterpret_cast<uintptr_t>(G.data_ptr()) % 16 == 0,
+              "fc_bias_grad: 1 <= K <= 32, G of >= 32 columns, row stride % 8 == 0, 16-B aligned");
   TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() >= 1, "fc_bias_grad: fp32 device scale");
   TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == K, "fc_bias_grad: fp32 out [K]");
   check(ds2_fc_bias_grad(G.data_ptr(), (int)G.size(0), (int)G.stride(0), (int)K, scale.data_ptr<float>(),
@@ -1521,7 +1536,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("adam_ema", &adam_ema, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("ema"),
         py::arg("p16"), py::arg("lr_t"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("gscale"),
-        py::arg("ema_keep"), py::arg("skip"), py::arg("max_grid"), py::arg("hyper") = py::none());
+        py::arg("ema_keep"), py::arg("skip"), py::arg("max_grid"), py::arg("hyper") = py::none(),
+        py::arg("lds_reserve") = 0);
   m.def("adam_ema_ranges", &adam_ema_ranges, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"),
         py::arg("ema"), py::arg("p16"), py::arg("lohi"), py::arg("lr_t"), py::arg("b1"), py::arg("b2"),
         py::arg("eps"), py::arg("gscale"), py::arg("ema_keep"), py::arg("hyper") = py::none());
@@ -1548,6 +1564,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm8_splits", [](int64_t K, bool fp8, int64_t S) { return ds2_gemm8_splits((int)K, fp8 ? 1 : 0, (int)S); });
   m.def("multi_fill", &multi_fill);
   m.def("col_sum", &col_sum);
+  m.def("wait_resident", &wait_resident);
   m.def("fc_bias_grad", &fc_bias_grad);
   m.def("event_new", &event_new, py::arg("flags") = 0);
   m.def("arm_stop_event", &arm_stop_event);

@@ -43,6 +43,30 @@ extern "C" hipEvent_t ds2_take_stop_event() {
   return e;
 }
 
+// ---------------------------------------------------------------------------------------
+// Residency gate: one wave spins (bounded) until a persistent recurrence launch's LAST
+// workgroup has published its census word (csrc/rnn_xcd.hip group_census; pre-filled
+// 0xFFFFFFFF). Workgroups are dispatched in order, so the whole grid then holds its CUs, and
+// the work queued behind this gate on another stream (the weight-gradient GEMMs beside a
+// BPTT, the carried optimizer chunks beside a forward recurrence) lands only on the CUs the
+// recurrence left idle instead of racing it for them at dispatch. A pure scheduling hint: on a
+// timeout (a launch that never came, e.g. a different plan than expected) the wave just exits.
+namespace {
+__global__ __launch_bounds__(64) void wait_resident_kernel(const unsigned* word, long long timeout) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0xFFFFFFFFu) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) return;
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+}  // namespace
+
+extern "C" int ds2_wait_resident(const unsigned* word, long long timeout, hipStream_t st) {
+  ds2_launch(wait_resident_kernel, dim3(1), dim3(64), 0, st, word, timeout);
+  return (int)hipGetLastError();
+}
+
 extern "C" int ds2_multi_fill(int n, void* const* ptrs, const unsigned long long* bytes, const unsigned* patterns,
                               hipStream_t st) {
   if (n < 0 || n > MF_MAX) return -50;

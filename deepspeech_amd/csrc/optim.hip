@@ -195,9 +195,26 @@ extern "C" {
 
 // max_grid > 0 caps the grid (an update issued beside a persistent kernel that holds most
 // of the CUs: a few workgroups stream the range instead of queueing behind it)
+// lds_reserve > 0: every block also reserves that many bytes of (unused) dynamic LDS, so no
+// block fits on a CU whose LDS a persistent recurrence workgroup holds: a range streaming beside
+// a forward recurrence (132 KB of LDS per workgroup; 32 KB keeps the blocks off its CUs) then
+// runs only on the CUs it leaves idle, several blocks per idle CU.
 int ds2_adam_ema(float* p, const float* g, float* m, float* v, float* ema, void* p16, long long n, float lr_t,
                  float b1, float b2, float eps, float gscale, float ema_keep, const int* skip, int max_grid,
-                 const float* hyper, hipStream_t st) {
+                 const float* hyper, int lds_reserve, hipStream_t st) {
+  if (lds_reserve > 0) {
+    static int configured = 0;
+    if (lds_reserve > configured) {
+      DS2_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(adam_ema_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds_reserve));
+      configured = lds_reserve;
+    }
+    int grid = grid_for(n);
+    if (max_grid > 0 && grid > max_grid) grid = max_grid;
+    hipLaunchKernelGGL(adam_ema_kernel, dim3(grid), dim3(OPT_THREADS), (unsigned)lds_reserve, st, p, g, m, v, ema,
+                       (bf16_t*)p16, n, lr_t, b1, b2, eps, gscale, ema_keep, skip, hyper);
+    return (int)hipGetLastError();
+  }
   // arenas past ~120 M parameters (config 5: 146 M) stream faster block-contiguous (1098 vs
   // 1200 us, interleaved A/B in tools/bench_adam.py); smaller ones (46 M: 278 vs 328 us, 89 M:
   // 634 vs 748) faster grid-strided

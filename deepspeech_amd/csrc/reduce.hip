@@ -47,21 +47,33 @@ __global__ __launch_bounds__(256) void col_sum_kernel(ColSum a) {
   }
 }
 
-// one workgroup: thread (rg, k) = (tid / 32, tid % 32) sums rows rg, rg + 32, ... of column k,
-// then the 32 row groups are reduced through LDS in a fixed order
+// one workgroup: thread (rg, q) = (tid / 4, tid % 4) sums rows rg, rg + 256, ... of the 16-B
+// chunk q (8 columns) with one 16-B load per row; the 256 row groups are then reduced through
+// LDS in a fixed order (bitwise reproducible). ldg % 8 == 0 and a 16-B aligned G (checked on
+// the host) keep every chunk load aligned; columns >= K are loaded and never stored.
 __global__ __launch_bounds__(1024) void fc_bias_kernel(const bf16_t* __restrict__ G, int M, int ldg, int K,
                                                        const float* __restrict__ scale, float alpha,
                                                        float* __restrict__ out, int acc) {
-  __shared__ float part[32][33];
-  const int k = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  float s = 0.f;
-  if (k < K)
-    for (int m = rg; m < M; m += 32) s += bf2f(G[(long long)m * ldg + k]);
-  part[rg][k] = s;
+  __shared__ float part[256][33];
+  const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (8 * q < K) {
+    for (int m = rg; m < M; m += 256) {
+      const i32x4 v = *reinterpret_cast<const i32x4*>(G + (long long)m * ldg + 8 * q);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[2 * i] += bf2f((bf16_t)((unsigned)v[i] & 0xffffu));
+        s[2 * i + 1] += bf2f((bf16_t)((unsigned)v[i] >> 16));
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) part[rg][8 * q + i] = s[i];
   __syncthreads();
-  if (rg == 0 && k < K) {
+  const int k = threadIdx.x;
+  if (k < K) {
     float t = 0.f;
-    for (int r = 0; r < 32; ++r) t += part[r][k];
+    for (int r = 0; r < 256; ++r) t += part[r][k];
     t = t * scale[0] * alpha;
     if (acc) out[k] += t;
     else out[k] = t;
@@ -94,7 +106,7 @@ extern "C" int ds2_col_sum(int n, const float* const* in, float* const* out, con
 
 extern "C" int ds2_fc_bias_grad(const void* G, int M, int ldg, int K, const float* scale, float alpha, float* out,
                                 int acc, hipStream_t st) {
-  if (K < 1 || K > 32 || ldg < K || M < 0) return -50;
+  if (K < 1 || K > 32 || ldg < 32 || ldg % 8 != 0 || (reinterpret_cast<uintptr_t>(G) & 15) != 0 || M < 0) return -50;
   ds2_launch(fc_bias_kernel, dim3(1), dim3(1024), 0, st, static_cast<const bf16_t*>(G), M, ldg, K, scale, alpha, out,
              acc);
   return (int)hipGetLastError();

@@ -114,13 +114,18 @@ class ParamArena:
         self._event_next += 1
         return ev
 
-    def issue_pending_update(self, grid: int = 0, count: int = 1) -> None:
+    def issue_pending_update(self, grid: int = 0, count: int = 1, gate=None) -> None:
         """Enqueue the next ``count`` chunks of the carried update on the weight-gradient side
         stream, behind everything the current stream has enqueued (a recurrent layer's
         projection): each then runs on the CUs that layer's persistent recurrence leaves idle,
-        and the reader of its weights waits only for its own chunk (:meth:`await_params`)."""
+        and the reader of its weights waits only for its own chunk (:meth:`await_params`).
+        Chunks without parameters (a carried weight-gradient GEMM of the layer above) go out
+        with the chunk before them. ``gate()``, if given, is enqueued on the side stream first
+        (ops/rnn.py _gate: wait until the recurrence beside which the chunk runs is resident)."""
         if not self._pending_chunks:
             return
+        while count < len(self._pending_chunks) and not self._pending_chunks[count][1]:
+            count += 1
         take, self._pending_chunks = self._pending_chunks[:count], self._pending_chunks[count:]
         dev = self.flat.device
         side = self.wgrad.stream(dev) if dev.type == "cuda" else None
@@ -130,8 +135,12 @@ class ParamArena:
             return
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
+            if gate is not None:
+                gate()
             for fn, params in take:
                 fn(grid)
+                if not params:
+                    continue
                 ev = self._event()
                 ev.record(side)
                 for p in params:
@@ -225,6 +234,14 @@ class ParamArena:
 
     def set_known_zero(self, p) -> None:
         self._known_zero.add(id(p))
+
+    def mark_written(self, *params) -> None:
+        """Count these gradients as produced this step without reporting them (a GEMM carried
+        into the next step writes them; lazy zeroing must not clear their slots meanwhile)."""
+        for p in params:
+            if p is not None:
+                self._written.add(id(p))
+                self._known_zero.discard(id(p))
 
     def first_write(self, p) -> bool:
         """True if ``p``'s gradient has not been written yet this step (fused ops then
@@ -412,7 +429,7 @@ class FusedAdamEMA:
 
     @torch.no_grad()
     def apply_range(self, lo: int, hi: int, lr_t: float, keep: float, gscale: float = 1.0,
-                    skip_flag: Optional[torch.Tensor] = None, max_grid: int = 0) -> None:
+                    skip_flag: Optional[torch.Tensor] = None, max_grid: int = 0, lds_reserve: int = 0) -> None:
         """Adam + EMA of arena elements [lo, hi) with a prepared (lr_t, keep), on the current
         stream. Every element's update is independent and rounds the same way whatever the
         launch split, so ranges compose bitwise into the whole-arena update (the DP bucketer
@@ -439,7 +456,7 @@ class FusedAdamEMA:
                             self.ema[sl] if self.ema is not None else None,
                             self.p16[sl] if self.p16 is not None else None,
                             lr_t, self.b1, self.b2, self.eps, gscale, keep, skip_flag, int(max_grid),
-                            self._hyper_arg())
+                            self._hyper_arg(), int(lds_reserve))
 
     @torch.no_grad()
     def apply_excluding(self, lo: int, hi: int, exclude, lr_t: float, keep: float, gscale: float = 1.0,

@@ -283,6 +283,26 @@ def check_errors(clear: bool = True) -> None:
                                "(error bits 0x%x; grid not co-resident?) — rerun with DS2_RNN_MODE=step" % v)
 
 
+# Side-stream work beside a persistent recurrence waits until that launch's last workgroup is
+# resident (csrc/fill.hip wait_resident on its census word) instead of racing it for CUs at
+# dispatch; a pure scheduling hint, bounded by _GATE_TICKS (5 ms of s_memrealtime)
+_RESIDENCY_GATE = True
+_GATE_TICKS = 500000
+
+
+def _gate(census: Optional[torch.Tensor]) -> None:
+    """On the current stream: wait until the persistent launch that owns ``census`` holds its
+    CUs (its last workgroup published its census word)."""
+    if _RESIDENCY_GATE and census is not None and census.is_cuda and census.numel() > 0:
+        _ext.ext().wait_resident(census[-1:], _GATE_TICKS)
+
+
+def _next_bptt_census(dev: torch.device) -> Optional[torch.Tensor]:
+    """Census of the BPTT launch prefilled for the next (lower) layer, if any."""
+    pre = _BWD_PREFILL.get(dev.index)
+    return pre[2][0] if pre is not None else None
+
+
 def _stamps(kind: str, plan: "RnnPlan", grid: int, dev) -> Optional[torch.Tensor]:
     if STAMP_LOG is None:
         return None
@@ -863,8 +883,9 @@ class FusedBiLayer(torch.autograd.Function):
         if arena is not None and x.is_cuda:
             # the next chunk of the optimizer update carried over from the previous step (the
             # layer above's, or the head's): on the side stream behind this projection, i.e.
-            # beside this layer's recurrence on the CUs it leaves idle
-            arena.issue_pending_update(_idle_cus(plan, x.device))
+            # beside this layer's recurrence on the CUs it leaves idle (gated on its residency)
+            census = bufs.census if bufs is not None else None
+            arena.issue_pending_update(_idle_cus(plan, x.device), gate=lambda: _gate(census))
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
@@ -973,6 +994,8 @@ class FusedBiLayer(torch.autograd.Function):
         _stream_wait(side, torch.cuda.current_stream(x16.device))
         sch.hold(x16, dgx, dgh, hx, parts)
         with torch.cuda.stream(side):
+            if ctx.idx >= 1:
+                _gate(_next_bptt_census(x16.device))      # the lower layer's BPTT holds its CUs first
             return FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx)
 
     @staticmethod
@@ -1049,7 +1072,21 @@ class FusedBiLayer(torch.autograd.Function):
                     except (RuntimeError, TypeError):
                         out.copy_(torch.bmm(g3, h3))
                 du_done()
-            if defer:
+            carry_from = (_upper_trigger(plan, x16.device, T) + 1) if sch.carry_du else 0
+            if beside and on_side and carry_from and ctx.idx >= carry_from:
+                # carried into the NEXT step's forward (Trainer defer_update): the GEMM runs on
+                # the side stream beside a forward recurrence, right before this layer's carried
+                # optimizer chunk, so only dW runs beside the next BPTT (dW + dU outlasted it by
+                # ~140 us, which landed on the next dx GEMM). The slots count as written now
+                # (no zeroing; first write overwrites) and the operands stay referenced.
+                arena.mark_written(U_f, U_b)
+
+                def du_carried(grid, g3=g3, h3=h3, out=out, hold=(dgh, hx)):
+                    sch.hold(*hold)
+                    if not (GM.enabled("wgrad") and GM.matmul(g3, h3, out, splits=_DU_SPLITS, max_grid=grid)):
+                        torch.bmm(g3, h3, out_dtype=torch.float32, out=out)
+                sch.carried_du[ctx.idx] = du_carried
+            elif defer:
                 # every weight gradient after the BPTT chain: a GEMM beside the latency-bound
                 # persistent BPTT slows it by 27-48 % (its L2 / fabric / clock share), more
                 # than the tail gains back (WgradScheduler)
@@ -1288,6 +1325,11 @@ class WgradScheduler:
         self._hold = []            # tensors read on the side stream, released by join()
         self._fused = None         # (arena, tensors, constants, store_g): set_fused_update
         self.fused_ranges = []     # arena element ranges the grouped epilogue updated this step
+        # Trainer defer_update (carry_du): the recurrent layers above the upper trigger hand their
+        # beside dU GEMM to the next step's forward (carried_du: layer -> fn(grid), taken by the
+        # Trainer with take_carried_du; whatever is not taken runs before this step's optimizer)
+        self.carry_du = False
+        self.carried_du = {}
         # every weight gradient on the current stream (a captured step graph: ROCm replays a
         # graph's cross-stream edges as barrier packets between its queues)
         self.single_stream = False
@@ -1332,6 +1374,7 @@ class WgradScheduler:
         self.transposes.clear()
         self._fused = None
         self.fused_ranges = []
+        self.carried_du = {}
 
     def flush_transposes(self) -> None:
         """Issue the queued W^T transposes on the side stream behind everything the current
@@ -1425,8 +1468,14 @@ class WgradScheduler:
         if arena is None or any(arena.first_write(p) for p in params):
             return
         _stream_wait(torch.cuda.current_stream(), main)   # readers of the weights issued so far
+        self._run_carried()                # dU GEMMs nobody carried: before their optimizer range
         fn()
         self.early_done = True
+
+    def _run_carried(self) -> None:
+        for k in sorted(self.carried_du, reverse=True):
+            self.carried_du[k](0)
+        self.carried_du = {}
 
     def set_fused_update(self, arena, tensors, constants, store_g: bool = False) -> None:
         """For THIS backward: the grouped tail launch applies the optimizer to its members'
@@ -1475,10 +1524,22 @@ class WgradScheduler:
             item = self.deferred.pop(0)
             (item.fn if isinstance(item, Deferred) else item)()
 
+    def take_carried_du(self) -> dict:
+        """The carried dU GEMMs of this backward (layer -> fn(grid)); the caller runs each before
+        that layer's optimizer update."""
+        c, self.carried_du = self.carried_du, {}
+        return c
+
     def drain(self) -> None:
         """Issue every deferred weight-gradient GEMM: leftover input-weight GEMMs (a backward
         that never reached layer 0) on the side stream, then the main-stream tail (the bottom
-        layer's dU behind the front-end backward)."""
+        layer's dU behind the front-end backward). Carried dU GEMMs nobody took run here."""
+        if self.carried_du:
+            for idx, s in self.streams.items():
+                _stream_wait(s, torch.cuda.current_stream(idx))
+                with torch.cuda.stream(s):
+                    self._run_carried()
+            self._run_carried()
         if self.deferred:
             for idx, s in self.streams.items():
                 _stream_wait(s, torch.cuda.current_stream(idx))

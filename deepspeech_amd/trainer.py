@@ -81,6 +81,15 @@ _LOWER_GRID = 0
 # BPTTs (0: uncapped). --force_dp at world 1, same box, 3 rounds: uncapped 7.754 / 7.747 / 7.705,
 # 512 7.782 / 7.725 / 7.719, 256 7.771 / 7.790 / 7.814, 128 7.86-7.88 ms/step
 _BUCKET_GRID = 0
+# with defer_update, the beside dU GEMMs of the layers above the upper trigger go to the next
+# step's forward too (ops/rnn.py WgradScheduler.carry_du)
+_CARRY_DU = True
+# carried optimizer chunks beside a forward recurrence: blocks per idle CU, and the unused LDS
+# each block reserves so that it cannot share a CU with a recurrence workgroup (132 KB of LDS).
+# Same box, 3 rounds: 1 block, no reservation 7.388-7.407 ms/step; 2 blocks + 32 KB 7.405-7.426;
+# 4 blocks + 32 KB 7.432-7.435
+_CARRY_BLOCKS_PER_CU = 1
+_CARRY_LDS = 0
 # capture step graphs on one stream (False: the weight-gradient side stream too; single-stream
 # capture is not bitwise at H = 800, where the deferral needs the side stream)
 _GRAPH_SINGLE_STREAM = False
@@ -209,16 +218,17 @@ class Trainer:
         if c is not None:
             return c
         starts = sorted((self.arena.offsets[i][0], k) for k, i in self._layer_first.items())
+        layer_at = {s: k for s, k in starts}
         bounds = [0] + [s for s, _ in starts if 0 < s < hi] + [hi]
         out = []
         for lo, up in zip(bounds[:-1], bounds[1:]):
             params = [p for p, (o, n) in zip(self.arena.params, self.arena.offsets) if lo <= o < up]
             if up > lo:
-                out.append((lo, up, params))
+                out.append((lo, up, params, layer_at.get(lo, -1)))
         c = self._chunk_cache[key] = list(reversed(out))
         return c
 
-    def _carry_update(self, hi: int, lr_t: float, keep: float, gscale: float) -> None:
+    def _carry_update(self, hi: int, lr_t: float, keep: float, gscale: float, dus=None) -> None:
         """Register the optimizer update of arena range [0, hi) (FC head + recurrent layers >= 1,
         whose gradients are final once layer 1's weight gradients are issued) with the arena, to
         be enqueued by the NEXT forward one chunk beside each recurrence (ops/rnn.py FusedBiLayer:
@@ -226,12 +236,39 @@ class Trainer:
         projection waiting only for its own chunk. In this
         step's tail it ran beside the conv front-end's backward and the bottom layer's weight
         gradients, which it slowed (r5 profile: 387 us of HBM-bound work on the critical tail).
-        Bitwise the same update (every element's Adam + EMA is independent of the launch split)."""
+        Bitwise the same update (every element's Adam + EMA is independent of the launch split).
+
+        ``dus``: layer -> the beside dU GEMM of that layer, carried too (ops/rnn.py
+        WgradScheduler.carry_du): it runs right after the chunk of the layer below, so layer k's
+        chunk is [Adam + EMA of layer k, dU GEMM of layer k+1] and each dU precedes its own
+        layer's update on the side stream."""
         opt = self.opt
+        dus = dict(dus or {})
 
         def chunk(lo, up):
-            return lambda grid: opt.apply_range(lo, up, lr_t, keep, gscale, max_grid=grid)
-        self.arena.set_pending_update([(chunk(lo, up), params) for lo, up, params in self._chunks(hi)])
+            # beside a forward recurrence (grid = the CUs it leaves idle): _CARRY_BLOCKS_PER_CU
+            # blocks per idle CU, each reserving LDS so none lands on a recurrence CU
+            def fn(grid):
+                if grid > 0:
+                    opt.apply_range(lo, up, lr_t, keep, gscale, max_grid=grid * _CARRY_BLOCKS_PER_CU,
+                                    lds_reserve=_CARRY_LDS if _CARRY_BLOCKS_PER_CU > 1 else 0)
+                else:
+                    opt.apply_range(lo, up, lr_t, keep, gscale)
+            return fn
+        chunks = self._chunks(hi)
+        todo = []
+        for lo, up, params, k in chunks:
+            todo.append((chunk(lo, up), params))
+            du = dus.pop(k + 1, None) if k >= 0 else None
+            if du is not None:
+                # its own (parameter-less) chunk right behind: the event readers of layer k wait
+                # for is recorded before it, so the next projection does not wait for this GEMM
+                todo.append((du, []))
+        if dus:
+            # a carried dU whose layer has no chunk below it (not expected): first, before any update
+            first = list(dus.values())
+            todo.insert(0, (lambda grid: [f(grid) for f in first], []))
+        self.arena.set_pending_update(todo)
 
     def flush(self) -> None:
         """Complete an optimizer update carried into the next step (``defer_update``): after
@@ -440,6 +477,8 @@ class Trainer:
                  self.arena.wgrad.grouped and self.arena.wgrad.defer_input)
         carry = early and self.defer_update and not torch.cuda.is_current_stream_capturing()
         carried = [0]
+        carried_du = {}
+        self.arena.wgrad.carry_du = carry and _CARRY_DU
         if early:
             # single device: the FC head's and recurrent stack's Adam + EMA range runs on the
             # weight-gradient stream right after the grouped tail GEMMs, beside the conv
@@ -460,12 +499,14 @@ class Trainer:
                 if carry:
                     def upper(hi, grid):
                         carried[0] = hi
+                        carried_du.update(self.arena.wgrad.take_carried_du())
                 else:
                     def upper(hi, grid):
                         self.opt.apply_range(0, hi, lr_t, keep, gscale, max_grid=grid)
                 sch.set_early_upper(self.upper_range, upper, _UPPER_GRID)
         loss.backward(one)
         self.arena.wgrad.join()
+        self.arena.wgrad.carry_du = False
         if lazy:
             self.arena.zero_unwritten()
         with TR.phase(TR.ALLREDUCE):
@@ -478,7 +519,7 @@ class Trainer:
                 lo = split if sch.early_done else (sch.early_upper_hi if sch.early_upper_done else 0)
                 self.opt.apply_excluding(lo, self.arena.numel, sch.fused_ranges, lr_t, keep, gscale)
             if carried[0] > 0:
-                self._carry_update(carried[0], lr_t, keep, gscale)
+                self._carry_update(carried[0], lr_t, keep, gscale, carried_du)
         elif not per_bucket:
             skip = None
             if self.nan_policy == "skip":
