@@ -189,12 +189,14 @@ __device__ __forceinline__ void stage_half(unsigned char* dst, __amdgpu_buffer_r
 
 // cache policy of the weight-gradient (column-column) kernels' operand loads: these launches
 // run beside the latency-bound persistent BPTT, whose per-step loads and partial-sum exchange
-// live in the same XCD L2. nt (aux 2, a streaming hint): headline, same
-// box, 3 rounds alternating, 7.549 / 7.583 / 7.560 ms/step vs 7.584 / 7.683 / 7.594 with the
-// default policy (scripts/r6_defer2.sh). Compile-time A/B: build.py --variant NAME
-// -D G8_COL_AUX=0.
+// live in the same XCD L2. nt (aux 2, a streaming hint) measured, not kept:
+// with dW + dU beside each BPTT, 7.549 / 7.583 / 7.560 ms/step vs 7.584 / 7.683 / 7.594 default
+// (scripts/r6_defer2.sh); once the dU GEMMs moved to the next forward (trainer.py _CARRY_DU),
+// 7.450 / 7.439 vs 7.422 / 7.430, and on the ReLU-1760 stack, whose weight gradients all run
+// as ONE grouped tail launch with nothing beside it, 14.54 / 14.54 vs 13.83 / 13.79; config 5
+// fp8 neutral (scripts/r6_nt.sh). Compile-time A/B: build.py --variant NAME -D G8_COL_AUX=2.
 #ifndef G8_COL_AUX
-#define G8_COL_AUX 2
+#define G8_COL_AUX 0
 #endif
 
 __device__ __forceinline__ i32x4 rd16(const unsigned char* half, int r, int chunk) {

@@ -285,22 +285,26 @@ def check_errors(clear: bool = True) -> None:
 
 # Side-stream work beside a persistent recurrence waits until that launch's last workgroup is
 # resident (csrc/fill.hip wait_resident on its census word) instead of racing it for CUs at
-# dispatch; a pure scheduling hint, bounded by _GATE_TICKS (5 ms of s_memrealtime)
+# dispatch; a pure scheduling hint, bounded by _GATE_TICKS (2 ms of s_memrealtime)
 _RESIDENCY_GATE = True
-_GATE_TICKS = 500000
+_GATE_TICKS = 200000
 
 
-def _gate(census: Optional[torch.Tensor]) -> None:
-    """On the current stream: wait until the persistent launch that owns ``census`` holds its
-    CUs (its last workgroup published its census word)."""
-    if _RESIDENCY_GATE and census is not None and census.is_cuda and census.numel() > 0:
-        _ext.ext().wait_resident(census[-1:], _GATE_TICKS)
+def _gate(census: Optional[torch.Tensor], plan: Optional["RnnPlan"]) -> None:
+    """On the current stream: wait until the persistent XCD launch of ``plan`` that owns
+    ``census`` holds its CUs: its last workgroup (group ngroups-1, member P-1) published its
+    census word, slot ngroups * P - 1 (the buffer may be longer: wide plans use P = H / 64)."""
+    if not (_RESIDENCY_GATE and census is not None and census.is_cuda and plan is not None and plan.kind == "xcd"):
+        return
+    last = plan.ndir * plan.BG * _xcd_p(plan.H, plan.cell) - 1
+    if 0 <= last < census.numel():
+        _ext.ext().wait_resident(census[last:last + 1], _GATE_TICKS)
 
 
-def _next_bptt_census(dev: torch.device) -> Optional[torch.Tensor]:
-    """Census of the BPTT launch prefilled for the next (lower) layer, if any."""
+def _next_bptt(dev: torch.device):
+    """(census, plan) of the BPTT launch prefilled for the next (lower) layer, if any."""
     pre = _BWD_PREFILL.get(dev.index)
-    return pre[2][0] if pre is not None else None
+    return (pre[2][0], pre[0]) if pre is not None else (None, None)
 
 
 def _stamps(kind: str, plan: "RnnPlan", grid: int, dev) -> Optional[torch.Tensor]:
@@ -885,7 +889,7 @@ class FusedBiLayer(torch.autograd.Function):
             # layer above's, or the head's): on the side stream behind this projection, i.e.
             # beside this layer's recurrence on the CUs it leaves idle (gated on its residency)
             census = bufs.census if bufs is not None else None
-            arena.issue_pending_update(_idle_cus(plan, x.device), gate=lambda: _gate(census))
+            arena.issue_pending_update(_idle_cus(plan, x.device), gate=lambda: _gate(census, plan))
         lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
         U = [_bf16(U_f), _bf16(U_b) if U_b is not None else None]
         bh = [b.float() if b is not None else None for b in (bh_f, bh_b)]
@@ -994,8 +998,8 @@ class FusedBiLayer(torch.autograd.Function):
         _stream_wait(side, torch.cuda.current_stream(x16.device))
         sch.hold(x16, dgx, dgh, hx, parts)
         with torch.cuda.stream(side):
-            if ctx.idx >= 1:
-                _gate(_next_bptt_census(x16.device))      # the lower layer's BPTT holds its CUs first
+            if ctx.idx >= 1 and not (sch.defer_input and _defer_layer(plan, x16.device, ctx.idx, x16.shape[0])):
+                _gate(*_next_bptt(x16.device))        # the lower layer's BPTT holds its CUs first
             return FusedBiLayer._weight_grads(ctx, x16, dgx2, dgh, hx, parts, dx)
 
     @staticmethod
@@ -1073,7 +1077,7 @@ class FusedBiLayer(torch.autograd.Function):
                         out.copy_(torch.bmm(g3, h3))
                 du_done()
             carry_from = (_upper_trigger(plan, x16.device, T) + 1) if sch.carry_du else 0
-            if beside and on_side and carry_from and ctx.idx >= carry_from:
+            if beside and on_side and carry_from and ctx.idx >= carry_from and cap_u:
                 # carried into the NEXT step's forward (Trainer defer_update): the GEMM runs on
                 # the side stream beside a forward recurrence, right before this layer's carried
                 # optimizer chunk, so only dW runs beside the next BPTT (dW + dU outlasted it by

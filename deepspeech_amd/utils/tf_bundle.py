@@ -6,7 +6,8 @@ and ``saver.save(sess, train_dir/model.ckpt, global_step=step)`` every 10 steps
 ``get_checkpoint_state`` (:383-398), and evaluates the EMA shadows restored from the same files
 (src/deepSpeech_test.py:93-109, :217-220). Those files are a V2 *tensor bundle*:
 
-  <prefix>.data-00000-of-00001   every tensor's raw little-endian bytes, back to back
+  <prefix>.data-00000-of-00001   every tensor's raw little-endian bytes, back to back (a big
+                                 bundle: .data-0000i-of-0000N shards, TF's sharded layout)
   <prefix>.index                 SSTable (LevelDB table format): "" -> BundleHeaderProto,
                                  variable name -> BundleEntryProto
 
@@ -28,7 +29,9 @@ not supported; the reference creates neither.
 """
 from __future__ import annotations
 
+import glob
 import os
+from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
@@ -38,6 +41,15 @@ from ..runtime import native
 
 DATA_SUFFIX = ".data-00000-of-00001"
 INDEX_SUFFIX = ".index"
+# a bundle of more than this many bytes is written as several data shards, each by its own
+# thread: buffered writes to ONE file serialise on its inode lock (~5.5 GB/s per file measured on
+# the MI355X boxes: 0.14 s for the headline's 0.74 GB), separate files do not
+SHARD_BYTES = 96 << 20
+MAX_SHARDS = 8
+
+
+def shard_name(prefix: str, i: int, n: int) -> str:
+    return "%s.data-%05d-of-%05d" % (prefix, i, n)
 
 # tensorflow/core/framework/types.proto
 _DT = {torch.float32: 1, torch.float64: 2, torch.int32: 3, torch.uint8: 4, torch.int16: 5, torch.int8: 6,
@@ -114,9 +126,11 @@ def encode_header(num_shards: int = 1) -> bytes:
     return _field_varint(1, num_shards) + _field_bytes(3, _field_varint(1, _KTENSOR_BUNDLE_VERSION))
 
 
-def encode_entry(dtype: torch.dtype, shape, offset: int, size: int, crc: int) -> bytes:
+def encode_entry(dtype: torch.dtype, shape, offset: int, size: int, crc: int, shard: int = 0) -> bytes:
     dims = b"".join(_field_bytes(2, _field_varint(1, int(d))) for d in shape)
     msg = _field_varint(1, _DT[dtype]) + _field_bytes(2, dims)
+    if shard:
+        msg += _field_varint(3, shard)
     if offset:
         msg += _field_varint(4, offset)
     if size:
@@ -157,7 +171,7 @@ def bundle_exists(prefix: str) -> bool:
 
 
 def bundle_files(prefix: str) -> List[str]:
-    return [prefix + INDEX_SUFFIX, prefix + DATA_SUFFIX]
+    return [prefix + INDEX_SUFFIX] + sorted(glob.glob(glob.escape(prefix) + ".data-*-of-*"))
 
 
 def _host_bytes(t: torch.Tensor) -> Tuple[int, int, torch.Tensor]:
@@ -169,34 +183,62 @@ def _host_bytes(t: torch.Tensor) -> Tuple[int, int, torch.Tensor]:
     return t.data_ptr(), t.numel() * t.element_size(), t
 
 
-def write_bundle(prefix: str, tensors: Dict[str, torch.Tensor], threads: int = 8) -> None:
+def write_bundle(prefix: str, tensors: Dict[str, torch.Tensor], threads: int = 8,
+                 num_shards: Optional[int] = None) -> None:
     """Write ``tensors`` (name -> CPU tensor; views of pinned buffers are written in place,
-    without a copy) as a V2 bundle at ``prefix``. The data shard is written first and the index
+    without a copy) as a V2 bundle at ``prefix``. ``num_shards`` data files (default: one per
+    SHARD_BYTES, at most MAX_SHARDS), balanced by bytes and written in parallel (TF's sharded
+    Saver layout: each entry names its shard). The data shards are written first and the index
     last, each through a temporary name, so a reader never sees an index without its data."""
     N = native.load()
     names = sorted(tensors)
     for n in names:
         if n == "" or tensors[n].dtype not in _DT:
             raise ValueError("bundle: cannot store %r (%s)" % (n, tensors[n].dtype))
-    keep, ptrs, sizes = [], [], []
+    keep, ptrs, sizes = {}, {}, {}
     for n in names:
         p, nb, k = _host_bytes(tensors[n].detach())
-        keep.append(k)
-        ptrs.append(p)
-        sizes.append(nb)
+        keep[n], ptrs[n], sizes[n] = k, p, nb
+    total = sum(sizes.values())
+    ns = num_shards or max(1, min(MAX_SHARDS, -(-total // SHARD_BYTES)))
+    ns = max(1, min(ns, len(names) or 1))
+    # greedy balance: largest tensors first, each to the lightest shard
+    shard_of, load = {}, [0] * ns
+    for n in sorted(names, key=lambda x: -sizes[x]):
+        i = min(range(ns), key=lambda j: load[j])
+        shard_of[n] = i
+        load[i] += sizes[n]
+    members = [[n for n in names if shard_of[n] == i] for i in range(ns)]
     d = os.path.dirname(prefix)
     if d:
         os.makedirs(d, exist_ok=True)
-    tmp_data = prefix + DATA_SUFFIX + ".tmp"
-    crcs = N.bundle_write_shard(tmp_data, ptrs, sizes, int(threads))
-    items = [(b"", encode_header(1))]
-    off = 0
-    for n, t, nb, c in zip(names, keep, sizes, crcs):
-        items.append((n.encode(), encode_entry(t.dtype, t.shape, off, nb, c)))
-        off += nb
+    per = max(1, int(threads) // ns)
+
+    def write(i):
+        return N.bundle_write_shard(shard_name(prefix, i, ns) + ".tmp", [ptrs[n] for n in members[i]],
+                                    [sizes[n] for n in members[i]], per)
+    if ns == 1:
+        crc_lists = [write(0)]
+    else:
+        with ThreadPoolExecutor(max_workers=ns) as ex:
+            crc_lists = list(ex.map(write, range(ns)))
+    where = {}
+    for i in range(ns):
+        off = 0
+        for n, c in zip(members[i], crc_lists[i]):
+            where[n] = (i, off, c)
+            off += sizes[n]
+    items = [(b"", encode_header(ns))]
+    for n in names:
+        i, off, c = where[n]
+        items.append((n.encode(), encode_entry(keep[n].dtype, keep[n].shape, off, sizes[n], c, shard=i)))
     tmp_index = prefix + INDEX_SUFFIX + ".tmp"
     N.bundle_write_file(tmp_index, N.bundle_build_table(items))
-    os.replace(tmp_data, prefix + DATA_SUFFIX)
+    for old in glob.glob(glob.escape(prefix) + ".data-*-of-*"):
+        if not old.endswith(".tmp"):
+            os.remove(old)                       # a previous bundle at this prefix
+    for i in range(ns):
+        os.replace(shard_name(prefix, i, ns) + ".tmp", shard_name(prefix, i, ns))
     os.replace(tmp_index, prefix + INDEX_SUFFIX)
 
 
@@ -214,23 +256,32 @@ def read_index(prefix: str, verify: bool = True) -> Tuple[dict, Dict[str, dict]]
         raise ValueError("bundle %s: index has no header entry" % prefix)
     if header["endianness"] != 0:
         raise ValueError("bundle %s: big-endian bundles are not supported" % prefix)
-    if header["num_shards"] != 1:
-        raise ValueError("bundle %s: %d data shards (only single-shard bundles are read)" % (prefix, header["num_shards"]))
+    if header["num_shards"] < 1:
+        raise ValueError("bundle %s: bad shard count %d" % (prefix, header["num_shards"]))
     return header, entries
 
 
 def read_bundle(prefix: str, names: Optional[Iterable[str]] = None, verify: bool = True) -> Dict[str, torch.Tensor]:
     """name -> CPU tensor of every (or the named) variable of the bundle at ``prefix``; with
     ``verify`` each tensor's bytes are checked against the index's crc32c."""
-    _, entries = read_index(prefix, verify)
+    header, entries = read_index(prefix, verify)
     want = list(entries) if names is None else list(names)
     N = native.load()
-    data = np.memmap(prefix + DATA_SUFFIX, dtype=np.uint8, mode="r") if os.path.getsize(prefix + DATA_SUFFIX) else \
-        np.zeros(0, np.uint8)
+    ns = header["num_shards"]
+    maps = {}
+
+    def shard(i):
+        if i not in maps:
+            path = shard_name(prefix, i, ns)
+            maps[i] = np.memmap(path, dtype=np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+        return maps[i]
     out = {}
     for n in want:
         e = entries[n]
         nb = int(e["size"])
+        if not 0 <= e["shard_id"] < ns:
+            raise ValueError("bundle %s: %s names shard %d of %d" % (prefix, n, e["shard_id"], ns))
+        data = shard(e["shard_id"])
         raw = np.array(data[e["offset"]:e["offset"] + nb])          # a private copy off the map
         if raw.size != nb:
             raise ValueError("bundle %s: %s lies beyond the data shard" % (prefix, n))
@@ -238,5 +289,5 @@ def read_bundle(prefix: str, names: Optional[Iterable[str]] = None, verify: bool
             raise ValueError("bundle %s: checksum mismatch for %s" % (prefix, n))
         t = torch.from_numpy(raw).view(e["dtype"]) if nb else torch.empty(0, dtype=e["dtype"])
         out[n] = t.reshape(e["shape"])
-    del data
+    maps.clear()
     return out

@@ -196,6 +196,35 @@ def test_many_entries_span_blocks_and_roundtrip(tmp_path):
         assert got[k].dtype == t.dtype and got[k].shape == t.shape and torch.equal(got[k], t), k
 
 
+def test_sharded_bundle(tmp_path):
+    """A big bundle goes out as several data shards written in parallel (TF's sharded Saver
+    layout: the header counts them, each entry names its shard); the independent reader agrees."""
+    tensors = {"w%d" % i: torch.randn(1000 + 37 * i) for i in range(10)}
+    tensors["step"] = torch.tensor(3, dtype=torch.int64)
+    prefix = str(tmp_path / "model.ckpt-3")
+    TB.write_bundle(prefix, tensors, num_shards=3)
+    files = sorted(os.listdir(tmp_path))
+    assert files == ["model.ckpt-3.data-0000%d-of-00003" % i for i in range(3)] + ["model.ckpt-3.index"]
+    kv = _spec_parse_table(open(prefix + ".index", "rb").read())
+    hdr = TB.decode_header(kv[0][1])
+    assert hdr["num_shards"] == 3
+    shards = [open(TB.shard_name(prefix, i, 3), "rb").read() for i in range(3)]
+    used = set()
+    for k, v in kv[1:]:
+        e = TB.decode_entry(v)
+        used.add(e["shard_id"])
+        raw = shards[e["shard_id"]][e["offset"]:e["offset"] + e["size"]]
+        assert raw == tensors[k.decode()].numpy().tobytes() and e["crc32c"] == _mask(_crc32c(raw))
+    assert used == {0, 1, 2}
+    got = TB.read_bundle(prefix)
+    for k, t in tensors.items():
+        assert torch.equal(got[k], t)
+    # rewriting the prefix with another shard count leaves no stale shard behind
+    TB.write_bundle(prefix, tensors, num_shards=1)
+    assert sorted(os.listdir(tmp_path)) == ["model.ckpt-3.data-00000-of-00001", "model.ckpt-3.index"]
+    assert torch.equal(TB.read_bundle(prefix)["w9"], tensors["w9"])
+
+
 def test_corruption_is_detected(tmp_path):
     prefix = str(tmp_path / "c")
     TB.write_bundle(prefix, {"a": torch.randn(100), "b": torch.randn(10)})
