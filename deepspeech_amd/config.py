@@ -134,6 +134,9 @@ def build_train_parser() -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=32.0,
                    help="gradient all-reduce bucket size (MB) for data parallel")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--dummy_frames", type=int, default=0,
+                   help="--dummy True: fixed-length synthetic batches of this many frames (bench.py's "
+                        "headline shape: 1000) instead of the reference's bucket walk (0)")
     p.add_argument("--max_frames", type=int, default=1800,
                    help="drop utterances longer than this (frames)")
     p.add_argument("--fault_inject_step", type=int, default=-1,

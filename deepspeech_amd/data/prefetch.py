@@ -66,7 +66,7 @@ class DevicePrefetcher:
                 k += 1
                 if slot.event is not None:
                     slot.event.synchronize()         # previous upload out of this slot done
-                flat = hb.flat_labels().astype(np.int32)
+                flat = hb.validate().flat_labels().astype(np.int32)
                 host = {
                     "feats": slot.stage("feats", hb.feats.astype(np.float32, copy=False)),
                     "seq_lens": slot.stage("seq_lens", hb.seq_lens.astype(np.int32)),

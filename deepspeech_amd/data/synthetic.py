@@ -49,6 +49,21 @@ class Batch:
     def flat_labels(self) -> np.ndarray:
         return np.concatenate([self.labels[i, : self.label_lens[i]] for i in range(len(self.label_lens))])
 
+    def validate(self) -> "Batch":
+        """Reject lengths the CTC kernels cannot honour, on the host before upload: a label
+        length past the padded label width (the kernels clamp it only as an out-of-bounds guard,
+        which would train on a truncated transcript; the reference's ctc_loss rejects it,
+        src/deepSpeech_NCHW.py:225) or a sequence length past the padded frame count."""
+        if len(self.label_lens) and int(self.label_lens.max()) > self.labels.shape[1]:
+            raise ValueError("label length %d exceeds the padded label width %d"
+                             % (int(self.label_lens.max()), self.labels.shape[1]))
+        if len(self.seq_lens) and int(self.seq_lens.max()) > self.feats.shape[1]:
+            raise ValueError("sequence length %d exceeds the padded frame count %d"
+                             % (int(self.seq_lens.max()), self.feats.shape[1]))
+        if len(self.label_lens) and int(self.label_lens.min()) < 0:
+            raise ValueError("negative label length")
+        return self
+
 
 def random_labels(rng: np.random.Generator, n: int, length: int) -> np.ndarray:
     return rng.integers(0, NUM_CLASSES - 1, size=(n, length), dtype=np.int32)
@@ -170,7 +185,7 @@ def to_device(batch: Batch, device: torch.device, non_blocking: bool = True) -> 
             t = t.pin_memory()
         return t.to(device, non_blocking=non_blocking)
 
-    flat = batch.flat_labels().astype(np.int32)
+    flat = batch.validate().flat_labels().astype(np.int32)
     return {
         "feats": mv(batch.feats),
         "seq_lens": mv(batch.seq_lens.astype(np.int32)),

@@ -89,6 +89,8 @@ class GradBucketer:
         self._handles = []
         self._opt = None                   # per-bucket optimizer: fn(lo, hi) on the current stream
         self._opt_pending: List[int] = []  # buckets whose collective is issued, update not yet
+        self._carry_hi = 0                 # buckets inside arena [0, carry_hi): update carried
+        self._carried: List[Tuple[int, int, "torch.cuda.Event"]] = []
         self._main_stream = None
         self.enabled = self.world > 1 or (force and dist.is_initialized())
         self._order_stream = None
@@ -132,16 +134,29 @@ class GradBucketer:
         self._works = []
         self._opt = None
         self._opt_pending = []
+        self._carry_hi = 0
 
-    def set_optimizer(self, fn) -> None:
+    def set_optimizer(self, fn, carry_hi: int = 0) -> None:
         """Apply ``fn(lo, hi)`` (an optimizer update of arena elements [lo, hi), enqueued on
         the current stream) to each bucket right behind its collective, for THIS step only
         (:meth:`finish` clears it). Call before backward, on the stream that runs it (the
-        ranges wait for that stream's progress; a hook may fire on a side stream)."""
+        ranges wait for that stream's progress; a hook may fire on a side stream).
+
+        ``carry_hi`` (GPU): buckets lying wholly inside arena [0, carry_hi) (the FC head and the
+        recurrent layers >= 1) get no update here; an event behind each one's collective is kept
+        instead (:meth:`take_carried`) and the Trainer applies their updates beside the next
+        step's forward recurrences, as on one device (Trainer defer_update): the per-bucket
+        ranges then no longer stream beside the BPTTs."""
         if self.enabled:
             self._opt = fn
             if self.arena.grad.is_cuda:
                 self._main_stream = torch.cuda.current_stream(self.arena.grad.device)
+                self._carry_hi = int(carry_hi)
+
+    def take_carried(self) -> List[Tuple[int, int, "torch.cuda.Event"]]:
+        """(lo, hi, event behind the collective) of the buckets whose update was carried."""
+        c, self._carried = self._carried, []
+        return c
 
     def _flush_updates(self) -> None:
         """Issue the pending buckets' optimizer ranges behind their collectives (ordering
@@ -167,7 +182,12 @@ class GradBucketer:
                 waits[b].wait()                  # the ordering stream waits for the collective
                 if self.compress:
                     self.arena.grad[s:e].copy_(self._shadow[b])
-                self._opt(s, e)
+                if e <= self._carry_hi:
+                    ev = torch.cuda.Event()
+                    ev.record(os_)               # the reduced gradient is final here
+                    self._carried.append((s, e, ev))
+                else:
+                    self._opt(s, e)
 
     def _launch(self, b: int) -> None:
         if self._launched[b]:

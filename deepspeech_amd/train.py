@@ -62,6 +62,11 @@ def collapse_batch_labels(batch):
 def build_data(args, ctx, train_dir):
     """Returns (source with .next(), steps_per_epoch)."""
     if args.dummy:
+        if args.dummy_frames > 0:
+            # fixed-length synthetic batches (bench.py's shape) instead of the reference's walk
+            from .data.synthetic import FixedShapeBatches
+            src = FixedShapeBatches(args.batch_size, max_frames=args.dummy_frames, seed=args.seed + ctx.rank, pool=4)
+            return src, 1000
         src = DummyBucketWalk(args.batch_size, seed=args.seed + ctx.rank)
         return src, src.steps_per_epoch()
     from .data.store import StoreBatches, find_partition_files, find_store, tfrecords_to_store

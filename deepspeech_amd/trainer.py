@@ -270,6 +270,26 @@ class Trainer:
             todo.insert(0, (lambda grid: [f(grid) for f in first], []))
         self.arena.set_pending_update(todo)
 
+    def _carry_buckets(self, carried, lr_t: float, keep: float, gscale: float) -> None:
+        """Data parallel: the Adam + EMA ranges of the gradient buckets inside the head + upper
+        layers' arena range go to the next forward (one chunk per bucket, in the order the
+        forward reads their weights: highest arena offset first), each waiting for its bucket's
+        all-reduce event. Same update as the per-bucket range behind the collective."""
+        opt = self.opt
+        todo = []
+        for lo, hi, ev in sorted(carried, key=lambda c: -c[0]):
+            params = [p for p, (o, n) in zip(self.arena.params, self.arena.offsets) if lo <= o < hi]
+
+            def fn(grid, lo=lo, hi=hi, ev=ev):
+                torch.cuda.current_stream(self.arena.flat.device).wait_event(ev)
+                if grid > 0:
+                    opt.apply_range(lo, hi, lr_t, keep, gscale, max_grid=grid * _CARRY_BLOCKS_PER_CU,
+                                    lds_reserve=_CARRY_LDS if _CARRY_BLOCKS_PER_CU > 1 else 0)
+                else:
+                    opt.apply_range(lo, hi, lr_t, keep, gscale)
+            todo.append((fn, params))
+        self.arena.set_pending_update(todo)
+
     def flush(self) -> None:
         """Complete an optimizer update carried into the next step (``defer_update``): after
         this, on the current stream, the weights, Adam moments, EMA and bf16 shadows are those
@@ -468,11 +488,17 @@ class Trainer:
             one = self._seed[(loss.device, loss.dtype)] = torch.ones((), device=loss.device, dtype=loss.dtype)
         gscale = 1.0 / self.world
         per_bucket = self.bucketer.enabled and self.nan_policy != "skip" and self.per_bucket_update
+        dp_carry = (per_bucket and self.defer_update and self.arena.flat.is_cuda and self._layer_first and
+                    not torch.cuda.is_current_stream_capturing())
         if per_bucket:
             # DP-native ordering: each gradient bucket's Adam + EMA range runs on the
-            # bucketer's ordering stream right behind its all-reduce (bitwise the same update)
+            # bucketer's ordering stream right behind its all-reduce (bitwise the same update);
+            # with defer_update, the head's and upper layers' buckets carry theirs into the next
+            # forward (GradBucketer carry_hi)
+            up = self.upper_range(1) if dp_carry else None
             self.bucketer.set_optimizer(lambda lo, hi: self.opt.apply_range(lo, hi, lr_t, keep, gscale,
-                                                                            max_grid=_BUCKET_GRID))
+                                                                            max_grid=_BUCKET_GRID),
+                                        carry_hi=up[0] if up else 0)
         early = (not per_bucket and self.nan_policy != "skip" and self._early_split > 0 and lazy and
                  self.arena.wgrad.grouped and self.arena.wgrad.defer_input)
         carry = early and self.defer_update and not torch.cuda.is_current_stream_capturing()
@@ -510,7 +536,11 @@ class Trainer:
         if lazy:
             self.arena.zero_unwritten()
         with TR.phase(TR.ALLREDUCE):
+            carried_buckets = self.bucketer.take_carried() if per_bucket else []
             self.bucketer.finish()
+            carried_buckets += self.bucketer.take_carried() if per_bucket else []
+        if carried_buckets:
+            self._carry_buckets(carried_buckets, lr_t, keep, gscale)
         if early:
             with TR.phase(TR.EMA):
                 # the upper range [0, usplit) may have been applied beside layer 0's BPTT even

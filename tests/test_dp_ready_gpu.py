@@ -94,3 +94,40 @@ def test_dp_machinery_world1_matches_plain_step(cuda, H, layers, fp8, N, split_a
         assert (outs[0][2] != outs[1][2]).float().mean() < 1e-3     # bf16 shadows: rare 1-ulp flips
     finally:
         shutdown(ctx)           # later GPU tests must not run with a live RCCL group
+
+
+@pytest.mark.parametrize("H,layers,N,mb", [(128, 3, 8, 1.0), (800, 5, 32, 32.0)])
+def test_dp_carried_bucket_updates_bitwise(cuda, H, layers, N, mb):
+    """Data parallel + defer_update (world size 1 over RCCL, force_buckets): the head's and upper
+    layers' bucket updates go to the next forward (waiting for their all-reduce events), the
+    rest stay behind their collectives. 6 steps over two shapes: bitwise the per-bucket run."""
+    import copy
+    from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.parallel.dist import init_distributed, shutdown
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    ctx = init_distributed("cuda", force_group=True)
+    try:
+        torch.manual_seed(3)
+        base = DeepSpeech2(num_filters=32, num_hidden=H, num_rnn_layers=layers, cell="gru").to(cuda)
+        bs = [to_device(FixedShapeBatches(N, max_frames=T, seed=T, pool=1).next(), cuda) for T in (300, 1000)]
+        outs, losses = [], []
+        for carry in (False, True):
+            m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+            tr = Trainer(m, LRSchedule(1e-3, 2, 0.5), force_buckets=True, defer_update=carry,
+                         bucket_mb=mb)
+            ls = []
+            for i in range(6):
+                ls.append(float(tr.step(bs[i % 2])))
+                if carry and i == 0:
+                    assert tr.arena.has_pending_update()     # something really was carried
+            tr.flush()
+            torch.cuda.synchronize()
+            losses.append(ls)
+            outs.append((tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone(),
+                         tr.arena.p16.clone()))
+        assert losses[0] == losses[1]
+        for x, y in zip(*outs):
+            assert torch.equal(x, y), (x.float() - y.float()).abs().max()
+    finally:
+        shutdown(ctx)
