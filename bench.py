@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--force_dp", action="store_true",
                    help="run the data-parallel machinery (process group, gradient buckets, "
                         "collectives on the ordering stream) even on one GPU, to time its overhead")
+    p.add_argument("--dp_graphs", action="store_true",
+                   help="data parallel: the epoch walk's per-shape step graphs capture the bucketed "
+                        "step too (Trainer dp_graphs)")
     p.add_argument("--no_infer", action="store_true",
                    help="skip the streaming-inference RTF measured after the training timing "
                         "(BASELINE metric's inference half; rank 0, outside the timed region)")
@@ -119,7 +122,7 @@ def main():
     trainer = Trainer(model, LRSchedule(1e-4, 10 ** 9, 0.9), moving_avg_decay=0.9999,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
                       allreduce_bf16=args.allreduce_bf16, force_buckets=args.force_dp,
-                      defer_update=not args.no_defer_update)
+                      defer_update=not args.no_defer_update, dp_graphs=args.dp_graphs)
     feed = FixedShapeBatches(args.batch_size, max_frames=args.frames, seed=1000 + ctx.rank, pool=4)
     batches = [to_device(feed.next(), dev) for _ in range(4)]
     audio_per_step = [float(b["seq_lens"].sum().item()) / 100.0 for b in batches]

@@ -131,6 +131,11 @@ def build_train_parser() -> argparse.ArgumentParser:
                    help="single-GPU HIP engine: replay each batch shape's captured training step "
                         "(HIP graph) instead of launching it eagerly; auto: time both once per "
                         "shape and keep the faster (trainer.py _graph_step)")
+    p.add_argument("--dp_step_graphs", type=str2bool, default=False,
+                   help="data parallel over RCCL: --step_graphs also captures the bucketed step "
+                        "(all-reduces and per-bucket optimizer ranges inside the graph; trainer.py "
+                        "graphs_active). Checked bitwise at world size 1; off by default until "
+                        "measured at world size > 1")
     p.add_argument("--bucket_mb", type=float, default=32.0,
                    help="gradient all-reduce bucket size (MB) for data parallel")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", choices=["fp32", "bf16"])

@@ -185,6 +185,12 @@ int ds2_col_sum(int n, const float* const* in, float* const* out, const int* R, 
                 const int* acc, hipStream_t st);
 int ds2_fc_bias_grad(const void* G, int M, int ldg, int K, const float* scale, float alpha, float* out, int acc,
                      hipStream_t st);
+int ds2_ctc_beam(const float* lp, const int* frames, int T, int B, int K, int W, int blank, float prune, int* node,
+                 int* last, int* parent, float* pb, float* pnb, int* nbeam, void* nodes, int* nnodes, int cap,
+                 unsigned* err, hipStream_t st);
+int ds2_ctc_beam_backtrack(const void* nodes, int cap, const int* node, const int* nbeam, const float* pb,
+                           const float* pnb, int B, int W, int* out, int* out_len, float* score, int Lcap,
+                           hipStream_t st);
 int ds2_ctc_greedy(const void* logits, int bf16, const int* lens, int T, int N, int K, int blank,
                    int* labels, int* counts, float* score, hipStream_t st);
 size_t ds2_conv2_fwd_smem(int F1);
@@ -1074,6 +1080,72 @@ void col_sum(std::vector<at::Tensor> ins, std::vector<at::Tensor> outs, std::vec
   check(ds2_col_sum((int)ins.size(), ip, op, R, B, C, a, cur_stream()), "col_sum");
 }
 
+// CTC prefix beam search (csrc/beam.hip): advance the device-resident beams of B streams by the
+// frames of lp [T, B, K] (fp32 log-probs; frames [B] int32 per-stream frame counts, or all T)
+static void beam_state_check(const at::Tensor& node, const at::Tensor& last, const at::Tensor& parent,
+                             const at::Tensor& pb, const at::Tensor& pnb, const at::Tensor& nbeam,
+                             const at::Tensor& nodes, const at::Tensor& nnodes, int64_t B) {
+  for (const at::Tensor* t : {&node, &last, &parent, &pb, &pnb, &nbeam, &nodes, &nnodes}) {
+    need_gpu(*t, "beam state");
+    TORCH_CHECK(t->is_contiguous() && t->size(0) == B, "beam state: contiguous, leading dim B");
+  }
+  const int64_t W = node.size(1);
+  for (const at::Tensor* t : {&node, &last, &parent, &nbeam, &nodes, &nnodes})
+    TORCH_CHECK(t->scalar_type() == at::kInt, "beam state: int32 node / label / count tensors");
+  TORCH_CHECK(pb.scalar_type() == at::kFloat && pnb.scalar_type() == at::kFloat, "beam state: fp32 scores");
+  TORCH_CHECK(node.dim() == 2 && last.sizes() == node.sizes() && parent.sizes() == node.sizes() &&
+                  pb.sizes() == node.sizes() && pnb.sizes() == node.sizes() && W >= 1 && W <= 32,
+              "beam state: [B, W] tensors, 1 <= W <= 32");
+  TORCH_CHECK(nodes.dim() == 3 && nodes.size(2) == 2, "beam state: nodes [B, cap, 2]");
+  TORCH_CHECK(nbeam.numel() == B && nnodes.numel() == B, "beam state: nbeam / nnodes [B]");
+}
+
+void ctc_beam(at::Tensor lp, OptT frames, int64_t blank, double prune, at::Tensor node, at::Tensor last,
+              at::Tensor parent, at::Tensor pb, at::Tensor pnb, at::Tensor nbeam, at::Tensor nodes,
+              at::Tensor nnodes, at::Tensor err) {
+  need_gpu(lp, "lp");
+  TORCH_CHECK(lp.dim() == 3 && lp.scalar_type() == at::kFloat && lp.is_contiguous(),
+              "ctc_beam: lp must be contiguous fp32 [T, B, K]");
+  const int64_t T = lp.size(0), B = lp.size(1), K = lp.size(2);
+  TORCH_CHECK(K >= 2 && K <= 64 && blank >= 0 && blank < K, "ctc_beam: 2 <= K <= 64, 0 <= blank < K");
+  beam_state_check(node, last, parent, pb, pnb, nbeam, nodes, nnodes, B);
+  need_gpu(err, "err");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "ctc_beam: err int32 [1]");
+  const int* fr = nullptr;
+  if (frames) {
+    need_gpu(*frames, "frames");
+    TORCH_CHECK(frames->scalar_type() == at::kInt && frames->is_contiguous() && frames->numel() == B,
+                "ctc_beam: frames int32 [B]");
+    fr = frames->data_ptr<int>();
+  }
+  check(ds2_ctc_beam(lp.data_ptr<float>(), fr, (int)T, (int)B, (int)K, (int)node.size(1), (int)blank, (float)prune,
+                     node.data_ptr<int>(), last.data_ptr<int>(), parent.data_ptr<int>(), pb.data_ptr<float>(),
+                     pnb.data_ptr<float>(), nbeam.data_ptr<int>(), nodes.data_ptr(), nnodes.data_ptr<int>(),
+                     (int)nodes.size(1), reinterpret_cast<unsigned*>(err.data_ptr<int>()), cur_stream()),
+        "ctc_beam");
+}
+
+// labels [B, W, Lcap] (back-aligned prefix walk: the first out_len entries), out_len [B, W] (-1:
+// no hypothesis), score [B, W] of the device beams
+void ctc_beam_backtrack(at::Tensor node, at::Tensor last, at::Tensor parent, at::Tensor pb, at::Tensor pnb,
+                        at::Tensor nbeam, at::Tensor nodes, at::Tensor nnodes, at::Tensor out, at::Tensor out_len,
+                        at::Tensor score) {
+  const int64_t B = node.size(0), W = node.size(1);
+  beam_state_check(node, last, parent, pb, pnb, nbeam, nodes, nnodes, B);
+  need_gpu(out, "out");
+  need_gpu(out_len, "out_len");
+  need_gpu(score, "score");
+  TORCH_CHECK(out.dim() == 3 && out.size(0) == B && out.size(1) == W && out.scalar_type() == at::kInt &&
+                  out.is_contiguous(), "ctc_beam_backtrack: out int32 [B, W, L]");
+  TORCH_CHECK(out_len.numel() == B * W && out_len.scalar_type() == at::kInt && out_len.is_contiguous() &&
+                  score.numel() == B * W && score.scalar_type() == at::kFloat && score.is_contiguous(),
+              "ctc_beam_backtrack: out_len int32 / score fp32 [B, W]");
+  check(ds2_ctc_beam_backtrack(nodes.data_ptr(), (int)nodes.size(1), node.data_ptr<int>(), nbeam.data_ptr<int>(),
+                               pb.data_ptr<float>(), pnb.data_ptr<float>(), (int)B, (int)W, out.data_ptr<int>(),
+                               out_len.data_ptr<int>(), score.data_ptr<float>(), (int)out.size(2), cur_stream()),
+        "ctc_beam_backtrack");
+}
+
 // out[k] (= or +=) scale[0] * alpha * sum_m G[m, k] for k < K (G bf16 [M, ldg] with unit column
 // stride, scale a device fp32 scalar): the FC head's bias gradient (csrc/reduce.hip)
 void fc_bias_grad(at::Tensor G, int64_t K, at::Tensor scale, double alpha, at::Tensor out, bool acc) {
@@ -1566,6 +1638,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("col_sum", &col_sum);
   m.def("wait_resident", &wait_resident);
   m.def("fc_bias_grad", &fc_bias_grad);
+  m.def("ctc_beam", &ctc_beam);
+  m.def("ctc_beam_backtrack", &ctc_beam_backtrack);
   m.def("event_new", &event_new, py::arg("flags") = 0);
   m.def("arm_stop_event", &arm_stop_event);
   m.def("disarm_stop_event", &disarm_stop_event);

@@ -13,8 +13,10 @@ arrives:
   * recurrent stack: every layer carries its final hidden state to the next chunk (the
     persistent kernels start from an initial state: ops/rnn.py:recurrent_layer_infer);
   * head + log-softmax per new frame; greedy decoding collapses across chunk boundaries
-    incrementally, and the prefix beam search (native runtime, one host thread per stream
-    group) also advances chunk by chunk, so a transcript is ready when the audio ends.
+    incrementally, and the prefix beam search also advances chunk by chunk, so a transcript is
+    ready when the audio ends: on the GPU the beams stay on the device (csrc/beam.hip, one
+    launch per chunk, no log-prob copy), on the CPU the native runtime runs it (one host
+    thread per stream group).
 
 Batched streams: ``StreamingRecognizer`` takes [B, T_chunk, F] chunks of B concurrent
 streams (equal chunk schedule, per-stream valid lengths), which is how a server batches.
@@ -72,9 +74,14 @@ class StreamingRecognizer:
                 h.zero_()
         self.logprobs: List[torch.Tensor] = []
         self.beams = None
+        self.gbeams = None
         if self.decoder == "beam":
-            from .runtime import native
-            self.beams = native.load().BatchBeamSearch(self.B, self.beam_width, BLANK, -10.0)
+            from .ops.decode import GpuBeamSearch
+            if self.dev.type == "cuda" and self.beam_width <= GpuBeamSearch.MAX_BEAM:
+                self.gbeams = GpuBeamSearch(self.B, self.beam_width, BLANK, -10.0, self.dev)
+            else:
+                from .runtime import native
+                self.beams = native.load().BatchBeamSearch(self.B, self.beam_width, BLANK, -10.0)
         self.last_sym = [-1] * self.B
         self.greedy: List[List[int]] = [[] for _ in range(self.B)]
         self.compute_s = 0.0
@@ -113,7 +120,10 @@ class StreamingRecognizer:
         assert lp.shape[0] == new, (lp.shape, new)
         self.logprobs.append(lp)
         best = best_t.cpu().numpy()                            # [new, B]
-        if self.beams is not None:
+        if self.gbeams is not None:
+            # prefix beam search advances chunk by chunk, beams resident on the device
+            self.gbeams.feed(lp)
+        elif self.beams is not None:
             # prefix beam search advances chunk by chunk (beams carried in the native
             # runtime, streams decoded on parallel host threads)
             self.beams.feed(lp.cpu().numpy(), np.full((self.B,), new, dtype=np.int32))
@@ -194,6 +204,8 @@ class StreamingRecognizer:
     def finish(self) -> List[List[int]]:
         """Final transcript label ids per stream (beam search over the whole stream if the
         decoder is 'beam', otherwise the incremental greedy result)."""
+        if self.gbeams is not None:
+            return self.gbeams.best()
         if self.beams is None:
             return [list(g) for g in self.greedy]
         return self.beams.best()

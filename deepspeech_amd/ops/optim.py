@@ -216,6 +216,9 @@ class ParamArena:
         if not lazy:
             self.grad.zero_()
         self._written.clear()
+        if self._ready_events is not None:
+            self._ready_next = 0
+            self._ready_events = [None] * len(self.params)
         # re-attach in case an op replaced a .grad (e.g. set_to_none elsewhere)
         for p, (o, n) in zip(self.params, self.offsets):
             if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():
@@ -251,13 +254,16 @@ class ParamArena:
     def grad_done(self, *params) -> None:
         """Report gradients written straight into ``main_grad`` (fires bucket hooks). Call
         right after enqueueing the write, on the stream that carries it."""
+        idx = []
         for p in params:
             if p is None:
                 continue
             self._written.add(id(p))
             self._known_zero.discard(id(p))
-            i = self._index[id(p)]
-            self.record_ready(i)
+            idx.append(self._index[id(p)])
+        # one ready event for the whole call (the same enqueued work produced them all)
+        self.record_ready(*idx)
+        for i in idx:
             for cb in self._ready_cbs:
                 cb(i)
 
@@ -266,7 +272,11 @@ class ParamArena:
 
     def enable_ready_events(self) -> None:
         if self.grad.is_cuda and self._ready_events is None:
-            self._ready_events = [torch.cuda.Event() for _ in self.params]
+            # per parameter: the event of the record that covered it this step, drawn from a pool
+            # reused every step (a wait enqueued earlier keeps the record it saw)
+            self._ready_events = [None] * len(self.params)
+            self._ready_pool = []
+            self._ready_next = 0
             self._ready_seq = 0
             self._ready_at = [(0, 0)] * len(self.params)   # (record order, stream) per parameter
 
@@ -275,18 +285,29 @@ class ParamArena:
         written: per recording stream, the latest-recorded member (streams run in order)."""
         last = {}
         for i in idx:
+            if self._ready_events[i] is None:      # marked written, produced by a later launch
+                continue
             seq, st = self._ready_at[i]
             if st not in last or seq > last[st][0]:
                 last[st] = (seq, i)
         return [self._ready_events[i] for _, i in last.values()]
 
-    def record_ready(self, i: int) -> None:
-        """Mark parameter i's gradient as produced by the work enqueued so far on the
-        current stream."""
-        if self._ready_events is not None:
-            self._ready_events[i].record()
-            self._ready_seq += 1
-            self._ready_at[i] = (self._ready_seq, torch.cuda.current_stream(self.grad.device).cuda_stream)
+    def record_ready(self, *idx: int) -> None:
+        """Mark the gradients of parameters ``idx`` as produced by the work enqueued so far on
+        the current stream: ONE event record for all of them (each record is a marker packet
+        in the stream's queue)."""
+        if self._ready_events is None or not idx:
+            return
+        if self._ready_next == len(self._ready_pool):
+            self._ready_pool.append(torch.cuda.Event())
+        ev = self._ready_pool[self._ready_next]
+        self._ready_next += 1
+        ev.record()
+        self._ready_seq += 1
+        at = (self._ready_seq, torch.cuda.current_stream(self.grad.device).cuda_stream)
+        for i in idx:
+            self._ready_events[i] = ev
+            self._ready_at[i] = at
 
     def ready_event(self, i: int) -> Optional["torch.cuda.Event"]:
         return self._ready_events[i] if self._ready_events is not None else None

@@ -296,6 +296,10 @@ def _gate(census: Optional[torch.Tensor], plan: Optional["RnnPlan"]) -> None:
     census word, slot ngroups * P - 1 (the buffer may be longer: wide plans use P = H / 64)."""
     if not (_RESIDENCY_GATE and census is not None and census.is_cuda and plan is not None and plan.kind == "xcd"):
         return
+    if torch.cuda.is_current_stream_capturing():
+        # a replayed graph orders its nodes itself (one queue, DEBUG_HIP_FORCE_GRAPH_QUEUES):
+        # a spin on a launch the replay may issue after it would only wait for its timeout
+        return
     last = plan.ndir * plan.BG * _xcd_p(plan.H, plan.cell) - 1
     if 0 <= last < census.numel():
         _ext.ext().wait_resident(census[last:last + 1], _GATE_TICKS)

@@ -153,6 +153,16 @@ class GradBucketer:
                 self._main_stream = torch.cuda.current_stream(self.arena.grad.device)
                 self._carry_hi = int(carry_hi)
 
+    def capturable(self) -> bool:
+        """True when this bucketer's collectives can be captured into a HIP graph (RCCL
+        process group, GPU gradients; gloo runs its collectives on the host)."""
+        if not (self.enabled and self.arena.grad.is_cuda and self._order_stream is not None):
+            return False
+        try:
+            return dist.get_backend(self.pg) == "nccl"
+        except (RuntimeError, ValueError):
+            return False
+
     def take_carried(self) -> List[Tuple[int, int, "torch.cuda.Event"]]:
         """(lo, hi, event behind the collective) of the buckets whose update was carried."""
         c, self._carried = self._carried, []
@@ -173,13 +183,15 @@ class GradBucketer:
         for b in pend:
             s, e, _ = self.buckets[b]
             if os_ is None:
-                waits[b].wait()
+                if waits[b] is not None:
+                    waits[b].wait()
                 if self.compress:
                     self.arena.grad[s:e].copy_(self._shadow[b])
                 self._opt(s, e)
                 continue
             with torch.cuda.stream(os_):
-                waits[b].wait()                  # the ordering stream waits for the collective
+                if waits[b] is not None:
+                    waits[b].wait()              # the ordering stream waits for the collective
                 if self.compress:
                     self.arena.grad[s:e].copy_(self._shadow[b])
                 if e <= self._carry_hi:
@@ -218,14 +230,24 @@ class GradBucketer:
             self._flush_updates()                # this bucket's readers are enqueued already
 
     def _collective(self, b: int, g: torch.Tensor):
+        # under HIP-graph capture (Trainer dp_graphs) the blocking form: the issuing (ordering)
+        # stream itself is ordered behind the collective, and there is no Work to wait on. An
+        # async_op collective issued from a side stream during capture crashes this image's
+        # ProcessGroupNCCL at issue (tools/probe_rccl_graph.py: "async" / "side_async_norec"
+        # segfault, "side_sync" / "main_async" / "sync" capture and replay correctly)
+        capturing = g.is_cuda and torch.cuda.is_current_stream_capturing()
+        t = g
         if self.compress:
             sh = self._shadow[b]
             if sh is None or sh.numel() != g.numel():
                 sh = torch.empty(g.numel(), device=g.device, dtype=torch.bfloat16)
                 self._shadow[b] = sh
             sh.copy_(g)
-            return dist.all_reduce(sh, group=self.pg, async_op=True)
-        return dist.all_reduce(g, group=self.pg, async_op=True)
+            t = sh
+        if capturing:
+            dist.all_reduce(t, group=self.pg)
+            return None
+        return dist.all_reduce(t, group=self.pg, async_op=True)
 
     def finish(self) -> None:
         """Launch buckets whose params got no gradient (in index order on every rank),
@@ -246,8 +268,12 @@ class GradBucketer:
                 self._main_stream.wait_stream(self._order_stream)
             self.prepare()
             return
+        if self._order_stream is not None and any(w is None for _, w in self._works):
+            # captured blocking collectives ordered the ordering stream only
+            torch.cuda.current_stream(self.arena.grad.device).wait_stream(self._order_stream)
         for b, w in self._works:
-            w.wait()
+            if w is not None:
+                w.wait()
             if self.compress:
                 s, e, _ = self.buckets[b]
                 self.arena.grad[s:e].copy_(self._shadow[b])

@@ -188,7 +188,7 @@ def main(argv=None) -> int:
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
                       allreduce_bf16=args.allreduce_dtype == "bf16", nan_policy=args.nan_policy,
                       step_graphs={"auto": "auto", "on": True, "off": False}[args.step_graphs],
-                      defer_update=True)
+                      defer_update=True, dp_graphs=args.dp_step_graphs)
     start = 0
     rdir = resume_dir(args)
     if rdir is not None:

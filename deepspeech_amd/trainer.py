@@ -112,6 +112,13 @@ def _check_hw_queues() -> None:
                       "call deepspeech_amd.utils.setenvs.setenvs() before anything initialises HIP" % q)
 
 
+def _long_sequence(batch: Dict[str, torch.Tensor]) -> bool:
+    """True when the batch's recurrence runs >= ops/rnn.py _PARTIAL_MIN_T steps."""
+    from .models.deepspeech2 import conv_out_len
+    from .ops import rnn as RNN
+    return conv_out_len(int(batch["feats"].shape[1]))[1] >= RNN._PARTIAL_MIN_T
+
+
 @dataclass
 class _ShapeState:
     seen: int = 0
@@ -129,14 +136,19 @@ class _StepGraph:
     labels: torch.Tensor
     label_lens: torch.Tensor
     loss: torch.Tensor
+    ptrs: tuple = ()          # the state buffers the graph was captured on (Trainer._state_ptrs)
 
 
 class Trainer:
     def __init__(self, model: DeepSpeech2, lr_schedule: LRSchedule, moving_avg_decay: Optional[float] = 0.9999,
                  world_size: int = 1, bucket_mb: float = 32.0, allreduce_bf16: bool = False,
                  nan_policy: str = "abort", collapse_repeated: bool = False, force_buckets: bool = False,
-                 step_graphs=False, graph_warmup: int = 2, bucket_split_after=(), defer_update: bool = False):
+                 step_graphs=False, graph_warmup: int = 2, bucket_split_after=(), defer_update: bool = False,
+                 dp_graphs: bool = False):
         self.model = model
+        # data parallel: capture the bucketed step too (RCCL all-reduces and the per-bucket
+        # optimizer ranges inside the shape's graph); opt-in, see graphs_active()
+        self.dp_graphs = bool(dp_graphs)
         # carry the optimizer update of the FC head and recurrent layers >= 1 into the next
         # step's forward (see _body); readers of the weights between steps call flush()
         self.defer_update = bool(defer_update)
@@ -302,12 +314,24 @@ class Trainer:
         return self.lr_schedule(self.global_step)
 
     def graphs_active(self) -> bool:
-        """True when :meth:`step` runs captured step graphs: single device, HIP engine, no
-        gradient buckets (data parallelism keeps the eager step: its collectives are issued
-        from backward hooks as buckets fill)."""
-        return (bool(self.step_graphs) and self.arena.flat.is_cuda and self.model.engine == "hip"
-                and self.world == 1 and not self.bucketer.enabled and not _FUSED_OPT
-                and not getattr(self.model, "capture", False))     # activation taps: eager
+        """True when :meth:`step` runs captured step graphs: HIP engine on a GPU, and either one
+        device without gradient buckets, or data parallel over RCCL with ``dp_graphs``.
+
+        A data-parallel capture records the step's collectives exactly as the eager step
+        issues them: each bucket's all-reduce on the bucketer's ordering stream behind its
+        members' producer events, its Adam + EMA range behind the collective, the main stream
+        joined at the end. Bucket launch order is fixed per shape (autograd's hook order for a
+        given graph), so every rank's graph issues the same collective sequence as its eager
+        step, and ranks may even differ in eager / replay per shape (``auto``): the sequence on
+        the communicator is the same. The communicator is initialised by the shape's eager
+        warm-up steps before any capture. gloo cannot be captured: its process groups keep the
+        eager step."""
+        if not (bool(self.step_graphs) and self.arena.flat.is_cuda and self.model.engine == "hip"
+                and not _FUSED_OPT and not getattr(self.model, "capture", False)):   # taps: eager
+            return False
+        if not self.bucketer.enabled:
+            return self.world == 1
+        return self.dp_graphs and self.bucketer.capturable()
 
     def step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         # one Adam step count / EMA decay per training step, on the host, whatever runs it
@@ -399,8 +423,18 @@ class Trainer:
         st.spans.append((a, b))
         return loss
 
+    def _state_ptrs(self) -> tuple:
+        """Addresses of the buffers a captured step reads and writes in place (weights,
+        gradients, bf16 shadows, Adam moments, EMA): a replay after any of them was re-allocated
+        would write freed memory."""
+        ts = (self.arena.flat, self.arena.grad, getattr(self.arena, "p16", None), self.opt.m, self.opt.v,
+              self.opt.ema)
+        return tuple(t.data_ptr() if t is not None else 0 for t in ts)
+
     def _replay(self, g: "_StepGraph", batch: Dict[str, torch.Tensor], width: int, lr_t: float,
                 keep: float, events=None) -> torch.Tensor:
+        if g.ptrs != self._state_ptrs():
+            raise RuntimeError("step graph captured on re-allocated training state: call Trainer.drop_graphs()")
         self.flush()           # a graph never carries or consumes an update across steps
         feats, labels = batch["feats"], batch["labels"]
         pairs = [(g.feats, feats), (g.seq_lens, batch["seq_lens"]), (g.label_lens, batch["label_lens"]),
@@ -451,7 +485,8 @@ class Trainer:
         finally:
             self.opt.device_hyper = False
             sch.single_stream = False
-        return _StepGraph(graph, static["feats"], static["seq_lens"], static["labels"], static["label_lens"], loss)
+        return _StepGraph(graph, static["feats"], static["seq_lens"], static["labels"], static["label_lens"], loss,
+                          self._state_ptrs())
 
     def drop_graphs(self) -> None:
         """Forget every captured step (after anything that re-allocates the arena, optimizer
@@ -488,8 +523,11 @@ class Trainer:
             one = self._seed[(loss.device, loss.dtype)] = torch.ones((), device=loss.device, dtype=loss.dtype)
         gscale = 1.0 / self.world
         per_bucket = self.bucketer.enabled and self.nan_policy != "skip" and self.per_bucket_update
+        # (sequences of >= _PARTIAL_MIN_T recurrence steps only: beside a short recurrence the
+        # carried ranges, capped to its idle CUs, outlast it and the projections wait for them)
         dp_carry = (per_bucket and self.defer_update and self.arena.flat.is_cuda and self._layer_first and
-                    not torch.cuda.is_current_stream_capturing())
+                    not torch.cuda.is_current_stream_capturing() and
+                    _long_sequence(batch))
         if per_bucket:
             # DP-native ordering: each gradient bucket's Adam + EMA range runs on the
             # bucketer's ordering stream right behind its all-reduce (bitwise the same update);

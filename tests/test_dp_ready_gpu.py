@@ -100,7 +100,8 @@ def test_dp_machinery_world1_matches_plain_step(cuda, H, layers, fp8, N, split_a
 def test_dp_carried_bucket_updates_bitwise(cuda, H, layers, N, mb):
     """Data parallel + defer_update (world size 1 over RCCL, force_buckets): the head's and upper
     layers' bucket updates go to the next forward (waiting for their all-reduce events), the
-    rest stay behind their collectives. 6 steps over two shapes: bitwise the per-bucket run."""
+    rest stay behind their collectives; only for long sequences. 6 steps over two shapes:
+    bitwise the per-bucket run."""
     import copy
     from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
     from deepspeech_amd.models import DeepSpeech2
@@ -119,14 +120,51 @@ def test_dp_carried_bucket_updates_bitwise(cuda, H, layers, N, mb):
             ls = []
             for i in range(6):
                 ls.append(float(tr.step(bs[i % 2])))
-                if carry and i == 0:
-                    assert tr.arena.has_pending_update()     # something really was carried
+                if carry:
+                    # carried after the 1000-frame steps only (>= 200 recurrence steps)
+                    assert tr.arena.has_pending_update() == (i % 2 == 1)
             tr.flush()
             torch.cuda.synchronize()
             losses.append(ls)
             outs.append((tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone(),
                          tr.arena.p16.clone()))
         assert losses[0] == losses[1]
+        for x, y in zip(*outs):
+            assert torch.equal(x, y), (x.float() - y.float()).abs().max()
+    finally:
+        shutdown(ctx)
+
+
+def test_dp_step_graphs_bitwise_eager(cuda):
+    """The data-parallel step captured into per-shape HIP graphs (Trainer dp_graphs: RCCL
+    all-reduces, per-bucket Adam + EMA and the ordering stream inside the graph) at world size 1
+    over RCCL: 10 steps over two shapes, bitwise the eager --force_dp step in losses, weights,
+    Adam moments, EMA and bf16 shadows."""
+    import copy
+    from deepspeech_amd.data.synthetic import FixedShapeBatches, to_device
+    from deepspeech_amd.models import DeepSpeech2
+    from deepspeech_amd.parallel.dist import init_distributed, shutdown
+    from deepspeech_amd.trainer import LRSchedule, Trainer
+    ctx = init_distributed("cuda", force_group=True)
+    try:
+        torch.manual_seed(5)
+        base = DeepSpeech2(num_filters=32, num_hidden=256, num_rnn_layers=3, cell="gru").to(cuda)
+        bs = [to_device(FixedShapeBatches(16, max_frames=T, seed=T, pool=1).next(), cuda) for T in (100, 300)]
+        outs, losses = [], []
+        for graphs in (False, True):
+            m = copy.deepcopy(base).set_engine("hip", torch.bfloat16)
+            tr = Trainer(m, LRSchedule(1e-3, 3, 0.5), force_buckets=True, bucket_mb=1.0,
+                         step_graphs=graphs, dp_graphs=graphs, graph_warmup=1, defer_update=True)
+            assert tr.graphs_active() == graphs
+            ls = [float(tr.step(bs[(i // 2) % 2])) for i in range(10)]
+            if graphs:
+                assert len(tr._graphs) == 2                   # both shapes captured and replayed
+            tr.flush()
+            torch.cuda.synchronize()
+            losses.append(ls)
+            outs.append((tr.arena.flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(), tr.opt.ema.clone(),
+                         tr.arena.p16.clone()))
+        assert losses[0] == losses[1], losses
         for x, y in zip(*outs):
             assert torch.equal(x, y), (x.float() - y.float()).abs().max()
     finally:
