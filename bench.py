@@ -56,6 +56,10 @@ def parse():
     p.add_argument("--force_dp", action="store_true",
                    help="run the data-parallel machinery (process group, gradient buckets, "
                         "collectives on the ordering stream) even on one GPU, to time its overhead")
+    p.add_argument("--step_graphs", action="store_true",
+                   help="time the captured step (HIP step graphs; with --force_dp / N > 1 the "
+                        "bucketed step, Trainer dp_graphs) instead of the eager one: the short "
+                        "SortaGrad lengths (--frames 100) are host-bound eagerly")
     p.add_argument("--dp_graphs", action="store_true",
                    help="data parallel: the epoch walk's per-shape step graphs capture the bucketed "
                         "step too (Trainer dp_graphs)")
@@ -74,6 +78,8 @@ def parse():
                    help="with the carried update, keep the upper layers' dU GEMMs beside the next BPTT (A/B)")
     p.add_argument("--no_gate", action="store_true",
                    help="side-stream work beside a persistent recurrence without the residency gate (A/B)")
+    p.add_argument("--no_proj_beside", action="store_true",
+                   help="A/B: projections keep the whole grid while a carried dU GEMM runs beside")
     p.add_argument("--carry_blocks", type=int, default=0,
                    help="blocks per idle CU of the carried optimizer chunks (A/B; 0: the default)")
     p.add_argument("--fp8", action="store_true",
@@ -116,13 +122,16 @@ def main():
         _T._CARRY_DU = False
     if args.no_gate:
         RNN._RESIDENCY_GATE = False
+    if args.no_proj_beside:
+        RNN._PROJ_BESIDE = False
     if args.carry_blocks:
         import deepspeech_amd.trainer as _T
         _T._CARRY_BLOCKS_PER_CU, _T._CARRY_LDS = args.carry_blocks, 32768
     trainer = Trainer(model, LRSchedule(1e-4, 10 ** 9, 0.9), moving_avg_decay=0.9999,
                       world_size=ctx.world_size, bucket_mb=args.bucket_mb,
                       allreduce_bf16=args.allreduce_bf16, force_buckets=args.force_dp,
-                      defer_update=not args.no_defer_update, dp_graphs=args.dp_graphs)
+                      defer_update=not args.no_defer_update, dp_graphs=args.dp_graphs or args.step_graphs,
+                      step_graphs=bool(args.step_graphs))
     feed = FixedShapeBatches(args.batch_size, max_frames=args.frames, seed=1000 + ctx.rank, pool=4)
     batches = [to_device(feed.next(), dev) for _ in range(4)]
     audio_per_step = [float(b["seq_lens"].sum().item()) / 100.0 for b in batches]

@@ -76,6 +76,7 @@ class ParamArena:
         # the producers of its bucket instead of joining whole streams
         self._ready_events: Optional[List[torch.cuda.Event]] = None
         self._written = set()
+        self._held = set()         # gradients a queued (deferred) GEMM will report
         self._known_zero = set()
         for i, (p, (o, n)) in enumerate(zip(self.params, self.offsets)):
             self.flat[o:o + n].copy_(p.data.reshape(-1).float())
@@ -95,6 +96,7 @@ class ParamArena:
         self._update_events: Dict[int, "torch.cuda.Event"] = {}
         self._event_pool: List["torch.cuda.Event"] = []
         self._event_next = 0
+        self._gemm_beside = False          # a carried weight-gradient GEMM went out this step
 
     # ---- deferred optimizer update ----------------------------------------------------
     def set_pending_update(self, chunks) -> None:
@@ -140,11 +142,17 @@ class ParamArena:
             for fn, params in take:
                 fn(grid)
                 if not params:
+                    self._gemm_beside = True
                     continue
                 ev = self._event()
                 ev.record(side)
                 for p in params:
                     self._update_events[id(p)] = ev
+
+    def carried_gemm_beside(self) -> bool:
+        """True once a carried weight-gradient GEMM was issued beside this step's forward (it
+        may still hold the CUs the recurrence left idle; ops/rnn.py _proj_grid)."""
+        return self._gemm_beside
 
     def await_params(self, *params) -> None:
         """Make the current stream wait for the carried update of ``params`` (no-op when none
@@ -174,6 +182,7 @@ class ParamArena:
         chunks nothing issued yet here, and wait for every chunk still in flight. After this
         the master weights, bf16 shadows, Adam moments and EMA are those of the last step."""
         take, self._pending_chunks = self._pending_chunks, []
+        self._gemm_beside = False
         for fn, _ in take:
             fn(0)
         if self._update_events:
@@ -216,6 +225,7 @@ class ParamArena:
         if not lazy:
             self.grad.zero_()
         self._written.clear()
+        self._held.clear()
         if self._ready_events is not None:
             self._ready_next = 0
             self._ready_events = [None] * len(self.params)
@@ -237,6 +247,17 @@ class ParamArena:
 
     def set_known_zero(self, p) -> None:
         self._known_zero.add(id(p))
+
+    def hold_report(self, *params) -> None:
+        """These gradients are produced by a GEMM queued for later (weight-gradient deferral):
+        autograd's post-accumulate hook, which fires when the op returns, must not count them
+        as ready; the queued GEMM reports them (:meth:`grad_done`) once it is enqueued."""
+        for p in params:
+            if p is not None:
+                self._held.add(id(p))
+
+    def held(self, p) -> bool:
+        return id(p) in self._held
 
     def mark_written(self, *params) -> None:
         """Count these gradients as produced this step without reporting them (a GEMM carried

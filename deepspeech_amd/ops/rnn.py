@@ -319,8 +319,27 @@ def _stamps(kind: str, plan: "RnnPlan", grid: int, dev) -> Optional[torch.Tensor
     return t
 
 
+_PROJ_BESIDE = True   # projection grid = the CUs a carried dU GEMM leaves (see _proj_grid)
+
+
+def _proj_grid(arena, plan: "RnnPlan", M: int, Nout: int, dev: torch.device) -> int:
+    """Grid cap of a projection GEMM (256 x 256 tiles) launched while a carried dU GEMM
+    (Trainer defer_update) still holds the CUs the previous recurrence left idle: the other
+    CUs, when that costs no extra round of tiles (headline: 589 tiles are 3 rounds on 256 CUs
+    and on 200). Uncapped, the projection's workgroups queued behind the dU GEMM finish a
+    third of a tile round late (in-step projection ~120 us against ~92 us alone). 0 = no cap."""
+    if not (_PROJ_BESIDE and arena is not None and arena.carried_gemm_beside()):
+        return 0
+    cus, carry = _cus(dev), _idle_cus(plan, dev)
+    if carry <= 0 or cus <= carry:
+        return 0
+    tiles = -(-M // 256) * -(-Nout // 256)
+    g = cus - carry
+    return g if -(-tiles // g) == -(-tiles // cus) else 0
+
+
 def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], alpha: float,
-            fill=None) -> torch.Tensor:
+            fill=None, max_grid: int = 0) -> torch.Tensor:
     """gx = alpha * x2 W16^T + b16 (bf16): the hand-written MFMA GEMM (csrc/gemm.hip) with the
     sequence-BN scale and the bias fused in its epilogue; library GEMM only for shapes the
     kernel does not cover (K % 32 != 0) or under DS2_GEMM=torch. fill: (regions, patterns) of
@@ -329,7 +348,7 @@ def _linear(x2: torch.Tensor, W16: torch.Tensor, b16: Optional[torch.Tensor], al
     N = W16.shape[0]
     if GM.enabled("proj") and x2.is_cuda:
         out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
-        if GM.matmul(x2, W16.t(), out, alpha=alpha, bias=b16, fill=fill):
+        if GM.matmul(x2, W16.t(), out, alpha=alpha, bias=b16, fill=fill, max_grid=max_grid):
             return out
     if b16 is None:
         out = torch.mm(x2, W16.t()) * alpha if alpha != 1.0 else torch.mm(x2, W16.t())
@@ -887,7 +906,8 @@ class FusedBiLayer(torch.autograd.Function):
             if fill is not None:
                 _ext.ext().multi_fill(*fill)
         else:
-            gx = _linear(x2, W16, b16, alpha, fill=fill).view(T, N, -1)
+            pg = _proj_grid(arena, plan, T * N, W16.shape[0], x.device) if x.is_cuda else 0
+            gx = _linear(x2, W16, b16, alpha, fill=fill, max_grid=pg).view(T, N, -1)
         if arena is not None and x.is_cuda:
             # the next chunk of the optimizer update carried over from the previous step (the
             # layer above's, or the head's): on the side stream behind this projection, i.e.
@@ -1038,6 +1058,7 @@ class FusedBiLayer(torch.autograd.Function):
                 ops = GM.group_operands(dgx2.t(), x2, grp.view(plan.ndir * GH, D)) if grouped else None
                 sch.deferred.append(Deferred(dw, (dgx2, x2), [ops + (grp.view(plan.ndir * GH, D),)] if ops else None,
                                              dw_done))
+                arena.hold_report(W_f, W_b if d1 else None)
                 sch.queue_end_of_backward()
             else:
                 dw()
@@ -1101,12 +1122,14 @@ class FusedBiLayer(torch.autograd.Function):
                 ops = [GM.group_operands(g3[d], h3[d], out[d]) for d in range(2)] if grouped else None
                 members = [o + (out[d],) for d, o in enumerate(ops)] if ops and all(ops) else None
                 sch.deferred.append(Deferred(du, (dgh, hx), members, du_done))
+                arena.hold_report(U_f, U_b)
                 sch.queue_end_of_backward()
             elif sch.defer_input and on_side and ctx.idx == 0 and _defer_wgrad(plan, x16.device):
                 # the side stream already carries dW_0 + every deferred dW and ends after the
                 # conv front-end's backward on the main stream: balance by issuing the
                 # bottom layer's dU on the main stream behind the front-end (WgradScheduler.join)
                 sch.main_tail.append(du)
+                arena.hold_report(U_f, U_b)
                 sch.queue_end_of_backward()
             else:
                 du()

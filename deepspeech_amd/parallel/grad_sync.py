@@ -117,6 +117,8 @@ class GradBucketer:
         # returned no gradient for it (the fused ops deliver theirs through the arena and
         # return None): count each parameter once per step, whichever path reports first
         def hook(p):
+            if getattr(self.arena, "_held", None) and id(p) in self.arena._held:
+                return               # a deferred GEMM reports it (ParamArena.hold_report)
             written = getattr(self.arena, "_written", None)
             if written is not None:
                 if id(p) in written:

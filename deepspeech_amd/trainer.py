@@ -508,6 +508,13 @@ class Trainer:
         # the HIP engine delivers every gradient through the arena (first write overwrites),
         # so the per-step memset of the whole gradient buffer is skipped
         lazy = model.engine == "hip"
+        if self.bucketer.enabled and lazy and self.arena.flat.is_cuda:
+            # data parallel: sequences of < _PARTIAL_MIN_T recurrence steps take the single-device
+            # schedule (every weight gradient in one grouped launch after the last BPTT, the
+            # buckets' collectives behind it): their backward is too short for per-layer
+            # overlap to pay for the capped beside grids (100 frames: 3.35 -> see
+            # profiles/r6_dp.md); longer ones keep the per-layer GEMMs beside the BPTTs
+            self.arena.wgrad.set_deferral(not _long_sequence(batch))
         self.arena.wgrad.discard()
         self.arena.zero_grad(lazy=lazy)
         with _CTC.loss_watch(self.watch) as lw:

@@ -40,7 +40,7 @@ def _loss(model, batch, fused=False):
     return model.loss(logits, lens, batch["labels"], batch["label_lens"])
 
 
-def _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=None):
+def _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=None, tol_names=None):
     assert abs(float(lh) - float(lr)) / abs(float(lr)) < 3e-2, (float(lh), float(lr))
     gref = dict((n, p.grad) for n, p in ref.named_parameters())
     errs, bad = {}, []
@@ -59,6 +59,7 @@ def _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=None):
         # layer, so its gradients carry the most accumulated rounding
         # (ReLU-RNN: bf16 rounding also flips clip masks, so the front-end sees more)
         tol = (tol_conv or (0.12 if cell == "gru" else 0.2)) if n.startswith("conv") else tol_rnn
+        tol = (tol_names or {}).get(n, tol)
         if errs[n] > tol:
             bad.append(n)
     worst = ", ".join("%s %.4f" % kv for kv in sorted(errs.items(), key=lambda kv: -kv[1])[:12])
@@ -105,12 +106,23 @@ def test_headline_geometry_matches_reference(cuda, cell):
     lr.backward()
     torch.cuda.synchronize()
     RNN.check_errors()
-    # Every recurrent / FC parameter within 6 %. The conv front-end sits under 5 bf16
-    # layers of rounding: measured on MI355X (GRU) conv1.weight 7.2 %, conv1.bn_beta 13 %
-    # (a sum over 1.2 M positions with cancellation), conv2 within 6 %; clipped-ReLU RNN
-    # (loss ~2.8e4 at this random init, bf16 rounding flips clip masks at 20 in every layer)
-    # conv1.weight 27 %, bn_beta 27 %, bn_gamma 19 %.
-    _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.06, tol_conv=0.15 if cell == "gru" else 0.35)
+    # Per-parameter bounds at ~1.5x the errors measured on MI355X (round 6, fixed seeds, bitwise
+    # reproducible engine), so a 2x regression of any one gradient fails. GRU: every recurrent /
+    # FC parameter <= 1.06 %; the conv front-end under 5 bf16 layers of rounding conv1.bn_beta
+    # 13.1 % (a sum over 1.2 M positions with cancellation), conv1.weight 7.2 %, conv2.weight
+    # 5.1 %, conv1.bn_gamma 4.2 %, conv2.bn_* 0.8 %. Clipped-ReLU RNN (loss ~2.8e4 at this random
+    # init, bf16 rounding flips clip masks at 20 in every layer): recurrent <= 1.92 %,
+    # conv1.weight 23.1 %, conv1.bn_beta 21.0 %, conv1.bn_gamma 16.6 %, conv2.weight 16.1 %.
+    if cell == "gru":
+        names = {"conv1.bn_beta": 0.20, "conv1.weight": 0.11, "conv2.weight": 0.08, "conv1.bn_gamma": 0.065,
+                 "conv2.bn_beta": 0.015, "conv2.bn_gamma": 0.015}
+        errs = _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.016, tol_conv=0.2, tol_names=names)
+    else:
+        names = {"conv1.weight": 0.35, "conv1.bn_beta": 0.32, "conv1.bn_gamma": 0.25, "conv2.weight": 0.25,
+                 "conv2.bn_beta": 0.015, "conv2.bn_gamma": 0.015}
+        errs = _compare_grads(ref, hip, lh, lr, cell, tol_rnn=0.03, tol_conv=0.35, tol_names=names)
+    print("headline %s relative gradient errors:" % cell,
+          ", ".join("%s %.4f" % kv for kv in sorted(errs.items(), key=lambda kv: -kv[1])))
 
 
 @pytest.mark.parametrize("cell,H", [("gru", 1280), ("rnn_relu", 1760)])
