@@ -236,6 +236,18 @@ __device__ __forceinline__ bool poll_mfma(__amdgpu_buffer_rsrc_t rs, const unsig
 // late. (poll_mfma reloads only the granule it is waiting on, so k-steps whose first load
 // came back early-stale cost one serial round trip each.) The MFMAs still run in k order,
 // so the accumulation order — and the result — is deterministic.
+// Explicit vmcnt(0) at the poll's exits. Every load of the poll has been waited for there
+// already (the last check consumed it), but the CFG also has an edge from a re-issue to the
+// exit, so the waitcnt pass assumed loads in flight and put a vmcnt(0) at the head of the
+// NEXT step — behind the step's own h store, whose write acknowledgement then delayed the
+// next step's first poll by an L2 round trip. A counted wait here costs nothing (nothing is
+// in flight) and tells the pass so.
+__device__ __forceinline__ void drain_vm() {
+#ifndef DS2_NO_DRAIN          // A/B: build.py --variant nodrain -D DS2_NO_DRAIN
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
+}
+
 template <int KB, typename MfmaFn>
 __device__ __forceinline__ bool poll_mfma_par(__amdgpu_buffer_rsrc_t rs, const unsigned (&off)[KB],
                                               const bool (&kval)[KB], long long timeout, int nap, MfmaFn&& mfma) {
@@ -257,8 +269,8 @@ __device__ __forceinline__ bool poll_mfma_par(__amdgpu_buffer_rsrc_t rs, const u
         }
       }
     }
-    if (done == FULL) return true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) return false;
+    if (done == FULL) { drain_vm(); return true; }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) { drain_vm(); return false; }
     if (nap == 1) __builtin_amdgcn_s_sleep(1);           // retry back-off (0: busy re-poll)
     else if (nap == 2) __builtin_amdgcn_s_sleep(3);
 #pragma unroll
@@ -762,6 +774,7 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
     const int nap = (a.knobs >> 12) & 3;
     const bool erow_ok = erow < R;
     const int L = len_s[erow];
+    drain_vm();        // the U / bias / h0 loads: nothing from before the loop is pending inside it
     for (int s = 0; s < a.steps; ++s) {
       st.mark(-1);
       float gxv[G];                    // slot s&1 was filled before the previous barrier
@@ -1099,8 +1112,12 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
     const int nap = (a.knobs >> 12) & 3;
     const bool erow_ok = erow < R;
     const int L = len_s[erow];
+    drain_vm();        // the U / bias / h0 loads: nothing from before the loop is pending inside it
+    const int presleep = (a.knobs >> 17) & 7;
     for (int s = 0; s < a.steps; ++s) {
       st.mark(-1);
+      if (s > 0)
+        for (int i = 0; i < presleep; ++i) __builtin_amdgcn_s_sleep(1);
       float gxv[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) gxv[g] = bf2f(gxr_s[s & 1][erow][g * UPW + ec]);
@@ -1442,9 +1459,12 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   };
 
   if (wave < MW) {
+    const int presleep = (a.knobs >> 20) & 7;     // A/B: s_sleep 1 units before the gather
     for (int s = a.steps - 1; s >= 0; --s) {
       st.mark(-1);
       const bool has_next = s + 1 < a.steps;
+      if (has_next)
+        for (int i = 0; i < presleep; ++i) __builtin_amdgcn_s_sleep(1);
       // (G) sum this thread's producers' partials of dh_rec
       if constexpr (PBF == 2) {
         // 8 < R <= 16: lane -> (row, granule g), one producer per load instruction
@@ -2221,9 +2241,12 @@ __global__ __launch_bounds__(NTH) void rnnw_bwd_kernel(XBwdRS a) {
   };
 
   if (wave < MW) {
+    const int presleep = (a.knobs >> 20) & 7;     // A/B: s_sleep 1 units before the gather
     for (int s = a.steps - 1; s >= 0; --s) {
       st.mark(-1);
       const bool has_next = s + 1 < a.steps;
+      if (has_next)
+        for (int i = 0; i < presleep; ++i) __builtin_amdgcn_s_sleep(1);
       // (G) lane -> (producer half h, row, granule g); the two unit pairs of this workgroup
       {
         const int h = lane >> 5, grow = (lane >> 2) & 7, gg = lane & 3;

@@ -30,6 +30,23 @@ BN_MOMENTUM = 0.01
 # conv1 weight-gradient workgroups per CU (its 67.5 KB of LDS allows two)
 _C1W_BPC = 1
 
+# conv2's weight gradient on a stream of its own, beside the conv2 data gradient -> BN1 ->
+# conv1 weight-gradient chain it does not feed (A/B: DS2_CONV_WSIDE)
+_CONV_WSIDE = os.environ.get("DS2_CONV_WSIDE", "0") == "1"
+_conv_streams = {}
+
+
+def _conv_side_stream(dev, w):
+    """The conv2 weight-gradient stream, or None (off, no GPU, or a single-stream capture)."""
+    a = arena_of(w)
+    if not _CONV_WSIDE or dev.type != "cuda" or (a is not None and a.wgrad.single_stream):
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _conv_streams.get(idx)
+    if s is None:
+        s = _conv_streams[idx] = torch.cuda.Stream(device=torch.device("cuda", idx))
+    return s
+
 def bn_eval_stats(block, eps: float):
     """(mean, invstd) for eval: running statistics (fused variant) or the debiased EMA of
     the moments (moments_ema variant, NHWC graph)."""
@@ -286,10 +303,20 @@ class FrontendCL(torch.autograd.Function):
             (dg2, ipg2), (db2, ipb2) = _grad_buffer(g2), _grad_buffer(be2)
             dy2 = torch.empty_like(y2)
             C_.bn_cl_bwd(dout, y2, mean2, inv2, g2f, be2f, part, nb2, dg2, db2, dy2, True)
+        side = _conv_side_stream(dev, w2)
+        main = torch.cuda.current_stream(dev) if side is not None else None
         with TR.phase(TR.conv(2, True)):
             wpart = torch.empty(int(C_.conv2_wgrad_part_floats(grid)), **f32)
             dw2, ip2 = _grad_buffer(w2)
-            C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
+            if side is None:
+                C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
+            else:
+                # dy2, z1 and wpart are freed on the main stream only after it has joined
+                # the side stream below, so no allocator block is reused under the kernel
+                from .rnn import _stream_wait
+                _stream_wait(side, main)
+                with torch.cuda.stream(side):
+                    C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
             dz1 = torch.empty_like(y1)
             # two workgroups per CU; the epilogue also leaves conv1's BN-backward sums in part
             dgrid = max(1, min(N * ((T1 + 1) // 2), 2 * ctx.ncu))
@@ -297,7 +324,7 @@ class FrontendCL(torch.autograd.Function):
             # reported only after the dgrad has been enqueued: a bucket whose last reporter is
             # conv2.weight may launch its all-reduce + optimizer range (which rewrites the bf16
             # shadow w2_16) at this call, so every reader of w2_16 must already be on the stream
-            gw2 = _deliver(w2, dw2, ip2)
+            gw2 = _deliver(w2, dw2, ip2) if side is None else None
         gg2, gb2, gbias2 = _deliver(g2, dg2, ipg2), _deliver(be2, db2, ipb2), _zero_grad_of(b2)
         with TR.phase(TR.bn(1, True)):
             (dg1, ipg1), (db1, ipb1) = _grad_buffer(g1), _grad_buffer(be1)
@@ -309,6 +336,10 @@ class FrontendCL(torch.autograd.Function):
             wpart1 = torch.empty(int(C_.conv1_wgrad_part_floats(g1grid)), **f32)
             dw1, ip1 = _grad_buffer(w1)
             C_.conv1_wgrad(dz1, x, wpart1, dw1, g1grid, y1, mean1, inv1, g1f, be1f, db1, dg1)
+            if side is not None:
+                # conv2's weight gradient joins here and is reported from the main stream
+                _stream_wait(main, side)
+                gw2 = _deliver(w2, dw2, ip2)
             gw1 = _deliver(w1, dw1, ip1)
         gg1, gb1, gbias1 = _deliver(g1, dg1, ipg1), _deliver(be1, db1, ipb1), _zero_grad_of(b1)
         return None, gw1, gbias1, gg1, gb1, gw2, gbias2, gg2, gb2, None

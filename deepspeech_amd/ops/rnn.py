@@ -81,9 +81,24 @@ def _timing_only() -> bool:
     return os.environ.get("DS2_TIMING_ONLY") == "1"
 
 
+# Poll timing of the persistent recurrences (csrc/rnn_xcd.hip): bits 17-19 = s_sleep units a
+# forward wave waits after publishing its h before polling the next step, bits 20-22 the same
+# before a BPTT gather. The forward's poll exits drain vmcnt (drain_vm), so its first poll is no
+# longer held behind its own store's write acknowledgement; polling right away then measured
+# slower (stale reads contend with the producers' stores in the XCD's L2), 4 units faster than
+# both (scripts/r6_presleep*.sh, profiles/r6_recurrence_poll.md). Bit 23: take bits 17-22 as
+# given (an explicit 0) instead of these defaults.
+POLL_DEFAULT = (4 << 17) | (0 << 20)
+POLL_EXPLICIT = 1 << 23
+
+
 def _kernel_knobs() -> int:
-    """DS2_RNNX_KNOBS as the kernels receive it: timing-only bits dropped outside a timing session."""
-    return RNNX_KNOBS if _timing_only() else RNNX_KNOBS & ~TIMING_ONLY_KNOBS
+    """DS2_RNNX_KNOBS as the kernels receive it: timing-only bits dropped outside a timing
+    session, the default poll timing unless set explicitly."""
+    k = RNNX_KNOBS if _timing_only() else RNNX_KNOBS & ~TIMING_ONLY_KNOBS
+    if not (k & POLL_EXPLICIT) and not (k & (0x3f << 17)):
+        k |= POLL_DEFAULT
+    return k
 
 
 def check_knobs() -> None:
@@ -948,10 +963,13 @@ class FusedBiLayer(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         if dy.dim() == 4:
-            # the pair output's gradient: the next layer returns the sum's gradient for both
-            # halves (one tensor expanded); anything else would need per-direction dy
-            if dy.stride(0) != 0 and not torch.equal(dy[0], dy[1]):
-                raise RuntimeError("direction-pair output with different gradients per direction")
+            # the pair output's gradient: the next layer's quantiser returns the sum's gradient
+            # for both halves (one tensor expanded). A materialised dy means a second consumer
+            # (the model only pairs a layer with the fp8 layer above it, deepspeech2.py
+            # recurrent): refused without comparing the halves, which would sync the host
+            # (and raise inside a step-graph capture)
+            if dy.stride(0) != 0:
+                raise RuntimeError("direction-pair output consumed other than by the next layer's quantiser")
             dy = dy[0]
         with TR.phase(TR.rnn_cell(ctx.idx, True)):
             return FusedBiLayer._backward(ctx, dy)
