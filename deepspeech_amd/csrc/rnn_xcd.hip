@@ -1145,14 +1145,22 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
       st.mark(1);
       lds_barrier();
       st.mark(2);
-      if (s_abort) break;
+      // the abort word is read together with the partials and tested only before the first
+      // store: testing it first put one more LDS round trip (~100 cycles) on every step's path
+      const int ab = s_abort;
       float pre[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float v = 0.f;
+        // pairwise tree over the 8 K-eighths (fixed order: deterministic), 3 dependent adds
+        // instead of a chain of 8 on the step's critical path
+        float p[QW];
 #pragma unroll
-        for (int w = 0; w < QW; ++w) v += red_s[SB ? 0 : (s & 1)][w][3 * uh + g][jo][lane];
-        pre[g] = v;
+        for (int w = 0; w < QW; ++w) p[w] = red_s[SB ? 0 : (s & 1)][w][3 * uh + g][jo][lane];
+#pragma unroll
+        for (int d = 1; d < QW; d *= 2)
+#pragma unroll
+          for (int w = 0; w + d < QW; w += 2 * d) p[w] += p[w + d];
+        pre[g] = p[0];
       }
       if constexpr (SB) lds_barrier();               // every partial read before the next step's writes
       const bool act = s < L;
@@ -1171,6 +1179,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
       const int q1 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x102, 0xf, 0xf, false);
       const int q2 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x104, 0xf, 0xf, false);
       const int q3 = __builtin_amdgcn_update_dpp(0, (int)pr, 0x106, 0xf, 0xf, false);
+      if (ab) break;
       if ((lane & 7) == 0 && erow_ok) {
         const i32x4 v = {(int)pr, q1, q2, q3};
         const unsigned off2 = (unsigned)((((size_t)(s + 1) * NP + r0 + erow) * H + u0 + ec) * 2);
@@ -1191,8 +1200,9 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
       st.mark(0);
       lds_barrier();
       st.mark(1);
-      if (s_abort) break;
+      const int ab = s_abort;     // same value the MFMA waves test (written before the barrier)
       if constexpr (SB) lds_barrier();
+      if (ab) break;
     }
   }
   __syncthreads();
@@ -1584,7 +1594,9 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
       st.mark(0);
       lds_barrier();                                                        // #1
       st.mark(1);
-      if (s_abort) break;
+      // abort word read beside the partials, tested before barrier #2 (the memory wave tests
+      // it there too): one LDS round trip less in front of the cell on every step
+      const int ab = s_abort;
       // (E) cell backward (waves 0..3): dgh tile for the MFMA, dgx / dgh staging
       if (wave < EW) {
 #pragma unroll
@@ -1594,12 +1606,20 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
           if (row < R) {
             float dhrec = 0.f;
             if (has_next) {
+              // pairwise tree over the worker waves' partials (fixed order: deterministic):
+              // 3-4 dependent adds on the step's critical path instead of a chain of 7 / 14
+              constexpr int NPART = (PBF == 1) ? 2 * MW : MW;
+              float p[NPART];
 #pragma unroll
-              for (int w = 0; w < MW; ++w) dhrec += red_s[w][row][c];
-              if constexpr (PBF == 1) {
-#pragma unroll
-                for (int w = 0; w < MW; ++w) dhrec += red_s[w][row + 8][c];
+              for (int w = 0; w < MW; ++w) {
+                p[w] = red_s[w][row][c];
+                if constexpr (PBF == 1) p[MW + w] = red_s[w][row + 8][c];
               }
+#pragma unroll
+              for (int d = 1; d < NPART; d *= 2)
+#pragma unroll
+                for (int w = 0; w + d < NPART; w += 2 * d) p[w] += p[w + d];
+              dhrec = p[0];
             }
             const bool act = s < len_s[row];
             const float dh = dyr_s[s & 1][row][c] + carry[i] + dhrec;
@@ -1643,6 +1663,7 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
         }
       }
       st.mark(2);
+      if (ab) break;
       lds_barrier();                                                        // #2
       st.mark(3);
       // (M) publish P(s) = dgh_s[:, own cols] . U[own cols, :] into ring slot s % 3

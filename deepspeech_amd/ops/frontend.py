@@ -32,7 +32,7 @@ _C1W_BPC = 1
 
 # conv2's weight gradient on a stream of its own, beside the conv2 data gradient -> BN1 ->
 # conv1 weight-gradient chain it does not feed (A/B: DS2_CONV_WSIDE)
-_CONV_WSIDE = os.environ.get("DS2_CONV_WSIDE", "0") == "1"
+_CONV_WSIDE = os.environ.get("DS2_CONV_WSIDE", "1") == "1"
 _conv_streams = {}
 
 
