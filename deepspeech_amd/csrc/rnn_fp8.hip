@@ -66,6 +66,22 @@ struct XF8 {
   long long timeout;
 };
 
+// Pre-poll sleep (s_sleep 1 units) after a step's publish, before the next step's first
+// exchange poll: these kernels issue that poll right behind their own store, where the bf16
+// forward measured stale reads competing with the producers' stores in the XCD's L2
+// (profiles/r6_recurrence_poll.md). Compile-time (A/B: build.py --variant ... -D).
+#ifndef DS2_F8_FWD_SLEEP
+#define DS2_F8_FWD_SLEEP 0
+#endif
+#ifndef DS2_F8_BWD_SLEEP
+#define DS2_F8_BWD_SLEEP 3          // config-5 fp8: 17.30-17.39 vs 17.55-17.65 ms/step (scripts/r6_f8sleep2.sh)
+#endif
+template <int N>
+__device__ __forceinline__ void f8_presleep() {
+#pragma unroll
+  for (int i = 0; i < N; ++i) __builtin_amdgcn_s_sleep(1);
+}
+
 __device__ __forceinline__ unsigned xcc_id8() {
   unsigned v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
@@ -277,6 +293,7 @@ __global__ __launch_bounds__(F8TH) void rnnf8_fwd_kernel(XF8 a) {
     // padding rows of the 16-row tile re-read row R - 1 (a real, polled row)
     const int arow = r0 + min(lane & 15, R - 1);
     for (int s = 0; s < a.steps; ++s) {
+      if (s > 0) f8_presleep<DS2_F8_FWD_SLEEP>();
       float gxv[2][G3];
 #pragma unroll
       for (int e = 0; e < 2; ++e)
@@ -537,6 +554,7 @@ __global__ __launch_bounds__(F8TH) void rnnf8h_fwd_kernel(XF8 a) {
     }
     const int arow = r0 + min(lane & 15, R - 1);
     for (int s = 0; s < a.steps; ++s) {
+      if (s > 0) f8_presleep<DS2_F8_FWD_SLEEP>();
       // every granule of this lane's K-quarter at once: k-step kk's two granules are 64 B
       // apart, consecutive k-steps of the quarter 512 B
       const unsigned o0 = (unsigned)(((size_t)s * NP + arow) * H + kq * 128 + 16 * g16);
@@ -857,6 +875,7 @@ __global__ __launch_bounds__(BTH8) void rnnf8_bwd_kernel(XF8B a) {
     const int saw = sa | (sa << 8) | (sa << 16) | (sa << 24);       // U^T: one E8M0 for all blocks
     for (int s = a.steps - 1; s >= 0; --s) {
       const bool has_next = s + 1 < a.steps;
+      if (has_next) f8_presleep<DS2_F8_BWD_SLEEP>();
       // (G) lane -> (producer half h, row, granule g); the two unit pairs of this workgroup
       {
         const int h = lane >> 5, grow = (lane >> 2) & 7, gg = lane & 3;

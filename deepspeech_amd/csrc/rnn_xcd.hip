@@ -1080,7 +1080,8 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
   const unsigned hx_bytes = (unsigned)((size_t)(a.steps + 1) * NP * H * 2);
   bf16_t* hxd = a.hx[dir];
   const __amdgpu_buffer_rsrc_t rs_hx = make_rsrc(hxd, hx_bytes);
-  StampT st(a.stamps != nullptr && (wave == 0 || wave == QW) && lane == 0);
+  const int stw = (a.knobs >> 24) & 7;   // stamps: the MFMA wave recorded (diagnostics; 0 = wave 0)
+  StampT st(a.stamps != nullptr && (wave == stw || wave == QW) && lane == 0);
 
   if (wave < QW) {
     // resident U fragments: B[k][c] = U[g H + u0 + 16 h + c][ks*32 + k], tile 3 h + g, ks = wave + 8 kk
@@ -1216,7 +1217,7 @@ __global__ __launch_bounds__(QTH) void rnne_fwd_kernel(XFwd a) {
       mw_store(a.steps - 1);
     }
   }
-  if (STAMPS && wave == 0) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
+  if (STAMPS && wave == stw) { st.acc[5] = (unsigned long long)(s_mode + 10); st.store(a.stamps, 0); }
   if (STAMPS && wave == QW && st.on) { a.stamps[(size_t)blockIdx.x * 8 + 6] = st.acc[0]; a.stamps[(size_t)blockIdx.x * 8 + 7] = st.acc[1]; }
 }
 

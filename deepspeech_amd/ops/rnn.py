@@ -88,15 +88,16 @@ def _timing_only() -> bool:
 # slower (stale reads contend with the producers' stores in the XCD's L2), 4 units faster than
 # both (scripts/r6_presleep*.sh, profiles/r6_recurrence_poll.md). Bit 23: take bits 17-22 as
 # given (an explicit 0) instead of these defaults.
-POLL_DEFAULT = (4 << 17) | (0 << 20)
+POLL_DEFAULT = (4 << 17) | (2 << 20)
 POLL_EXPLICIT = 1 << 23
+POLL_MASK = 0x7f << 17
 
 
 def _kernel_knobs() -> int:
     """DS2_RNNX_KNOBS as the kernels receive it: timing-only bits dropped outside a timing
     session, the default poll timing unless set explicitly."""
     k = RNNX_KNOBS if _timing_only() else RNNX_KNOBS & ~TIMING_ONLY_KNOBS
-    if not (k & POLL_EXPLICIT) and not (k & (0x3f << 17)):
+    if not (k & POLL_MASK):
         k |= POLL_DEFAULT
     return k
 

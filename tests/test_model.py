@@ -259,3 +259,22 @@ def test_env_knobs_are_few():
             if f.endswith(".py"):
                 names |= set(re.findall(r"DS2_[A-Z0-9_]+", open(os.path.join(d, f)).read()))
     assert len(names) < 20, sorted(names)
+
+
+def test_recurrence_poll_timing_knob_defaults(monkeypatch):
+    """The persistent recurrences' poll timing (ops/rnn.py POLL_DEFAULT: forward pre-poll sleep
+    4, BPTT pre-gather sleep 2, profiles/r6_recurrence_poll.md) reaches every launch unless
+    DS2_RNNX_KNOBS sets a poll-timing bit; bit 23 alone asks for no sleep at all."""
+    from deepspeech_amd.ops import rnn as RNN
+    monkeypatch.delenv("DS2_TIMING_ONLY", raising=False)
+    monkeypatch.setattr(RNN, "RNNX_KNOBS", 0)
+    assert RNN._kernel_knobs() == RNN.POLL_DEFAULT
+    assert (RNN.POLL_DEFAULT >> 17) & 7 == 4 and (RNN.POLL_DEFAULT >> 20) & 7 == 2
+    monkeypatch.setattr(RNN, "RNNX_KNOBS", 16384)
+    assert RNN._kernel_knobs() == 16384 | RNN.POLL_DEFAULT
+    monkeypatch.setattr(RNN, "RNNX_KNOBS", 6 << 17)
+    assert RNN._kernel_knobs() == 6 << 17
+    monkeypatch.setattr(RNN, "RNNX_KNOBS", RNN.POLL_EXPLICIT)
+    assert RNN._kernel_knobs() & RNN.POLL_MASK == RNN.POLL_EXPLICIT
+    monkeypatch.setattr(RNN, "RNNX_KNOBS", 1 << 24)          # stamp-wave selection: not a poll bit
+    assert RNN._kernel_knobs() == (1 << 24) | RNN.POLL_DEFAULT

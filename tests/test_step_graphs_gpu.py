@@ -148,10 +148,14 @@ def test_timing_only_knobs_refused_and_masked(cuda, monkeypatch):
         monkeypatch.setattr(RNN, "RNNX_KNOBS", bit | 16384)
         with pytest.raises(RuntimeError, match="timing only"):
             Trainer(m, LRSchedule(1e-3, 10, 0.9))
-        assert RNN._kernel_knobs() == 16384              # masked at every launch regardless
+        # masked at every launch regardless (the poll-timing default bits aside)
+        assert RNN._kernel_knobs() & ~RNN.POLL_MASK == 16384
+        assert RNN._kernel_knobs() & RNN.POLL_MASK == RNN.POLL_DEFAULT
     monkeypatch.setattr(RNN, "RNNX_KNOBS", 16384)      # a schedule variant with correct results
     RNN.check_knobs()
     monkeypatch.setenv("DS2_TIMING_ONLY", "1")
     monkeypatch.setattr(RNN, "RNNX_KNOBS", 4)
     RNN.check_knobs()
-    assert RNN._kernel_knobs() == 4
+    assert RNN._kernel_knobs() == 4 | RNN.POLL_DEFAULT
+    monkeypatch.setattr(RNN, "RNNX_KNOBS", 4 | RNN.POLL_EXPLICIT)    # explicit poll timing 0
+    assert RNN._kernel_knobs() == 4 | RNN.POLL_EXPLICIT
