@@ -775,8 +775,13 @@ __global__ __launch_bounds__(QTH) void rnnq_fwd_kernel(XFwd a) {
     const bool erow_ok = erow < R;
     const int L = len_s[erow];
     drain_vm();        // the U / bias / h0 loads: nothing from before the loop is pending inside it
+    // pre-poll sleep (ops/rnn.py _kernel_knobs), in units of s_sleep 4 here: the cross-XCD
+    // write-through exchange of this kernel's wide groups lands later than the XCD-local one
+    const int presleep = (a.knobs >> 17) & 7;
     for (int s = 0; s < a.steps; ++s) {
       st.mark(-1);
+      if (s > 0)
+        for (int i = 0; i < presleep; ++i) __builtin_amdgcn_s_sleep(4);
       float gxv[G];                    // slot s&1 was filled before the previous barrier
 #pragma unroll
       for (int g = 0; g < G; ++g) gxv[g] = gxr_s[s & 1][erow][g * UPW + ec];
@@ -2031,8 +2036,12 @@ __global__ __launch_bounds__(QTH) void rnnw_fwd_kernel(XFwd a) {
       }
     }
     const int arow = r0 + min(lane & 15, R - 1);
+    drain_vm();        // nothing from before the loop pending inside it (as rnne_fwd_kernel)
+    const int presleep = (a.knobs >> 17) & 7;   // pre-poll sleep (ops/rnn.py POLL_DEFAULT)
     for (int s = 0; s < a.steps; ++s) {
       st.mark(-1);
+      if (s > 0)
+        for (int i = 0; i < presleep; ++i) __builtin_amdgcn_s_sleep(1);
       float gxv[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) gxv[e] = gxr_s[s & 1][erow[e]][lu];

@@ -93,12 +93,24 @@ POLL_EXPLICIT = 1 << 23
 POLL_MASK = 0x7f << 17
 
 
-def _kernel_knobs() -> int:
-    """DS2_RNNX_KNOBS as the kernels receive it: timing-only bits dropped outside a timing
-    session, the default poll timing unless set explicitly."""
+# GRU layers wider than 1024 (config 5 bf16: rnnq_fwd_kernel, whose groups straddle XCDs and
+# exchange write-through) poll later: the forward field counts s_sleep 4 units there (config 5
+# bf16 20.74-20.81 vs 21.49-21.51 ms/step, scripts/r6_c5poll3.sh)
+POLL_WIDE = (5 << 17) | (0 << 20)
+
+
+def poll_default(plan=None) -> int:
+    if plan is not None and plan.cell == "gru" and plan.H > 1024:
+        return POLL_WIDE
+    return POLL_DEFAULT
+
+
+def _kernel_knobs(plan=None) -> int:
+    """DS2_RNNX_KNOBS as the kernels of ``plan`` receive it: timing-only bits dropped outside a
+    timing session, the plan's default poll timing unless set explicitly."""
     k = RNNX_KNOBS if _timing_only() else RNNX_KNOBS & ~TIMING_ONLY_KNOBS
     if not (k & POLL_MASK):
-        k |= POLL_DEFAULT
+        k |= poll_default(plan)
     return k
 
 
@@ -452,7 +464,7 @@ def _alloc_fwd(T: int, N: int, plan: RnnPlan, dev) -> _FwdBufs:
     # sum buffer, one direction writes through, the other adds): no torch.add launch and no
     # per-direction output round trip
     b.fuse = (plan.kind == "xcd" and d1 and _FUSE_DIRSUM and
-              bool(C.rnnx_fwd_fuses_sum(H, CELL_CODE[plan.cell], plan.mt, ndir, _kernel_knobs())))
+              bool(C.rnnx_fwd_fuses_sum(H, CELL_CODE[plan.cell], plan.mt, ndir, _kernel_knobs(plan))))
     b.y2 = None if b.fuse else torch.empty(ndir, T, N, H, device=dev, dtype=bf16)
     b.ysum = torch.empty(T, N, H, device=dev, dtype=bf16) if b.fuse else None
     b.hx = torch.empty(ndir, T + 1, plan.NP, H, device=dev, dtype=bf16)
@@ -507,7 +519,7 @@ def _run_fwd(gx, lens, U, bh, plan: RnnPlan, h0=None, bufs: Optional[_FwdBufs] =
                    gates[0] if gates is not None else None,
                    gates[1] if (gates is not None and d1) else None,
                    census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
-                   CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, _kernel_knobs(),
+                   CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, _kernel_knobs(plan),
                    _stamps("fwd", plan, int(C.rnnx_info(H, GATES[plan.cell], plan.mt, ndir * plan.BG,
                                                          plan.xcd_map)["grid"]), dev), ysum)
         y = ysum if fuse else (torch.add(y2[0], y2[1]) if d1 else y2[0])
@@ -546,7 +558,7 @@ def kernel_families(plan: RnnPlan) -> Tuple[str, str]:
         g1 = "rnn_%s (gen 1, " + ("persistent)" if plan.persistent else "step launches)")
         return g1 % "fwd", g1 % "bwd"
     C = _ext.ext()
-    f = int(C.rnnx_fwd_family(plan.H, CELL_CODE[plan.cell], plan.mt, _kernel_knobs()))
+    f = int(C.rnnx_fwd_family(plan.H, CELL_CODE[plan.cell], plan.mt, _kernel_knobs(plan)))
     b = int(C.rnnx_bwd_family(plan.H, CELL_CODE[plan.cell], plan.mt, plan.R))
     if f not in _FWD_FAMILY or b not in _BWD_FAMILY:
         raise ValueError("xcd plan not covered by csrc/rnn_xcd.hip: %r" % (plan,))
@@ -723,7 +735,7 @@ def _run_bwd(dy, lens, U, hx, hs, gates, plan: RnnPlan, gstride: int, dgx_scale:
                    parts[0] if parts is not None else None,
                    parts[1] if (parts is not None and plan.cell == "gru") else None,
                    float(dgx_scale), census, err, T, N, plan.NP, H, plan.BG, plan.R, steps, gstride, ndir,
-                   CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, _kernel_knobs(),
+                   CELL_CODE[plan.cell], plan.mt, TIMEOUT_TICKS, plan.xcd_map, _kernel_knobs(plan),
                    _stamps("bwd", plan, int(C.rnnx_info(H, G, plan.mt, ndir * plan.BG, plan.xcd_map)["grid"]), dev),
                    ring[0], ring[1] if d1 else None)
         return dgx, dgh, parts

@@ -278,3 +278,9 @@ def test_recurrence_poll_timing_knob_defaults(monkeypatch):
     assert RNN._kernel_knobs() & RNN.POLL_MASK == RNN.POLL_EXPLICIT
     monkeypatch.setattr(RNN, "RNNX_KNOBS", 1 << 24)          # stamp-wave selection: not a poll bit
     assert RNN._kernel_knobs() == (1 << 24) | RNN.POLL_DEFAULT
+    # GRU wider than 1024 (config 5 bf16, cross-XCD groups): the wide poll timing
+    from types import SimpleNamespace
+    monkeypatch.setattr(RNN, "RNNX_KNOBS", 0)
+    assert RNN._kernel_knobs(SimpleNamespace(cell="gru", H=1280)) == RNN.POLL_WIDE
+    assert RNN._kernel_knobs(SimpleNamespace(cell="gru", H=800)) == RNN.POLL_DEFAULT
+    assert RNN._kernel_knobs(SimpleNamespace(cell="rnn_relu", H=1760)) == RNN.POLL_DEFAULT
