@@ -31,15 +31,22 @@ BN_MOMENTUM = 0.01
 _C1W_BPC = 1
 
 # conv2's weight gradient on a stream of its own, beside the conv2 data gradient -> BN1 ->
-# conv1 weight-gradient chain it does not feed (A/B: DS2_CONV_WSIDE)
-_CONV_WSIDE = os.environ.get("DS2_CONV_WSIDE", "1") == "1"
+# conv1 weight-gradient chain it does not feed. Off by default (DS2_CONV_WSIDE=1 turns it on):
+# single device 7.345 vs 7.354-7.361 ms/step (noise level), but the data-parallel step ran
+# 9.36-9.44 instead of 7.63 ms/step with it and its kernel trace showed ~0.7 ms of idle gaps
+# at the end of the single-device step too, a host-side stall not explained this round
+# (profiles/r6_negative_results.md)
+_CONV_WSIDE = os.environ.get("DS2_CONV_WSIDE", "0") == "1"
 _conv_streams = {}
 
 
 def _conv_side_stream(dev, w):
-    """The conv2 weight-gradient stream, or None (off, no GPU, or a single-stream capture)."""
+    """The conv2 weight-gradient stream, or None (off, no GPU, a single-stream capture, or a
+    gradient bucketer attached: the data-parallel step measured 9.36-9.44 ms/step with it
+    against 7.63 without at world 1, scripts/r6_dpcheck.sh, so DP keeps it in line)."""
     a = arena_of(w)
-    if not _CONV_WSIDE or dev.type != "cuda" or (a is not None and a.wgrad.single_stream):
+    if not _CONV_WSIDE or dev.type != "cuda" or (a is not None and (a.wgrad.single_stream or
+                                                                  getattr(a, "_ready_cbs", None))):
         return None
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _conv_streams.get(idx)
