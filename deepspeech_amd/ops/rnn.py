@@ -86,9 +86,10 @@ def _timing_only() -> bool:
 # before a BPTT gather. The forward's poll exits drain vmcnt (drain_vm), so its first poll is no
 # longer held behind its own store's write acknowledgement; polling right away then measured
 # slower (stale reads contend with the producers' stores in the XCD's L2), 4 units faster than
-# both (scripts/r6_presleep*.sh, profiles/r6_recurrence_poll.md). Bit 23: take bits 17-22 as
-# given (an explicit 0) instead of these defaults.
-POLL_DEFAULT = (4 << 17) | (2 << 20)
+# both (scripts/r6_presleep*.sh, profiles/r6_recurrence_poll.md); BPTT 4 units: 7.301-7.309 vs
+# 7.359-7.369 ms/step at 2 (scripts/r6_ab4.sh). Bit 23: take bits 17-22 as given (an explicit
+# 0) instead of these defaults.
+POLL_DEFAULT = (4 << 17) | (4 << 20)
 POLL_EXPLICIT = 1 << 23
 POLL_MASK = 0x7f << 17
 

@@ -263,13 +263,13 @@ def test_env_knobs_are_few():
 
 def test_recurrence_poll_timing_knob_defaults(monkeypatch):
     """The persistent recurrences' poll timing (ops/rnn.py POLL_DEFAULT: forward pre-poll sleep
-    4, BPTT pre-gather sleep 2, profiles/r6_recurrence_poll.md) reaches every launch unless
+    4, BPTT pre-gather sleep 4, profiles/r6_recurrence_poll.md) reaches every launch unless
     DS2_RNNX_KNOBS sets a poll-timing bit; bit 23 alone asks for no sleep at all."""
     from deepspeech_amd.ops import rnn as RNN
     monkeypatch.delenv("DS2_TIMING_ONLY", raising=False)
     monkeypatch.setattr(RNN, "RNNX_KNOBS", 0)
     assert RNN._kernel_knobs() == RNN.POLL_DEFAULT
-    assert (RNN.POLL_DEFAULT >> 17) & 7 == 4 and (RNN.POLL_DEFAULT >> 20) & 7 == 2
+    assert (RNN.POLL_DEFAULT >> 17) & 7 == 4 and (RNN.POLL_DEFAULT >> 20) & 7 == 4
     monkeypatch.setattr(RNN, "RNNX_KNOBS", 16384)
     assert RNN._kernel_knobs() == 16384 | RNN.POLL_DEFAULT
     monkeypatch.setattr(RNN, "RNNX_KNOBS", 6 << 17)
