@@ -40,6 +40,7 @@ _CONV_WSIDE = os.environ.get("DS2_CONV_WSIDE", "0") == "1"
 _conv_streams = {}
 
 
+
 def _conv_side_stream(dev, w):
     """The conv2 weight-gradient stream, or None (off, no GPU, a single-stream capture, or a
     gradient bucketer attached: the data-parallel step measured 9.36-9.44 ms/step with it
@@ -315,9 +316,11 @@ class FrontendCL(torch.autograd.Function):
         with TR.phase(TR.conv(2, True)):
             wpart = torch.empty(int(C_.conv2_wgrad_part_floats(grid)), **f32)
             dw2, ip2 = _grad_buffer(w2)
-            if side is None:
-                C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
-            else:
+            # in line (no side stream): conv2's weight gradient goes AFTER the dgrad -> BN1 ->
+            # conv1-wgrad chain, which then shares the tail with the grouped weight-gradient
+            # launch instead of running alone after it (7.298-7.314 vs 7.308-7.333 ms/step,
+            # scripts/r6_wlast.sh)
+            if side is not None:
                 # dy2, z1 and wpart are freed on the main stream only after it has joined
                 # the side stream below, so no allocator block is reused under the kernel
                 from .rnn import _stream_wait
@@ -328,10 +331,9 @@ class FrontendCL(torch.autograd.Function):
             # two workgroups per CU; the epilogue also leaves conv1's BN-backward sums in part
             dgrid = max(1, min(N * ((T1 + 1) // 2), 2 * ctx.ncu))
             C_.conv2_dgrad(dy2, w2_16, dz1, dgrid, y1, mean1, inv1, g1f, be1f, part)
-            # reported only after the dgrad has been enqueued: a bucket whose last reporter is
-            # conv2.weight may launch its all-reduce + optimizer range (which rewrites the bf16
-            # shadow w2_16) at this call, so every reader of w2_16 must already be on the stream
-            gw2 = _deliver(w2, dw2, ip2) if side is None else None
+            # conv2.weight is reported below, after its GEMM and after the dgrad: a bucket whose
+            # last reporter it is may launch its all-reduce + optimizer range (which rewrites the
+            # bf16 shadow w2_16) at that call, so every reader of w2_16 must be on the stream
         gg2, gb2, gbias2 = _deliver(g2, dg2, ipg2), _deliver(be2, db2, ipb2), _zero_grad_of(b2)
         with TR.phase(TR.bn(1, True)):
             (dg1, ipg1), (db1, ipb1) = _grad_buffer(g1), _grad_buffer(be1)
@@ -346,6 +348,9 @@ class FrontendCL(torch.autograd.Function):
             if side is not None:
                 # conv2's weight gradient joins here and is reported from the main stream
                 _stream_wait(main, side)
+                gw2 = _deliver(w2, dw2, ip2)
+            else:
+                C_.conv2_wgrad(dy2, z1, wpart, dw2, grid)
                 gw2 = _deliver(w2, dw2, ip2)
             gw1 = _deliver(w1, dw1, ip1)
         gg1, gb1, gbias1 = _deliver(g1, dg1, ipg1), _deliver(be1, db1, ipb1), _zero_grad_of(b1)
