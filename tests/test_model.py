@@ -216,10 +216,10 @@ def test_recurrence_kernel_family_map():
 
 
 @pytest.mark.parametrize("name,N,H,cell,T,dp,fp8,want", [
-    # headline 5 x BiGRU-800, batch 32, 10 s (T = 241): 200 CUs, layer 0 deferred, beside GEMMs on
-    # the 56 idle CUs, carried optimizer chunks on 56 blocks
+    # headline 5 x BiGRU-800, batch 32, 10 s (T = 241): 200 CUs, layer 0 deferred, beside GEMMs on 40 of
+    # the 56 idle CUs (5 per XCD), carried optimizer chunks on 56 blocks
     ("headline", 32, 800, "gru", 241, False, False,
-     dict(bptt_cus=200, idle_cus=56, defer_wgrad=True, defer_layers=1, upper_trigger=1, beside_grid=56,
+     dict(bptt_cus=200, idle_cus=56, defer_wgrad=True, defer_layers=1, upper_trigger=1, beside_grid=40,
           carry_grid=56, group_cap=192)),
     # the short SortaGrad buckets (< 200 recurrence steps): every layer deferred
     ("headline-short", 32, 800, "gru", 116, False, False,
