@@ -1206,7 +1206,7 @@ _BESIDE_MIN_IDLE_CUS = 96
 #   config 5 fp8: idle CUs (96) 18.13 / 18.14, whole chip 18.50 / 18.29
 #   config 5 bf16: idle CUs 23.37 / 23.42, whole chip 23.16 / 23.18 (kept uncapped)
 _BESIDE_GRID = -1
-_BESIDE_SINGLE_PER_XCD = 5
+_BESIDE_SPARE_PER_XCD = 2
 
 
 # bottom layer: the grouped launch before layer 0's dx GEMM (same-box A/B, 3 rounds: 8.025 /
@@ -1291,13 +1291,15 @@ def schedule_for(plan: RnnPlan, T: int, dp: bool, fp8: bool, num_cus: int) -> St
     beside = 0
     if _BESIDE_GRID != 0 and (_BESIDE_GRID != -1 or dp or fp8 or defer):
         cap = idle if _BESIDE_GRID < 0 else min(_BESIDE_GRID, idle)
-        if _BESIDE_GRID < 0 and defer and layers == 1 and not (dp or fp8):
-            # single device, partial deferral (the headline): the upper layers' dW beside each
-            # BPTT on 5 of each XCD's idle CUs, not all 7: 7.280-7.307 vs 7.315-7.338 ms/step
-            # (4 rounds; 3 more on another box: 7.26-7.305 vs 7.296-7.324); 6 per XCD measured
-            # 7.445-7.459, 4: 7.318-7.322; data parallel keeps every idle CU (7.607-7.62 vs
-            # 7.547-7.548 at 5) (scripts/r6_beside*.sh)
-            cap = min(cap, 8 * _BESIDE_SINGLE_PER_XCD)
+        if (_BESIDE_GRID < 0 and not dp and ((defer and layers == 1) or fp8) and
+                cap > 8 * _BESIDE_SPARE_PER_XCD):
+            # single device: the GEMMs beside a BPTT leave 2 of each XCD's idle CUs free.
+            # Headline (partial deferral: the upper layers' dW, 5 of 7 per XCD): 7.280-7.307 vs
+            # 7.315-7.338 ms/step (4 rounds; another box 7.26-7.305 vs 7.296-7.324); 6 of 7
+            # measured 7.445-7.459, 4 of 7: 7.318-7.322. Config 5 fp8 (10 of 12): 17.17-17.21 vs
+            # 17.30-17.31, 8 of 12: 17.28. Data parallel keeps every idle CU (headline 7.607-7.62
+            # at 5 of 7 vs 7.547-7.548) (scripts/r6_beside*.sh)
+            cap -= 8 * _BESIDE_SPARE_PER_XCD
         beside = max(8, cap // 8 * 8)
     carry = idle // 8 * 8 if (plan.kind == "xcd" and idle >= 16) else 0
     group = _GROUP_CAP or (3 * num_cus) // 4

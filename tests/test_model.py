@@ -227,10 +227,11 @@ def test_recurrence_kernel_family_map():
     # data parallel: same plan, beside grids capped for the collectives' sake
     ("headline-dp", 32, 800, "gru", 241, True, False, dict(beside_grid=56)),
     # config 5, 7 x BiGRU-1280: 160 CUs, 96 idle: nothing deferred, bf16 beside GEMMs uncapped,
-    # the fp8 BPTT's capped
+    # the fp8 BPTT's capped (10 of each XCD's 12 idle CUs on one device, all 12 with DP)
     ("config5-bf16", 32, 1280, "gru", 241, False, False,
      dict(bptt_cus=160, idle_cus=96, defer_wgrad=False, upper_trigger=1, beside_grid=0, carry_grid=96)),
-    ("config5-fp8", 32, 1280, "gru", 241, False, True, dict(beside_grid=96)),
+    ("config5-fp8", 32, 1280, "gru", 241, False, True, dict(beside_grid=80)),
+    ("config5-fp8-dp", 32, 1280, "gru", 241, True, True, dict(beside_grid=96)),
     # reference headline 7 x bi-ReLU-1760: 224 CUs, everything deferred (32 idle < 56)
     ("relu1760", 32, 1760, "rnn_relu", 241, False, False,
      dict(bptt_cus=224, idle_cus=32, defer_wgrad=True, defer_layers=1 << 30, beside_grid=32, carry_grid=32)),
