@@ -1475,7 +1475,9 @@ __global__ __launch_bounds__(NTH) void rnnrs_bwd_kernel(XBwdRS a) {
   };
 
   if (wave < MW) {
-    const int presleep = (a.knobs >> 20) & 7;     // A/B: s_sleep 1 units before the gather
+    // pre-gather sleep (ops/rnn.py poll_default), s_sleep 1 units; bit 29: units of 4 (the wide
+    // plans, whose groups exchange across XCDs)
+    const int presleep = ((a.knobs >> 20) & 7) << (((a.knobs >> 29) & 1) ? 2 : 0);
     for (int s = a.steps - 1; s >= 0; --s) {
       st.mark(-1);
       const bool has_next = s + 1 < a.steps;

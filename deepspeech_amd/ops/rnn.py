@@ -96,8 +96,10 @@ POLL_MASK = 0x7f << 17
 
 # GRU layers wider than 1024 (config 5 bf16: rnnq_fwd_kernel, whose groups straddle XCDs and
 # exchange write-through) poll later: the forward field counts s_sleep 4 units there (config 5
-# bf16 20.74-20.81 vs 21.49-21.51 ms/step, scripts/r6_c5poll3.sh)
-POLL_WIDE = (5 << 17) | (0 << 20)
+# bf16 20.74-20.81 vs 21.49-21.51 ms/step, scripts/r6_c5poll3.sh), and bit 29 makes the BPTT's
+# field count 4 units too: 3 x 4 = 12, 20.84-20.85 vs 21.03-21.04 (20: 20.89-20.90, 28:
+# 20.99-21.06; scripts/r6_c5bwd.sh)
+POLL_WIDE = (5 << 17) | (3 << 20) | (1 << 29)
 
 
 def poll_default(plan=None) -> int:
