@@ -102,9 +102,16 @@ POLL_MASK = 0x7f << 17
 POLL_WIDE = (5 << 17) | (3 << 20) | (1 << 29)
 
 
+# clipped-ReLU stacks (the reference's 7 x bi-RNN-1760: rnnw kernels, 64-unit workgroups):
+# forward sleep 2, 13.561-13.575 vs 13.603-13.659 ms/step at 4 (scripts/r6_relu2.sh)
+POLL_RELU = (2 << 17) | (4 << 20)
+
+
 def poll_default(plan=None) -> int:
     if plan is not None and plan.cell == "gru" and plan.H > 1024:
         return POLL_WIDE
+    if plan is not None and plan.cell != "gru":
+        return POLL_RELU
     return POLL_DEFAULT
 
 

@@ -284,4 +284,4 @@ def test_recurrence_poll_timing_knob_defaults(monkeypatch):
     monkeypatch.setattr(RNN, "RNNX_KNOBS", 0)
     assert RNN._kernel_knobs(SimpleNamespace(cell="gru", H=1280)) == RNN.POLL_WIDE
     assert RNN._kernel_knobs(SimpleNamespace(cell="gru", H=800)) == RNN.POLL_DEFAULT
-    assert RNN._kernel_knobs(SimpleNamespace(cell="rnn_relu", H=1760)) == RNN.POLL_DEFAULT
+    assert RNN._kernel_knobs(SimpleNamespace(cell="rnn_relu", H=1760)) == RNN.POLL_RELU
